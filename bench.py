@@ -1,0 +1,233 @@
+#!/usr/bin/env python3
+"""Merkle-tree build throughput on MI355X (BASELINE.json metric), device-resident inputs.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3|c1]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+A step = one RawPartitionMerkleTree build of every partition this rank holds (bucket digest
+kernel + digest/tree kernel), plus -- for N > 1 -- the RCCL all-gather of the per-partition roots
+(the one exchange step of the path). Default workload = BASELINE config 4: 10M keys x 1 KiB values
+over 1024 partitions, partition p on GPU p % N (total work fixed: strong scaling). The output is
+one JSON line on rank 0 with `roofline` (digest kernel, HIP events on the launch stream) and
+`cpu_baseline` (the C restatement on the host cores, rank 0 at N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "Merkle-tree build GiB/s (device-resident KV bytes hashed/s) at 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (n_keys, n_partitions, value_len, n_buckets, part_mode, description)
+    "c4": (10_000_000, 1024, 1024, 64, "mod",
+           "C4: 10M keys x 1 KiB values, 1024 partitions round-robin (p = gid % 1024, GPU p % N), B=64"),
+    "c2": (25_600_000, 256, 256, 64, "block",
+           "C2: 256 partitions x 100k keys x 256 B values, B=64"),
+    "c3": (64_000_000, 64, 1024, 64, "block",
+           "C3: 64 partitions x 1M keys x 1 KiB values, B=64"),
+    "c1": (1_000, 1, 64, 64, "block", "C1: 1 partition x 1k keys x 64 B values, B=64"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no baseline)")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, seconds: float):
+    """The C restatement of RawPartitionMerkleTree (oracle/, kind "port") timed on the host on a
+    bounded sample of the same workload: the first partitions of the config, generated on the
+    host with the same generator, built repeatedly for ~`seconds`."""
+    from tests.oracle_c import COracle
+    n_keys, P, V, B, mode, _ = cfg
+    co = COracle()
+    sample_parts = min(P, 32)
+    if mode == "mod":
+        per = -(-n_keys // P)
+        g = (np.arange(per, dtype=np.uint64)[None, :] * np.uint64(P) +
+             np.arange(sample_parts, dtype=np.uint64)[:, None]).reshape(-1)
+        g = np.sort(g[g < n_keys])
+    else:
+        kpp = -(-n_keys // P)
+        g = np.arange(min(n_keys, sample_parts * kpp), dtype=np.uint64)
+    kpp = -(-n_keys // P)
+    part, bk = co.synth_tags(g, P, B, {"block": 0, "mod": 1}[mode], kpp)
+    order, seg = co.layout_a(part, bk, P, B)
+    seg = seg[:sample_parts * B + 1]
+    values = co.synth_values(g[order], V, 0x4D445354)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    res = {}
+    for t in sorted({1, threads}):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            co.build(values, seg, sample_parts, B, V, threads=t, want_nodes=False)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds / 2 or reps >= 1000:
+                break
+        res[t] = values.nbytes * reps / el / 2**30
+    return {
+        "value": round(res[threads], 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "single_thread_value": round(res[1], 3),
+        "sample": f"{sample_parts} of {P} partitions ({len(g)} records x {V} B = "
+                  f"{values.nbytes / 2**20:.0f} MiB), oracle/mde_oracle.c oracle_build with "
+                  f"{threads} threads (1-thread value in single_thread_value); Badger iteration "
+                  f"excluded, so an upper bound on the reference Go CPU rate",
+    }
+
+
+def pmc_traffic(config_name: str, local_bytes: int):
+    """HBM bytes per digest launch from the committed rocprofv3 PMC summary (FETCH_SIZE x 1024 x 2
+    on gfx950, MI355X_MICROARCH.md section HBM), when it was taken on this workload; else None."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        e = d.get(config_name)
+        if e and int(e["algorithmic_bytes"]) == int(local_bytes):
+            return int(e["hbm_read_bytes_per_launch"])
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import mydatastore_amd as mde
+    from mydatastore_amd.workload import make_workload
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = CONFIGS[args.config]
+    n_keys, P, V, B, mode, desc = cfg
+    eng = mde.Engine(local_rank)
+    kpp = -(-n_keys // P)
+    w = make_workload(eng, n_partitions=P, n_buckets=B, value_len=V, part_mode=mode,
+                      keys_per_partition=kpp, n_keys=n_keys, rank=rank, world=world)
+    stream = torch.cuda.current_stream(dev)
+    eng.set_stream(stream.cuda_stream)
+
+    # per-rank fixed-size root slab for the all-gather (partitions are p % world)
+    slab = -(-P // world)
+    roots_slab = torch.zeros(slab * 32, dtype=torch.uint8, device=dev)
+    gathered = torch.zeros(world * slab * 32, dtype=torch.uint8, device=dev) if world > 1 else None
+
+    def step(ev_a=None, ev_b=None):
+        if ev_a is not None:
+            ev_a.record(stream)
+        w.digest_async()
+        if ev_b is not None:
+            ev_b.record(stream)
+        w.tree_async()
+        if world > 1:
+            roots_slab[:w.n_partitions * 32].copy_(w.out["root"], non_blocking=True)
+            dist.all_gather_into_tensor(gathered, roots_slab)
+
+    # parity gate on this rank's workload before timing: tree(digests) == device roots
+    step()
+    torch.cuda.synchronize(dev)
+    root_ref, _ = eng.tree_from_digests(w.out["digest"].cpu().numpy().view(np.uint64), B)
+    parity_ok = bool(np.array_equal(root_ref, w.out["root"].cpu().numpy()))
+
+    for _ in range(args.warmup):
+        step()
+    n_ev = args.steps
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(*evs[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ms = (t1 - t0) * 1e3 / args.steps
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if world > 1:
+        t = torch.tensor([ms, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms, kern_ms_max = float(t[0]), float(t[1])
+        tot = torch.tensor([w.value_bytes], dtype=torch.int64, device=dev)
+        dist.all_reduce(tot)
+        total_bytes = int(tot.item())
+        ok = torch.tensor([int(parity_ok)], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        parity_ok = bool(ok.item())
+        # gathered roots: slot (r, i) = partition r + i*world
+        gr = gathered.view(world, slab, 32).cpu()
+    else:
+        total_bytes = w.value_bytes
+
+    if rank == 0:
+        local_bytes = w.value_bytes
+        achieved = local_bytes / (kern_ms * 1e-3) / 1e9
+        result = {
+            "metric": METRIC,
+            "value": round(total_bytes / 2**30 / (ms * 1e-3), 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 5),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (device-generated splitmix64 values, 'k%016x' keys, SHA-256 bucket tags)",
+            "config": {"workload": desc, "n_keys": n_keys, "value_len": V, "n_partitions": P,
+                       "n_buckets": B, "bytes_hashed_per_step": total_bytes,
+                       "partitions_per_gpu": w.n_partitions, "parallelism": f"partition-shard x{world}",
+                       "root_gather": "rccl all_gather_into_tensor" if world > 1 else None},
+            "roofline": {"bound": "hbm", "kernel": "bucket_digest_kernel",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": pmc_traffic(args.config, local_bytes),
+                         "kernel_ms": round(kern_ms, 5),
+                         "algorithmic_bytes_per_launch": local_bytes},
+            "parity": {"tree_of_device_digests_equals_device_roots": parity_ok},
+        }
+        if world == 1 and not args.no_cpu_baseline and not args.profile:
+            result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_baseline_seconds)
+        else:
+            result["cpu_baseline"] = None
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

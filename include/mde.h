@@ -1,0 +1,155 @@
+/*
+ * mde.h -- MI355X anti-entropy Merkle engine, C ABI (the drop-in boundary).
+ *
+ * Replaces the hot path of andrew-delph/MyDataStore main/merkle_tree.go. Paths below are relative
+ * to the reference root. The reference has no Go `interface` for this path; it is four concrete
+ * functions called from Manager.VerifyEpoch (main/manager.go:1036,1041,1076,1081):
+ *
+ *   RawPartitionMerkleTree(partitionId, lowerEpoch, upperEpoch)      main/merkle_tree.go:86-116
+ *       -> mde_build / mde_build_async (many partitions per call)
+ *   MerkleTreeToPartitionEpochObject(tree, p, lo, hi)                main/merkle_tree.go:118-138
+ *       -> the digest/size/items outputs of mde_build (wire object assembly stays in the caller)
+ *   EpochTreeObjectToMerkleTree(obj)                                 main/merkle_tree.go:140-157
+ *       -> mde_tree_from_digests / _async
+ *   DifferentMerkleTreeBuckets(tree1, tree2)                         main/merkle_tree.go:159-216
+ *       -> mde_diff / mde_diff_async
+ *
+ * plus the write-time tagging the records carry (main/manager.go:773-778 getKeyBucket,
+ * hashring/hashring.go:108-110 FindPartitionID) -> mde_tag_keys_async.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only. `*_async` entry points take DEVICE pointers and enqueue on the
+ *    context's stream (mde_set_stream); the others take HOST pointers and are synchronous.
+ *  - Return 0 (MDE_OK) or a negative MDE_E_* code; never abort or throw across the ABI. The Go
+ *    shim maps codes to errors.Errorf. mde_last_error(ctx) gives the message for the calling
+ *    context (one context per calling thread, or share one: every entry point locks the context).
+ *  - Host input buffers are read only during the call and never retained (cgo pointer rules).
+ *    Outputs are caller-allocated.
+ */
+#ifndef MDE_H_
+#define MDE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MDE_ABI_VERSION 1
+
+#define MDE_OK 0
+#define MDE_E_INVAL -1    /* bad argument (null pointer, zero buckets, inconsistent sizes) */
+#define MDE_E_NOMEM -2    /* host or device allocation failed */
+#define MDE_E_DEVICE -3   /* HIP runtime / kernel failure, or no usable gfx950 device */
+#define MDE_E_TREE -4     /* diff: node/bucket-id mismatch (main/merkle_tree.go:168-170,194-196) */
+#define MDE_E_CAPACITY -5 /* caller-supplied output too small */
+#define MDE_E_DECODE -6   /* bucket hash not 8 bytes (utils/utils.go:80-82) */
+
+/* CustomHash modulus, main/merkle_tree.go:19. */
+#define MDE_HASH_MOD 999999ULL
+
+typedef struct mde_ctx mde_ctx;
+
+/* The records of P partitions in layout A (the order the reference's LSM range scans yield them,
+ * main/merkle_tree.go:90-113): a contiguous value arena, records sorted by (partition, bucket).
+ * Bucket s = p*n_buckets + b holds records seg_rec[s] .. seg_rec[s+1]-1 -- exactly the records
+ * the iterator over [epoch_p_b_{lo}_, epoch_p_b_{hi}_) yields (main/indexs.go:13-20). */
+typedef struct mde_records {
+  const uint8_t* values;     /* value arena: the bytes CustomHash.Add consumes */
+  uint64_t values_bytes;     /* arena size in bytes */
+  uint32_t value_stride;     /* > 0: record r = values[r*stride, (r+1)*stride) */
+  uint32_t reserved0;
+  const uint64_t* value_off; /* value_stride == 0: [n_records+1] byte offsets into values */
+  uint64_t n_records;
+  uint32_t n_partitions;
+  uint32_t n_buckets;        /* PartitionBuckets (config/config.go:20); any value >= 1 */
+  const uint64_t* seg_rec;   /* [n_partitions*n_buckets + 1], nondecreasing, <= n_records */
+} mde_records;
+
+/* Per-partition results. Any pointer may be NULL except root. */
+typedef struct mde_tree_out {
+  uint64_t* digest; /* [P*B] CustomHash value of each bucket, in [0, 999999) */
+  int32_t* size;    /* [P*B] MerkleBucket.size (record count, int32) */
+  int32_t* items;   /* [P]   EpochTreeObject.items = sum of sizes (int32, wraps like Go) */
+  uint8_t* root;    /* [P*32] tree.MerkleRoot() */
+  uint8_t* nodes;   /* [P*mde_tree_internal_nodes(B)*32] internal node hashes, level 1 .. root */
+} mde_tree_out;
+
+int mde_abi_version(void);
+const char* mde_strerror(int code);
+
+/* Context: one HIP device, one stream, device scratch. */
+int mde_create(int device, mde_ctx** out);
+void mde_destroy(mde_ctx* ctx);
+const char* mde_last_error(mde_ctx* ctx);
+int mde_set_stream(mde_ctx* ctx, void* hip_stream); /* NULL: the context's own stream */
+void* mde_get_stream(mde_ctx* ctx);
+int mde_synchronize(mde_ctx* ctx);
+int mde_device_info(mde_ctx* ctx, int* cu_count, char* arch_name, int arch_cap);
+
+/* Tree geometry (merkletree v0.2.0 shape: dup last leaf if odd, self-pair odd levels). */
+uint32_t mde_tree_depth(uint32_t n_buckets);          /* internal levels, root included */
+uint64_t mde_tree_internal_nodes(uint32_t n_buckets); /* nodes per tree in mde_tree_out.nodes */
+uint64_t mde_diff_capacity(uint32_t n_buckets_a, uint32_t n_buckets_b); /* max ids one diff emits */
+
+/* RawPartitionMerkleTree for P partitions: bucket digests + sizes + SHA-256 tree on device.
+ * Host pointers; synchronous (H2D, build, D2H). */
+int mde_build(mde_ctx* ctx, const mde_records* rec, const mde_tree_out* out);
+/* Same, device pointers, enqueued on the context stream (inputs resident in HBM). */
+int mde_build_async(mde_ctx* ctx, const mde_records* rec, const mde_tree_out* out);
+/* The two stages of mde_build_async, for stage timing: bucket byte-sum kernel, then the
+ * digest/size/tree kernel. mde_build_async == mde_digest_async + mde_tree_async. */
+int mde_digest_async(mde_ctx* ctx, const mde_records* rec);
+int mde_tree_async(mde_ctx* ctx, const mde_records* rec, const mde_tree_out* out);
+
+/* EpochTreeObjectToMerkleTree for n_trees trees of n_buckets leaves each: digests -> nodes.
+ * `buckets` are the 8-byte LE bucket hashes exactly as carried on the wire (EpochTreeObject
+ * .buckets); each must be 8 bytes, mirroring utils.DecodeBytesToInt64. */
+int mde_tree_from_digests(mde_ctx* ctx, uint32_t n_trees, uint32_t n_buckets,
+                          const uint64_t* digest, uint8_t* root, uint8_t* nodes);
+int mde_tree_from_digests_async(mde_ctx* ctx, uint32_t n_trees, uint32_t n_buckets,
+                                const uint64_t* digest, uint8_t* root, uint8_t* nodes);
+int mde_decode_bucket_hashes(const uint8_t* const* hashes, const uint32_t* lens, uint32_t n,
+                             uint64_t* digest_out);
+
+/* DifferentMerkleTreeBuckets for n_pairs tree pairs (tree i of A vs tree i of B): bucket ids in
+ * the reference's DFS order, duplicates included (a differing self-paired node emits its subtree
+ * twice). Tree inputs are (digest[n_buckets], nodes[mde_tree_internal_nodes*32]) per tree.
+ * out_ids: [n_pairs * out_stride] with out_stride >= mde_diff_capacity(b_a, b_b);
+ * out_count[i] = number of ids, or MDE_E_TREE where the reference returns an error. */
+int mde_diff(mde_ctx* ctx, uint32_t n_pairs, uint32_t n_buckets_a, const uint64_t* digest_a,
+             const uint8_t* nodes_a, uint32_t n_buckets_b, const uint64_t* digest_b,
+             const uint8_t* nodes_b, int32_t* out_ids, uint64_t out_stride, int32_t* out_count);
+int mde_diff_async(mde_ctx* ctx, uint32_t n_pairs, uint32_t n_buckets_a, const uint64_t* digest_a,
+                   const uint8_t* nodes_a, uint32_t n_buckets_b, const uint64_t* digest_b,
+                   const uint8_t* nodes_b, int32_t* out_ids, uint64_t out_stride,
+                   int32_t* out_count);
+
+/* Write-time tagging of raw keys (device): bucket = BE64(SHA256(key)[:8]) % n_buckets
+ * (main/manager.go:773-778), partition = XXH64(key, 0) % n_partitions (hashring.go:108-110).
+ * key i = keys[key_off[i] .. key_off[i+1]). Either output may be NULL. */
+int mde_tag_keys_async(mde_ctx* ctx, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
+                       uint32_t n_buckets, uint32_t n_partitions, uint32_t* bucket,
+                       uint32_t* partition);
+int mde_tag_keys(mde_ctx* ctx, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
+                 uint32_t n_buckets, uint32_t n_partitions, uint32_t* bucket, uint32_t* partition);
+
+/* Synthetic workload, device side, for benches and tests:
+ * key of record gid = "k%016x" % gid; value word w = splitmix64(seed ^ (gid*2^20 + w)), LE bytes.
+ * part_mode: 0 = gid / keys_per_partition, 1 = gid % P, 2 = FindPartitionID(key). */
+int mde_synth_tags_async(mde_ctx* ctx, const uint64_t* gids, uint64_t n, uint32_t n_partitions,
+                         uint32_t n_buckets, int part_mode, uint64_t keys_per_partition,
+                         uint32_t* partition, uint32_t* bucket);
+int mde_synth_values_async(mde_ctx* ctx, uint8_t* dst, const uint64_t* gids, uint64_t n,
+                           uint32_t value_len, uint64_t seed);
+
+/* Plain device memory helpers for callers without a device allocator of their own. */
+int mde_dev_alloc(mde_ctx* ctx, uint64_t bytes, void** ptr);
+int mde_dev_free(mde_ctx* ctx, void* ptr);
+int mde_memcpy_h2d(mde_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+int mde_memcpy_d2h(mde_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MDE_H_ */

@@ -1,0 +1,286 @@
+"""mydatastore_amd -- MI355X anti-entropy Merkle engine (drop-in for main/merkle_tree.go).
+
+The product is ``libmde.so`` (C ABI, ``include/mde.h``; gfx950 HIP kernels). This module is a
+thin ctypes binding over that ABI for tests and benches; there is no Python or CPU fallback:
+every call goes to the device and raises :class:`MdeError` when the library, the device or a
+kernel fails.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("MDE_LIB", _PKG / "libmde.so"))
+
+MDE_OK = 0
+MDE_E_INVAL = -1
+MDE_E_NOMEM = -2
+MDE_E_DEVICE = -3
+MDE_E_TREE = -4
+MDE_E_CAPACITY = -5
+MDE_E_DECODE = -6
+HASH_MOD = 999999
+
+# Every symbol include/mde.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "mde_abi_version", "mde_strerror", "mde_create", "mde_destroy", "mde_last_error",
+    "mde_set_stream", "mde_get_stream", "mde_synchronize", "mde_device_info", "mde_tree_depth",
+    "mde_tree_internal_nodes", "mde_diff_capacity", "mde_build", "mde_build_async",
+    "mde_digest_async", "mde_tree_async", "mde_tree_from_digests", "mde_tree_from_digests_async",
+    "mde_decode_bucket_hashes", "mde_diff", "mde_diff_async", "mde_tag_keys_async", "mde_tag_keys",
+    "mde_synth_tags_async", "mde_synth_values_async", "mde_dev_alloc", "mde_dev_free",
+    "mde_memcpy_h2d", "mde_memcpy_d2h",
+)
+
+
+class MdeError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mde error {code}: {msg}")
+        self.code = code
+
+
+class Records(C.Structure):
+    """struct mde_records (include/mde.h)."""
+    _fields_ = [
+        ("values", C.c_void_p), ("values_bytes", C.c_uint64), ("value_stride", C.c_uint32),
+        ("reserved0", C.c_uint32), ("value_off", C.c_void_p), ("n_records", C.c_uint64),
+        ("n_partitions", C.c_uint32), ("n_buckets", C.c_uint32), ("seg_rec", C.c_void_p),
+    ]
+
+
+class TreeOut(C.Structure):
+    """struct mde_tree_out (include/mde.h)."""
+    _fields_ = [("digest", C.c_void_p), ("size", C.c_void_p), ("items", C.c_void_p),
+                ("root", C.c_void_p), ("nodes", C.c_void_p)]
+
+
+_lib = None
+
+
+def load_library() -> C.CDLL:
+    """Load libmde.so (raises if it has not been built -- there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(f"{LIB_PATH} not built: run `python -m mydatastore_amd._build`")
+    lib = C.CDLL(str(LIB_PATH))
+    u32, u64, i32, vp = C.c_uint32, C.c_uint64, C.c_int32, C.c_void_p
+    sig = {
+        "mde_abi_version": (C.c_int, []),
+        "mde_strerror": (C.c_char_p, [C.c_int]),
+        "mde_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+        "mde_destroy": (None, [vp]),
+        "mde_last_error": (C.c_char_p, [vp]),
+        "mde_set_stream": (C.c_int, [vp, vp]),
+        "mde_get_stream": (vp, [vp]),
+        "mde_synchronize": (C.c_int, [vp]),
+        "mde_device_info": (C.c_int, [vp, C.POINTER(C.c_int), C.c_char_p, C.c_int]),
+        "mde_tree_depth": (u32, [u32]),
+        "mde_tree_internal_nodes": (u64, [u32]),
+        "mde_diff_capacity": (u64, [u32, u32]),
+        "mde_build": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
+        "mde_build_async": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
+        "mde_digest_async": (C.c_int, [vp, C.POINTER(Records)]),
+        "mde_tree_async": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
+        "mde_tree_from_digests": (C.c_int, [vp, u32, u32, vp, vp, vp]),
+        "mde_tree_from_digests_async": (C.c_int, [vp, u32, u32, vp, vp, vp]),
+        "mde_decode_bucket_hashes": (C.c_int, [vp, vp, u32, vp]),
+        "mde_diff": (C.c_int, [vp, u32, u32, vp, vp, u32, vp, vp, vp, u64, vp]),
+        "mde_diff_async": (C.c_int, [vp, u32, u32, vp, vp, u32, vp, vp, vp, u64, vp]),
+        "mde_tag_keys_async": (C.c_int, [vp, vp, vp, u64, u32, u32, vp, vp]),
+        "mde_tag_keys": (C.c_int, [vp, vp, vp, u64, u32, u32, vp, vp]),
+        "mde_synth_tags_async": (C.c_int, [vp, vp, u64, u32, u32, C.c_int, u64, vp, vp]),
+        "mde_synth_values_async": (C.c_int, [vp, vp, vp, u64, u32, u64]),
+        "mde_dev_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
+        "mde_dev_free": (C.c_int, [vp, vp]),
+        "mde_memcpy_h2d": (C.c_int, [vp, vp, vp, u64]),
+        "mde_memcpy_d2h": (C.c_int, [vp, vp, vp, u64]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def tree_internal_nodes(n_buckets: int) -> int:
+    return int(load_library().mde_tree_internal_nodes(n_buckets))
+
+
+def tree_depth(n_buckets: int) -> int:
+    return int(load_library().mde_tree_depth(n_buckets))
+
+
+def diff_capacity(b1: int, b2: int) -> int:
+    return int(load_library().mde_diff_capacity(b1, b2))
+
+
+def _ptr(a) -> int:
+    """Address of a numpy array or a torch tensor (None -> NULL)."""
+    if a is None:
+        return 0
+    if isinstance(a, np.ndarray):
+        if not a.flags["C_CONTIGUOUS"]:
+            raise ValueError("array must be C-contiguous")
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):
+        if not a.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+        return a.data_ptr()
+    raise TypeError(f"unsupported buffer type {type(a)}")
+
+
+def _nbytes(a) -> int:
+    if isinstance(a, np.ndarray):
+        return a.nbytes
+    return a.numel() * a.element_size()
+
+
+class Engine:
+    """One mde_ctx (device, stream, scratch). Host-array methods are synchronous; ``*_async``
+    methods take device tensors and enqueue on the context stream (see :meth:`set_stream`)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = C.c_void_p()
+        rc = self.lib.mde_create(device, C.byref(h))
+        if rc != MDE_OK:
+            raise MdeError(rc, f"mde_create(device={device}) failed: "
+                               f"{self.lib.mde_strerror(rc).decode()} (needs a gfx950 GPU)")
+        self.ctx = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.mde_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != MDE_OK:
+            msg = self.lib.mde_last_error(self.ctx)
+            raise MdeError(rc, (msg or b"").decode() or self.lib.mde_strerror(rc).decode())
+
+    # -- context ------------------------------------------------------------------------------
+    def set_stream(self, stream_handle: int | None):
+        self._check(self.lib.mde_set_stream(self.ctx, stream_handle or None))
+
+    def synchronize(self):
+        self._check(self.lib.mde_synchronize(self.ctx))
+
+    def device_info(self):
+        cus = C.c_int()
+        arch = C.create_string_buffer(64)
+        self._check(self.lib.mde_device_info(self.ctx, C.byref(cus), arch, 64))
+        return cus.value, arch.value.decode()
+
+    # -- build --------------------------------------------------------------------------------
+    @staticmethod
+    def records(values, n_partitions, n_buckets, seg_rec, value_stride=0, value_off=None,
+                n_records=None) -> Records:
+        if n_records is None:
+            n_records = int(seg_rec[-1]) if isinstance(seg_rec, np.ndarray) else None
+        if n_records is None:
+            raise ValueError("n_records required for device seg_rec")
+        return Records(_ptr(values), _nbytes(values) if values is not None else 0, value_stride, 0,
+                       _ptr(value_off), n_records, n_partitions, n_buckets, _ptr(seg_rec))
+
+    def build(self, values: np.ndarray, seg_rec: np.ndarray, n_partitions: int, n_buckets: int,
+              value_stride: int = 0, value_off: np.ndarray | None = None, want_nodes=True):
+        """RawPartitionMerkleTree for P partitions from host arrays (H2D, build, D2H)."""
+        P, B = n_partitions, n_buckets
+        seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
+        values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)
+        if value_off is not None:
+            value_off = np.ascontiguousarray(value_off, dtype=np.uint64)
+        n_rec = (value_off.size - 1) if value_off is not None else (
+            values.size // value_stride if value_stride else 0)
+        rec = Records(_ptr(values), values.nbytes, value_stride, 0, _ptr(value_off), n_rec, P, B,
+                      _ptr(seg_rec))
+        out = {
+            "digest": np.zeros(P * B, np.uint64), "size": np.zeros(P * B, np.int32),
+            "items": np.zeros(P, np.int32), "root": np.zeros(P * 32, np.uint8),
+            "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
+        }
+        to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
+        self._check(self.lib.mde_build(self.ctx, C.byref(rec), C.byref(to)))
+        return out
+
+    def build_async(self, rec: Records, out: TreeOut):
+        self._check(self.lib.mde_build_async(self.ctx, C.byref(rec), C.byref(out)))
+
+    def digest_async(self, rec: Records):
+        self._check(self.lib.mde_digest_async(self.ctx, C.byref(rec)))
+
+    def tree_async(self, rec: Records, out: TreeOut):
+        self._check(self.lib.mde_tree_async(self.ctx, C.byref(rec), C.byref(out)))
+
+    # -- tree from digests (EpochTreeObjectToMerkleTree) --------------------------------------
+    def tree_from_digests(self, digests: np.ndarray, n_buckets: int, want_nodes=True):
+        d = np.ascontiguousarray(digests, dtype=np.uint64).reshape(-1)
+        T = d.size // n_buckets
+        root = np.zeros(T * 32, np.uint8)
+        nodes = np.zeros(T * tree_internal_nodes(n_buckets) * 32, np.uint8) if want_nodes else None
+        self._check(self.lib.mde_tree_from_digests(self.ctx, T, n_buckets, _ptr(d), _ptr(root),
+                                                   _ptr(nodes)))
+        return root, nodes
+
+    def tree_from_digests_async(self, n_trees, n_buckets, digest, root, nodes=None):
+        self._check(self.lib.mde_tree_from_digests_async(self.ctx, n_trees, n_buckets, _ptr(digest),
+                                                         _ptr(root), _ptr(nodes)))
+
+    # -- diff (DifferentMerkleTreeBuckets) ----------------------------------------------------
+    def diff(self, ba: int, da: np.ndarray, na: np.ndarray, bb: int, db: np.ndarray,
+             nb: np.ndarray, n_pairs: int = 1):
+        """Returns a list (per pair) of bucket-id lists, or MDE_E_TREE where the reference errors."""
+        cap = diff_capacity(ba, bb)
+        ids = np.zeros(n_pairs * cap, np.int32)
+        cnt = np.zeros(n_pairs, np.int32)
+        da, db = (np.ascontiguousarray(x, dtype=np.uint64) for x in (da, db))
+        na, nb = (np.ascontiguousarray(x, dtype=np.uint8) for x in (na, nb))
+        self._check(self.lib.mde_diff(self.ctx, n_pairs, ba, _ptr(da), _ptr(na), bb, _ptr(db),
+                                      _ptr(nb), _ptr(ids), cap, _ptr(cnt)))
+        res = []
+        for i in range(n_pairs):
+            c = int(cnt[i])
+            res.append(c if c < 0 else ids[i * cap:i * cap + c].tolist())
+        return res
+
+    def diff_async(self, n_pairs, ba, da, na, bb, db, nb, out_ids, out_stride, out_count):
+        self._check(self.lib.mde_diff_async(self.ctx, n_pairs, ba, _ptr(da), _ptr(na), bb, _ptr(db),
+                                            _ptr(nb), _ptr(out_ids), out_stride, _ptr(out_count)))
+
+    # -- tagging / synthetic workload ---------------------------------------------------------
+    def tag_keys(self, keys, n_buckets: int, n_partitions: int):
+        """(bucket, partition) for a list of byte keys (getKeyBucket / FindPartitionID)."""
+        offs = np.zeros(len(keys) + 1, np.uint64)
+        offs[1:] = np.cumsum([len(k) for k in keys])
+        blob = np.frombuffer(b"".join(keys) or b"\0", dtype=np.uint8).copy()
+        bk = np.zeros(len(keys), np.uint32)
+        pt = np.zeros(len(keys), np.uint32)
+        self._check(self.lib.mde_tag_keys(self.ctx, _ptr(blob), _ptr(offs), len(keys), n_buckets,
+                                          n_partitions, _ptr(bk), _ptr(pt)))
+        return bk, pt
+
+    def tag_keys_async(self, keys, key_off, n, n_buckets, n_partitions, bucket, partition):
+        self._check(self.lib.mde_tag_keys_async(self.ctx, _ptr(keys), _ptr(key_off), n, n_buckets,
+                                                n_partitions, _ptr(bucket), _ptr(partition)))
+
+    def synth_tags_async(self, gids, n, n_partitions, n_buckets, part_mode, kpp, part, bucket):
+        self._check(self.lib.mde_synth_tags_async(self.ctx, _ptr(gids), n, n_partitions, n_buckets,
+                                                  part_mode, kpp, _ptr(part), _ptr(bucket)))
+
+    def synth_values_async(self, dst, gids, n, value_len, seed):
+        self._check(self.lib.mde_synth_values_async(self.ctx, _ptr(dst), _ptr(gids), n, value_len,
+                                                    seed))

@@ -1,0 +1,94 @@
+"""Build the engine's native libraries in-tree (hipcc for gfx950; gcc for the oracle).
+
+  python -m mydatastore_amd._build            # libmde.so (+ host mirror, C++ tests, oracle)
+
+Outputs (git-ignored, but shipped to the GPU box with the snapshot):
+  mydatastore_amd/libmde.so         C ABI (include/mde.h) + gfx950 kernels
+  mydatastore_amd/libmde_host.so    C++ mirror of main/merkle_tree.go over the C ABI
+  tests/cpp/build/test_merkle_tree  C++ port of the reference's Merkle tests
+  oracle/build/liboracle.so         CPU restatement (test infrastructure only)
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+OBJ = PKG / "build"
+HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+HIP_FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall",
+             "-Wno-unused-function", f"-I{ROOT / 'include'}"]
+
+LIB = PKG / "libmde.so"
+HOST_LIB = PKG / "libmde_host.so"
+ORACLE_LIB = ROOT / "oracle" / "build" / "liboracle.so"
+CPP_TEST = ROOT / "tests" / "cpp" / "build" / "test_merkle_tree"
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(str(c) for c in cmd), flush=True)
+    subprocess.run([str(c) for c in cmd], check=True)
+
+
+def build_engine(verbose: bool = True) -> Path:
+    OBJ.mkdir(exist_ok=True)
+    headers = list(CSRC.glob("*.hpp")) + [ROOT / "include" / "mde.h"]
+    sources = sorted(CSRC.glob("*.hip")) + [CSRC / "mde_api.cpp"]
+    objs = []
+    for src in sources:
+        obj = OBJ / (src.stem + ".o")
+        if _stale(obj, [src, *headers]):
+            lang = ["-x", "hip"] if src.suffix == ".hip" else []
+            _run([HIPCC, *HIP_FLAGS, *lang, "-c", src, "-o", obj], verbose)
+        objs.append(obj)
+    if _stale(LIB, objs):
+        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs], verbose)
+    return LIB
+
+
+def build_host(verbose: bool = True) -> Path:
+    hdir = PKG / "host"
+    srcs = sorted(hdir.glob("*.cpp"))
+    deps = [*srcs, *hdir.glob("*.hpp"), ROOT / "include" / "mde.h", LIB]
+    if srcs and _stale(HOST_LIB, deps):
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{ROOT / 'include'}",
+              *srcs, "-o", HOST_LIB, f"-L{PKG}", "-lmde", f"-Wl,-rpath,$ORIGIN"], verbose)
+    test_src = ROOT / "tests" / "cpp" / "test_merkle_tree.cpp"
+    if test_src.exists() and _stale(CPP_TEST, [test_src, *deps, HOST_LIB]):
+        CPP_TEST.parent.mkdir(parents=True, exist_ok=True)
+        _run(["g++", "-O2", "-std=c++17", "-Wall", f"-I{ROOT / 'include'}", f"-I{hdir}", test_src,
+              "-o", CPP_TEST, f"-L{PKG}", "-lmde_host", "-lmde",
+              f"-Wl,-rpath,{PKG}", "-Wl,-rpath,$ORIGIN/../../../mydatastore_amd"], verbose)
+    return HOST_LIB
+
+
+def build_oracle(verbose: bool = True) -> Path:
+    src = ROOT / "oracle" / "mde_oracle.c"
+    if _stale(ORACLE_LIB, [src]):
+        ORACLE_LIB.parent.mkdir(parents=True, exist_ok=True)
+        _run(["gcc", "-O2", "-fPIC", "-shared", "-Wall", src, "-o", ORACLE_LIB, "-lpthread"], verbose)
+    return ORACLE_LIB
+
+
+def build_all(verbose: bool = True) -> None:
+    build_engine(verbose)
+    build_host(verbose)
+    build_oracle(verbose)
+
+
+if __name__ == "__main__":
+    build_all(verbose="-q" not in sys.argv)

@@ -1,0 +1,179 @@
+// digest.hip -- bucket digest kernel (the HBM-bound hot loop of RawPartitionMerkleTree).
+//
+// Reference: main/merkle_tree.go:90-113 walks every bucket's records and folds
+// CustomHash.Add (:25-32): value = (value + sum(bytes)) % 999999. Non-negative modular addition
+// is associative, so a bucket's digest is (sum of all its value bytes) % 999999; this kernel
+// produces the exact u64 byte sum per bucket and the tree kernel applies the modulus.
+//
+// Layout A: values form one contiguous arena ordered by (partition, bucket) -- the order the
+// reference's per-bucket LSM range scans yield -- so bucket s is the byte range
+// [segpos(s), segpos(s+1)). The arena is split into equal contiguous ranges, one per wave
+// (64 lanes); a wave streams its range in 8 KiB steps (8 x 16-B nontemporal loads per lane,
+// 1 KiB per wave-instruction, fully coalesced), byte-sums each dword with v_sad_u8 into a u32
+// lane accumulator, and tracks the bucket it is in with wave-uniform scalar state. A step that
+// lies wholly inside one bucket takes the fast path (loads + 32 v_sad_u8 per lane); a step that
+// crosses bucket boundaries is split with byte masks. When the wave leaves a bucket it reduces
+// its lanes (6 shuffles) and issues ONE u64 atomic add for that bucket: no LDS, no barriers,
+// at most (#buckets touched) atomics per wave.
+//
+// Algorithmic bytes per launch: sum of value lengths.
+#include "mde_device.hpp"
+#include "mde_internal.hpp"
+
+namespace mde {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 8;
+constexpr uint64_t kStepBytes = 64ull * 16ull * kUnroll;  // 8 KiB per wave step
+
+__device__ __forceinline__ uint64_t segpos(const SegDesc& d, uint32_t s) {
+  const uint64_t r = d.seg_rec[s];
+  return d.shift + (d.stride ? r * (uint64_t)d.stride : d.value_off[r]);
+}
+
+// Largest s in [lo, S) with segpos(s) <= x (lo if none). 64-ary search: one vector load and one
+// ballot per round, log64(S) rounds. Must be called by all 64 lanes.
+__device__ __forceinline__ uint32_t seg_search(const SegDesc& d, uint32_t lo, uint64_t x, int lane) {
+  uint32_t hi = d.S;
+  while (hi - lo > 1) {
+    const uint32_t n = hi - lo;
+    const uint32_t step = (n + 63u) / 64u;
+    const uint32_t idx = lo + (uint32_t)lane * step;
+    const bool pred = idx < hi && segpos(d, idx) <= x;
+    const int c = __popcll(__ballot(pred));
+    if (c == 0) return lo;
+    lo = lo + (uint32_t)(c - 1) * step;
+    hi = min(lo + step, hi);
+  }
+  return lo;
+}
+
+// Next bucket after s that contains position x == segpos(s+1) (skips empty buckets).
+__device__ __forceinline__ uint32_t seg_next(const SegDesc& d, uint32_t s, uint64_t x, int lane) {
+  const uint32_t idx = s + 1u + (uint32_t)lane;
+  const bool pred = idx < d.S && segpos(d, idx) <= x;
+  const int c = __popcll(__ballot(pred));
+  if (c < 64) return s + (uint32_t)c;
+  return seg_search(d, s + 64u, x, lane);
+}
+
+__device__ __forceinline__ uint32_t byte_mask(int lo, int hi) {  // bytes [lo, hi) of a dword
+  const uint32_t mh = hi >= 4 ? 0xffffffffu : ((1u << (8 * hi)) - 1u);
+  const uint32_t ml = lo >= 4 ? 0xffffffffu : ((1u << (8 * lo)) - 1u);
+  return hi > lo ? (mh & ~ml) : 0u;
+}
+
+// Sum of bytes [a, b) (clamped to [0, 16]) of one 16-byte vector.
+__device__ __forceinline__ uint32_t masked_sum16(u32x4 v, int64_t a, int64_t b, uint32_t acc) {
+  const int ia = (int)min<int64_t>(max<int64_t>(a, 0), 16);
+  const int ib = (int)min<int64_t>(max<int64_t>(b, 0), 16);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int lo = min(max(ia - 4 * k, 0), 4), hi = min(max(ib - 4 * k, 0), 4);
+    acc = __builtin_amdgcn_sad_u8(v[k] & byte_mask(lo, hi), 0u, acc);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ void flush(unsigned long long* sums, uint32_t s, uint32_t acc) {
+  unsigned long long v = acc;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(sums + s, v);
+}
+
+__global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (wave >= a.n_waves) return;
+  const SegDesc& d = a.seg;
+  const uint64_t first = segpos(d, 0) & ~15ull;
+  const uint64_t last = segpos(d, d.S);
+  const uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
+  if (beg >= last) return;
+  const uint64_t end = min(beg + a.wave_bytes, last);
+
+  uint32_t s = seg_search(d, 0u, beg, lane);
+  uint64_t sb = segpos(d, s), se = segpos(d, s + 1);
+  uint32_t acc = 0;
+  const u32x4* lane_base = reinterpret_cast<const u32x4*>(d.base) + lane;
+
+  for (uint64_t p = beg; p < end; p += kStepBytes) {
+    u32x4 v[kUnroll];
+    const bool full = p + kStepBytes <= end;
+    const u32x4* src = lane_base + (p >> 4);
+    if (full) {
+#pragma unroll
+      for (int u = 0; u < kUnroll; u++) v[u] = __builtin_nontemporal_load(src + u * 64);
+    } else {
+#pragma unroll
+      for (int u = 0; u < kUnroll; u++) {
+        const uint64_t x = p + (uint64_t)u * 1024u + (uint64_t)lane * 16u;
+        v[u] = x < end ? __builtin_nontemporal_load(src + u * 64) : u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+    if (full && sb <= p && p + kStepBytes <= se) {
+#pragma unroll
+      for (int u = 0; u < kUnroll; u++) {
+        acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
+      }
+    } else {
+      const uint64_t q = min(p + kStepBytes, end);
+      for (;;) {
+        const uint64_t lo = max(sb, p), hi = min(se, q);
+        if (lo < hi) {
+#pragma unroll
+          for (int u = 0; u < kUnroll; u++) {
+            const int64_t x = (int64_t)(p + (uint64_t)u * 1024u + (uint64_t)lane * 16u);
+            acc = masked_sum16(v[u], (int64_t)lo - x, (int64_t)hi - x, acc);
+          }
+        }
+        if (se >= q) break;
+        flush(a.sums, s, acc);
+        acc = 0;
+        s = seg_next(d, s, se, lane);
+        sb = segpos(d, s);
+        se = segpos(d, s + 1);
+      }
+    }
+  }
+  flush(a.sums, s, acc);
+}
+
+}  // namespace
+
+int bucket_digest_blocks_per_cu() {
+  int blocks = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, bucket_digest_kernel, kThreads, 0) !=
+          hipSuccess ||
+      blocks <= 0)
+    blocks = 4;
+  return blocks;
+}
+
+// One contiguous range per resident wave: every wave of the grid is co-resident and all ranges
+// are equal, so the launch has no tail of late waves.
+void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, uint64_t* wave_bytes,
+                        uint32_t* n_waves) {
+  const uint64_t target_waves =
+      (uint64_t)(cus > 0 ? cus : 256) * (uint64_t)(blocks_per_cu > 0 ? blocks_per_cu : 4) * (kThreads / 64);
+  uint64_t wb = (bytes + target_waves - 1) / target_waves;
+  wb = (wb + kStepBytes - 1) / kStepBytes * kStepBytes;
+  if (wb < 2 * kStepBytes) wb = 2 * kStepBytes;
+  if (wb > (8ull << 20)) wb = 8ull << 20;  // keeps every u32 lane accumulator exact
+  *wave_bytes = wb;
+  *n_waves = (uint32_t)((bytes + 16 + wb - 1) / wb);
+}
+
+hipError_t launch_bucket_digest(const DigestLaunch& a, hipStream_t st) {
+  if (a.n_waves == 0) return hipSuccess;
+  const uint32_t blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);
+  hipLaunchKernelGGL(bucket_digest_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace mde

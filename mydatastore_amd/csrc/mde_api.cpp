@@ -1,0 +1,521 @@
+// mde_api.cpp -- C ABI of the MI355X Merkle engine (include/mde.h).
+//
+// One context = one HIP device + one stream + grow-only device scratch. Every entry point takes
+// the context lock and makes the context's device current on the calling thread, so a context can
+// be shared by many goroutine-backed OS threads (VerifyEpoch runs on any of WORKERS_COUNT workers,
+// main/manager.go:166-170) or each thread can own one. Errors are returned as MDE_E_* codes with
+// the message kept per context; nothing throws or aborts across the ABI.
+#include "../../include/mde.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+
+#include "mde_internal.hpp"
+
+struct mde_ctx {
+  int device = 0;
+  int cus = 256;
+  int digest_blocks_per_cu = 0;  // occupancy of the digest kernel (queried once)
+  char arch[64] = {0};
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  // Byte-sum accumulators: zero between builds (the tree kernel clears what it reads).
+  unsigned long long* sums = nullptr;
+  uint64_t sums_cap = 0;
+  bool sums_dirty = false;
+  // Host-API staging (device) and a scratch node array for B > kTreeLdsMaxBuckets.
+  struct Buf { void* p = nullptr; uint64_t cap = 0; };
+  Buf stage[12];
+  Buf nodes_scratch;
+};
+
+namespace {
+
+int set_err(mde_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define MDE_HIP(c, expr)                                                                  \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) {                                                               \
+      if (c) c->sums_dirty = true;                                                        \
+      return set_err((c), MDE_E_DEVICE, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),  \
+                     __FILE__, __LINE__);                                                 \
+    }                                                                                     \
+  } while (0)
+
+int ensure_buf(mde_ctx* c, mde_ctx::Buf& b, uint64_t bytes) {
+  if (b.cap >= bytes && b.p) return MDE_OK;
+  if (b.p) {
+    MDE_HIP(c, hipStreamSynchronize(c->stream));
+    MDE_HIP(c, hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  uint64_t cap = bytes < 256 ? 256 : bytes;
+  if (hipMalloc(&b.p, cap) != hipSuccess) {
+    b.p = nullptr;
+    return set_err(c, MDE_E_NOMEM, "device allocation of %llu bytes failed", (unsigned long long)cap);
+  }
+  b.cap = cap;
+  return MDE_OK;
+}
+
+int ensure_sums(mde_ctx* c, uint64_t S) {
+  if (c->sums_cap < S || !c->sums) {
+    if (c->sums) {
+      MDE_HIP(c, hipStreamSynchronize(c->stream));
+      MDE_HIP(c, hipFree(c->sums));
+      c->sums = nullptr;
+    }
+    uint64_t cap = S < 1024 ? 1024 : S;
+    if (hipMalloc(&c->sums, cap * 8) != hipSuccess) {
+      c->sums = nullptr;
+      c->sums_cap = 0;
+      return set_err(c, MDE_E_NOMEM, "sums allocation failed");
+    }
+    c->sums_cap = cap;
+    c->sums_dirty = true;
+  }
+  if (c->sums_dirty) {
+    MDE_HIP(c, hipMemsetAsync(c->sums, 0, c->sums_cap * 8, c->stream));
+    c->sums_dirty = false;
+  }
+  return MDE_OK;
+}
+
+struct Guard {
+  mde_ctx* c;
+  std::lock_guard<std::mutex> lk;
+  explicit Guard(mde_ctx* ctx) : c(ctx), lk(ctx->mu) { (void)hipSetDevice(ctx->device); c->err.clear(); }
+};
+
+int check_records(mde_ctx* c, const mde_records* r) {
+  if (!r) return set_err(c, MDE_E_INVAL, "records is NULL");
+  if (r->n_buckets == 0) return set_err(c, MDE_E_INVAL, "n_buckets must be >= 1");
+  if (!r->seg_rec) return set_err(c, MDE_E_INVAL, "seg_rec is NULL");
+  if ((uint64_t)r->n_partitions * r->n_buckets > 0xffffffffull)
+    return set_err(c, MDE_E_INVAL, "n_partitions * n_buckets exceeds 2^32");
+  if (r->value_stride == 0 && !r->value_off && r->n_records)
+    return set_err(c, MDE_E_INVAL, "variable-length values need value_off");
+  if (!r->values && r->values_bytes) return set_err(c, MDE_E_INVAL, "values is NULL");
+  if (r->value_stride && (uint64_t)r->value_stride * r->n_records > r->values_bytes)
+    return set_err(c, MDE_E_INVAL, "n_records * value_stride exceeds values_bytes");
+  return MDE_OK;
+}
+
+int digest_async(mde_ctx* c, const mde_records* r) {
+  const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
+  int rc = ensure_sums(c, S);
+  if (rc) return rc;
+  if (S == 0 || r->n_records == 0 || r->values_bytes == 0) return MDE_OK;
+  mde::DigestLaunch a{};
+  const uintptr_t v = reinterpret_cast<uintptr_t>(r->values);
+  a.seg.base = reinterpret_cast<const uint8_t*>(v & ~uintptr_t(15));
+  a.seg.shift = v & 15u;
+  a.seg.stride = r->value_stride;
+  a.seg.value_off = r->value_off;
+  a.seg.seg_rec = r->seg_rec;
+  a.seg.S = (uint32_t)S;
+  a.sums = c->sums;
+  if (!c->digest_blocks_per_cu) c->digest_blocks_per_cu = mde::bucket_digest_blocks_per_cu();
+  mde::plan_bucket_digest(r->values_bytes + a.seg.shift, c->cus, c->digest_blocks_per_cu,
+                          &a.wave_bytes, &a.n_waves);
+  MDE_HIP(c, mde::launch_bucket_digest(a, c->stream));
+  return MDE_OK;
+}
+
+int tree_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
+  if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
+  const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
+  int rc = ensure_sums(c, S);
+  if (rc) return rc;
+  mde::TreeLaunch t{};
+  t.P = r->n_partitions;
+  t.B = r->n_buckets;
+  t.sums_in = c->sums;
+  t.sums_clear = c->sums;
+  t.seg_rec = r->seg_rec;
+  t.digest_out = o->digest;
+  t.size_out = o->size;
+  t.items_out = o->items;
+  t.root_out = o->root;
+  t.nodes_out = o->nodes;
+  t.n_int = mde::tree_internal(r->n_buckets);
+  if (!t.nodes_out && r->n_buckets > mde::kTreeLdsMaxBuckets) {
+    rc = ensure_buf(c, c->nodes_scratch, (uint64_t)t.P * t.n_int * 32);
+    if (rc) return rc;
+    t.nodes_out = static_cast<uint8_t*>(c->nodes_scratch.p);
+  }
+  MDE_HIP(c, mde::launch_tree(t, c->stream));
+  return MDE_OK;
+}
+
+int tree_digests_async(mde_ctx* c, uint32_t n_trees, uint32_t B, const uint64_t* digest,
+                       uint8_t* root, uint8_t* nodes) {
+  if (B == 0 || !digest || !root) return set_err(c, MDE_E_INVAL, "bad tree_from_digests arguments");
+  mde::TreeLaunch t{};
+  t.P = n_trees;
+  t.B = B;
+  t.digest_in = digest;
+  t.root_out = root;
+  t.nodes_out = nodes;
+  t.n_int = mde::tree_internal(B);
+  if (!t.nodes_out && B > mde::kTreeLdsMaxBuckets) {
+    int rc = ensure_buf(c, c->nodes_scratch, (uint64_t)n_trees * t.n_int * 32);
+    if (rc) return rc;
+    t.nodes_out = static_cast<uint8_t*>(c->nodes_scratch.p);
+  }
+  MDE_HIP(c, mde::launch_tree(t, c->stream));
+  return MDE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mde_abi_version(void) { return MDE_ABI_VERSION; }
+
+const char* mde_strerror(int code) {
+  switch (code) {
+    case MDE_OK: return "ok";
+    case MDE_E_INVAL: return "invalid argument";
+    case MDE_E_NOMEM: return "out of memory";
+    case MDE_E_DEVICE: return "device error";
+    case MDE_E_TREE: return "merkle trees do not match in shape";
+    case MDE_E_CAPACITY: return "output capacity too small";
+    case MDE_E_DECODE: return "byte slice should be 8 bytes long for int64 decoding";
+    default: return "unknown error";
+  }
+}
+
+int mde_create(int device, mde_ctx** out) {
+  if (!out) return MDE_E_INVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MDE_E_DEVICE;
+  if (device < 0 || device >= n) return MDE_E_INVAL;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return MDE_E_DEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return MDE_E_DEVICE;  // gfx950-only code objects
+  mde_ctx* c = new (std::nothrow) mde_ctx();
+  if (!c) return MDE_E_NOMEM;
+  c->device = device;
+  c->cus = prop.multiProcessorCount;
+  std::snprintf(c->arch, sizeof c->arch, "%s", prop.gcnArchName);
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return MDE_E_DEVICE;
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return MDE_OK;
+}
+
+void mde_destroy(mde_ctx* c) {
+  if (!c) return;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->sums) (void)hipFree(c->sums);
+    for (auto& b : c->stage)
+      if (b.p) (void)hipFree(b.p);
+    if (c->nodes_scratch.p) (void)hipFree(c->nodes_scratch.p);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  }
+  delete c;
+}
+
+const char* mde_last_error(mde_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int mde_set_stream(mde_ctx* c, void* s) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  return MDE_OK;
+}
+
+void* mde_get_stream(mde_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+
+int mde_synchronize(mde_ctx* c) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  return MDE_OK;
+}
+
+int mde_device_info(mde_ctx* c, int* cu_count, char* arch, int cap) {
+  if (!c) return MDE_E_INVAL;
+  if (cu_count) *cu_count = c->cus;
+  if (arch && cap > 0) std::snprintf(arch, (size_t)cap, "%s", c->arch);
+  return MDE_OK;
+}
+
+uint32_t mde_tree_depth(uint32_t B) { return B ? mde::tree_levels(B, nullptr) - 1 : 0; }
+uint64_t mde_tree_internal_nodes(uint32_t B) { return B ? mde::tree_internal(B) : 0; }
+uint64_t mde_diff_capacity(uint32_t a, uint32_t b) {
+  if (!a || !b) return 0;
+  uint32_t d = mde_tree_depth(a) < mde_tree_depth(b) ? mde_tree_depth(a) : mde_tree_depth(b);
+  return 1ull << d;
+}
+
+int mde_digest_async(mde_ctx* c, const mde_records* r) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  int rc = check_records(c, r);
+  return rc ? rc : digest_async(c, r);
+}
+
+int mde_tree_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  int rc = check_records(c, r);
+  return rc ? rc : tree_async(c, r, o);
+}
+
+int mde_build_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  int rc = check_records(c, r);
+  if (rc) return rc;
+  if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
+  rc = digest_async(c, r);
+  return rc ? rc : tree_async(c, r, o);
+}
+
+int mde_build(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  int rc = check_records(c, r);
+  if (rc) return rc;
+  if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
+  const uint64_t P = r->n_partitions, S = P * r->n_buckets, NI = mde::tree_internal(r->n_buckets);
+  const uint64_t nvo = r->value_stride ? 0 : (r->n_records + 1);
+  const uint64_t sizes[9] = {r->values_bytes, nvo * 8, (S + 1) * 8, S * 8, S * 4, P * 4, P * 32,
+                             o->nodes ? P * NI * 32 : 0, 0};
+  for (int i = 0; i < 8; i++)
+    if ((rc = ensure_buf(c, c->stage[i], sizes[i]))) return rc;
+  auto dp = [&](int i) { return c->stage[i].p; };
+  if (r->values_bytes)
+    MDE_HIP(c, hipMemcpyAsync(dp(0), r->values, r->values_bytes, hipMemcpyHostToDevice, c->stream));
+  if (nvo)
+    MDE_HIP(c, hipMemcpyAsync(dp(1), r->value_off, nvo * 8, hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(dp(2), r->seg_rec, (S + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  mde_records dr = *r;
+  dr.values = static_cast<const uint8_t*>(dp(0));
+  dr.value_off = nvo ? static_cast<const uint64_t*>(dp(1)) : nullptr;
+  dr.seg_rec = static_cast<const uint64_t*>(dp(2));
+  mde_tree_out dout{static_cast<uint64_t*>(dp(3)), static_cast<int32_t*>(dp(4)),
+                    static_cast<int32_t*>(dp(5)), static_cast<uint8_t*>(dp(6)),
+                    o->nodes ? static_cast<uint8_t*>(dp(7)) : nullptr};
+  if ((rc = digest_async(c, &dr))) return rc;
+  if ((rc = tree_async(c, &dr, &dout))) return rc;
+  if (o->digest) MDE_HIP(c, hipMemcpyAsync(o->digest, dout.digest, S * 8, hipMemcpyDeviceToHost, c->stream));
+  if (o->size) MDE_HIP(c, hipMemcpyAsync(o->size, dout.size, S * 4, hipMemcpyDeviceToHost, c->stream));
+  if (o->items) MDE_HIP(c, hipMemcpyAsync(o->items, dout.items, P * 4, hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(o->root, dout.root, P * 32, hipMemcpyDeviceToHost, c->stream));
+  if (o->nodes) MDE_HIP(c, hipMemcpyAsync(o->nodes, dout.nodes, P * NI * 32, hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  return MDE_OK;
+}
+
+int mde_tree_from_digests_async(mde_ctx* c, uint32_t n_trees, uint32_t B, const uint64_t* digest,
+                                uint8_t* root, uint8_t* nodes) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  return tree_digests_async(c, n_trees, B, digest, root, nodes);
+}
+
+int mde_tree_from_digests(mde_ctx* c, uint32_t n_trees, uint32_t B, const uint64_t* digest,
+                          uint8_t* root, uint8_t* nodes) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (B == 0 || !digest || !root) return set_err(c, MDE_E_INVAL, "bad tree_from_digests arguments");
+  const uint64_t T = n_trees, NI = mde::tree_internal(B);
+  int rc;
+  if ((rc = ensure_buf(c, c->stage[8], T * B * 8))) return rc;
+  if ((rc = ensure_buf(c, c->stage[9], T * 32))) return rc;
+  if ((rc = ensure_buf(c, c->stage[10], nodes ? T * NI * 32 : 0))) return rc;
+  MDE_HIP(c, hipMemcpyAsync(c->stage[8].p, digest, T * B * 8, hipMemcpyHostToDevice, c->stream));
+  rc = tree_digests_async(c, n_trees, B, static_cast<const uint64_t*>(c->stage[8].p),
+                          static_cast<uint8_t*>(c->stage[9].p),
+                          nodes ? static_cast<uint8_t*>(c->stage[10].p) : nullptr);
+  if (rc) return rc;
+  MDE_HIP(c, hipMemcpyAsync(root, c->stage[9].p, T * 32, hipMemcpyDeviceToHost, c->stream));
+  if (nodes) MDE_HIP(c, hipMemcpyAsync(nodes, c->stage[10].p, T * NI * 32, hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  return MDE_OK;
+}
+
+int mde_decode_bucket_hashes(const uint8_t* const* hashes, const uint32_t* lens, uint32_t n,
+                             uint64_t* out) {
+  if ((!hashes || !lens || !out) && n) return MDE_E_INVAL;
+  for (uint32_t i = 0; i < n; i++) {
+    if (lens[i] != 8 || !hashes[i]) return MDE_E_DECODE;  // utils.DecodeBytesToInt64
+    uint64_t v = 0;
+    for (int k = 7; k >= 0; k--) v = (v << 8) | hashes[i][k];
+    out[i] = v;
+  }
+  return MDE_OK;
+}
+
+int mde_diff_async(mde_ctx* c, uint32_t n_pairs, uint32_t Ba, const uint64_t* da,
+                   const uint8_t* na, uint32_t Bb, const uint64_t* db, const uint8_t* nb,
+                   int32_t* out_ids, uint64_t out_stride, int32_t* out_count) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (!Ba || !Bb || !da || !db || !na || !nb || !out_ids || !out_count)
+    return set_err(c, MDE_E_INVAL, "bad diff arguments");
+  if (out_stride < mde_diff_capacity(Ba, Bb))
+    return set_err(c, MDE_E_CAPACITY, "out_stride %llu < mde_diff_capacity %llu",
+                   (unsigned long long)out_stride, (unsigned long long)mde_diff_capacity(Ba, Bb));
+  mde::DiffLaunch a{n_pairs, Ba, Bb, da, na, db, nb, out_ids, out_stride, out_count};
+  MDE_HIP(c, mde::launch_diff(a, c->stream));
+  return MDE_OK;
+}
+
+int mde_diff(mde_ctx* c, uint32_t n_pairs, uint32_t Ba, const uint64_t* da, const uint8_t* na,
+             uint32_t Bb, const uint64_t* db, const uint8_t* nb, int32_t* out_ids,
+             uint64_t out_stride, int32_t* out_count) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (!Ba || !Bb || !da || !db || !na || !nb || !out_ids || !out_count)
+    return set_err(c, MDE_E_INVAL, "bad diff arguments");
+  if (out_stride < mde_diff_capacity(Ba, Bb))
+    return set_err(c, MDE_E_CAPACITY, "out_stride too small");
+  const uint64_t T = n_pairs, NA = mde::tree_internal(Ba), NB = mde::tree_internal(Bb);
+  const uint64_t sz[6] = {T * Ba * 8, T * NA * 32, T * Bb * 8, T * NB * 32, T * out_stride * 4, T * 4};
+  int rc;
+  for (int i = 0; i < 6; i++)
+    if ((rc = ensure_buf(c, c->stage[i], sz[i]))) return rc;
+  MDE_HIP(c, hipMemcpyAsync(c->stage[0].p, da, sz[0], hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(c->stage[1].p, na, sz[1], hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(c->stage[2].p, db, sz[2], hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(c->stage[3].p, nb, sz[3], hipMemcpyHostToDevice, c->stream));
+  mde::DiffLaunch a{n_pairs,
+                    Ba,
+                    Bb,
+                    static_cast<const uint64_t*>(c->stage[0].p),
+                    static_cast<const uint8_t*>(c->stage[1].p),
+                    static_cast<const uint64_t*>(c->stage[2].p),
+                    static_cast<const uint8_t*>(c->stage[3].p),
+                    static_cast<int32_t*>(c->stage[4].p),
+                    out_stride,
+                    static_cast<int32_t*>(c->stage[5].p)};
+  MDE_HIP(c, mde::launch_diff(a, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(out_ids, c->stage[4].p, sz[4], hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(out_count, c->stage[5].p, sz[5], hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  return MDE_OK;
+}
+
+int mde_tag_keys_async(mde_ctx* c, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
+                       uint32_t B, uint32_t P, uint32_t* bucket, uint32_t* partition) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if ((bucket && !B) || (partition && !P) || (n && (!keys || !key_off)))
+    return set_err(c, MDE_E_INVAL, "bad tag_keys arguments");
+  MDE_HIP(c, mde::launch_tag_keys(keys, key_off, n, B, P, bucket, partition, c->stream));
+  return MDE_OK;
+}
+
+int mde_tag_keys(mde_ctx* c, const uint8_t* keys, const uint64_t* key_off, uint64_t n, uint32_t B,
+                 uint32_t P, uint32_t* bucket, uint32_t* partition) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if ((bucket && !B) || (partition && !P) || (n && (!keys || !key_off)))
+    return set_err(c, MDE_E_INVAL, "bad tag_keys arguments");
+  if (n == 0) return MDE_OK;
+  const uint64_t kb = key_off[n];
+  const uint64_t sz[4] = {kb, (n + 1) * 8, n * 4, n * 4};
+  int rc;
+  for (int i = 0; i < 4; i++)
+    if ((rc = ensure_buf(c, c->stage[i], sz[i]))) return rc;
+  if (kb) MDE_HIP(c, hipMemcpyAsync(c->stage[0].p, keys, kb, hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(c->stage[1].p, key_off, sz[1], hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, mde::launch_tag_keys(static_cast<const uint8_t*>(c->stage[0].p),
+                                  static_cast<const uint64_t*>(c->stage[1].p), n, B, P,
+                                  bucket ? static_cast<uint32_t*>(c->stage[2].p) : nullptr,
+                                  partition ? static_cast<uint32_t*>(c->stage[3].p) : nullptr,
+                                  c->stream));
+  if (bucket) MDE_HIP(c, hipMemcpyAsync(bucket, c->stage[2].p, sz[2], hipMemcpyDeviceToHost, c->stream));
+  if (partition) MDE_HIP(c, hipMemcpyAsync(partition, c->stage[3].p, sz[3], hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  return MDE_OK;
+}
+
+int mde_synth_tags_async(mde_ctx* c, const uint64_t* gids, uint64_t n, uint32_t P, uint32_t B,
+                         int mode, uint64_t kpp, uint32_t* part, uint32_t* bucket) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (!B || !P || mode < 0 || mode > 2 || (mode == 0 && !kpp) || (n && (!gids || !part || !bucket)))
+    return set_err(c, MDE_E_INVAL, "bad synth_tags arguments");
+  MDE_HIP(c, mde::launch_synth_tags(gids, n, P, B, mode, kpp, part, bucket, c->stream));
+  return MDE_OK;
+}
+
+int mde_synth_values_async(mde_ctx* c, uint8_t* dst, const uint64_t* gids, uint64_t n,
+                           uint32_t len, uint64_t seed) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (n && len && (!dst || !gids)) return set_err(c, MDE_E_INVAL, "bad synth_values arguments");
+  MDE_HIP(c, mde::launch_synth_values(dst, gids, n, len, seed, c->stream));
+  return MDE_OK;
+}
+
+int mde_dev_alloc(mde_ctx* c, uint64_t bytes, void** p) {
+  if (!c || !p) return MDE_E_INVAL;
+  Guard g(c);
+  if (hipMalloc(p, bytes ? bytes : 1) != hipSuccess) {
+    *p = nullptr;
+    return set_err(c, MDE_E_NOMEM, "hipMalloc(%llu) failed", (unsigned long long)bytes);
+  }
+  return MDE_OK;
+}
+
+int mde_dev_free(mde_ctx* c, void* p) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (p) {
+    MDE_HIP(c, hipStreamSynchronize(c->stream));
+    MDE_HIP(c, hipFree(p));
+  }
+  return MDE_OK;
+}
+
+int mde_memcpy_h2d(mde_ctx* c, void* dst, const void* src, uint64_t bytes) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (!bytes) return MDE_OK;
+  MDE_HIP(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  return MDE_OK;
+}
+
+int mde_memcpy_d2h(mde_ctx* c, void* dst, const void* src, uint64_t bytes) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (!bytes) return MDE_OK;
+  MDE_HIP(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  return MDE_OK;
+}
+
+}  // extern "C"

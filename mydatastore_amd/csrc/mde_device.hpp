@@ -1,0 +1,174 @@
+// mde_device.hpp -- device-side primitives shared by the gfx950 kernels.
+//
+// SHA-256 (FIPS 180-4) specialised for the three message shapes the Merkle path hashes:
+//   * level-1 nodes: SHA256(LE64(d_l) || LE64(d_r)) -- one 16-byte message, one block
+//     (leaf bytes: MerkleBucket.CalculateHash, main/merkle_tree.go:64-71 -> utils/utils.go:67-74);
+//   * upper nodes:   SHA256(h_l || h_r) -- 64-byte message, data block + constant padding block
+//     (cbergoon/merkletree v0.2.0 buildIntermediate);
+//   * keys:          SHA256(key) of any length (getKeyBucket, main/manager.go:773-778).
+// Integer/bit operations only (v_alignbit for rotates, v_perm for byte swaps) -- no MFMA.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mde {
+
+// CustomHash modulus, main/merkle_tree.go:19.
+constexpr uint64_t kHashMod = 999999ull;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__host__ __device__ constexpr uint32_t kSha256K(int i) {
+  constexpr uint32_t K[64] = {
+      0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4,
+      0xab1c5ed5, 0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe,
+      0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f,
+      0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7,
+      0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc,
+      0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b,
+      0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116,
+      0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+      0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
+      0xc67178f2};
+  return K[i];
+}
+
+__host__ __device__ constexpr uint32_t c_ror(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+// Message schedule of the constant padding block of a 64-byte message
+// (W0 = 0x80000000, W1..W14 = 0, W15 = 512 bits), pre-added to K: KW[i] = K[i] + W[i].
+struct PadSchedule {
+  uint32_t kw[64];
+  constexpr PadSchedule() : kw() {
+    uint32_t w[64] = {};
+    w[0] = 0x80000000u;
+    w[15] = 512u;
+    for (int i = 16; i < 64; i++) {
+      uint32_t s0 = c_ror(w[i - 15], 7) ^ c_ror(w[i - 15], 18) ^ (w[i - 15] >> 3);
+      uint32_t s1 = c_ror(w[i - 2], 17) ^ c_ror(w[i - 2], 19) ^ (w[i - 2] >> 10);
+      w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+    }
+    for (int i = 0; i < 64; i++) kw[i] = kSha256K(i) + w[i];
+  }
+};
+
+__device__ __forceinline__ uint32_t ror(uint32_t x, int n) {
+  return __builtin_amdgcn_alignbit(x, x, n);
+}
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ void sha256_init(uint32_t st[8]) {
+  st[0] = 0x6a09e667u; st[1] = 0xbb67ae85u; st[2] = 0x3c6ef372u; st[3] = 0xa54ff53au;
+  st[4] = 0x510e527fu; st[5] = 0x9b05688cu; st[6] = 0x1f83d9abu; st[7] = 0x5be0cd19u;
+}
+
+#define MDE_SHA_ROUND(a, b, c, d, e, f, g, h, kw)                                       \
+  do {                                                                                \
+    uint32_t t1_ = (h) + (ror((e), 6) ^ ror((e), 11) ^ ror((e), 25)) +                \
+                   (((e) & (f)) ^ (~(e) & (g))) + (kw);                               \
+    uint32_t t2_ = (ror((a), 2) ^ ror((a), 13) ^ ror((a), 22)) +                      \
+                   (((a) & (b)) ^ ((a) & (c)) ^ ((b) & (c)));                         \
+    (d) += t1_;                                                                       \
+    (h) = t1_ + t2_;                                                                  \
+  } while (0)
+
+// One compression of a 16-word big-endian message block (w is clobbered).
+__device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) {
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+  for (int i = 0; i < 64; i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int t = i + j;
+      uint32_t wt;
+      if (t < 16) {
+        wt = w[t];
+      } else {
+        uint32_t x15 = w[(t - 15) & 15], x2 = w[(t - 2) & 15];
+        uint32_t s0 = ror(x15, 7) ^ ror(x15, 18) ^ (x15 >> 3);
+        uint32_t s1 = ror(x2, 17) ^ ror(x2, 19) ^ (x2 >> 10);
+        wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+      }
+      const uint32_t kw = kSha256K(t) + wt;
+      switch (j) {
+        case 0: MDE_SHA_ROUND(a, b, c, d, e, f, g, h, kw); break;
+        case 1: MDE_SHA_ROUND(h, a, b, c, d, e, f, g, kw); break;
+        case 2: MDE_SHA_ROUND(g, h, a, b, c, d, e, f, kw); break;
+        case 3: MDE_SHA_ROUND(f, g, h, a, b, c, d, e, kw); break;
+        case 4: MDE_SHA_ROUND(e, f, g, h, a, b, c, d, kw); break;
+        case 5: MDE_SHA_ROUND(d, e, f, g, h, a, b, c, kw); break;
+        case 6: MDE_SHA_ROUND(c, d, e, f, g, h, a, b, kw); break;
+        case 7: MDE_SHA_ROUND(b, c, d, e, f, g, h, a, kw); break;
+      }
+    }
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// Compression of the constant padding block of a 64-byte message (schedule folded into KW).
+__device__ __forceinline__ void sha256_compress_pad64(uint32_t st[8]) {
+  constexpr PadSchedule P;
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+  for (int i = 0; i < 64; i += 8) {
+    MDE_SHA_ROUND(a, b, c, d, e, f, g, h, P.kw[i + 0]);
+    MDE_SHA_ROUND(h, a, b, c, d, e, f, g, P.kw[i + 1]);
+    MDE_SHA_ROUND(g, h, a, b, c, d, e, f, P.kw[i + 2]);
+    MDE_SHA_ROUND(f, g, h, a, b, c, d, e, P.kw[i + 3]);
+    MDE_SHA_ROUND(e, f, g, h, a, b, c, d, P.kw[i + 4]);
+    MDE_SHA_ROUND(d, e, f, g, h, a, b, c, P.kw[i + 5]);
+    MDE_SHA_ROUND(c, d, e, f, g, h, a, b, P.kw[i + 6]);
+    MDE_SHA_ROUND(b, c, d, e, f, g, h, a, P.kw[i + 7]);
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// Level-1 node: SHA256(LE64(dl) || LE64(dr)) -> state words (big-endian digest words).
+__device__ __forceinline__ void sha256_leaf_pair(uint64_t dl, uint64_t dr, uint32_t st[8]) {
+  uint32_t w[16];
+  w[0] = bswap((uint32_t)dl);
+  w[1] = bswap((uint32_t)(dl >> 32));
+  w[2] = bswap((uint32_t)dr);
+  w[3] = bswap((uint32_t)(dr >> 32));
+  w[4] = 0x80000000u;
+#pragma unroll
+  for (int i = 5; i < 15; i++) w[i] = 0;
+  w[15] = 128u;
+  sha256_init(st);
+  sha256_compress(st, w);
+}
+
+// Upper node: SHA256(hl || hr) where hl, hr are 8-word digests (state-word form).
+__device__ __forceinline__ void sha256_node_pair(const uint32_t hl[8], const uint32_t hr[8],
+                                                 uint32_t st[8]) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) { w[i] = hl[i]; w[8 + i] = hr[i]; }
+  sha256_init(st);
+  sha256_compress(st, w);
+  sha256_compress_pad64(st);
+}
+
+// ------------------------------------------------------------------ XXH64 (xxHash spec)
+constexpr uint64_t XP1 = 0x9E3779B185EBCA87ULL, XP2 = 0xC2B2AE3D27D4EB4FULL,
+                   XP3 = 0x165667B19E3779F9ULL, XP4 = 0x85EBCA77C2B2AE63ULL,
+                   XP5 = 0x27D4EB2F165667C5ULL;
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint64_t xx_round(uint64_t acc, uint64_t in) {
+  acc += in * XP2;
+  acc = rotl64(acc, 31);
+  return acc * XP1;
+}
+__device__ __forceinline__ uint64_t xx_merge(uint64_t acc, uint64_t v) {
+  acc ^= xx_round(0, v);
+  return acc * XP1 + XP4;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+}  // namespace mde

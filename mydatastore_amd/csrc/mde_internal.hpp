@@ -1,0 +1,72 @@
+// mde_internal.hpp -- host-side launch interfaces between the C ABI (mde_api.cpp) and the
+// gfx950 kernels (*.hip). Not installed; the public surface is include/mde.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mde {
+
+// Segment s = bucket (p, b), s = p*B + b; its bytes are [segpos(s), segpos(s+1)) of the arena,
+// segpos(s) = shift + (stride ? seg_rec[s]*stride : value_off[seg_rec[s]]).
+struct SegDesc {
+  const uint8_t* base;        // values rounded down to 16 B
+  uint64_t shift;             // values - base (0..15)
+  uint32_t stride;            // fixed value length, or 0
+  const uint64_t* value_off;  // variable-length offsets (stride == 0)
+  const uint64_t* seg_rec;    // [S+1]
+  uint32_t S;                 // P*B
+};
+
+struct DigestLaunch {
+  SegDesc seg;
+  unsigned long long* sums;   // [S] u64 accumulators (zero on entry)
+  uint64_t wave_bytes;        // contiguous bytes per wave (multiple of the 8 KiB block)
+  uint32_t n_waves;
+};
+hipError_t launch_bucket_digest(const DigestLaunch& a, hipStream_t st);
+// Waves and wave range for an arena of `bytes` on a device with `cus` CUs.
+void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, uint64_t* wave_bytes,
+                        uint32_t* n_waves);
+int bucket_digest_blocks_per_cu();
+
+struct TreeLaunch {
+  uint32_t P, B;
+  const unsigned long long* sums_in;  // [P*B] byte sums (digest = sum % 999999), or
+  const uint64_t* digest_in;          // [P*B] digests (tree-from-digests mode)
+  unsigned long long* sums_clear;     // zeroed after read (may be null)
+  const uint64_t* seg_rec;            // [P*B+1] for sizes (may be null)
+  uint64_t* digest_out;               // [P*B] (may be null)
+  int32_t* size_out;                  // [P*B]
+  int32_t* items_out;                 // [P]
+  uint8_t* root_out;                  // [P*32]
+  uint8_t* nodes_out;                 // [P*n_int*32]; required when B > kTreeLdsMaxBuckets
+  uint64_t n_int;
+};
+constexpr uint32_t kTreeLdsMaxBuckets = 4096;
+hipError_t launch_tree(const TreeLaunch& a, hipStream_t st);
+
+struct DiffLaunch {
+  uint32_t n_pairs;
+  uint32_t Ba, Bb;
+  const uint64_t* da;
+  const uint8_t* na;
+  const uint64_t* db;
+  const uint8_t* nb;
+  int32_t* out_ids;
+  uint64_t out_stride;
+  int32_t* out_count;
+};
+hipError_t launch_diff(const DiffLaunch& a, hipStream_t st);
+
+hipError_t launch_tag_keys(const uint8_t* keys, const uint64_t* key_off, uint64_t n, uint32_t B,
+                           uint32_t P, uint32_t* bucket, uint32_t* partition, hipStream_t st);
+hipError_t launch_synth_tags(const uint64_t* gids, uint64_t n, uint32_t P, uint32_t B, int mode,
+                             uint64_t kpp, uint32_t* part, uint32_t* bucket, hipStream_t st);
+hipError_t launch_synth_values(uint8_t* dst, const uint64_t* gids, uint64_t n, uint32_t len,
+                               uint64_t seed, hipStream_t st);
+
+// Tree geometry helpers (host).
+uint32_t tree_levels(uint32_t B, uint32_t* sizes /* cap 64, may be null */);
+uint64_t tree_internal(uint32_t B);
+
+}  // namespace mde

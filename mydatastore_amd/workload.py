@@ -1,0 +1,140 @@
+"""Device-resident synthetic KV workloads in layout A.
+
+Records are generated directly in HBM by the engine's own kernels: the key of record ``gid`` is
+``"k%016x" % gid``; its bucket is ``BE64(SHA256(key)[:8]) % B`` (main/manager.go:773-778); its
+partition is ``gid // keys_per_partition`` ("block"), ``gid % P`` ("mod", round-robin) or
+``FindPartitionID(key)`` ("hash"). Records are ordered by (partition, bucket) -- the order the
+reference's per-bucket LSM range scans yield -- and the value bytes are splitmix64 words.
+torch is used only to allocate HBM and to sort the tags (plumbing); hashing and value generation
+run in the engine's HIP kernels.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+import mydatastore_amd as mde
+
+SYNTH_SEED = 0x4D445354
+_MODES = {"block": 0, "mod": 1, "hash": 2}
+
+
+@dataclass
+class Workload:
+    engine: "mde.Engine"
+    values: "object"        # torch.uint8 [n * value_len] on device
+    seg_rec: "object"       # torch.int64 [P*B + 1] on device (u64 bit pattern)
+    n_partitions: int       # partitions held here (local)
+    n_buckets: int
+    n_records: int
+    value_len: int
+    partition_ids: np.ndarray  # global partition id of each local partition
+
+    def __post_init__(self):
+        import torch
+        P, B, dev = self.n_partitions, self.n_buckets, self.values.device
+        self.n_int = mde.tree_internal_nodes(B)
+        self.rec = mde.Records(self.values.data_ptr() if self.values.numel() else 0,
+                               self.values.numel(), self.value_len, 0, 0, self.n_records, P, B,
+                               self.seg_rec.data_ptr())
+
+        def outs():
+            o = {"digest": torch.zeros(P * B, dtype=torch.int64, device=dev),
+                 "size": torch.zeros(P * B, dtype=torch.int32, device=dev),
+                 "items": torch.zeros(P, dtype=torch.int32, device=dev),
+                 "root": torch.zeros(P * 32, dtype=torch.uint8, device=dev),
+                 "nodes": torch.zeros(P * self.n_int * 32, dtype=torch.uint8, device=dev)}
+            return o, mde.TreeOut(*(o[k].data_ptr() for k in ("digest", "size", "items", "root", "nodes")))
+
+        self.out, self.tree_out = outs()
+        self._outs = outs
+
+    @property
+    def value_bytes(self) -> int:
+        return self.n_records * self.value_len
+
+    def build_async(self, out=None):
+        """One Merkle build of every local partition, enqueued on the engine stream."""
+        self.engine.build_async(self.rec, out if out is not None else self.tree_out)
+
+    def digest_async(self):
+        self.engine.digest_async(self.rec)
+
+    def tree_async(self, out=None):
+        self.engine.tree_async(self.rec, out if out is not None else self.tree_out)
+
+    def build(self):
+        """Synchronous build into fresh output tensors (for tests)."""
+        o, to = self._outs()
+        self.engine.build_async(self.rec, to)
+        self.engine.synchronize()
+        return o
+
+    def diff(self, a, b):
+        """DifferentMerkleTreeBuckets for every local partition between two builds."""
+        import torch
+        P, B = self.n_partitions, self.n_buckets
+        cap = mde.diff_capacity(B, B)
+        ids = torch.zeros(P * cap, dtype=torch.int32, device=self.values.device)
+        cnt = torch.zeros(P, dtype=torch.int32, device=self.values.device)
+        self.engine.diff_async(P, B, a["digest"], a["nodes"], B, b["digest"], b["nodes"], ids, cap, cnt)
+        self.engine.synchronize()
+        ids, cnt = ids.cpu().numpy(), cnt.cpu().numpy()
+        return [int(c) if c < 0 else ids[p * cap:p * cap + c].tolist() for p, c in enumerate(cnt)]
+
+
+def shard_gids(n_keys: int, n_partitions: int, part_mode: str, keys_per_partition: int,
+               rank: int = 0, world: int = 1) -> np.ndarray:
+    """Global record ids whose partition lands on `rank` (partition p -> rank p % world)."""
+    g = np.arange(n_keys, dtype=np.uint64)
+    if world == 1:
+        return g
+    if part_mode == "block":
+        p = g // np.uint64(keys_per_partition)
+    elif part_mode == "mod":
+        p = g % np.uint64(n_partitions)
+    else:
+        raise ValueError("hash partitioning is sharded after tagging; use world == 1")
+    return g[(p % np.uint64(world)) == np.uint64(rank)]
+
+
+def local_partitions(n_partitions: int, rank: int, world: int) -> np.ndarray:
+    return np.arange(rank, n_partitions, world, dtype=np.int64)
+
+
+def make_workload(engine: "mde.Engine", n_partitions: int, n_buckets: int, value_len: int,
+                  part_mode: str = "block", keys_per_partition: int = 0, n_keys: int = 0,
+                  rank: int = 0, world: int = 1, seed: int = SYNTH_SEED,
+                  device: str = "cuda") -> Workload:
+    import torch
+    if not n_keys:
+        n_keys = n_partitions * keys_per_partition
+    if part_mode == "block" and not keys_per_partition:
+        keys_per_partition = -(-n_keys // n_partitions)
+    dev = torch.device(f"{device}:{engine.device}") if device == "cuda" else torch.device(device)
+    gids_np = shard_gids(n_keys, n_partitions, part_mode, keys_per_partition, rank, world)
+    n = int(gids_np.size)
+    pids = local_partitions(n_partitions, rank, world)
+    P = int(pids.size)
+    gids = torch.from_numpy(gids_np.view(np.int64)).to(dev)
+    part = torch.empty(n, dtype=torch.int32, device=dev)
+    bkt = torch.empty(n, dtype=torch.int32, device=dev)
+    engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    engine.synth_tags_async(gids, n, n_partitions, n_buckets, _MODES[part_mode],
+                            max(keys_per_partition, 1), part, bkt)
+    local = part.to(torch.int64) // world   # partition p lives on rank p % world at slot p // world
+    comp = local * n_buckets + bkt.to(torch.int64)
+    del part, bkt
+    comp_sorted, order = torch.sort(comp, stable=True)
+    counts = torch.bincount(comp_sorted, minlength=P * n_buckets)
+    del comp, comp_sorted
+    seg_rec = torch.zeros(P * n_buckets + 1, dtype=torch.int64, device=dev)
+    seg_rec[1:] = torch.cumsum(counts, 0)
+    sorted_gids = gids[order].contiguous()
+    del order, gids, counts
+    values = torch.empty(n * value_len, dtype=torch.uint8, device=dev)
+    engine.synth_values_async(values, sorted_gids, n, value_len, seed)
+    torch.cuda.synchronize(dev)
+    del sorted_gids
+    return Workload(engine, values, seg_rec, P, n_buckets, n, value_len, pids)

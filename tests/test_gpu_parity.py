@@ -1,0 +1,278 @@
+"""GPU parity: the HIP engine (through the C ABI) against the golden fixtures and the C oracle.
+
+Bit-exact for every output (digests, sizes, items, roots, every internal node, diff id lists).
+Full-size configs are checked through size-independent properties (mod-sum linearity per
+partition, single-byte perturbation -> single-bucket diff, determinism, tree-of-digests).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.datasets import mtr_arena, synth_arrays
+
+pytestmark = pytest.mark.gpu
+
+
+def _roots(out, P):
+    return [out["root"][32 * p:32 * p + 32].tobytes().hex() for p in range(P)]
+
+
+def _node_shas(out, P, B):
+    ni = O.n_internal_nodes(B) * 32
+    return [hashlib.sha256(out["nodes"][p * ni:(p + 1) * ni].tobytes()).hexdigest() for p in range(P)]
+
+
+def test_synth_cases_host_api(engine, golden, coracle):
+    for case in golden("synth_cases.json"):
+        values, voff, stride, seg = synth_arrays(case, coracle)
+        out = engine.build(values, seg, case["P"], case["B"], stride, voff)
+        assert out["digest"].tolist() == case["digest"], case["name"]
+        assert out["size"].tolist() == case["size"], case["name"]
+        assert out["items"].tolist() == case["items"], case["name"]
+        assert _roots(out, case["P"]) == case["root"], case["name"]
+        assert _node_shas(out, case["P"], case["B"]) == case["nodes_sha256"], case["name"]
+
+
+def test_synth_cases_device_api(engine, golden, coracle):
+    """Device-resident path (mde_build_async) on torch-allocated HBM buffers, with a misaligned
+    arena start (the kernel realigns to 16 B)."""
+    import torch
+    import mydatastore_amd as mde
+    dev = torch.device("cuda:0")
+    engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    for case in golden("synth_cases.json"):
+        values, voff, stride, seg = synth_arrays(case, coracle)
+        P, B = case["P"], case["B"]
+        for shift in (0, 5, 11):
+            buf = torch.zeros(values.size + 32, dtype=torch.uint8, device=dev)
+            buf[shift:shift + values.size] = torch.from_numpy(values).to(dev)
+            dv = buf[shift:shift + values.size]
+            dseg = torch.from_numpy(seg.view(np.int64)).to(dev)
+            dvo = torch.from_numpy(voff.view(np.int64)).to(dev) if voff is not None else None
+            rec = mde.Records(dv.data_ptr() if values.size else 0, values.size, stride, 0,
+                              dvo.data_ptr() if dvo is not None else 0, case["n"], P, B,
+                              dseg.data_ptr())
+            o = {"digest": torch.zeros(P * B, dtype=torch.int64, device=dev),
+                 "size": torch.zeros(P * B, dtype=torch.int32, device=dev),
+                 "items": torch.zeros(P, dtype=torch.int32, device=dev),
+                 "root": torch.zeros(P * 32, dtype=torch.uint8, device=dev),
+                 "nodes": torch.zeros(P * O.n_internal_nodes(B) * 32, dtype=torch.uint8, device=dev)}
+            to = mde.TreeOut(*(o[k].data_ptr() for k in ("digest", "size", "items", "root", "nodes")))
+            engine.build_async(rec, to)
+            engine.synchronize()
+            out = {k: v.cpu().numpy() for k, v in o.items()}
+            assert out["digest"].view(np.uint64).tolist() == case["digest"], (case["name"], shift)
+            assert out["size"].tolist() == case["size"]
+            assert out["items"].tolist() == case["items"]
+            assert _roots(out, P) == case["root"]
+            assert _node_shas(out, P, B) == case["nodes_sha256"]
+
+
+@pytest.mark.parametrize("name", ["testmerkletreeraw_n100.json", "testmerkletreeraw_n10.json"])
+def test_testmerkletreeraw(engine, golden, name):
+    """main/merkle_tree_test.go:15-185 on the device: tagging, three builds, wire round trip,
+    diffs -- every relation the reference asserts plus the absolute oracle bytes."""
+    fix = golden(name)
+    B = fix["n_buckets"]
+    keys = [k.encode() for k, _, _ in fix["writes"]]
+    bk, pt = engine.tag_keys(keys, B, 1)
+    assert bk.tolist() == [fix["bucket_of"][k.decode()] for k in keys]
+    assert pt.tolist() == [0] * len(keys)
+    outs = {}
+    for key, tr in fix["trees"].items():
+        lo, hi = map(int, key.split("_"))
+        vals, seg = mtr_arena(fix, lo, hi)
+        out = engine.build(vals, seg, 1, B, 8)
+        assert out["digest"].tolist() == tr["digests"]
+        assert out["size"].tolist() == tr["sizes"]
+        assert int(out["items"][0]) == tr["items"]
+        assert out["root"].tobytes().hex() == tr["root"]
+        assert out["nodes"].tobytes().hex() == tr["nodes"]
+        # EpochTreeObjectToMerkleTree(MerkleTreeToPartitionEpochObject(tree)) keeps the root
+        dec = np.array([int.from_bytes(bytes.fromhex(h), "little") for h in tr["object_buckets"]],
+                       np.uint64)
+        root, _ = engine.tree_from_digests(dec, len(dec))
+        assert root.tobytes().hex() == tr["root"]
+        outs[key] = out
+    t1, t2, t3 = outs["0_3"], outs["1_3"], outs["2_3"]
+    assert t1["root"].tobytes() == t2["root"].tobytes() != t3["root"].tobytes()
+
+    def d(a, b):
+        return engine.diff(B, a["digest"], a["nodes"], B, b["digest"], b["nodes"])[0]
+
+    assert d(t1, t2) == fix["diffs"]["t1_t2"] == []
+    assert d(t2, t1) == fix["diffs"]["t2_t1"] == []
+    assert d(t1, t3) == fix["diffs"]["t1_t3"] and len(d(t1, t3)) > 0
+    assert d(t3, t1) == fix["diffs"]["t3_t1"]
+
+
+def test_diff_cases(engine, golden):
+    import mydatastore_amd as mde
+    for c in golden("diff_cases.json"):
+        da, db = np.array(c["d1"], np.uint64), np.array(c["d2"], np.uint64)
+        ra, na = engine.tree_from_digests(da, c["b1"])
+        rb, nb = engine.tree_from_digests(db, c["b2"])
+        got = engine.diff(c["b1"], da, na, c["b2"], db, nb)[0]
+        if "error" in c:
+            assert got == mde.MDE_E_TREE, c["name"]
+        else:
+            assert got == c["ids"], c["name"]
+
+
+def test_diff_batched(engine, coracle):
+    """Many pairs per launch (the C5 compare step), random perturbations, B = 64 and 30."""
+    rng = np.random.default_rng(11)
+    for B in (64, 30, 1000):
+        P = 40
+        da = rng.integers(0, O.HASH_MOD, P * B).astype(np.uint64)
+        db = da.copy()
+        for p in range(P):
+            k = rng.integers(0, 4)
+            idx = rng.choice(B, size=k, replace=False)
+            db[p * B + idx] = (db[p * B + idx] + 1) % O.HASH_MOD
+        _, na = engine.tree_from_digests(da, B)
+        _, nb = engine.tree_from_digests(db, B)
+        got = engine.diff(B, da, na, B, db, nb, n_pairs=P)
+        for p in range(P):
+            assert got[p] == coracle.diff(da[p * B:(p + 1) * B], db[p * B:(p + 1) * B]), (B, p)
+
+
+def test_tree_from_digests_matches_oracle(engine, coracle):
+    rng = np.random.default_rng(3)
+    for B in (1, 2, 3, 5, 30, 64, 100, 1000, 4096, 4097, 10001):
+        T = 3
+        d = rng.integers(0, 2**63, T * B, dtype=np.int64).astype(np.uint64)  # any int64 on the wire
+        root, nodes = engine.tree_from_digests(d, B)
+        ni = O.n_internal_nodes(B) * 32
+        for t in range(T):
+            r, n = coracle.tree(d[t * B:(t + 1) * B], B)
+            assert root[32 * t:32 * t + 32].tobytes() == r, B
+            assert nodes[t * ni:(t + 1) * ni].tobytes() == n, B
+
+
+def test_tag_kernels(engine, golden, coracle):
+    import torch
+    k = golden("kat_hash.json")
+    keys = [bytes.fromhex(r[0]) for r in k["key_tags"]]
+    b64, p15 = engine.tag_keys(keys, 64, 15)
+    b1000, p1024 = engine.tag_keys(keys, 1000, 1024)
+    assert b64.tolist() == [r[1] for r in k["key_tags"]]
+    assert b1000.tolist() == [r[2] for r in k["key_tags"]]
+    assert p15.tolist() == [r[3] for r in k["key_tags"]]
+    assert p1024.tolist() == [r[4] for r in k["key_tags"]]
+    # variable-length keys exercising multi-block SHA and every XXH64 branch
+    keys = [bytes.fromhex(m) for m, _ in k["xxh64"]]
+    bk, pt = engine.tag_keys(keys, 1 << 31, 2**32 - 1)
+    for key, b, p in zip(keys, bk, pt):
+        assert b == O.get_key_bucket(key, 1 << 31)
+        assert p == O.xxh64(key) % (2**32 - 1)
+    # synthetic tag + value kernels == C oracle
+    dev = torch.device("cuda:0")
+    engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    gids = np.arange(5000, dtype=np.uint64) * np.uint64(7919) + np.uint64(3)
+    dg = torch.from_numpy(gids.view(np.int64)).to(dev)
+    for mode, P, kpp in ((0, 7, 800), (1, 1024, 0), (2, 15, 0)):
+        part = torch.zeros(5000, dtype=torch.int32, device=dev)
+        bkt = torch.zeros(5000, dtype=torch.int32, device=dev)
+        engine.synth_tags_async(dg, 5000, P, 64, mode, max(kpp, 1) if mode == 0 else 0, part, bkt)
+        engine.synchronize()
+        ep, eb = coracle.synth_tags(gids, P, 64, mode, max(kpp, 1))
+        assert part.cpu().numpy().view(np.uint32).tolist() == ep.tolist()
+        assert bkt.cpu().numpy().view(np.uint32).tolist() == eb.tolist()
+    for vl in (8, 13, 64, 1024):
+        dst = torch.zeros(5000 * vl, dtype=torch.uint8, device=dev)
+        engine.synth_values_async(dst, dg, 5000, vl, O.SYNTH_SEED)
+        engine.synchronize()
+        assert np.array_equal(dst.cpu().numpy(), coracle.synth_values(gids, vl, O.SYNTH_SEED))
+
+
+def test_edge_cases(engine, coracle):
+    rng = np.random.default_rng(5)
+    # zero records, all buckets empty
+    out = engine.build(np.zeros(0, np.uint8), np.zeros(3 * 8 + 1, np.uint64), 3, 8, 16)
+    exp = coracle.build(np.zeros(0, np.uint8), np.zeros(3 * 8 + 1, np.uint64), 3, 8, 16)
+    assert out["root"].tobytes() == exp["root"].tobytes() and out["digest"].sum() == 0
+    # one huge bucket spanning many wave ranges, tiny neighbours, odd stride
+    for stride, counts in ((7, [1, 200000, 0, 3]), (1, [5, 0, 0, 9, 1]), (1024, [3000, 1, 0, 2999])):
+        B = len(counts)
+        seg = np.zeros(B + 1, np.uint64)
+        np.cumsum(counts, out=seg[1:])
+        vals = rng.integers(0, 256, int(seg[-1]) * stride, dtype=np.uint8)
+        out = engine.build(vals, seg, 1, B, stride)
+        exp = coracle.build(vals, seg, 1, B, stride)
+        for k in ("digest", "size", "items", "root", "nodes"):
+            assert np.array_equal(out[k], exp[k]), (stride, k)
+    # values of 0xff everywhere: sums close to the u32 lane limits stay exact
+    vals = np.full(1 << 24, 255, np.uint8)
+    seg = np.array([0, 1 << 20, 1 << 24], np.uint64)
+    out = engine.build(vals, seg, 1, 2, 16)
+    assert out["digest"].tolist() == [((1 << 24) * 255) % O.HASH_MOD,
+                                      ((1 << 28) - (1 << 24)) * 255 % O.HASH_MOD]
+    # records before seg_rec[0] are not part of any bucket
+    vals = rng.integers(0, 256, 64 * 10, dtype=np.uint8)
+    seg = np.array([2, 5, 9], np.uint64)
+    out = engine.build(vals, seg, 1, 2, 64)
+    exp = coracle.build(vals, seg, 1, 2, 64)
+    assert out["digest"].tolist() == exp["digest"].tolist()
+
+
+def test_many_tiny_buckets(engine, coracle):
+    """Production-shaped tiny values (8-byte LE timestamps), B = 1000, sparse partitions."""
+    rng = np.random.default_rng(9)
+    P, B = 37, 1000
+    counts = rng.integers(0, 4, P * B) * (rng.random(P * B) < 0.4)
+    seg = np.zeros(P * B + 1, np.uint64)
+    np.cumsum(counts, out=seg[1:])
+    vals = rng.integers(0, 2**40, int(seg[-1]), dtype=np.int64).view(np.uint8)
+    out = engine.build(vals, seg, P, B, 8)
+    exp = coracle.build(vals, seg, P, B, 8)
+    for k in ("digest", "size", "items", "root", "nodes"):
+        assert np.array_equal(out[k], exp[k]), k
+
+
+def test_full_size_properties(engine):
+    """BASELINE config 2 shape (256 partitions x 100k keys x 256 B, B = 64) generated on device:
+    per-partition mod-sum linearity, sizes, roots == tree(digests), exact recomputation of
+    sampled buckets, single-byte perturbation -> exactly one differing bucket, determinism."""
+    import torch
+    from mydatastore_amd.workload import make_workload
+    w = make_workload(engine, n_partitions=256, keys_per_partition=100_000, value_len=256,
+                      n_buckets=64, part_mode="block")
+    P, B = 256, 64
+    out1 = w.build()
+    out2 = w.build()
+    for k in out1:
+        assert torch.equal(out1[k], out2[k]), k
+    digest = out1["digest"].cpu().numpy().view(np.uint64)
+    seg = w.seg_rec.cpu().numpy().view(np.uint64)
+    assert out1["size"].cpu().numpy().tolist() == np.diff(seg).astype(np.int32).tolist()
+    assert int(out1["items"].sum()) == P * 100_000
+    # per-partition sum of values (torch on device) mod m == sum of digests mod m
+    vals = w.values.view(torch.uint8)
+    V = 256
+    for p in list(range(0, P, 17)) + [P - 1]:
+        lo, hi = int(seg[p * B]) * V, int(seg[(p + 1) * B]) * V
+        tot = int(vals[lo:hi].to(torch.int64).sum().item())
+        assert tot % O.HASH_MOD == int(digest[p * B:(p + 1) * B].sum()) % O.HASH_MOD
+        # sampled exact buckets
+        b = (p * 7) % B
+        s0, s1 = int(seg[p * B + b]) * V, int(seg[p * B + b + 1]) * V
+        assert int(vals[s0:s1].to(torch.int64).sum().item()) % O.HASH_MOD == int(digest[p * B + b])
+    roots = out1["root"].cpu().numpy()
+    for p in range(0, P, 31):
+        lv = O.tree_levels_from_digests([int(x) for x in digest[p * B:(p + 1) * B]])
+        assert roots[32 * p:32 * p + 32].tobytes() == lv[-1][0]
+    # perturb one byte in bucket (p*37) % 64 of every 16th partition: diff == [that bucket]
+    touched = {}
+    for p in range(0, P, 16):
+        b = (p * 37) % B
+        r = int(seg[p * B + b])
+        if int(seg[p * B + b + 1]) > r:
+            vals[r * V] = (vals[r * V].to(torch.int32) + 1).remainder(256).to(torch.uint8)
+            touched[p] = b
+    out3 = w.build()
+    ids = w.diff(out1, out3)
+    for p in range(P):
+        assert ids[p] == ([touched[p]] if p in touched else []), p
