@@ -82,7 +82,11 @@ const char* mde_strerror(int code);
 int mde_create(int device, mde_ctx** out);
 void mde_destroy(mde_ctx* ctx);
 const char* mde_last_error(mde_ctx* ctx);
-int mde_set_stream(mde_ctx* ctx, void* hip_stream); /* NULL: the context's own stream */
+/* Launch stream for *_async calls and internal copies. A new context uses its own stream (a
+ * blocking stream: ordered after work on the null stream). NULL selects the null stream, which
+ * is torch's default stream. */
+int mde_set_stream(mde_ctx* ctx, void* hip_stream);
+int mde_use_own_stream(mde_ctx* ctx);
 void* mde_get_stream(mde_ctx* ctx);
 int mde_synchronize(mde_ctx* ctx);
 int mde_device_info(mde_ctx* ctx, int* cu_count, char* arch_name, int arch_cap);

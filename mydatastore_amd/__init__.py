@@ -28,7 +28,7 @@ HASH_MOD = 999999
 # Every symbol include/mde.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
     "mde_abi_version", "mde_strerror", "mde_create", "mde_destroy", "mde_last_error",
-    "mde_set_stream", "mde_get_stream", "mde_synchronize", "mde_device_info", "mde_tree_depth",
+    "mde_set_stream", "mde_use_own_stream", "mde_get_stream", "mde_synchronize", "mde_device_info", "mde_tree_depth",
     "mde_tree_internal_nodes", "mde_diff_capacity", "mde_build", "mde_build_async",
     "mde_digest_async", "mde_tree_async", "mde_tree_from_digests", "mde_tree_from_digests_async",
     "mde_decode_bucket_hashes", "mde_diff", "mde_diff_async", "mde_tag_keys_async", "mde_tag_keys",
@@ -68,6 +68,14 @@ def load_library() -> C.CDLL:
         return _lib
     if not LIB_PATH.exists():
         raise ImportError(f"{LIB_PATH} not built: run `python -m mydatastore_amd._build`")
+    # One HIP runtime per process. torch ships its own libamdhip64 (SONAME libamdhip64.so.7, the
+    # same SONAME as /opt/rocm's) but its libc10_hip asks for the unversioned file name, so if
+    # libmde.so loaded /opt/rocm's runtime first, torch would load a second one and fail to find
+    # the GPU. Loading torch first makes libmde.so bind to torch's runtime by SONAME.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # standalone use: libmde.so binds /opt/rocm's runtime
+        pass
     lib = C.CDLL(str(LIB_PATH))
     u32, u64, i32, vp = C.c_uint32, C.c_uint64, C.c_int32, C.c_void_p
     sig = {
@@ -77,6 +85,7 @@ def load_library() -> C.CDLL:
         "mde_destroy": (None, [vp]),
         "mde_last_error": (C.c_char_p, [vp]),
         "mde_set_stream": (C.c_int, [vp, vp]),
+        "mde_use_own_stream": (C.c_int, [vp]),
         "mde_get_stream": (vp, [vp]),
         "mde_synchronize": (C.c_int, [vp]),
         "mde_device_info": (C.c_int, [vp, C.POINTER(C.c_int), C.c_char_p, C.c_int]),
@@ -173,8 +182,12 @@ class Engine:
             raise MdeError(rc, (msg or b"").decode() or self.lib.mde_strerror(rc).decode())
 
     # -- context ------------------------------------------------------------------------------
-    def set_stream(self, stream_handle: int | None):
-        self._check(self.lib.mde_set_stream(self.ctx, stream_handle or None))
+    def set_stream(self, stream_handle: int):
+        """Launch on a HIP stream handle (0 = the null stream = torch's default stream)."""
+        self._check(self.lib.mde_set_stream(self.ctx, C.c_void_p(int(stream_handle))))
+
+    def use_own_stream(self):
+        self._check(self.lib.mde_use_own_stream(self.ctx))
 
     def synchronize(self):
         self._check(self.lib.mde_synchronize(self.ctx))

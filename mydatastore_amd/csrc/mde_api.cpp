@@ -119,6 +119,27 @@ int check_records(mde_ctx* c, const mde_records* r) {
   return MDE_OK;
 }
 
+// Full validation of host-resident inputs (mde_build): the device API trusts its inputs but the
+// kernels clamp every index, so bad device input gives wrong digests, never a fault.
+int check_host_records(mde_ctx* c, const mde_records* r) {
+  const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
+  for (uint64_t s = 0; s < S; s++)
+    if (r->seg_rec[s] > r->seg_rec[s + 1])
+      return set_err(c, MDE_E_INVAL, "seg_rec not nondecreasing at %llu", (unsigned long long)s);
+  if (r->seg_rec[S] > r->n_records)
+    return set_err(c, MDE_E_INVAL, "seg_rec[%llu] = %llu exceeds n_records %llu",
+                   (unsigned long long)S, (unsigned long long)r->seg_rec[S],
+                   (unsigned long long)r->n_records);
+  if (!r->value_stride && r->n_records) {
+    for (uint64_t i = 0; i < r->n_records; i++)
+      if (r->value_off[i] > r->value_off[i + 1])
+        return set_err(c, MDE_E_INVAL, "value_off not nondecreasing at %llu", (unsigned long long)i);
+    if (r->value_off[r->n_records] > r->values_bytes)
+      return set_err(c, MDE_E_INVAL, "value_off[n_records] exceeds values_bytes");
+  }
+  return MDE_OK;
+}
+
 int digest_async(mde_ctx* c, const mde_records* r) {
   const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
   int rc = ensure_sums(c, S);
@@ -132,6 +153,8 @@ int digest_async(mde_ctx* c, const mde_records* r) {
   a.seg.value_off = r->value_off;
   a.seg.seg_rec = r->seg_rec;
   a.seg.S = (uint32_t)S;
+  a.seg.n_records = r->n_records;
+  a.seg.end = a.seg.shift + r->values_bytes;
   a.sums = c->sums;
   if (!c->digest_blocks_per_cu) c->digest_blocks_per_cu = mde::bucket_digest_blocks_per_cu();
   mde::plan_bucket_digest(r->values_bytes + a.seg.shift, c->cus, c->digest_blocks_per_cu,
@@ -219,7 +242,7 @@ int mde_create(int device, mde_ctx** out) {
   c->cus = prop.multiProcessorCount;
   std::snprintf(c->arch, sizeof c->arch, "%s", prop.gcnArchName);
   if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->own_stream, hipStreamDefault) != hipSuccess) {
     delete c;
     return MDE_E_DEVICE;
   }
@@ -245,10 +268,17 @@ void mde_destroy(mde_ctx* c) {
 
 const char* mde_last_error(mde_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+int mde_use_own_stream(mde_ctx* c) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  c->stream = c->own_stream;
+  return MDE_OK;
+}
+
 int mde_set_stream(mde_ctx* c, void* s) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
-  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  c->stream = static_cast<hipStream_t>(s);  // NULL = the null stream (torch's default stream)
   return MDE_OK;
 }
 
@@ -305,6 +335,7 @@ int mde_build(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   Guard g(c);
   int rc = check_records(c, r);
   if (rc) return rc;
+  if ((rc = check_host_records(c, r))) return rc;
   if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
   const uint64_t P = r->n_partitions, S = P * r->n_buckets, NI = mde::tree_internal(r->n_buckets);
   const uint64_t nvo = r->value_stride ? 0 : (r->n_records + 1);

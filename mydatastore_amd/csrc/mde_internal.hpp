@@ -15,6 +15,8 @@ struct SegDesc {
   const uint64_t* value_off;  // variable-length offsets (stride == 0)
   const uint64_t* seg_rec;    // [S+1]
   uint32_t S;                 // P*B
+  uint64_t n_records;         // record indices are clamped to this ...
+  uint64_t end;               // ... and positions to shift + values_bytes: bad input never faults
 };
 
 struct DigestLaunch {

@@ -206,10 +206,17 @@ def test_edge_cases(engine, coracle):
             assert np.array_equal(out[k], exp[k]), (stride, k)
     # values of 0xff everywhere: sums close to the u32 lane limits stay exact
     vals = np.full(1 << 24, 255, np.uint8)
-    seg = np.array([0, 1 << 20, 1 << 24], np.uint64)
+    seg = np.array([0, 1 << 16, 1 << 20], np.uint64)  # record indices (16-byte records)
     out = engine.build(vals, seg, 1, 2, 16)
-    assert out["digest"].tolist() == [((1 << 24) * 255) % O.HASH_MOD,
-                                      ((1 << 28) - (1 << 24)) * 255 % O.HASH_MOD]
+    assert out["digest"].tolist() == [((1 << 20) * 255) % O.HASH_MOD,
+                                      ((1 << 24) - (1 << 20)) * 255 % O.HASH_MOD]
+    # malformed input is rejected on the host API (never reaches a kernel)
+    import mydatastore_amd as mde
+    with pytest.raises(mde.MdeError) as e:
+        engine.build(vals, np.array([0, 1 << 16, 1 << 24], np.uint64), 1, 2, 16)
+    assert e.value.code == mde.MDE_E_INVAL
+    with pytest.raises(mde.MdeError):
+        engine.build(vals, np.array([0, 1 << 17, 1 << 16], np.uint64), 1, 2, 16)
     # records before seg_rec[0] are not part of any bucket
     vals = rng.integers(0, 256, 64 * 10, dtype=np.uint8)
     seg = np.array([2, 5, 9], np.uint64)
