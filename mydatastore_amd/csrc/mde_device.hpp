@@ -62,63 +62,85 @@ __device__ __forceinline__ void sha256_init(uint32_t st[8]) {
   st[4] = 0x510e527fu; st[5] = 0x9b05688cu; st[6] = 0x1f83d9abu; st[7] = 0x5be0cd19u;
 }
 
+// gfx950 v_bitop3_b32: any 3-input boolean function in one instruction. Truth-table immediates
+// for inputs (a, b, c) = (0xF0, 0xCC, 0xAA): xor3 = 0x96, ch = a ? b : c = 0xCA, maj = 0xE8.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
+  return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+
 #define MDE_SHA_ROUND(a, b, c, d, e, f, g, h, kw)                                       \
   do {                                                                                \
-    uint32_t t1_ = (h) + (ror((e), 6) ^ ror((e), 11) ^ ror((e), 25)) +                \
-                   (((e) & (f)) ^ (~(e) & (g))) + (kw);                               \
-    uint32_t t2_ = (ror((a), 2) ^ ror((a), 13) ^ ror((a), 22)) +                      \
-                   (((a) & (b)) ^ ((a) & (c)) ^ ((b) & (c)));                         \
+    uint32_t t1_ = (h) + (kw) + ch((e), (f), (g)) + xor3(ror((e), 6), ror((e), 11), ror((e), 25)); \
+    uint32_t t2_ = xor3(ror((a), 2), ror((a), 13), ror((a), 22)) + maj((a), (b), (c));  \
     (d) += t1_;                                                                       \
     (h) = t1_ + t2_;                                                                  \
   } while (0)
 
-// One compression of a 16-word big-endian message block (w is clobbered).
+// Round constants in constant memory; the round loops index them with a wave-uniform counter,
+// so they are read with scalar loads (one s_load_dwordx16 per 16 rounds).
+__device__ static constexpr uint32_t kK[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+__device__ static constexpr PadSchedule kPad{};
+
+#define MDE_SHA_8ROUNDS(KW)                                \
+  MDE_SHA_ROUND(a, b, c, d, e, f, g, h, KW(0));            \
+  MDE_SHA_ROUND(h, a, b, c, d, e, f, g, KW(1));            \
+  MDE_SHA_ROUND(g, h, a, b, c, d, e, f, KW(2));            \
+  MDE_SHA_ROUND(f, g, h, a, b, c, d, e, KW(3));            \
+  MDE_SHA_ROUND(e, f, g, h, a, b, c, d, KW(4));            \
+  MDE_SHA_ROUND(d, e, f, g, h, a, b, c, KW(5));            \
+  MDE_SHA_ROUND(c, d, e, f, g, h, a, b, KW(6));            \
+  MDE_SHA_ROUND(b, c, d, e, f, g, h, a, KW(7))
+
+__device__ __forceinline__ void sha_sched16(uint32_t w[16]) {
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const uint32_t x15 = w[(j + 1) & 15], x2 = w[(j + 14) & 15];
+    w[j] += xor3(ror(x15, 7), ror(x15, 18), x15 >> 3) + w[(j + 9) & 15] +
+            xor3(ror(x2, 17), ror(x2, 19), x2 >> 10);
+  }
+}
+
+// One compression of a 16-word big-endian message block (w is clobbered). Compact form: a loop of
+// four 16-round bodies (the schedule for rounds 16..63 is computed 16 words at a time), which keeps
+// the code ~6x smaller than a full unroll -- several trees in flight on one CU no longer thrash the
+// instruction cache.
 __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) {
   uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll
-  for (int i = 0; i < 64; i += 8) {
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const int t = i + j;
-      uint32_t wt;
-      if (t < 16) {
-        wt = w[t];
-      } else {
-        uint32_t x15 = w[(t - 15) & 15], x2 = w[(t - 2) & 15];
-        uint32_t s0 = ror(x15, 7) ^ ror(x15, 18) ^ (x15 >> 3);
-        uint32_t s1 = ror(x2, 17) ^ ror(x2, 19) ^ (x2 >> 10);
-        wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
-      }
-      const uint32_t kw = kSha256K(t) + wt;
-      switch (j) {
-        case 0: MDE_SHA_ROUND(a, b, c, d, e, f, g, h, kw); break;
-        case 1: MDE_SHA_ROUND(h, a, b, c, d, e, f, g, kw); break;
-        case 2: MDE_SHA_ROUND(g, h, a, b, c, d, e, f, kw); break;
-        case 3: MDE_SHA_ROUND(f, g, h, a, b, c, d, e, kw); break;
-        case 4: MDE_SHA_ROUND(e, f, g, h, a, b, c, d, kw); break;
-        case 5: MDE_SHA_ROUND(d, e, f, g, h, a, b, c, kw); break;
-        case 6: MDE_SHA_ROUND(c, d, e, f, g, h, a, b, kw); break;
-        case 7: MDE_SHA_ROUND(b, c, d, e, f, g, h, a, kw); break;
-      }
-    }
+#pragma unroll 1
+  for (int i = 0; i < 64; i += 16) {
+    if (i) sha_sched16(w);
+#define MDE_KW_LO(j) (kK[i + (j)] + w[(j)])
+#define MDE_KW_HI(j) (kK[i + 8 + (j)] + w[8 + (j)])
+    MDE_SHA_8ROUNDS(MDE_KW_LO);
+    MDE_SHA_8ROUNDS(MDE_KW_HI);
+#undef MDE_KW_LO
+#undef MDE_KW_HI
   }
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
 // Compression of the constant padding block of a 64-byte message (schedule folded into KW).
 __device__ __forceinline__ void sha256_compress_pad64(uint32_t st[8]) {
-  constexpr PadSchedule P;
   uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll
+#pragma unroll 1
   for (int i = 0; i < 64; i += 8) {
-    MDE_SHA_ROUND(a, b, c, d, e, f, g, h, P.kw[i + 0]);
-    MDE_SHA_ROUND(h, a, b, c, d, e, f, g, P.kw[i + 1]);
-    MDE_SHA_ROUND(g, h, a, b, c, d, e, f, P.kw[i + 2]);
-    MDE_SHA_ROUND(f, g, h, a, b, c, d, e, P.kw[i + 3]);
-    MDE_SHA_ROUND(e, f, g, h, a, b, c, d, P.kw[i + 4]);
-    MDE_SHA_ROUND(d, e, f, g, h, a, b, c, P.kw[i + 5]);
-    MDE_SHA_ROUND(c, d, e, f, g, h, a, b, P.kw[i + 6]);
-    MDE_SHA_ROUND(b, c, d, e, f, g, h, a, P.kw[i + 7]);
+#define MDE_KW_PAD(j) (kPad.kw[i + (j)])
+    MDE_SHA_8ROUNDS(MDE_KW_PAD);
+#undef MDE_KW_PAD
   }
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }

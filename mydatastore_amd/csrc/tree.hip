@@ -14,6 +14,7 @@
 #include "mde_device.hpp"
 #include "mde_internal.hpp"
 
+
 namespace mde {
 namespace {
 
@@ -48,31 +49,41 @@ __device__ __forceinline__ uint64_t leaf(const TreeLaunch& a, uint64_t s, uint32
   return v;
 }
 
+// A "group" of G threads builds one partition's tree (see launch_tree for the choice of G). Every
+// group of a workgroup has the same B, hence the same level count, so the per-level
+// __syncthreads() is uniform.
 template <bool kLds>
-__global__ __launch_bounds__(256) void tree_kernel(TreeLaunch a) {
+__global__ __launch_bounds__(256) void tree_kernel(TreeLaunch a, uint32_t G, uint32_t lds_words) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const uint32_t p = blockIdx.x;
+  const uint32_t groups = blockDim.x / G;
+  const uint32_t gi = threadIdx.x / G, tid = threadIdx.x % G;
+  const uint32_t p = blockIdx.x * groups + gi;
+  const bool live = p < a.P;
   const uint32_t B = a.B;
   const uint32_t n1 = (B + 1) / 2;  // level-1 nodes (leaf count incl. dup / 2)
   const uint64_t s0 = (uint64_t)p * B;
-  uint32_t* node_base = a.nodes_out ? reinterpret_cast<uint32_t*>(a.nodes_out + (uint64_t)p * a.n_int * 32)
-                                    : nullptr;
-  uint32_t* counter = lds;  // lds[0]: items accumulator
-  uint32_t* buf0 = kLds ? lds + 4 : node_base;
-  uint32_t* buf1 = kLds ? lds + 4 + (uint64_t)n1 * 8 : nullptr;
-  if (threadIdx.x == 0) counter[0] = 0;
+  uint32_t* node_base = (a.nodes_out && live)
+                            ? reinterpret_cast<uint32_t*>(a.nodes_out + (uint64_t)p * a.n_int * 32)
+                            : nullptr;
+  uint32_t* region = lds + (uint64_t)gi * lds_words;
+  uint32_t* counter = region;  // region[0]: items accumulator
+  uint32_t* buf0 = kLds ? region + 4 : node_base;
+  uint32_t* buf1 = kLds ? region + 4 + (uint64_t)n1 * 8 : nullptr;
+  if (tid == 0) counter[0] = 0;
   __syncthreads();
 
   // Leaves + level 1.
   uint32_t items = 0;
-  for (uint32_t j = threadIdx.x; j < n1; j += blockDim.x) {
-    const uint32_t bl = 2 * j, br = (2 * j + 1 < B) ? 2 * j + 1 : 2 * j;
-    const uint64_t dl = leaf(a, s0 + bl, items);
-    const uint64_t dr = (br != bl) ? leaf(a, s0 + br, items) : dl;
-    uint32_t st[8];
-    sha256_leaf_pair(dl, dr, st);
-    store_node(buf0 + (uint64_t)j * 8, st);
-    if (kLds && node_base) store_node(node_base + (uint64_t)j * 8, st);
+  if (live) {
+    for (uint32_t j = tid; j < n1; j += G) {
+      const uint32_t bl = 2 * j, br = (2 * j + 1 < B) ? 2 * j + 1 : 2 * j;
+      const uint64_t dl = leaf(a, s0 + bl, items);
+      const uint64_t dr = (br != bl) ? leaf(a, s0 + br, items) : dl;
+      uint32_t st[8];
+      sha256_leaf_pair(dl, dr, st);
+      store_node(buf0 + (uint64_t)j * 8, st);
+      if (kLds && node_base) store_node(node_base + (uint64_t)j * 8, st);
+    }
   }
   if (items) atomicAdd(counter, items);
 
@@ -80,34 +91,35 @@ __global__ __launch_bounds__(256) void tree_kernel(TreeLaunch a) {
   uint32_t n = n1;
   uint64_t level_off = 0;  // node index of the current level's first node in node_base
   uint32_t* cur = buf0;
-  uint32_t* nxt = kLds ? buf1 : node_base + (uint64_t)n1 * 8;
+  uint32_t* nxt = kLds ? buf1 : (node_base ? node_base + (uint64_t)n1 * 8 : nullptr);
   while (n > 1) {
     __syncthreads();
     const uint32_t m = (n + 1) / 2;
-    for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
-      const uint32_t l = 2 * j, r = (2 * j + 1 < n) ? 2 * j + 1 : 2 * j;
-      uint32_t hl[8], hr[8], st[8];
-      load_node(cur + (uint64_t)l * 8, hl);
-      load_node(cur + (uint64_t)r * 8, hr);
-      sha256_node_pair(hl, hr, st);
-      store_node(nxt + (uint64_t)j * 8, st);
-      if (kLds && node_base) store_node(node_base + (level_off + n + j) * 8, st);
+    if (live) {
+      for (uint32_t j = tid; j < m; j += G) {
+        const uint32_t l = 2 * j, r = (2 * j + 1 < n) ? 2 * j + 1 : 2 * j;
+        uint32_t hl[8], hr[8], st[8];
+        load_node(cur + (uint64_t)l * 8, hl);
+        load_node(cur + (uint64_t)r * 8, hr);
+        sha256_node_pair(hl, hr, st);
+        store_node(nxt + (uint64_t)j * 8, st);
+        if (kLds && node_base) store_node(node_base + (level_off + n + j) * 8, st);
+      }
     }
     level_off += n;
     n = m;
     if (kLds) {
       uint32_t* t = cur; cur = nxt; nxt = t;
-    } else {
+    } else if (node_base) {
       cur = nxt;
       nxt = node_base + (level_off + n) * 8;
     }
   }
   __syncthreads();
-  if (threadIdx.x < 8) {
-    const uint32_t w = cur[threadIdx.x];
-    reinterpret_cast<uint32_t*>(a.root_out + (uint64_t)p * 32)[threadIdx.x] = w;
+  if (live) {
+    if (tid < 8) reinterpret_cast<uint32_t*>(a.root_out + (uint64_t)p * 32)[tid] = cur[tid];
+    if (tid == 0 && a.items_out) a.items_out[p] = (int32_t)counter[0];
   }
-  if (threadIdx.x == 0 && a.items_out) a.items_out[p] = (int32_t)counter[0];
 }
 
 }  // namespace
@@ -133,15 +145,28 @@ uint64_t tree_internal(uint32_t B) {
 
 hipError_t launch_tree(const TreeLaunch& a, hipStream_t st) {
   if (a.P == 0) return hipSuccess;
+  // Tree building is latency-bound (11 dependent SHA-256 compressions at B = 64) and several tree
+  // waves on one CU slow each other down, so use as few waves as possible: a group of G lanes per
+  // partition, G = the level-1 width rounded up to a power of two, 64/G partitions per wave, one
+  // wave per workgroup (so workgroups spread over CUs). Wide trees (level 1 > 64) get a whole
+  // 256-thread workgroup each.
   const uint32_t n1 = (a.B + 1) / 2;
-  uint32_t threads = ((n1 + 63) / 64) * 64;
-  if (threads > 256) threads = 256;
+  uint32_t G = 8, threads = 64;
+  if (n1 > 64) {
+    G = threads = 256;
+  } else {
+    while (G < n1) G <<= 1;
+  }
+  const uint32_t groups = threads / G;
+  const uint32_t blocks = (a.P + groups - 1) / groups;
   if (a.B <= kTreeLdsMaxBuckets) {
-    const size_t lds = 16 + ((size_t)n1 + (n1 + 1) / 2) * 32;
-    hipLaunchKernelGGL(tree_kernel<true>, dim3(a.P), dim3(threads), lds, st, a);
+    // per group: 16-byte counter slot + level 1 + level 2 (ping-pong), 16-byte aligned
+    const uint32_t words = 4 + (n1 + (n1 + 1) / 2) * 8;
+    hipLaunchKernelGGL(tree_kernel<true>, dim3(blocks), dim3(threads), (size_t)words * 4 * groups,
+                       st, a, G, words);
   } else {
     if (!a.nodes_out) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(tree_kernel<false>, dim3(a.P), dim3(threads), 16, st, a);
+    hipLaunchKernelGGL(tree_kernel<false>, dim3(blocks), dim3(threads), 16 * groups, st, a, G, 4u);
   }
   return hipGetLastError();
 }

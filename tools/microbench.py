@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Kernel micro-benchmarks (HIP events on the launch stream).
+
+    python tools/microbench.py tree            # tree kernel vs partitions / buckets
+    python tools/microbench.py digest          # digest kernel vs arena size (C4 shards)
+"""
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def timeit(fn, reps=20, warm=3):
+    import torch
+    for _ in range(warm):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3  # us
+
+
+def bench_tree(eng):
+    import torch
+    import mydatastore_amd as mde
+    res = []
+    for B in (64, 1000):
+        for P in (1, 8, 128, 256, 1024, 4096):
+            d = torch.randint(0, 999999, (P * B,), dtype=torch.int64, device="cuda")
+            root = torch.zeros(P * 32, dtype=torch.uint8, device="cuda")
+            nodes = torch.zeros(P * mde.tree_internal_nodes(B) * 32, dtype=torch.uint8, device="cuda")
+            us = timeit(lambda: eng.tree_from_digests_async(P, B, d, root, nodes))
+            res.append({"kernel": "tree", "B": B, "P": P, "us": round(us, 2)})
+            print(json.dumps(res[-1]), flush=True)
+    return res
+
+
+def bench_digest(eng):
+    from mydatastore_amd.workload import make_workload
+    res = []
+    for world in (8, 4, 2, 1):
+        w = make_workload(eng, n_partitions=1024, n_buckets=64, value_len=1024, part_mode="mod",
+                          n_keys=10_000_000, rank=0, world=world)
+        us = timeit(w.digest_async)
+        ust = timeit(w.tree_async)
+        usb = timeit(w.build_async)
+        res.append({"kernel": "digest", "world": world, "bytes": w.value_bytes, "digest_us": round(us, 2),
+                    "GBps": round(w.value_bytes / us / 1e3, 1), "tree_us": round(ust, 2),
+                    "build_us": round(usb, 2)})
+        print(json.dumps(res[-1]), flush=True)
+        del w
+    return res
+
+
+def main():
+    import torch
+    import mydatastore_amd as mde
+    eng = mde.Engine(0)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    what = sys.argv[1:] or ["tree", "digest"]
+    out = {}
+    if "tree" in what:
+        out["tree"] = bench_tree(eng)
+    if "digest" in what:
+        out["digest"] = bench_digest(eng)
+    Path("gpurun_out").mkdir(exist_ok=True)
+    Path("gpurun_out/microbench.json").write_text(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
