@@ -1,0 +1,71 @@
+"""Partition sharding across GPUs and the per-build root gather.
+
+Partitions are independent (main/merkle_tree.go:86-116 reads only one partition's records), so
+partition p lives on rank p % world and each rank builds its partitions with no data exchange.
+The single exchange step is the gather of the per-partition roots: every rank contributes one
+fixed-size slab of ceil(P / world) x 32 bytes and `all_gather_into_tensor` (RCCL over xGMI with
+the "nccl" backend; gloo on CPU for tests) delivers all roots to every rank. That is the in-node
+analogue of the reference's gRPC fan-out of epoch trees (main/manager.go:729-771).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def partition_rank(p: int, world: int) -> int:
+    return p % world
+
+
+def local_partitions(n_partitions: int, rank: int, world: int) -> np.ndarray:
+    """Global ids of the partitions rank `rank` holds, in local slot order (slot i = p // world)."""
+    return np.arange(rank, n_partitions, world, dtype=np.int64)
+
+
+def shard_gids(n_keys: int, n_partitions: int, part_mode: str, keys_per_partition: int,
+               rank: int = 0, world: int = 1) -> np.ndarray:
+    """Global record ids whose partition lands on `rank`."""
+    g = np.arange(n_keys, dtype=np.uint64)
+    if world == 1:
+        return g
+    if part_mode == "block":
+        p = g // np.uint64(keys_per_partition)
+    elif part_mode == "mod":
+        p = g % np.uint64(n_partitions)
+    else:
+        raise ValueError("hash partitioning is sharded after tagging; use world == 1")
+    return g[(p % np.uint64(world)) == np.uint64(rank)]
+
+
+class RootGather:
+    """Fixed-size slab all-gather of per-partition 32-byte roots, double-buffered so a caller can
+    keep the gather of build i in flight while build i+1 computes."""
+
+    def __init__(self, n_partitions: int, world: int, device, nbuf: int = 2):
+        import torch
+        self.P, self.world = n_partitions, world
+        self.slab = -(-n_partitions // world)
+        self.send = [torch.zeros(self.slab * 32, dtype=torch.uint8, device=device) for _ in range(nbuf)]
+        self.recv = [torch.zeros(world * self.slab * 32, dtype=torch.uint8, device=device)
+                     for _ in range(nbuf)]
+
+    def gather(self, roots, buf: int = 0):
+        """roots: this rank's [n_local * 32] uint8 tensor. Enqueued on the current stream."""
+        import torch.distributed as dist
+        n = roots.numel()
+        self.send[buf][:n].copy_(roots, non_blocking=True)
+        if dist.get_backend() == "gloo":
+            parts = list(self.recv[buf].view(self.world, -1).unbind(0))
+            dist.all_gather(parts, self.send[buf])
+        else:
+            dist.all_gather_into_tensor(self.recv[buf], self.send[buf])
+        return self.recv[buf]
+
+    def assemble(self, buf: int = 0) -> np.ndarray:
+        """All roots in global partition order: [P, 32] uint8 (slot i of rank r = partition
+        r + i * world)."""
+        g = self.recv[buf].view(self.world, self.slab, 32).cpu().numpy()
+        out = np.zeros((self.P, 32), np.uint8)
+        for r in range(self.world):
+            pids = local_partitions(self.P, r, self.world)
+            out[pids] = g[r, :len(pids)]
+        return out

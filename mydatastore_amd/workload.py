@@ -15,6 +15,7 @@ from dataclasses import dataclass
 import numpy as np
 
 import mydatastore_amd as mde
+from mydatastore_amd.dist import local_partitions, shard_gids
 
 SYNTH_SEED = 0x4D445354
 _MODES = {"block": 0, "mod": 1, "hash": 2}
@@ -82,25 +83,6 @@ class Workload:
         self.engine.synchronize()
         ids, cnt = ids.cpu().numpy(), cnt.cpu().numpy()
         return [int(c) if c < 0 else ids[p * cap:p * cap + c].tolist() for p, c in enumerate(cnt)]
-
-
-def shard_gids(n_keys: int, n_partitions: int, part_mode: str, keys_per_partition: int,
-               rank: int = 0, world: int = 1) -> np.ndarray:
-    """Global record ids whose partition lands on `rank` (partition p -> rank p % world)."""
-    g = np.arange(n_keys, dtype=np.uint64)
-    if world == 1:
-        return g
-    if part_mode == "block":
-        p = g // np.uint64(keys_per_partition)
-    elif part_mode == "mod":
-        p = g % np.uint64(n_partitions)
-    else:
-        raise ValueError("hash partitioning is sharded after tagging; use world == 1")
-    return g[(p % np.uint64(world)) == np.uint64(rank)]
-
-
-def local_partitions(n_partitions: int, rank: int, world: int) -> np.ndarray:
-    return np.arange(rank, n_partitions, world, dtype=np.int64)
 
 
 def make_workload(engine: "mde.Engine", n_partitions: int, n_buckets: int, value_len: int,

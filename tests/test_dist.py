@@ -1,0 +1,81 @@
+"""CPU, gloo world_size 2 (and 3): partition sharding p % world and the root gather used by
+bench.py reassemble exactly the single-process roots. The C oracle stands in for the per-rank
+build (no GPU here); the device path of the same code is exercised by bench.py at N > 1."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from tests.conftest import ROOT
+
+P, B, N_KEYS, V = 12, 16, 3000, 40
+
+
+def _oracle_roots(co, gids, n_parts_global, rank, world, mode):
+    from mydatastore_amd.dist import local_partitions
+    kpp = -(-N_KEYS // n_parts_global)
+    part, bk = co.synth_tags(gids, n_parts_global, B, {"block": 0, "mod": 1}[mode], kpp)
+    local = (part // world).astype(np.uint32)
+    pl = len(local_partitions(n_parts_global, rank, world))
+    order, seg = co.layout_a(local, bk, pl, B)
+    vals = co.synth_values(gids[order], V, 0x4D445354)
+    out = co.build(vals, seg, pl, B, V)
+    return out["root"]
+
+
+def _worker(rank, world, port, mode, q):
+    import torch
+    import torch.distributed as dist
+    import sys
+    sys.path.insert(0, str(ROOT))
+    from mydatastore_amd.dist import RootGather, shard_gids
+    from tests.oracle_c import COracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        co = COracle()
+        kpp = -(-N_KEYS // P)
+        gids = shard_gids(N_KEYS, P, mode, kpp, rank, world)
+        roots = _oracle_roots(co, gids, P, rank, world, mode)
+        g = RootGather(P, world, torch.device("cpu"))
+        g.gather(torch.from_numpy(roots.copy()), 0)
+        allr = g.assemble(0)
+        if rank == 0:
+            q.put(allr)
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("world,mode", [(2, "mod"), (2, "block"), (3, "mod")])
+def test_sharded_gather_matches_single_process(world, mode, coracle):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = _oracle_roots(coracle, np.arange(N_KEYS, dtype=np.uint64), P, 0, 1, mode).reshape(P, 32)
+    assert np.array_equal(got, full)
+
+
+def test_shard_partitions_cover_everything():
+    from mydatastore_amd.dist import local_partitions, shard_gids
+    for world in (1, 2, 4, 8):
+        parts = np.concatenate([local_partitions(1024, r, world) for r in range(world)])
+        assert sorted(parts.tolist()) == list(range(1024))
+        gids = np.concatenate([shard_gids(10_000, 1024, "mod", 10, r, world) for r in range(world)])
+        assert sorted(gids.tolist()) == list(range(10_000))
