@@ -1,0 +1,355 @@
+// merkle_tree.cpp -- see merkle_tree.hpp. Host-side object plumbing only; every hash is computed
+// by the engine (libmde.so).
+#include "merkle_tree.hpp"
+
+#include <cstdio>
+#include <cstring>
+
+namespace mds {
+
+// ---------------------------------------------------------------- Engine
+Engine::Engine(int device) {
+  int rc = mde_create(device, &ctx_);
+  if (rc != MDE_OK) {
+    ctx_ = nullptr;
+    init_err_ = std::string("mde_create failed: ") + mde_strerror(rc);
+  }
+}
+
+Engine::~Engine() {
+  if (ctx_) mde_destroy(ctx_);
+}
+
+Error Engine::error(int rc) const {
+  const char* m = ctx_ ? mde_last_error(ctx_) : "";
+  return std::string(mde_strerror(rc)) + (m && *m ? std::string(": ") + m : std::string());
+}
+
+// ---------------------------------------------------------------- utils/utils.go:67-89
+Bytes EncodeInt64ToBytes(int64_t v) {
+  Bytes b(8);
+  const uint64_t u = (uint64_t)v;
+  for (int k = 0; k < 8; k++) b[k] = (uint8_t)(u >> (8 * k));
+  return b;
+}
+
+Error DecodeBytesToInt64(const Bytes& b, int64_t* out) {
+  if (b.size() != 8) return "byte slice should be 8 bytes long for int64 decoding";
+  uint64_t u = 0;
+  for (int k = 7; k >= 0; k--) u = (u << 8) | b[k];
+  *out = (int64_t)u;
+  return "";
+}
+
+// ---------------------------------------------------------------- MerkleTree
+MerkleTree MerkleTree::FromDevice(std::vector<uint64_t> digests, std::vector<int32_t> sizes, Bytes nodes) {
+  MerkleTree t;
+  const uint32_t B = (uint32_t)digests.size();
+  t.digests_ = std::move(digests);
+  t.nodes_ = std::move(nodes);
+  for (uint32_t b = 0; b < B; b++) {
+    MerkleBucket mb;
+    mb.bucketId = (int32_t)b;
+    mb.hasher.value = (int64_t)t.digests_[b];
+    mb.size = b < sizes.size() ? sizes[b] : 0;
+    t.buckets_.push_back(mb);
+  }
+  // level 0: leaves (+ duplicate of the last leaf when B is odd -- merkletree buildWithContent)
+  std::vector<Node*> level;
+  for (uint32_t b = 0; b < B; b++) {
+    t.pool_.push_back(Node{nullptr, nullptr, t.buckets_[b].CalculateHash(), &t.buckets_[b], true, false});
+    level.push_back(&t.pool_.back());
+  }
+  if (B % 2 == 1) {
+    t.pool_.push_back(Node{nullptr, nullptr, level.back()->Hash, level.back()->C, true, true});
+    level.push_back(&t.pool_.back());
+  }
+  t.Leafs = level;
+  // inner levels: hashes come from the device's node array (level 1 .. root, 32 B each)
+  uint64_t off = 0;
+  while (level.size() > 1) {
+    std::vector<Node*> up;
+    const size_t n = level.size(), m = (n + 1) / 2;
+    for (size_t j = 0; j < m; j++) {
+      Node nd;
+      nd.Left = level[2 * j];
+      nd.Right = (2 * j + 1 < n) ? level[2 * j + 1] : level[2 * j];
+      if ((off + j + 1) * 32 <= t.nodes_.size())
+        nd.Hash.assign(t.nodes_.begin() + (off + j) * 32, t.nodes_.begin() + (off + j + 1) * 32);
+      t.pool_.push_back(nd);
+      up.push_back(&t.pool_.back());
+    }
+    off += m;
+    level.swap(up);
+  }
+  t.Root = level.empty() ? nullptr : level[0];
+  return t;
+}
+
+// ---------------------------------------------------------------- main/merkle_tree.go:118-157
+Error MerkleTreeToPartitionEpochObject(const MerkleTree& tree, int partitionId, int64_t lowerEpoch,
+                                       int64_t upperEpoch, EpochTreeObject* out) {
+  EpochTreeObject o;
+  uint32_t items = 0;
+  for (const Node* leaf : tree.Leafs) {
+    if (!leaf->C) return "failed to decode MerkleBucket";
+    o.Buckets.push_back(leaf->C->CalculateHash());
+    o.BucketsSize.push_back(leaf->C->size);
+    items += (uint32_t)leaf->C->size;  // int32 arithmetic wraps like Go
+  }
+  o.Partition = partitionId;
+  o.LowerEpoch = lowerEpoch;
+  o.UpperEpoch = upperEpoch;
+  o.Items = (int32_t)items;
+  *out = std::move(o);
+  return "";
+}
+
+Error EpochTreeObjectToMerkleTree(Engine& eng, const EpochTreeObject& obj, MerkleTree* out) {
+  const uint32_t B = (uint32_t)obj.Buckets.size();
+  if (B == 0) return "error: cannot construct tree with no content";
+  std::vector<const uint8_t*> ptrs(B);
+  std::vector<uint32_t> lens(B);
+  for (uint32_t i = 0; i < B; i++) {
+    ptrs[i] = obj.Buckets[i].data();
+    lens[i] = (uint32_t)obj.Buckets[i].size();
+  }
+  std::vector<uint64_t> digests(B);
+  int rc = mde_decode_bucket_hashes(ptrs.data(), lens.data(), B, digests.data());
+  if (rc != MDE_OK) return "byte slice should be 8 bytes long for int64 decoding";
+  std::vector<int32_t> sizes(B, 0);
+  for (uint32_t i = 0; i < B && i < obj.BucketsSize.size(); i++) sizes[i] = obj.BucketsSize[i];
+  Bytes root(32), nodes(mde_tree_internal_nodes(B) * 32);
+  rc = mde_tree_from_digests(eng.ctx(), 1, B, digests.data(), root.data(), nodes.data());
+  if (rc != MDE_OK) return eng.error(rc);
+  *out = MerkleTree::FromDevice(std::move(digests), std::move(sizes), std::move(nodes));
+  return "";
+}
+
+Error DifferentMerkleTreeBuckets(Engine& eng, const MerkleTree& t1, const MerkleTree& t2,
+                                 std::vector<int32_t>* out) {
+  if (!t1.Root && !t2.Root) { out->clear(); return ""; }
+  if (!t1.Root || !t2.Root) return "a merkletree.Node is nil";
+  const uint64_t cap = mde_diff_capacity(t1.n_buckets(), t2.n_buckets());
+  std::vector<int32_t> ids(cap);
+  int32_t count = 0;
+  int rc = mde_diff(eng.ctx(), 1, t1.n_buckets(), t1.digests().data(), t1.nodes().data(),
+                    t2.n_buckets(), t2.digests().data(), t2.nodes().data(), ids.data(), cap, &count);
+  if (rc != MDE_OK) return eng.error(rc);
+  if (count == MDE_E_TREE) return "bucketIds dont match (or a merkletree.Node is nil)";
+  if (count < 0) return std::string("diff failed: ") + mde_strerror(count);
+  ids.resize((size_t)count);
+  *out = std::move(ids);
+  return "";
+}
+
+// ---------------------------------------------------------------- index keys
+Error Index::Build(std::string* out) const {
+  std::string s;
+  for (size_t i = 0; i < cols_.size(); i++) {
+    std::string v = cols_[i].value;
+    if (cols_[i].length >= 0) {
+      if ((int)v.size() > cols_[i].length) return "index value invalid length " + std::to_string(v.size());
+      v = std::string(cols_[i].length - v.size(), '0') + v;
+    }
+    if (i) s += "_";
+    s += v;
+  }
+  *out = s;
+  return "";
+}
+
+Error Index::Parse(const std::string& s, std::map<std::string, std::string>* out) const {
+  std::vector<std::string> parts;
+  size_t start = 0;
+  for (;;) {
+    size_t p = s.find('_', start);
+    parts.push_back(s.substr(start, p == std::string::npos ? std::string::npos : p - start));
+    if (p == std::string::npos) break;
+    start = p + 1;
+  }
+  if (parts.size() != cols_.size())
+    return "index columns #" + std::to_string(cols_.size() + 1) + " and parts #" + std::to_string(parts.size()) + " not equal";
+  out->clear();
+  for (size_t i = cols_.size(); i-- > 0;) {
+    std::string v = parts[i];
+    if (cols_[i].length >= 0) {
+      size_t nz = v.find_first_not_of('0');
+      v = nz == std::string::npos ? "0" : v.substr(nz);
+    }
+    (*out)[cols_[i].name] = v;
+  }
+  return "";
+}
+
+Error BuildEpochIndex(int partition, uint64_t bucket, int64_t epoch, const std::string& key, std::string* out) {
+  return Index("epoch")
+      .AddColumn(CreateUnorderedColumn("parition", std::to_string(partition)))
+      .AddColumn(CreateUnorderedColumn("bucket", std::to_string(bucket)))
+      .AddColumn(CreateOrderedColumn("epoch", std::to_string(epoch), epochLength))
+      .AddColumn(CreateUnorderedColumn("key", key))
+      .Build(out);
+}
+
+Error ParseEpochIndex(const std::string& s, int* partition, uint64_t* bucket, int64_t* epoch, std::string* key) {
+  std::map<std::string, std::string> m;
+  Error e = Index("epoch")
+                .AddColumn(CreateUnorderedColumn("parition", "1"))
+                .AddColumn(CreateUnorderedColumn("bucket", "1"))
+                .AddColumn(CreateOrderedColumn("epoch", "1", epochLength))
+                .AddColumn(CreateUnorderedColumn("key", "1"))
+                .Parse(s, &m);
+  if (!e.empty()) return e;
+  if (m["name"] != "epoch") return "index name is wrong";
+  try {
+    *partition = std::stoi(m["parition"]);
+    *bucket = std::stoull(m["bucket"]);
+    *epoch = std::stoll(m["epoch"]);
+  } catch (...) {
+    return "invalid syntax";
+  }
+  *key = m["key"];
+  return "";
+}
+
+Error BuildKeyIndex(const std::string& key, std::string* out) {
+  return Index("item").AddColumn(CreateUnorderedColumn("key", key)).Build(out);
+}
+
+Error BuildEpochTreeObjectIndex(int partition, int64_t epoch, std::string* out) {
+  return Index("epochtree")
+      .AddColumn(CreateUnorderedColumn("partition", std::to_string(partition)))
+      .AddColumn(CreateOrderedColumn("epoch", std::to_string(epoch), epochLength))
+      .Build(out);
+}
+
+// ---------------------------------------------------------------- storage slice
+Iterator::Iterator(const std::map<std::string, Bytes>* m, const std::string& start, const std::string& limit)
+    : m_(m), it_(m->lower_bound(start)), limit_(limit) {}
+
+bool Iterator::IsDone() const { return it_ == m_->end() || it_->first.compare(limit_) >= 0; }
+
+bool Iterator::Next() {
+  ++it_;
+  return !IsDone();
+}
+
+bool MemStorage::Get(const std::string& k, Bytes* v) const {
+  auto it = kv_.find(k);
+  if (it == kv_.end()) return false;
+  *v = it->second;
+  return true;
+}
+
+// ---------------------------------------------------------------- Manager slice
+Error Manager::KeyTags(const std::string& key, uint64_t* bucket, int* partition) {
+  const uint64_t off[2] = {0, key.size()};
+  uint32_t b = 0, p = 0;
+  int rc = mde_tag_keys(eng_.ctx(), reinterpret_cast<const uint8_t*>(key.data()), off, 1,
+                        (uint32_t)partitionBuckets_, (uint32_t)partitionCount_, &b, &p);
+  if (rc != MDE_OK) return eng_.error(rc);
+  *bucket = b;
+  *partition = (int)p;
+  return "";
+}
+
+static Bytes encode_item(const Value& v) {  // item_{key} record: epoch, timestamp, value bytes
+  Bytes b = EncodeInt64ToBytes(v.Epoch), t = EncodeInt64ToBytes(v.UnixTimestamp);
+  b.insert(b.end(), t.begin(), t.end());
+  b.insert(b.end(), v.Val.begin(), v.Val.end());
+  return b;
+}
+
+static void decode_item(const std::string& key, const Bytes& b, Value* v) {
+  v->Key = key;
+  DecodeBytesToInt64(Bytes(b.begin(), b.begin() + 8), &v->Epoch);
+  DecodeBytesToInt64(Bytes(b.begin() + 8, b.begin() + 16), &v->UnixTimestamp);
+  v->Val.assign(b.begin() + 16, b.end());
+}
+
+Error Manager::SetValue(const Value& v) {
+  uint64_t bucket;
+  int partition;
+  Error e = KeyTags(v.Key, &bucket, &partition);
+  if (!e.empty()) return e;
+  std::string epochIndex, keyIndex;
+  if (!(e = BuildEpochIndex(partition, bucket, v.Epoch, v.Key, &epochIndex)).empty()) return e;
+  if (!(e = BuildKeyIndex(v.Key, &keyIndex)).empty()) return e;
+  Bytes existing;
+  if (db_.Get(keyIndex, &existing)) {
+    Value ev;
+    decode_item(v.Key, existing, &ev);
+    if (ev.Epoch >= v.Epoch && ev.UnixTimestamp > v.UnixTimestamp) return "a newer value already exists";
+  }
+  db_.Put(keyIndex, encode_item(v));
+  db_.Put(epochIndex, EncodeInt64ToBytes(v.UnixTimestamp));
+  return "";
+}
+
+Error Manager::GetValue(const std::string& key, Value* out) {
+  std::string keyIndex;
+  Error e = BuildKeyIndex(key, &keyIndex);
+  if (!e.empty()) return e;
+  Bytes b;
+  if (!db_.Get(keyIndex, &b)) return "KEY_NOT_FOUND";
+  decode_item(key, b, out);
+  return "";
+}
+
+Error Manager::RawPartitionMerkleTree(int partitionId, int64_t lowerEpoch, int64_t upperEpoch, MerkleTree* out) {
+  std::vector<MerkleTree> trees;
+  Error e = RawPartitionMerkleTrees({partitionId}, lowerEpoch, upperEpoch, &trees);
+  if (!e.empty()) return e;
+  *out = std::move(trees[0]);
+  return "";
+}
+
+Error Manager::RawPartitionMerkleTrees(const std::vector<int>& partitionIds, int64_t lowerEpoch,
+                                       int64_t upperEpoch, std::vector<MerkleTree>* out) {
+  // Ingest: the per-bucket range scans of main/merkle_tree.go:90-113 copy each record's value into
+  // one contiguous arena (layout A); seg_rec marks the bucket boundaries.
+  const uint32_t B = (uint32_t)partitionBuckets_, P = (uint32_t)partitionIds.size();
+  Bytes arena;
+  std::vector<uint64_t> value_off{0}, seg_rec{0};
+  for (int p : partitionIds) {
+    for (uint32_t b = 0; b < B; b++) {
+      std::string i1, i2;
+      Error e = BuildEpochIndex(p, b, lowerEpoch, "", &i1);
+      if (!e.empty()) return e;
+      if (!(e = BuildEpochIndex(p, b, upperEpoch, "", &i2)).empty()) return e;
+      for (Iterator it = db_.NewIterator(i1, i2); !it.IsDone(); it.Next()) {
+        const Bytes v = it.Value();
+        arena.insert(arena.end(), v.begin(), v.end());
+        value_off.push_back(arena.size());
+      }
+      seg_rec.push_back(value_off.size() - 1);
+    }
+  }
+  if (arena.empty()) arena.push_back(0);  // keep a valid pointer for an all-empty build
+  mde_records rec{};
+  rec.values = arena.data();
+  rec.values_bytes = arena.size();
+  rec.value_stride = 0;
+  rec.value_off = value_off.data();
+  rec.n_records = value_off.size() - 1;
+  rec.n_partitions = P;
+  rec.n_buckets = B;
+  rec.seg_rec = seg_rec.data();
+  const uint64_t NI = mde_tree_internal_nodes(B);
+  std::vector<uint64_t> digest((size_t)P * B);
+  std::vector<int32_t> size((size_t)P * B), items(P);
+  Bytes root((size_t)P * 32), nodes((size_t)P * NI * 32);
+  mde_tree_out o{digest.data(), size.data(), items.data(), root.data(), nodes.data()};
+  int rc = mde_build(eng_.ctx(), &rec, &o);
+  if (rc != MDE_OK) return eng_.error(rc);
+  out->clear();
+  for (uint32_t i = 0; i < P; i++) {
+    out->push_back(MerkleTree::FromDevice(
+        std::vector<uint64_t>(digest.begin() + (size_t)i * B, digest.begin() + (size_t)(i + 1) * B),
+        std::vector<int32_t>(size.begin() + (size_t)i * B, size.begin() + (size_t)(i + 1) * B),
+        Bytes(nodes.begin() + (size_t)i * NI * 32, nodes.begin() + (size_t)(i + 1) * NI * 32)));
+  }
+  return "";
+}
+
+}  // namespace mds

@@ -1,0 +1,203 @@
+// test_merkle_tree.cpp -- C++ port of the reference's tests for the Merkle path, run against the
+// host mirror (mydatastore_amd/host) over the MI355X engine:
+//   TestMerkleTreeRaw   main/merkle_tree_test.go:15-185 (N = 100 and the -test.short N = 10)
+//   TestIndexManager    main/indexs_test.go:9-41
+//   TestIndexStorage    storage/index_test.go:9-40
+//   TestManagerStorage  main/manager_test.go:30-115 (range-iteration counts)
+// Prints "ROOT <name> <hex>" lines (checked against tests/golden by tests/test_cpp_port.py) and
+// exits non-zero on the first failed assertion.
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "merkle_tree.hpp"
+
+using namespace mds;
+
+static int failures = 0;
+#define CHECK(cond, msg)                                                            \
+  do {                                                                              \
+    if (!(cond)) {                                                                  \
+      std::fprintf(stderr, "FAIL %s:%d: %s (%s)\n", __FILE__, __LINE__, msg, #cond); \
+      failures++;                                                                   \
+    }                                                                               \
+  } while (0)
+#define CHECK_OK(err)                                                                       \
+  do {                                                                                      \
+    Error e_ = (err);                                                                       \
+    if (!e_.empty()) {                                                                      \
+      std::fprintf(stderr, "FAIL %s:%d: error: %s\n", __FILE__, __LINE__, e_.c_str());      \
+      failures++;                                                                           \
+    }                                                                                       \
+  } while (0)
+
+static std::string hex(const Bytes& b) {
+  static const char* d = "0123456789abcdef";
+  std::string s;
+  for (uint8_t x : b) { s += d[x >> 4]; s += d[x & 15]; }
+  return s;
+}
+
+static std::string ids(const std::vector<int32_t>& v) {
+  std::string s;
+  for (size_t i = 0; i < v.size(); i++) s += (i ? "," : "") + std::to_string(v[i]);
+  return s;
+}
+
+static void TestMerkleTreeRaw(Engine& eng, int writeValuesNum) {
+  Manager manager(eng, /*PartitionCount=*/1, /*PartitionBuckets=*/30);
+  int64_t timestamp = 0;
+  for (int i = 0; i < writeValuesNum; i++) {  // write to epoch 1
+    timestamp++;
+    Value v{"key" + std::to_string(i), "val" + std::to_string(i), 1, timestamp};
+    CHECK_OK(manager.SetValue(v));
+    Value got;
+    CHECK_OK(manager.GetValue(v.Key, &got));
+    CHECK(got.Val == v.Val, "get value is wrong");
+  }
+  for (int i = 0; i < writeValuesNum; i++) {  // write to epoch 2
+    timestamp++;
+    Value v{"keyz" + std::to_string(i), "valz" + std::to_string(i), 2, timestamp};
+    CHECK_OK(manager.SetValue(v));
+    Value got;
+    CHECK_OK(manager.GetValue(v.Key, &got));
+    CHECK(got.Val == v.Val, "get value is wrong");
+  }
+  MerkleTree tree1, tree2, tree3;
+  CHECK_OK(manager.RawPartitionMerkleTree(0, 0, 3, &tree1));
+  CHECK_OK(manager.RawPartitionMerkleTree(0, 1, 3, &tree2));
+  CHECK_OK(manager.RawPartitionMerkleTree(0, 2, 3, &tree3));
+
+  CHECK(tree1.Leafs.size() == 30, "confirm leafs num is the same as PartitionBuckets");
+  CHECK(tree2.Leafs.size() == 30, "confirm leafs num is the same as PartitionBuckets");
+  CHECK(tree3.Leafs.size() == 30, "confirm leafs num is the same as PartitionBuckets");
+  CHECK(tree1.MerkleRoot() == tree2.MerkleRoot(), "hash should be the same");
+  CHECK(tree1.MerkleRoot() != tree3.MerkleRoot(), "hash should be different");
+  CHECK(tree2.MerkleRoot() != tree3.MerkleRoot(), "hash should be different");
+  for (const MerkleTree* t : {&tree1, &tree2, &tree3})
+    for (size_t i = 0; i < t->Leafs.size(); i++)
+      CHECK(t->Leafs[i]->C && t->Leafs[i]->C->bucketId == (int32_t)i, "wrong bucket id");
+
+  EpochTreeObject obj1, obj2, obj3;
+  CHECK_OK(MerkleTreeToPartitionEpochObject(tree1, 0, 0, 3, &obj1));
+  CHECK_OK(MerkleTreeToPartitionEpochObject(tree2, 0, 1, 3, &obj2));
+  CHECK_OK(MerkleTreeToPartitionEpochObject(tree3, 0, 2, 3, &obj3));
+  MerkleTree stree1, stree2, stree3;
+  CHECK_OK(EpochTreeObjectToMerkleTree(eng, obj1, &stree1));
+  CHECK_OK(EpochTreeObjectToMerkleTree(eng, obj2, &stree2));
+  CHECK_OK(EpochTreeObjectToMerkleTree(eng, obj3, &stree3));
+  CHECK(tree1.MerkleRoot() == stree1.MerkleRoot(), "hash should be the same");
+  CHECK(tree2.MerkleRoot() == stree2.MerkleRoot(), "hash should be the same");
+  CHECK(tree3.MerkleRoot() == stree3.MerkleRoot(), "hash should be the same");
+
+  std::vector<int32_t> diff1, diff2, diff3, diff4, diff5;
+  CHECK_OK(DifferentMerkleTreeBuckets(eng, tree1, tree2, &diff1));
+  CHECK_OK(DifferentMerkleTreeBuckets(eng, tree2, tree1, &diff2));
+  CHECK_OK(DifferentMerkleTreeBuckets(eng, tree1, tree3, &diff3));
+  CHECK_OK(DifferentMerkleTreeBuckets(eng, tree1, stree1, &diff4));
+  CHECK_OK(DifferentMerkleTreeBuckets(eng, tree1, stree3, &diff5));
+  CHECK(diff1 == diff2, "diff should be the same");
+  CHECK(diff1.empty(), "should be no diff");
+  CHECK(diff1 == diff4, "diff should be the same");
+  CHECK(!diff3.empty(), "there should be a diff");
+  CHECK(!diff5.empty(), "there should be a diff");
+  CHECK(diff3 == diff5, "diff vs the round-tripped tree equals diff vs the tree");
+
+  const std::string n = std::to_string(writeValuesNum);
+  std::printf("ROOT n%s_0_3 %s\nROOT n%s_1_3 %s\nROOT n%s_2_3 %s\nDIFF n%s_t1_t3 %s\nITEMS n%s_0_3 %d\n",
+              n.c_str(), hex(tree1.MerkleRoot()).c_str(), n.c_str(), hex(tree2.MerkleRoot()).c_str(),
+              n.c_str(), hex(tree3.MerkleRoot()).c_str(), n.c_str(), ids(diff3).c_str(), n.c_str(),
+              obj1.Items);
+
+  // Batched build (one engine call for the partition) agrees with the single build.
+  std::vector<MerkleTree> batch;
+  CHECK_OK(manager.RawPartitionMerkleTrees({0, 0}, 0, 3, &batch));
+  CHECK(batch.size() == 2 && batch[0].MerkleRoot() == tree1.MerkleRoot() &&
+            batch[1].MerkleRoot() == tree1.MerkleRoot(), "batched build root");
+}
+
+static void TestIndexManager() {
+  std::string index1;
+  CHECK_OK(BuildEpochIndex(1, 2, 3, "zz", &index1));
+  CHECK(index1 == "epoch_1_2_0000000003_zz", "equal index");
+  int p;
+  uint64_t b;
+  int64_t e;
+  std::string k;
+  CHECK_OK(ParseEpochIndex(index1, &p, &b, &e, &k));
+  CHECK(p == 1 && b == 2 && e == 3 && k == "zz", "parsed fields");
+  std::string index2;
+  CHECK_OK(BuildEpochTreeObjectIndex(1, 2, &index2));
+  CHECK(index2 == "epochtree_1_0000000002", "equal index");
+}
+
+static void TestIndexStorage() {
+  std::string index;
+  CHECK_OK(Index("test")
+               .AddColumn(CreateUnorderedColumn("partition", "part1"))
+               .AddColumn(CreateUnorderedColumn("bucket", "bucket1"))
+               .AddColumn(CreateOrderedColumn("epoch", "1", 4))
+               .AddColumn(CreateUnorderedColumn("key", "mykey"))
+               .Build(&index));
+  CHECK(index == "test_part1_bucket1_0001_mykey", "index should be equal");
+  Index index2 = Index("zzz");
+  index2.AddColumn(CreateUnorderedColumn("partition", "part1"))
+      .AddColumn(CreateUnorderedColumn("bucket", "bucket1"))
+      .AddColumn(CreateOrderedColumn("epoch", "100", 4))
+      .AddColumn(CreateUnorderedColumn("key", "mykey"));
+  std::string s2;
+  CHECK_OK(index2.Build(&s2));
+  CHECK(s2 == "zzz_part1_bucket1_0100_mykey", "index2 should be equal");
+  std::map<std::string, std::string> m;
+  CHECK_OK(index2.Parse(s2, &m));
+  CHECK(m["name"] == "zzz" && m["partition"] == "part1" && m["bucket"] == "bucket1" &&
+            m["epoch"] == "100" && m["key"] == "mykey", "parsed columns");
+  std::string bad;
+  CHECK(!Index("x").AddColumn(CreateOrderedColumn("e", "12345", 4)).Build(&bad).empty(),
+        "too-long ordered column is an error");
+}
+
+static void TestManagerStorage(Engine& eng, int writeValuesNum) {
+  Manager manager(eng, 1, 1);
+  for (int i = 0; i < writeValuesNum; i++)
+    CHECK_OK(manager.SetValue({"key" + std::to_string(i), "val" + std::to_string(i), 1, 0}));
+  for (int i = 0; i < writeValuesNum; i++)
+    CHECK_OK(manager.SetValue({"keyz" + std::to_string(i), "valz" + std::to_string(i), 2, 0}));
+  std::string i1, i2, i3;
+  CHECK_OK(BuildEpochIndex(0, 0, 1, "", &i1));
+  CHECK_OK(BuildEpochIndex(0, 0, 2, "", &i2));
+  CHECK_OK(BuildEpochIndex(0, 0, 3, "", &i3));
+  int count = 0;
+  for (Iterator it = manager.db().NewIterator(i1, i2); !it.IsDone(); it.Next()) count++;
+  CHECK(count == writeValuesNum, "Should have iterated all inserted keys");
+  count = 0;
+  for (Iterator it = manager.db().NewIterator(i1, i3); !it.IsDone(); it.Next()) count++;
+  CHECK(count == 2 * writeValuesNum, "Should have iterated all inserted keys");
+  // B = 1: a single-bucket tree (leaf + its duplicate)
+  MerkleTree t;
+  CHECK_OK(manager.RawPartitionMerkleTree(0, 1, 3, &t));
+  CHECK(t.Leafs.size() == 2 && t.Leafs[1]->dup && t.Leafs[0]->C->size == 2 * writeValuesNum, "B = 1 tree");
+  // a newer value in an older-or-equal epoch is rejected (main/manager.go:807-809)
+  CHECK_OK(manager.SetValue({"kk", "a", 5, 100}));
+  CHECK(!manager.SetValue({"kk", "b", 5, 50}).empty(), "a newer value already exists");
+}
+
+int main() {
+  Engine eng(0);
+  if (!eng.ok()) {
+    std::fprintf(stderr, "engine unavailable: %s\n", eng.init_error().c_str());
+    return 2;
+  }
+  TestMerkleTreeRaw(eng, 100);
+  TestMerkleTreeRaw(eng, 10);
+  TestIndexManager();
+  TestIndexStorage();
+  TestManagerStorage(eng, 100);
+  if (failures) {
+    std::fprintf(stderr, "%d failure(s)\n", failures);
+    return 1;
+  }
+  std::printf("PASS\n");
+  return 0;
+}
