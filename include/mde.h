@@ -129,6 +129,13 @@ int mde_diff_async(mde_ctx* ctx, uint32_t n_pairs, uint32_t n_buckets_a, const u
                    const uint8_t* nodes_b, int32_t* out_ids, uint64_t out_stride,
                    int32_t* out_count);
 
+/* Convenience for callers that hold only bucket digests (e.g. the Go shim, whose trees are
+ * *merkletree.MerkleTree): builds both trees on device and diffs them. Host pointers, synchronous.
+ * Same output contract as mde_diff. */
+int mde_diff_digests(mde_ctx* ctx, uint32_t n_pairs, uint32_t n_buckets_a, const uint64_t* digest_a,
+                     uint32_t n_buckets_b, const uint64_t* digest_b, int32_t* out_ids,
+                     uint64_t out_stride, int32_t* out_count);
+
 /* Write-time tagging of raw keys (device): bucket = BE64(SHA256(key)[:8]) % n_buckets
  * (main/manager.go:773-778), partition = XXH64(key, 0) % n_partitions (hashring.go:108-110).
  * key i = keys[key_off[i] .. key_off[i+1]). Either output may be NULL. */

@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "mde_set_stream", "mde_use_own_stream", "mde_get_stream", "mde_synchronize", "mde_device_info", "mde_tree_depth",
     "mde_tree_internal_nodes", "mde_diff_capacity", "mde_build", "mde_build_async",
     "mde_digest_async", "mde_tree_async", "mde_tree_from_digests", "mde_tree_from_digests_async",
-    "mde_decode_bucket_hashes", "mde_diff", "mde_diff_async", "mde_tag_keys_async", "mde_tag_keys",
+    "mde_decode_bucket_hashes", "mde_diff", "mde_diff_async", "mde_diff_digests", "mde_tag_keys_async", "mde_tag_keys",
     "mde_synth_tags_async", "mde_synth_values_async", "mde_dev_alloc", "mde_dev_free",
     "mde_memcpy_h2d", "mde_memcpy_d2h",
 )
@@ -101,6 +101,7 @@ def load_library() -> C.CDLL:
         "mde_decode_bucket_hashes": (C.c_int, [vp, vp, u32, vp]),
         "mde_diff": (C.c_int, [vp, u32, u32, vp, vp, u32, vp, vp, vp, u64, vp]),
         "mde_diff_async": (C.c_int, [vp, u32, u32, vp, vp, u32, vp, vp, vp, u64, vp]),
+        "mde_diff_digests": (C.c_int, [vp, u32, u32, vp, u32, vp, vp, u64, vp]),
         "mde_tag_keys_async": (C.c_int, [vp, vp, vp, u64, u32, u32, vp, vp]),
         "mde_tag_keys": (C.c_int, [vp, vp, vp, u64, u32, u32, vp, vp]),
         "mde_synth_tags_async": (C.c_int, [vp, vp, u64, u32, u32, C.c_int, u64, vp, vp]),
@@ -269,6 +270,16 @@ class Engine:
             c = int(cnt[i])
             res.append(c if c < 0 else ids[i * cap:i * cap + c].tolist())
         return res
+
+    def diff_digests(self, ba: int, da: np.ndarray, bb: int, db: np.ndarray, n_pairs: int = 1):
+        """mde_diff_digests: trees built on device from the two digest vectors, then diffed."""
+        cap = diff_capacity(ba, bb)
+        ids = np.zeros(n_pairs * cap, np.int32)
+        cnt = np.zeros(n_pairs, np.int32)
+        da, db = (np.ascontiguousarray(x, dtype=np.uint64) for x in (da, db))
+        self._check(self.lib.mde_diff_digests(self.ctx, n_pairs, ba, _ptr(da), bb, _ptr(db),
+                                              _ptr(ids), cap, _ptr(cnt)))
+        return [int(c) if c < 0 else ids[i * cap:i * cap + int(c)].tolist() for i, c in enumerate(cnt)]
 
     def diff_async(self, n_pairs, ba, da, na, bb, db, nb, out_ids, out_stride, out_count):
         self._check(self.lib.mde_diff_async(self.ctx, n_pairs, ba, _ptr(da), _ptr(na), bb, _ptr(db),

@@ -457,6 +457,45 @@ int mde_diff(mde_ctx* c, uint32_t n_pairs, uint32_t Ba, const uint64_t* da, cons
   return MDE_OK;
 }
 
+int mde_diff_digests(mde_ctx* c, uint32_t n_pairs, uint32_t Ba, const uint64_t* da, uint32_t Bb,
+                     const uint64_t* db, int32_t* out_ids, uint64_t out_stride, int32_t* out_count) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (!Ba || !Bb || !da || !db || !out_ids || !out_count)
+    return set_err(c, MDE_E_INVAL, "bad diff arguments");
+  if (out_stride < mde_diff_capacity(Ba, Bb))
+    return set_err(c, MDE_E_CAPACITY, "out_stride too small");
+  const uint64_t T = n_pairs, NA = mde::tree_internal(Ba), NB = mde::tree_internal(Bb);
+  const uint64_t sz[8] = {T * Ba * 8, T * NA * 32, T * Bb * 8, T * NB * 32, T * out_stride * 4, T * 4,
+                          T * 32, T * 32};
+  int rc;
+  for (int i = 0; i < 8; i++)
+    if ((rc = ensure_buf(c, c->stage[i], sz[i]))) return rc;
+  MDE_HIP(c, hipMemcpyAsync(c->stage[0].p, da, sz[0], hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(c->stage[2].p, db, sz[2], hipMemcpyHostToDevice, c->stream));
+  if ((rc = tree_digests_async(c, n_pairs, Ba, static_cast<const uint64_t*>(c->stage[0].p),
+                               static_cast<uint8_t*>(c->stage[6].p), static_cast<uint8_t*>(c->stage[1].p))))
+    return rc;
+  if ((rc = tree_digests_async(c, n_pairs, Bb, static_cast<const uint64_t*>(c->stage[2].p),
+                               static_cast<uint8_t*>(c->stage[7].p), static_cast<uint8_t*>(c->stage[3].p))))
+    return rc;
+  mde::DiffLaunch a{n_pairs,
+                    Ba,
+                    Bb,
+                    static_cast<const uint64_t*>(c->stage[0].p),
+                    static_cast<const uint8_t*>(c->stage[1].p),
+                    static_cast<const uint64_t*>(c->stage[2].p),
+                    static_cast<const uint8_t*>(c->stage[3].p),
+                    static_cast<int32_t*>(c->stage[4].p),
+                    out_stride,
+                    static_cast<int32_t*>(c->stage[5].p)};
+  MDE_HIP(c, mde::launch_diff(a, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(out_ids, c->stage[4].p, sz[4], hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(out_count, c->stage[5].p, sz[5], hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  return MDE_OK;
+}
+
 int mde_tag_keys_async(mde_ctx* c, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
                        uint32_t B, uint32_t P, uint32_t* bucket, uint32_t* partition) {
   if (!c) return MDE_E_INVAL;

@@ -115,6 +115,8 @@ def test_diff_cases(engine, golden):
         ra, na = engine.tree_from_digests(da, c["b1"])
         rb, nb = engine.tree_from_digests(db, c["b2"])
         got = engine.diff(c["b1"], da, na, c["b2"], db, nb)[0]
+        got2 = engine.diff_digests(c["b1"], da, c["b2"], db)[0]
+        assert got == got2, c["name"]
         if "error" in c:
             assert got == mde.MDE_E_TREE, c["name"]
         else:
