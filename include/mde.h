@@ -136,6 +136,23 @@ int mde_diff_digests(mde_ctx* ctx, uint32_t n_pairs, uint32_t n_buckets_a, const
                      uint32_t n_buckets_b, const uint64_t* digest_b, int32_t* out_ids,
                      uint64_t out_stride, int32_t* out_count);
 
+/* Out-of-sync range extract (StreamBucketsTask, main/manager.go:445-487): for partition p, the
+ * records of the buckets ids[p*ids_stride .. +counts[p]) (duplicates removed -- VerifyEpoch's
+ * Int32Set, main/manager.go:1086; counts[p] < 0 extracts nothing), in ascending bucket order and
+ * LSM record order. Feed it mde_diff's output directly. n_buckets <= 65536.
+ * part_off[P+1]: record offsets of each partition in out_rec / out_value_off;
+ * out_rec[rec_cap]: source record indices; out_values[bytes_cap] (optional): the value bytes,
+ * concatenated; out_value_off[rec_cap+1] (optional): byte offset of each extracted value in
+ * out_values. *status = MDE_OK, or MDE_E_CAPACITY (then nothing is written past part_off). */
+int mde_extract_async(mde_ctx* ctx, const mde_records* rec, const int32_t* ids, uint64_t ids_stride,
+                      const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
+                      uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap,
+                      int32_t* status);
+/* Host-pointer version; returns MDE_E_CAPACITY when the outputs are too small. */
+int mde_extract(mde_ctx* ctx, const mde_records* rec, const int32_t* ids, uint64_t ids_stride,
+                const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
+                uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap);
+
 /* Write-time tagging of raw keys (device): bucket = BE64(SHA256(key)[:8]) % n_buckets
  * (main/manager.go:773-778), partition = XXH64(key, 0) % n_partitions (hashring.go:108-110).
  * key i = keys[key_off[i] .. key_off[i+1]). Either output may be NULL. */

@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "mde_tree_internal_nodes", "mde_diff_capacity", "mde_build", "mde_build_async",
     "mde_digest_async", "mde_tree_async", "mde_tree_from_digests", "mde_tree_from_digests_async",
     "mde_decode_bucket_hashes", "mde_diff", "mde_diff_async", "mde_diff_digests", "mde_tag_keys_async", "mde_tag_keys",
-    "mde_synth_tags_async", "mde_synth_values_async", "mde_dev_alloc", "mde_dev_free",
+    "mde_extract", "mde_extract_async", "mde_synth_tags_async", "mde_synth_values_async", "mde_dev_alloc", "mde_dev_free",
     "mde_memcpy_h2d", "mde_memcpy_d2h",
 )
 
@@ -104,6 +104,8 @@ def load_library() -> C.CDLL:
         "mde_diff_digests": (C.c_int, [vp, u32, u32, vp, u32, vp, vp, u64, vp]),
         "mde_tag_keys_async": (C.c_int, [vp, vp, vp, u64, u32, u32, vp, vp]),
         "mde_tag_keys": (C.c_int, [vp, vp, vp, u64, u32, u32, vp, vp]),
+        "mde_extract": (C.c_int, [vp, C.POINTER(Records), vp, u64, vp, vp, vp, u64, vp, vp, u64]),
+        "mde_extract_async": (C.c_int, [vp, C.POINTER(Records), vp, u64, vp, vp, vp, u64, vp, vp, u64, vp]),
         "mde_synth_tags_async": (C.c_int, [vp, vp, u64, u32, u32, C.c_int, u64, vp, vp]),
         "mde_synth_values_async": (C.c_int, [vp, vp, vp, u64, u32, u64]),
         "mde_dev_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
@@ -284,6 +286,42 @@ class Engine:
     def diff_async(self, n_pairs, ba, da, na, bb, db, nb, out_ids, out_stride, out_count):
         self._check(self.lib.mde_diff_async(self.ctx, n_pairs, ba, _ptr(da), _ptr(na), bb, _ptr(db),
                                             _ptr(nb), _ptr(out_ids), out_stride, _ptr(out_count)))
+
+    # -- out-of-sync range extract (StreamBucketsTask) ----------------------------------------
+    def extract(self, values, seg_rec, n_partitions, n_buckets, ids, ids_stride, counts,
+                value_stride=0, value_off=None, want_values=True):
+        """Records of the listed buckets per partition (dedup, ascending bucket, LSM order).
+        Returns (part_off, rec_idx, values_bytes, value_off)."""
+        seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
+        values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)
+        if value_off is not None:
+            value_off = np.ascontiguousarray(value_off, dtype=np.uint64)
+        n_rec = (value_off.size - 1) if value_off is not None else (
+            values.size // value_stride if value_stride else 0)
+        rec = Records(_ptr(values), values.nbytes, value_stride, 0, _ptr(value_off), n_rec,
+                      n_partitions, n_buckets, _ptr(seg_rec))
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        counts = np.ascontiguousarray(counts, dtype=np.int32)
+        rec_cap = max(int(n_rec), 1)
+        bytes_cap = max(values.nbytes, 1)
+        part_off = np.zeros(n_partitions + 1, np.uint64)
+        out_rec = np.zeros(rec_cap, np.uint64)
+        out_vals = np.zeros(bytes_cap, np.uint8) if want_values else None
+        out_voff = np.zeros(rec_cap + 1, np.uint64) if want_values else None
+        self._check(self.lib.mde_extract(self.ctx, C.byref(rec), _ptr(ids), ids_stride, _ptr(counts),
+                                         _ptr(part_off), _ptr(out_rec), rec_cap, _ptr(out_vals),
+                                         _ptr(out_voff), bytes_cap))
+        n = int(part_off[-1])
+        if not want_values:
+            return part_off, out_rec[:n], None, None
+        return part_off, out_rec[:n], out_vals[:int(out_voff[n])], out_voff[:n + 1]
+
+    def extract_async(self, rec: Records, ids, ids_stride, counts, part_off, out_rec, rec_cap,
+                      out_values, out_value_off, bytes_cap, status):
+        self._check(self.lib.mde_extract_async(self.ctx, C.byref(rec), _ptr(ids), ids_stride,
+                                               _ptr(counts), _ptr(part_off), _ptr(out_rec), rec_cap,
+                                               _ptr(out_values), _ptr(out_value_off), bytes_cap,
+                                               _ptr(status)))
 
     # -- tagging / synthetic workload ---------------------------------------------------------
     def tag_keys(self, keys, n_buckets: int, n_partitions: int):

@@ -27,11 +27,6 @@ constexpr int kThreads = 256;
 constexpr int kUnroll = 8;
 constexpr uint64_t kStepBytes = 64ull * 16ull * kUnroll;  // 8 KiB per wave step
 
-__device__ __forceinline__ uint64_t segpos(const SegDesc& d, uint32_t s) {
-  const uint64_t r = min(d.seg_rec[s], d.n_records);
-  return min(d.shift + (d.stride ? r * (uint64_t)d.stride : d.value_off[r]), d.end);
-}
-
 // Largest s in [lo, S) with segpos(s) <= x (lo if none). 64-ary search: one vector load and one
 // ballot per round, log64(S) rounds. Must be called by all 64 lanes.
 __device__ __forceinline__ uint32_t seg_search(const SegDesc& d, uint32_t lo, uint64_t x, int lane) {

@@ -1,0 +1,164 @@
+// extract.hip -- out-of-sync range extract on device.
+//
+// Reference: StreamBucketsTask (main/manager.go:445-487) walks, for each requested bucket of a
+// partition, the range [epoch_p_b_{lo}_, epoch_p_b_{hi}_) and emits every record; VerifyEpoch
+// requests the de-duplicated diff set (utils.Int32Set, main/manager.go:1073,1086,1114). In layout A
+// a bucket's records are one contiguous run, so the extract is a segmented gather: per partition
+// the records of the requested buckets, duplicates removed, in ascending bucket order and LSM
+// record order (the reference's bucket order is Go map iteration order, i.e. unspecified).
+//
+// Three launches, all device-side: count (one workgroup per partition: LDS bitmap of requested
+// buckets, record/byte totals), scan (one workgroup: exclusive prefix sums + capacity check),
+// copy (one workgroup per partition: record indices, value byte offsets and the value bytes,
+// 16-byte vector copies when source and destination allow it).
+#include "mde_device.hpp"
+#include "mde_internal.hpp"
+
+namespace mde {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr uint32_t kBitmapWords = kExtractMaxBuckets / 32;
+
+__device__ void load_bitmap(const ExtractLaunch& a, uint32_t p, uint32_t* bm) {
+  for (uint32_t w = threadIdx.x; w < (a.B + 31) / 32; w += kThreads) bm[w] = 0;
+  __syncthreads();
+  const int32_t n = a.counts[p];
+  const int32_t* ids = a.ids + (uint64_t)p * a.ids_stride;
+  for (int32_t i = threadIdx.x; i < n; i += kThreads) {
+    const int32_t b = ids[i];
+    if (b >= 0 && (uint32_t)b < a.B) atomicOr(&bm[b >> 5], 1u << (b & 31));
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ bool marked(const uint32_t* bm, uint32_t b) { return (bm[b >> 5] >> (b & 31)) & 1u; }
+
+__global__ __launch_bounds__(kThreads) void extract_count_kernel(ExtractLaunch a) {
+  __shared__ uint32_t bm[kBitmapWords];
+  __shared__ unsigned long long tot[2];
+  const uint32_t p = blockIdx.x;
+  if (threadIdx.x == 0) { tot[0] = 0; tot[1] = 0; }
+  load_bitmap(a, p, bm);
+  unsigned long long nr = 0, nb = 0;
+  for (uint32_t b = threadIdx.x; b < a.B; b += kThreads) {
+    if (!marked(bm, b)) continue;
+    const uint32_t s = p * a.B + b;
+    nr += a.seg.seg_rec[s + 1] - a.seg.seg_rec[s];
+    nb += segpos(a.seg, s + 1) - segpos(a.seg, s);
+  }
+  if (nr) atomicAdd(&tot[0], nr);
+  if (nb) atomicAdd(&tot[1], nb);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a.scratch[p] = tot[0];
+    a.scratch[(a.P + 1) + p] = tot[1];
+  }
+}
+
+// Exclusive scans of the per-partition record and byte counts (one workgroup).
+__global__ __launch_bounds__(kThreads) void extract_scan_kernel(ExtractLaunch a) {
+  __shared__ unsigned long long carry[2];
+  __shared__ unsigned long long part[2][kThreads];
+  if (threadIdx.x == 0) { carry[0] = 0; carry[1] = 0; }
+  __syncthreads();
+  for (uint32_t base = 0; base < a.P; base += kThreads) {
+    const uint32_t i = base + threadIdx.x;
+    part[0][threadIdx.x] = i < a.P ? a.scratch[i] : 0;
+    part[1][threadIdx.x] = i < a.P ? a.scratch[(a.P + 1) + i] : 0;
+    __syncthreads();
+    for (uint32_t o = 1; o < kThreads; o <<= 1) {  // Hillis-Steele inclusive scan
+      unsigned long long x0 = threadIdx.x >= o ? part[0][threadIdx.x - o] : 0;
+      unsigned long long x1 = threadIdx.x >= o ? part[1][threadIdx.x - o] : 0;
+      __syncthreads();
+      part[0][threadIdx.x] += x0;
+      part[1][threadIdx.x] += x1;
+      __syncthreads();
+    }
+    if (i < a.P) {
+      const unsigned long long inc0 = part[0][threadIdx.x], inc1 = part[1][threadIdx.x];
+      const unsigned long long own0 = a.scratch[i], own1 = a.scratch[(a.P + 1) + i];
+      a.part_off[i] = carry[0] + inc0 - own0;
+      a.scratch[2 * (a.P + 1) + i] = carry[1] + inc1 - own1;  // byte base
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      carry[0] += part[0][kThreads - 1];
+      carry[1] += part[1][kThreads - 1];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    a.part_off[a.P] = carry[0];
+    a.scratch[2 * (a.P + 1) + a.P] = carry[1];
+    const bool over = carry[0] > a.rec_cap || (a.out_values && carry[1] > a.bytes_cap);
+    *a.status = over ? -5 /* MDE_E_CAPACITY */ : 0;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void extract_copy_kernel(ExtractLaunch a) {
+  __shared__ uint32_t bm[kBitmapWords];
+  __shared__ unsigned long long run[2];
+  const uint32_t p = blockIdx.x;
+  if (*a.status != 0) return;  // capacity exceeded: nothing is written
+  if (threadIdx.x == 0) { run[0] = a.part_off[p]; run[1] = a.scratch[2 * (a.P + 1) + p]; }
+  load_bitmap(a, p, bm);
+  const int lane = threadIdx.x & 63;
+  for (uint32_t b0 = 0; b0 < a.B; b0 += 64) {
+    // one wave scans 64 buckets: offsets of the marked ones
+    const uint32_t b = b0 + lane;
+    const bool m = b < a.B && marked(bm, b);
+    const uint32_t s = p * a.B + (b < a.B ? b : 0);
+    unsigned long long nr = m ? a.seg.seg_rec[s + 1] - a.seg.seg_rec[s] : 0;
+    unsigned long long nb = m ? segpos(a.seg, s + 1) - segpos(a.seg, s) : 0;
+    unsigned long long er = nr, eb = nb;  // inclusive wave scan
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long xr = __shfl_up(er, o), xb = __shfl_up(eb, o);
+      if (lane >= o) { er += xr; eb += xb; }
+    }
+    const unsigned long long r_base = run[0] + er - nr, b_base = run[1] + eb - nb;
+    __syncthreads();
+    if (threadIdx.x == 63) { run[0] += er; run[1] += eb; }
+    // copy each marked bucket of this 64-bucket window with the whole workgroup
+    unsigned long long ball = __ballot(m);
+    while (ball) {
+      const int k = __ffsll((long long)ball) - 1;
+      ball &= ball - 1;
+      const uint32_t bs = p * a.B + b0 + k;
+      const uint64_t rb = __shfl(r_base, k), bb = __shfl(b_base, k);
+      const uint64_t r0 = a.seg.seg_rec[bs], r1 = a.seg.seg_rec[bs + 1];
+      const uint64_t src0 = segpos(a.seg, bs) - a.seg.shift, src1 = segpos(a.seg, bs + 1) - a.seg.shift;
+      // every wave computed the same window scan, so all 256 threads copy this bucket together
+      for (uint64_t r = r0 + threadIdx.x; r < r1; r += kThreads) {
+        a.out_rec[rb + (r - r0)] = r;
+        if (a.out_value_off) a.out_value_off[rb + (r - r0)] = bb + (recpos(a.seg, r) - src0);
+      }
+      if (a.out_values) {
+        const uint8_t* src = a.values + src0;
+        uint8_t* dst = a.out_values + bb;
+        const uint64_t len = src1 - src0;
+        if ((((uintptr_t)src | (uintptr_t)dst | len) & 15u) == 0) {
+          const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+          u32x4* d4 = reinterpret_cast<u32x4*>(dst);
+          for (uint64_t i = threadIdx.x; i < len / 16; i += kThreads) d4[i] = __builtin_nontemporal_load(s4 + i);
+        } else {
+          for (uint64_t i = threadIdx.x; i < len; i += kThreads) dst[i] = src[i];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && p == a.P - 1 && a.out_value_off) a.out_value_off[a.part_off[a.P]] = run[1];
+}
+
+}  // namespace
+
+hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
+  if (a.P == 0) return hipSuccess;
+  hipLaunchKernelGGL(extract_count_kernel, dim3(a.P), dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL(extract_scan_kernel, dim3(1), dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL(extract_copy_kernel, dim3(a.P), dim3(kThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace mde

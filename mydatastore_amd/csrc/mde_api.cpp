@@ -33,8 +33,9 @@ struct mde_ctx {
   bool sums_dirty = false;
   // Host-API staging (device) and a scratch node array for B > kTreeLdsMaxBuckets.
   struct Buf { void* p = nullptr; uint64_t cap = 0; };
-  Buf stage[12];
+  Buf stage[16];
   Buf nodes_scratch;
+  Buf extract_scratch;
 };
 
 namespace {
@@ -119,6 +120,20 @@ int check_records(mde_ctx* c, const mde_records* r) {
   return MDE_OK;
 }
 
+mde::SegDesc seg_desc(const mde_records* r) {
+  mde::SegDesc d{};
+  const uintptr_t v = reinterpret_cast<uintptr_t>(r->values);
+  d.base = reinterpret_cast<const uint8_t*>(v & ~uintptr_t(15));
+  d.shift = v & 15u;
+  d.stride = r->value_stride;
+  d.value_off = r->value_off;
+  d.seg_rec = r->seg_rec;
+  d.S = (uint32_t)((uint64_t)r->n_partitions * r->n_buckets);
+  d.n_records = r->n_records;
+  d.end = d.shift + r->values_bytes;
+  return d;
+}
+
 // Full validation of host-resident inputs (mde_build): the device API trusts its inputs but the
 // kernels clamp every index, so bad device input gives wrong digests, never a fault.
 int check_host_records(mde_ctx* c, const mde_records* r) {
@@ -146,15 +161,7 @@ int digest_async(mde_ctx* c, const mde_records* r) {
   if (rc) return rc;
   if (S == 0 || r->n_records == 0 || r->values_bytes == 0) return MDE_OK;
   mde::DigestLaunch a{};
-  const uintptr_t v = reinterpret_cast<uintptr_t>(r->values);
-  a.seg.base = reinterpret_cast<const uint8_t*>(v & ~uintptr_t(15));
-  a.seg.shift = v & 15u;
-  a.seg.stride = r->value_stride;
-  a.seg.value_off = r->value_off;
-  a.seg.seg_rec = r->seg_rec;
-  a.seg.S = (uint32_t)S;
-  a.seg.n_records = r->n_records;
-  a.seg.end = a.seg.shift + r->values_bytes;
+  a.seg = seg_desc(r);
   a.sums = c->sums;
   if (!c->digest_blocks_per_cu) c->digest_blocks_per_cu = mde::bucket_digest_blocks_per_cu();
   mde::plan_bucket_digest(r->values_bytes + a.seg.shift, c->cus, c->digest_blocks_per_cu,
@@ -186,6 +193,35 @@ int tree_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
     t.nodes_out = static_cast<uint8_t*>(c->nodes_scratch.p);
   }
   MDE_HIP(c, mde::launch_tree(t, c->stream));
+  return MDE_OK;
+}
+
+int extract_async(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t ids_stride,
+                  const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
+                  uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap, int32_t* status) {
+  if (r->n_buckets > mde::kExtractMaxBuckets)
+    return set_err(c, MDE_E_INVAL, "extract supports n_buckets <= %u", mde::kExtractMaxBuckets);
+  if (!ids || !counts || !part_off || !out_rec || !status || (out_values && !r->values))
+    return set_err(c, MDE_E_INVAL, "bad extract arguments");
+  int rc = ensure_buf(c, c->extract_scratch, 3 * ((uint64_t)r->n_partitions + 1) * 8);
+  if (rc) return rc;
+  mde::ExtractLaunch a{};
+  a.seg = seg_desc(r);
+  a.values = r->values;
+  a.P = r->n_partitions;
+  a.B = r->n_buckets;
+  a.ids = ids;
+  a.ids_stride = ids_stride;
+  a.counts = counts;
+  a.part_off = part_off;
+  a.out_rec = out_rec;
+  a.rec_cap = rec_cap;
+  a.out_values = out_values;
+  a.out_value_off = out_value_off;
+  a.bytes_cap = bytes_cap;
+  a.status = status;
+  a.scratch = static_cast<uint64_t*>(c->extract_scratch.p);
+  MDE_HIP(c, mde::launch_extract(a, c->stream));
   return MDE_OK;
 }
 
@@ -261,6 +297,7 @@ void mde_destroy(mde_ctx* c) {
     for (auto& b : c->stage)
       if (b.p) (void)hipFree(b.p);
     if (c->nodes_scratch.p) (void)hipFree(c->nodes_scratch.p);
+    if (c->extract_scratch.p) (void)hipFree(c->extract_scratch.p);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   }
   delete c;
@@ -492,6 +529,75 @@ int mde_diff_digests(mde_ctx* c, uint32_t n_pairs, uint32_t Ba, const uint64_t* 
   MDE_HIP(c, mde::launch_diff(a, c->stream));
   MDE_HIP(c, hipMemcpyAsync(out_ids, c->stage[4].p, sz[4], hipMemcpyDeviceToHost, c->stream));
   MDE_HIP(c, hipMemcpyAsync(out_count, c->stage[5].p, sz[5], hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  return MDE_OK;
+}
+
+int mde_extract_async(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t ids_stride,
+                      const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
+                      uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap,
+                      int32_t* status) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  int rc = check_records(c, r);
+  return rc ? rc : extract_async(c, r, ids, ids_stride, counts, part_off, out_rec, rec_cap, out_values,
+                                 out_value_off, bytes_cap, status);
+}
+
+int mde_extract(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t ids_stride,
+                const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
+                uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  int rc = check_records(c, r);
+  if (rc) return rc;
+  if ((rc = check_host_records(c, r))) return rc;
+  if (!ids || !counts || !part_off || !out_rec) return set_err(c, MDE_E_INVAL, "bad extract arguments");
+  const uint64_t P = r->n_partitions, S = P * r->n_buckets;
+  const uint64_t nvo = r->value_stride ? 0 : (r->n_records + 1);
+  const uint64_t sz[10] = {r->values_bytes, nvo * 8, (S + 1) * 8, P * ids_stride * 4, P * 4,
+                           (P + 1) * 8, rec_cap * 8, out_values ? bytes_cap : 0,
+                           out_value_off ? (rec_cap + 1) * 8 : 0, 4};
+  for (int i = 0; i < 10; i++)
+    if ((rc = ensure_buf(c, c->stage[i], sz[i]))) return rc;
+  auto dp = [&](int i) { return c->stage[i].p; };
+  if (r->values_bytes)
+    MDE_HIP(c, hipMemcpyAsync(dp(0), r->values, r->values_bytes, hipMemcpyHostToDevice, c->stream));
+  if (nvo) MDE_HIP(c, hipMemcpyAsync(dp(1), r->value_off, nvo * 8, hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(dp(2), r->seg_rec, (S + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(dp(3), ids, sz[3], hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(dp(4), counts, sz[4], hipMemcpyHostToDevice, c->stream));
+  mde_records dr = *r;
+  dr.values = static_cast<const uint8_t*>(dp(0));
+  dr.value_off = nvo ? static_cast<const uint64_t*>(dp(1)) : nullptr;
+  dr.seg_rec = static_cast<const uint64_t*>(dp(2));
+  rc = extract_async(c, &dr, static_cast<const int32_t*>(dp(3)), ids_stride,
+                     static_cast<const int32_t*>(dp(4)), static_cast<uint64_t*>(dp(5)),
+                     static_cast<uint64_t*>(dp(6)), rec_cap,
+                     out_values ? static_cast<uint8_t*>(dp(7)) : nullptr,
+                     out_value_off ? static_cast<uint64_t*>(dp(8)) : nullptr, bytes_cap,
+                     static_cast<int32_t*>(dp(9)));
+  if (rc) return rc;
+  int32_t status = 0;
+  MDE_HIP(c, hipMemcpyAsync(&status, dp(9), 4, hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(part_off, dp(5), (P + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  if (status != 0) return set_err(c, MDE_E_CAPACITY, "extract needs %llu records",
+                                  (unsigned long long)part_off[P]);
+  const uint64_t n = part_off[P];
+  if (n) MDE_HIP(c, hipMemcpyAsync(out_rec, dp(6), n * 8, hipMemcpyDeviceToHost, c->stream));
+  if (out_value_off)
+    MDE_HIP(c, hipMemcpyAsync(out_value_off, dp(8), (n + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+  if (out_values) {
+    uint64_t nbytes = 0;
+    if (out_value_off) {
+      MDE_HIP(c, hipStreamSynchronize(c->stream));
+      nbytes = out_value_off[n];
+    } else {
+      nbytes = bytes_cap;  // copy the whole buffer (unused tail is unspecified)
+    }
+    if (nbytes) MDE_HIP(c, hipMemcpyAsync(out_values, dp(7), nbytes, hipMemcpyDeviceToHost, c->stream));
+  }
   MDE_HIP(c, hipStreamSynchronize(c->stream));
   return MDE_OK;
 }

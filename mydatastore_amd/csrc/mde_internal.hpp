@@ -19,6 +19,18 @@ struct SegDesc {
   uint64_t end;               // ... and positions to shift + values_bytes: bad input never faults
 };
 
+// Byte position of bucket s's first value (clamped: bad input never faults).
+__host__ __device__ __forceinline__ uint64_t segpos(const SegDesc& d, uint32_t s) {
+  const uint64_t r0 = d.seg_rec[s];
+  const uint64_t r = r0 < d.n_records ? r0 : d.n_records;
+  const uint64_t p = d.shift + (d.stride ? r * (uint64_t)d.stride : d.value_off[r]);
+  return p < d.end ? p : d.end;
+}
+// Byte offset of record r's value relative to the arena start (no clamping).
+__host__ __device__ __forceinline__ uint64_t recpos(const SegDesc& d, uint64_t r) {
+  return d.stride ? r * (uint64_t)d.stride : d.value_off[r];
+}
+
 struct DigestLaunch {
   SegDesc seg;
   unsigned long long* sums;   // [S] u64 accumulators (zero on entry)
@@ -59,6 +71,25 @@ struct DiffLaunch {
   int32_t* out_count;
 };
 hipError_t launch_diff(const DiffLaunch& a, hipStream_t st);
+
+struct ExtractLaunch {
+  SegDesc seg;
+  const uint8_t* values;      // unaligned arena start (= seg.base + seg.shift)
+  uint32_t P, B;
+  const int32_t* ids;         // [P * ids_stride] bucket ids (e.g. diff output)
+  uint64_t ids_stride;
+  const int32_t* counts;      // [P] ids per partition (< 0: nothing)
+  uint64_t* part_off;         // [P+1] record offsets into out_rec
+  uint64_t* out_rec;          // [rec_cap]
+  uint64_t rec_cap;
+  uint8_t* out_values;        // [bytes_cap] (may be null)
+  uint64_t* out_value_off;    // [rec_cap + 1] (may be null)
+  uint64_t bytes_cap;
+  int32_t* status;            // MDE_OK or MDE_E_CAPACITY
+  uint64_t* scratch;          // [3 * (P + 1)] device scratch
+};
+constexpr uint32_t kExtractMaxBuckets = 1u << 16;
+hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st);
 
 hipError_t launch_tag_keys(const uint8_t* keys, const uint64_t* key_off, uint64_t n, uint32_t B,
                            uint32_t P, uint32_t* bucket, uint32_t* partition, hipStream_t st);

@@ -498,3 +498,28 @@ def layout_a(parts: np.ndarray, bks: np.ndarray, n_partitions: int, n_buckets: i
     seg_rec = np.zeros(n_partitions * n_buckets + 1, dtype=np.uint64)
     np.cumsum(counts, out=seg_rec[1:])
     return order, seg_rec
+
+
+# ---------------------------------------------------------------------------------------------
+# Out-of-sync range extract: StreamBucketsTask (main/manager.go:445-487) over the de-duplicated
+# diff set (utils.Int32Set, main/manager.go:1073,1086,1114), array form
+# ---------------------------------------------------------------------------------------------
+def extract_from_arena(values, value_off, seg_rec, n_partitions, n_buckets, ids, ids_stride, counts):
+    """Per partition: records of the requested buckets, duplicates removed, ascending bucket
+    order (the reference's order is Go map order, i.e. unspecified), LSM record order within a
+    bucket. Returns (part_off, rec_idx, value_bytes, value_off_out)."""
+    part_off, recs, chunks, voff = [0], [], [], [0]
+    for p in range(n_partitions):
+        c = int(counts[p])
+        row = ids[p * ids_stride:p * ids_stride + max(c, 0)]
+        for b in sorted({int(x) for x in row if 0 <= int(x) < n_buckets}):
+            s = p * n_buckets + b
+            for r in range(int(seg_rec[s]), int(seg_rec[s + 1])):
+                recs.append(r)
+                v = values[int(value_off[r]):int(value_off[r + 1])]
+                chunks.append(v)
+                voff.append(voff[-1] + len(v))
+        part_off.append(len(recs))
+    vb = np.concatenate(chunks) if chunks else np.zeros(0, np.uint8)
+    return (np.asarray(part_off, np.uint64), np.asarray(recs, np.uint64), vb.astype(np.uint8),
+            np.asarray(voff, np.uint64))

@@ -285,3 +285,63 @@ def test_full_size_properties(engine):
     ids = w.diff(out1, out3)
     for p in range(P):
         assert ids[p] == ([touched[p]] if p in touched else []), p
+
+
+def _extract_case(engine, values, voff, stride, seg, P, B, ids, stride_ids, counts):
+    vo = voff if voff is not None else np.arange(len(values) // stride + 1, dtype=np.uint64) * np.uint64(stride)
+    exp = O.extract_from_arena(values, vo, seg, P, B, ids, stride_ids, counts)
+    got = engine.extract(values, seg, P, B, ids, stride_ids, counts, stride, voff)
+    for g, e, name in zip(got, exp, ("part_off", "rec", "values", "value_off")):
+        assert np.array_equal(np.asarray(g), e), name
+
+
+def test_extract_matches_oracle(engine, golden, coracle):
+    """Range extract over random (duplicated, unordered, out-of-range) bucket lists."""
+    rng = np.random.default_rng(21)
+    for case in golden("synth_cases.json"):
+        P, B = case["P"], case["B"]
+        if B > 65536:
+            continue
+        values, voff, stride, seg = synth_arrays(case, coracle)
+        cap = 8
+        ids = rng.integers(-2, B + 2, P * cap).astype(np.int32)
+        counts = rng.integers(-1, cap + 1, P).astype(np.int32)
+        _extract_case(engine, values, voff, stride, seg, P, B, ids, cap, counts)
+        # every bucket requested (StreamBuckets with an empty list = all buckets)
+        ids = np.tile(np.arange(B, dtype=np.int32), P)
+        _extract_case(engine, values, voff, stride, seg, P, B, ids, B, np.full(P, B, np.int32))
+
+
+def test_extract_streambuckets_scenario(engine, golden):
+    """TestStreamBucketsTask-style (main/manager_test.go:117-211): the diff set of t1 vs t3 of the
+    TestMerkleTreeRaw scenario streams exactly the records the reference's range scans yield,
+    and their LE64 values decode to the written timestamps."""
+    fix = golden("testmerkletreeraw_n100.json")
+    B = fix["n_buckets"]
+    vals, seg = mtr_arena(fix, 0, 3)
+    diff = fix["diffs"]["t1_t3"]
+    part_off, rec, vbytes, voff = engine.extract(vals, seg, 1, B, np.array(diff, np.int32), len(diff),
+                                                 np.array([len(diff)], np.int32), 8)
+    want = sorted((fix["bucket_of"][k], f"{e:010d}", k, ts) for k, e, ts in fix["writes"]
+                  if fix["bucket_of"][k] in set(diff))
+    assert int(part_off[-1]) == len(want)
+    assert vbytes.view("<i8").tolist() == [w[3] for w in want]
+    # all buckets, epochs [0,3): 2N records (main/manager_test.go:210)
+    pa, _, _, _ = engine.extract(vals, seg, 1, B, np.arange(B, dtype=np.int32), B,
+                                 np.array([B], np.int32), 8, want_values=False)
+    assert int(pa[-1]) == 2 * fix["n"]
+
+
+def test_extract_capacity_error(engine):
+    import ctypes as C
+    import mydatastore_amd as mde
+    vals = np.arange(64 * 4, dtype=np.uint8)
+    seg = np.array([0, 2, 4], np.uint64)
+    rec = mde.Records(vals.ctypes.data, vals.nbytes, 64, 0, 0, 4, 1, 2, seg.ctypes.data)
+    ids = np.array([0, 1], np.int32)
+    cnt = np.array([2], np.int32)
+    po = np.zeros(2, np.uint64)
+    out = np.zeros(2, np.uint64)
+    rc = engine.lib.mde_extract(engine.ctx, C.byref(rec), ids.ctypes.data, 2, cnt.ctypes.data,
+                                po.ctypes.data, out.ctypes.data, 2, None, None, 0)
+    assert rc == mde.MDE_E_CAPACITY and int(po[-1]) == 4
