@@ -6,7 +6,9 @@
 
 A step = one RawPartitionMerkleTree build of every partition this rank holds (bucket digest
 kernel + digest/tree kernel), plus -- for N > 1 -- the RCCL all-gather of the per-partition roots
-(the one exchange step of the path). Default workload = BASELINE config 4: 10M keys x 1 KiB values
+(the one exchange step of the path). --config c5 (BASELINE config 5): build replicas A and B,
+device DFS-order diff of every partition, out-of-sync range extract of B's differing buckets;
+value counts the bytes of both builds. Default workload = BASELINE config 4: 10M keys x 1 KiB values
 over 1024 partitions, partition p on GPU p % N (total work fixed: strong scaling). The output is
 one JSON line on rank 0 with `roofline` (digest kernel, HIP events on the launch stream) and
 `cpu_baseline` (the C restatement on the host cores, rank 0 at N = 1 only).
@@ -45,7 +47,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS) + ["c5"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no baseline)")
@@ -110,13 +112,33 @@ def pmc_traffic(config_name: str, local_bytes: int):
     return None
 
 
+def perturb_replica(torch, w, n_buckets):
+    """Replica B of SURVEY.md section 8d config 5: A with one record per partition changed -- the
+    first record of bucket (p*37) % 64 (global partition id p) gets its first value byte +1 mod
+    256, which always changes that bucket's digest. Returns {local partition: bucket}."""
+    vb = w.values.clone()
+    seg = w.seg_rec.cpu().numpy()
+    touched = {}
+    idx = []
+    for lp, gp in enumerate(w.partition_ids):
+        b = int(gp * 37) % n_buckets
+        r0, r1 = int(seg[lp * n_buckets + b]), int(seg[lp * n_buckets + b + 1])
+        if r1 > r0:
+            touched[lp] = b
+            idx.append(r0 * w.value_len)
+    if idx:
+        ii = torch.tensor(idx, dtype=torch.int64, device=vb.device)
+        vb[ii] = ((vb[ii].to(torch.int32) + 1) % 256).to(torch.uint8)
+    return vb, touched
+
+
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
     import mydatastore_amd as mde
     from mydatastore_amd.dist import RootGather
-    from mydatastore_amd.workload import make_workload
+    from mydatastore_amd.workload import Workload, make_workload
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -129,7 +151,8 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
 
-    cfg = CONFIGS[args.config]
+    c5 = args.config == "c5"
+    cfg = CONFIGS["c4" if c5 else args.config]
     n_keys, P, V, B, mode, desc = cfg
     eng = mde.Engine(local_rank)
     kpp = -(-n_keys // P)
@@ -137,12 +160,31 @@ def main():
                       keys_per_partition=kpp, n_keys=n_keys, rank=rank, world=world)
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
+    Pl = w.n_partitions
+
+    # Config 5: replica B, diff and extract buffers (both replicas of a partition on one GPU).
+    if c5:
+        desc = ("C5: C4 data as replica A + replica B with one bucket per partition perturbed; "
+                "build both, device DFS-order diff, out-of-sync range extract of B")
+        vb, touched = perturb_replica(torch, w, B)
+        wb = Workload(eng, vb, w.seg_rec, Pl, B, w.n_records, V, w.partition_ids)
+        cap = mde.diff_capacity(B, B)
+        diff_ids = torch.zeros(Pl * cap, dtype=torch.int32, device=dev)
+        diff_cnt = torch.zeros(Pl, dtype=torch.int32, device=dev)
+        rec_cap = max(w.n_records // 8, 1024)
+        bytes_cap = rec_cap * V
+        part_off = torch.zeros(Pl + 1, dtype=torch.int64, device=dev)
+        out_rec = torch.zeros(rec_cap, dtype=torch.int64, device=dev)
+        out_vals = torch.zeros(bytes_cap, dtype=torch.uint8, device=dev)
+        out_voff = torch.zeros(rec_cap + 1, dtype=torch.int64, device=dev)
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
 
     # Two output sets and two gather slabs: the RCCL root gather of build i runs on a side stream
     # and overlaps build i+1 (the exchange step overlapped with compute); a build's output set is
     # reused only after the gather that read it (two builds earlier) has completed.
     outs = [(w.out, w.tree_out), w._outs()]
-    gather = RootGather(P, world, dev) if world > 1 else None
+    outs_b = [(wb.out, wb.tree_out), wb._outs()] if c5 else None
+    gather = RootGather(P, world, dev, width=64 if c5 else 32) if world > 1 else None
     side = torch.cuda.Stream(dev) if world > 1 else None
     ev_built = [torch.cuda.Event() for _ in range(2)]
     ev_gathered = [torch.cuda.Event() for _ in range(2)]
@@ -160,21 +202,52 @@ def main():
         if ev_b is not None:
             ev_b.record(stream)
         w.tree_async(to)
+        roots = o["root"]
+        if c5:
+            ob, tob = outs_b[i]
+            wb.digest_async()
+            wb.tree_async(tob)
+            eng.diff_async(Pl, B, o["digest"], o["nodes"], B, ob["digest"], ob["nodes"], diff_ids, cap, diff_cnt)
+            eng.extract_async(wb.rec, diff_ids, cap, diff_cnt, part_off, out_rec, rec_cap, out_vals,
+                              out_voff, bytes_cap, status)
+            roots = torch.cat([o["root"], ob["root"]]) if world > 1 else None
         if world > 1:
             ev_built[i].record(stream)
             side.wait_event(ev_built[i])
             with torch.cuda.stream(side):
-                gather.gather(o["root"], i)
+                gather.gather(roots, i)
                 ev_gathered[i].record(side)
 
-    # parity gate on this rank's workload before timing: tree(digests) == device roots
+    # parity gate on this rank's workload before timing: tree(digests) == device roots; for C5 the
+    # diff of every partition is exactly its perturbed bucket and the extract returns exactly
+    # that bucket's records of replica B.
     step()
     torch.cuda.synchronize(dev)
     root_ref, _ = eng.tree_from_digests(w.out["digest"].cpu().numpy().view(np.uint64), B)
-    parity_ok = bool(np.array_equal(root_ref, w.out["root"].cpu().numpy()))
-    if world > 1:  # the gathered slab of this rank holds exactly its own roots
+    parity = {"tree_of_device_digests_equals_device_roots":
+              bool(np.array_equal(root_ref, w.out["root"].cpu().numpy()))}
+    if world > 1 and not c5:  # the gathered slab of this rank holds exactly its own roots
         allr = gather.assemble(0)
-        parity_ok &= bool(np.array_equal(allr[w.partition_ids].reshape(-1), w.out["root"].cpu().numpy()))
+        parity["gathered_roots_match"] = bool(np.array_equal(allr[w.partition_ids].reshape(-1),
+                                                             w.out["root"].cpu().numpy()))
+    if c5:
+        cnt = diff_cnt.cpu().numpy()
+        ids = diff_ids.cpu().numpy().reshape(Pl, cap)
+        ok = all((ids[p, :cnt[p]].tolist() == ([touched[p]] if p in touched else [])) for p in range(Pl))
+        seg = w.seg_rec.cpu().numpy()
+        want = sum(int(seg[p * B + b + 1] - seg[p * B + b]) for p, b in touched.items())
+        po = part_off.cpu().numpy()
+        ok_ex = int(status.item()) == 0 and int(po[-1]) == want
+        if ok_ex and want:  # extracted bytes == replica B's bytes of the extracted records
+            r = out_rec[:want].cpu().numpy()
+            samp = r[:: max(1, len(r) // 64)]
+            got = out_vals[:want * V].view(want, V).cpu().numpy()[:: max(1, len(r) // 64)]
+            src = vb.view(-1, V)[torch.from_numpy(samp).to(dev)].cpu().numpy()
+            ok_ex = bool(np.array_equal(got, src))
+        parity["c5_diff_is_exactly_the_perturbed_bucket"] = bool(ok)
+        parity["c5_extract_records_and_bytes"] = bool(ok_ex)
+        parity["c5_extracted_records_per_step"] = want
+    parity_ok = all(v for k, v in parity.items() if isinstance(v, bool))
 
     for _ in range(args.warmup):
         step()
@@ -192,18 +265,20 @@ def main():
     t1 = time.perf_counter()
     ms = (t1 - t0) * 1e3 / args.steps
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    hashed = w.value_bytes * (2 if c5 else 1)
     if world > 1:
         t = torch.tensor([ms, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms, kern_ms_max = float(t[0]), float(t[1])
-        tot = torch.tensor([w.value_bytes], dtype=torch.int64, device=dev)
+        ms = float(t[0])
+        tot = torch.tensor([hashed], dtype=torch.int64, device=dev)
         dist.all_reduce(tot)
         total_bytes = int(tot.item())
         ok = torch.tensor([int(parity_ok)], dtype=torch.int32, device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         parity_ok = bool(ok.item())
     else:
-        total_bytes = w.value_bytes
+        total_bytes = hashed
+    parity["all_ranks_ok"] = parity_ok
 
     if rank == 0:
         local_bytes = w.value_bytes
@@ -223,16 +298,16 @@ def main():
             "data": "synthetic (device-generated splitmix64 values, 'k%016x' keys, SHA-256 bucket tags)",
             "config": {"workload": desc, "n_keys": n_keys, "value_len": V, "n_partitions": P,
                        "n_buckets": B, "bytes_hashed_per_step": total_bytes,
-                       "partitions_per_gpu": w.n_partitions, "parallelism": f"partition-shard x{world}",
+                       "partitions_per_gpu": Pl, "parallelism": f"partition-shard x{world}",
                        "root_gather": ("rccl all_gather_into_tensor of ceil(P/N) x 32 B slabs on a side "
                                        "stream, overlapped with the next build") if world > 1 else None},
             "roofline": {"bound": "hbm", "kernel": "bucket_digest_kernel",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(args.config, local_bytes),
+                         "traffic": pmc_traffic("c4" if c5 else args.config, local_bytes),
                          "kernel_ms": round(kern_ms, 5),
                          "algorithmic_bytes_per_launch": local_bytes},
-            "parity": {"tree_of_device_digests_equals_device_roots": parity_ok},
+            "parity": parity,
         }
         if world == 1 and not args.no_cpu_baseline and not args.profile:
             result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_baseline_seconds)

@@ -40,12 +40,13 @@ class RootGather:
     """Fixed-size slab all-gather of per-partition 32-byte roots, double-buffered so a caller can
     keep the gather of build i in flight while build i+1 computes."""
 
-    def __init__(self, n_partitions: int, world: int, device, nbuf: int = 2):
+    def __init__(self, n_partitions: int, world: int, device, nbuf: int = 2, width: int = 32):
+        """width: bytes per partition (32 = one root; 64 = the roots of two replicas)."""
         import torch
-        self.P, self.world = n_partitions, world
+        self.P, self.world, self.width = n_partitions, world, width
         self.slab = -(-n_partitions // world)
-        self.send = [torch.zeros(self.slab * 32, dtype=torch.uint8, device=device) for _ in range(nbuf)]
-        self.recv = [torch.zeros(world * self.slab * 32, dtype=torch.uint8, device=device)
+        self.send = [torch.zeros(self.slab * width, dtype=torch.uint8, device=device) for _ in range(nbuf)]
+        self.recv = [torch.zeros(world * self.slab * width, dtype=torch.uint8, device=device)
                      for _ in range(nbuf)]
 
     def gather(self, roots, buf: int = 0):
@@ -61,10 +62,10 @@ class RootGather:
         return self.recv[buf]
 
     def assemble(self, buf: int = 0) -> np.ndarray:
-        """All roots in global partition order: [P, 32] uint8 (slot i of rank r = partition
+        """All roots in global partition order: [P, width] uint8 (slot i of rank r = partition
         r + i * world)."""
-        g = self.recv[buf].view(self.world, self.slab, 32).cpu().numpy()
-        out = np.zeros((self.P, 32), np.uint8)
+        g = self.recv[buf].view(self.world, self.slab, self.width).cpu().numpy()
+        out = np.zeros((self.P, self.width), np.uint8)
         for r in range(self.world):
             pids = local_partitions(self.P, r, self.world)
             out[pids] = g[r, :len(pids)]
