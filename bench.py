@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no baseline)")
+    ap.add_argument("--tuning", default="", help="digest kernel 'variant,workgroups_per_cu' (A/B only)")
     return ap.parse_args()
 
 
@@ -155,6 +156,8 @@ def main():
     cfg = CONFIGS["c4" if c5 else args.config]
     n_keys, P, V, B, mode, desc = cfg
     eng = mde.Engine(local_rank)
+    if args.tuning:
+        eng.set_tuning(*map(int, args.tuning.split(",")))
     kpp = -(-n_keys // P)
     w = make_workload(eng, n_partitions=P, n_buckets=B, value_len=V, part_mode=mode,
                       keys_per_partition=kpp, n_keys=n_keys, rank=rank, world=world)

@@ -28,7 +28,7 @@ HASH_MOD = 999999
 # Every symbol include/mde.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
     "mde_abi_version", "mde_strerror", "mde_create", "mde_destroy", "mde_last_error",
-    "mde_set_stream", "mde_use_own_stream", "mde_get_stream", "mde_synchronize", "mde_device_info", "mde_tree_depth",
+    "mde_set_stream", "mde_use_own_stream", "mde_set_tuning", "mde_get_stream", "mde_synchronize", "mde_device_info", "mde_tree_depth",
     "mde_tree_internal_nodes", "mde_diff_capacity", "mde_build", "mde_build_async",
     "mde_digest_async", "mde_tree_async", "mde_tree_from_digests", "mde_tree_from_digests_async",
     "mde_decode_bucket_hashes", "mde_diff", "mde_diff_async", "mde_diff_digests", "mde_tag_keys_async", "mde_tag_keys",
@@ -86,6 +86,7 @@ def load_library() -> C.CDLL:
         "mde_last_error": (C.c_char_p, [vp]),
         "mde_set_stream": (C.c_int, [vp, vp]),
         "mde_use_own_stream": (C.c_int, [vp]),
+        "mde_set_tuning": (C.c_int, [vp, C.c_int, C.c_int]),
         "mde_get_stream": (vp, [vp]),
         "mde_synchronize": (C.c_int, [vp]),
         "mde_device_info": (C.c_int, [vp, C.POINTER(C.c_int), C.c_char_p, C.c_int]),
@@ -188,6 +189,9 @@ class Engine:
     def set_stream(self, stream_handle: int):
         """Launch on a HIP stream handle (0 = the null stream = torch's default stream)."""
         self._check(self.lib.mde_set_stream(self.ctx, C.c_void_p(int(stream_handle))))
+
+    def set_tuning(self, digest_variant: int = -1, digest_blocks_per_cu: int = -1):
+        self._check(self.lib.mde_set_tuning(self.ctx, digest_variant, digest_blocks_per_cu))
 
     def use_own_stream(self):
         self._check(self.lib.mde_use_own_stream(self.ctx))

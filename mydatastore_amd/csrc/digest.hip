@@ -20,12 +20,12 @@
 #include "mde_device.hpp"
 #include "mde_internal.hpp"
 
+
 namespace mde {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kUnroll = 8;
-constexpr uint64_t kStepBytes = 64ull * 16ull * kUnroll;  // 8 KiB per wave step
+constexpr uint64_t kMaxStepBytes = 16ull * 1024ull;  // largest wave step over all variants
 
 // Largest s in [lo, S) with segpos(s) <= x (lo if none). 64-ary search: one vector load and one
 // ballot per round, log64(S) rounds. Must be called by all 64 lanes.
@@ -78,7 +78,26 @@ __device__ __forceinline__ void flush(unsigned long long* sums, uint32_t s, uint
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(sums + s, v);
 }
 
+template <int U, bool NT>
+__device__ __forceinline__ void load_step(u32x4 (&v)[U], const u32x4* src, uint64_t p, uint64_t end,
+                                          int lane, bool full) {
+  if (full) {
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = NT ? __builtin_nontemporal_load(src + u * 64) : src[u * 64];
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t x = p + (uint64_t)u * 1024u + (uint64_t)lane * 16u;
+      v[u] = x < end ? (NT ? __builtin_nontemporal_load(src + u * 64) : src[u * 64]) : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+}
+
+// U = 16-byte loads per lane per step (step = U KiB per wave); NT = nontemporal loads;
+// PIPE = issue the next step's loads before reducing the current one (register double buffer).
+template <int U, bool NT, bool PIPE>
 __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a) {
+  constexpr uint64_t kStep = 1024ull * U;
   const int lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
   if (wave >= a.n_waves) return;
@@ -94,35 +113,35 @@ __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a)
   uint32_t acc = 0;
   const u32x4* lane_base = reinterpret_cast<const u32x4*>(d.base) + lane;
 
-  for (uint64_t p = beg; p < end; p += kStepBytes) {
-    u32x4 v[kUnroll];
-    const bool full = p + kStepBytes <= end;
-    const u32x4* src = lane_base + (p >> 4);
-    if (full) {
+  u32x4 cur[U];
+  if (PIPE) load_step<U, NT>(cur, lane_base + (beg >> 4), beg, end, lane, beg + kStep <= end);
+  for (uint64_t p = beg; p < end; p += kStep) {
+    u32x4 v[U];
+    const bool full = p + kStep <= end;
+    if (PIPE) {
+      const uint64_t pn = p + kStep;
+      u32x4 nxt[U];
+      if (pn < end) load_step<U, NT>(nxt, lane_base + (pn >> 4), pn, end, lane, pn + kStep <= end);
 #pragma unroll
-      for (int u = 0; u < kUnroll; u++) v[u] = __builtin_nontemporal_load(src + u * 64);
+      for (int u = 0; u < U; u++) { v[u] = cur[u]; cur[u] = nxt[u]; }
     } else {
-#pragma unroll
-      for (int u = 0; u < kUnroll; u++) {
-        const uint64_t x = p + (uint64_t)u * 1024u + (uint64_t)lane * 16u;
-        v[u] = x < end ? __builtin_nontemporal_load(src + u * 64) : u32x4{0u, 0u, 0u, 0u};
-      }
+      load_step<U, NT>(v, lane_base + (p >> 4), p, end, lane, full);
     }
-    if (full && sb <= p && p + kStepBytes <= se) {
+    if (full && sb <= p && p + kStep <= se) {
 #pragma unroll
-      for (int u = 0; u < kUnroll; u++) {
+      for (int u = 0; u < U; u++) {
         acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
         acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
         acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
         acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
       }
     } else {
-      const uint64_t q = min(p + kStepBytes, end);
+      const uint64_t q = min(p + kStep, end);
       for (;;) {
         const uint64_t lo = max(sb, p), hi = min(se, q);
         if (lo < hi) {
 #pragma unroll
-          for (int u = 0; u < kUnroll; u++) {
+          for (int u = 0; u < U; u++) {
             const int64_t x = (int64_t)(p + (uint64_t)u * 1024u + (uint64_t)lane * 16u);
             acc = masked_sum16(v[u], (int64_t)lo - x, (int64_t)hi - x, acc);
           }
@@ -139,14 +158,34 @@ __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a)
   flush(a.sums, s, acc);
 }
 
+typedef void (*DigestKernel)(DigestLaunch);
+struct Variant {
+  DigestKernel fn;
+  int unroll;
+};
+
+// Kernel variants (tuning knob MDE_DIGEST_VARIANT = index; default 0).
+const Variant kVariants[] = {
+    {bucket_digest_kernel<8, true, false>, 8},  {bucket_digest_kernel<8, false, false>, 8},
+    {bucket_digest_kernel<16, true, false>, 16}, {bucket_digest_kernel<4, true, false>, 4},
+    {bucket_digest_kernel<4, true, true>, 4},   {bucket_digest_kernel<8, true, true>, 8},
+    {bucket_digest_kernel<16, false, false>, 16},
+};
+
+constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
+
+const Variant& variant(int v) { return kVariants[(v >= 0 && v < kNumVariants) ? v : 0]; }
+
 }  // namespace
 
-int bucket_digest_blocks_per_cu() {
+int bucket_digest_variants() { return kNumVariants; }
+
+int bucket_digest_blocks_per_cu(int v, int cap) {
   int blocks = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, bucket_digest_kernel, kThreads, 0) !=
-          hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, variant(v).fn, kThreads, 0) != hipSuccess ||
       blocks <= 0)
     blocks = 4;
+  if (cap > 0 && cap < blocks) blocks = cap;
   return blocks;
 }
 
@@ -157,8 +196,8 @@ void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, uint64_t* wa
   const uint64_t target_waves =
       (uint64_t)(cus > 0 ? cus : 256) * (uint64_t)(blocks_per_cu > 0 ? blocks_per_cu : 4) * (kThreads / 64);
   uint64_t wb = (bytes + target_waves - 1) / target_waves;
-  wb = (wb + kStepBytes - 1) / kStepBytes * kStepBytes;
-  if (wb < 2 * kStepBytes) wb = 2 * kStepBytes;
+  wb = (wb + kMaxStepBytes - 1) / kMaxStepBytes * kMaxStepBytes;
+  if (wb < 2 * kMaxStepBytes) wb = 2 * kMaxStepBytes;
   if (wb > (8ull << 20)) wb = 8ull << 20;  // keeps every u32 lane accumulator exact
   *wave_bytes = wb;
   *n_waves = (uint32_t)((bytes + 16 + wb - 1) / wb);
@@ -167,7 +206,7 @@ void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, uint64_t* wa
 hipError_t launch_bucket_digest(const DigestLaunch& a, hipStream_t st) {
   if (a.n_waves == 0) return hipSuccess;
   const uint32_t blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);
-  hipLaunchKernelGGL(bucket_digest_kernel, dim3(blocks), dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL(variant(a.variant).fn, dim3(blocks), dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 

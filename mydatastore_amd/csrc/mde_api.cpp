@@ -18,10 +18,16 @@
 
 #include "mde_internal.hpp"
 
+// Digest-kernel tuning defaults (tools/digest_sweep.sh, profiles/r01_digest_sweep.json).
+constexpr int kDefaultDigestVariant = 4;  // U=4 nontemporal, register-prefetched
+constexpr int kDefaultDigestCap = 2;      // 2 workgroups (8 waves) per CU
+
 struct mde_ctx {
   int device = 0;
   int cus = 256;
-  int digest_blocks_per_cu = 0;  // occupancy of the digest kernel (queried once)
+  int digest_blocks_per_cu = 0;  // resident workgroups per CU for the digest kernel (queried)
+  int digest_variant = kDefaultDigestVariant;
+  int digest_cap = kDefaultDigestCap;
   char arch[64] = {0};
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
@@ -163,7 +169,9 @@ int digest_async(mde_ctx* c, const mde_records* r) {
   mde::DigestLaunch a{};
   a.seg = seg_desc(r);
   a.sums = c->sums;
-  if (!c->digest_blocks_per_cu) c->digest_blocks_per_cu = mde::bucket_digest_blocks_per_cu();
+  if (!c->digest_blocks_per_cu)
+    c->digest_blocks_per_cu = mde::bucket_digest_blocks_per_cu(c->digest_variant, c->digest_cap);
+  a.variant = c->digest_variant;
   mde::plan_bucket_digest(r->values_bytes + a.seg.shift, c->cus, c->digest_blocks_per_cu,
                           &a.wave_bytes, &a.n_waves);
   MDE_HIP(c, mde::launch_bucket_digest(a, c->stream));
@@ -304,6 +312,17 @@ void mde_destroy(mde_ctx* c) {
 }
 
 const char* mde_last_error(mde_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int mde_set_tuning(mde_ctx* c, int digest_variant, int digest_blocks_per_cu) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (digest_variant >= mde::bucket_digest_variants())
+    return set_err(c, MDE_E_INVAL, "digest variant %d out of range", digest_variant);
+  c->digest_variant = digest_variant < 0 ? kDefaultDigestVariant : digest_variant;
+  c->digest_cap = digest_blocks_per_cu < 0 ? kDefaultDigestCap : digest_blocks_per_cu;
+  c->digest_blocks_per_cu = 0;  // re-query
+  return MDE_OK;
+}
 
 int mde_use_own_stream(mde_ctx* c) {
   if (!c) return MDE_E_INVAL;

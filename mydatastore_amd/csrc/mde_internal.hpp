@@ -34,14 +34,16 @@ __host__ __device__ __forceinline__ uint64_t recpos(const SegDesc& d, uint64_t r
 struct DigestLaunch {
   SegDesc seg;
   unsigned long long* sums;   // [S] u64 accumulators (zero on entry)
-  uint64_t wave_bytes;        // contiguous bytes per wave (multiple of the 8 KiB block)
+  uint64_t wave_bytes;        // contiguous bytes per wave (multiple of the 16 KiB max step)
   uint32_t n_waves;
+  int variant;                // kernel variant (unroll / load policy), see digest.hip
 };
 hipError_t launch_bucket_digest(const DigestLaunch& a, hipStream_t st);
 // Waves and wave range for an arena of `bytes` on a device with `cus` CUs.
 void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, uint64_t* wave_bytes,
                         uint32_t* n_waves);
-int bucket_digest_blocks_per_cu();
+int bucket_digest_blocks_per_cu(int variant, int cap);
+int bucket_digest_variants();
 
 struct TreeLaunch {
   uint32_t P, B;

@@ -41,10 +41,10 @@ def bench_tree(eng):
     return res
 
 
-def bench_digest(eng):
+def bench_digest(eng, worlds=(8, 4, 2, 1)):
     from mydatastore_amd.workload import make_workload
     res = []
-    for world in (8, 4, 2, 1):
+    for world in worlds:
         w = make_workload(eng, n_partitions=1024, n_buckets=64, value_len=1024, part_mode="mod",
                           n_keys=10_000_000, rank=0, world=world)
         us = timeit(w.digest_async)
@@ -54,6 +54,32 @@ def bench_digest(eng):
                     "GBps": round(w.value_bytes / us / 1e3, 1), "tree_us": round(ust, 2),
                     "build_us": round(usb, 2)})
         print(json.dumps(res[-1]), flush=True)
+        del w
+    return res
+
+
+def bench_sweep(eng, worlds=(1, 8), reps=3):
+    """Interleaved A/B of digest variants x workgroups-per-CU in one process (same data, same
+    clocks): median digest time per setting."""
+    from mydatastore_amd.workload import make_workload
+    settings = [(v, c) for v in range(7) for c in (0, 2, 3, 4)]
+    res = []
+    for world in worlds:
+        w = make_workload(eng, n_partitions=1024, n_buckets=64, value_len=1024, part_mode="mod",
+                          n_keys=10_000_000, rank=0, world=world)
+        times = {s: [] for s in settings}
+        for _ in range(reps):
+            for v, c in settings:
+                eng.set_tuning(v, c)
+                times[(v, c)].append(timeit(w.digest_async, reps=10, warm=2))
+        eng.set_tuning(-1, -1)
+        for (v, c), t in times.items():
+            med = float(np.median(t))
+            res.append({"world": world, "variant": v, "cap": c, "digest_us": round(med, 2),
+                        "GBps": round(w.value_bytes / med / 1e3, 1)})
+        best = sorted([r for r in res if r["world"] == world], key=lambda r: r["digest_us"])[:6]
+        for r in best:
+            print(json.dumps(r), flush=True)
         del w
     return res
 
@@ -69,6 +95,11 @@ def main():
         out["tree"] = bench_tree(eng)
     if "digest" in what:
         out["digest"] = bench_digest(eng)
+    if "sweep" in what:
+        out["sweep"] = bench_sweep(eng)
+    for w in what:
+        if w.startswith("digest:"):
+            out["digest"] = bench_digest(eng, [int(x) for x in w.split(":")[1].split(",")])
     Path("gpurun_out").mkdir(exist_ok=True)
     Path("gpurun_out/microbench.json").write_text(json.dumps(out, indent=1))
 
