@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no baseline)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
     ap.add_argument("--tuning", default="", help="digest kernel 'variant,workgroups_per_cu' (A/B only)")
     return ap.parse_args()
 
@@ -111,6 +112,36 @@ def pmc_traffic(config_name: str, local_bytes: int):
     except Exception:
         return None
     return None
+
+
+def end_to_end(torch, eng, w, B, reps=3):
+    """Host-resident records -> device -> Merkle build -> host results, PCIe included
+    (mde_build_streamed from a pinned host arena; mde_build for comparison). Reported beside
+    `value`, never as it."""
+    host = torch.empty(w.values.numel(), dtype=torch.uint8, pin_memory=True)
+    host.copy_(w.values)
+    seg = w.seg_rec.cpu().numpy().view(np.uint64)
+    P = w.n_partitions
+    res = {}
+    for name, fn in (("streamed_pinned", lambda: eng.build_streamed(host, seg, P, B, w.value_len, want_nodes=False)),):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = fn()
+        dt = (time.perf_counter() - t0) / reps
+        res[name] = {"GiB_per_s": round(w.value_bytes / 2**30 / dt, 3), "s_per_build": round(dt, 4)}
+    ok = bool(np.array_equal(out["root"], w.out["root"].cpu().numpy()))
+    t0 = time.perf_counter()
+    torch.cuda.synchronize()
+    h2d = torch.empty_like(w.values)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        h2d.copy_(host, non_blocking=True)
+    torch.cuda.synchronize()
+    res["h2d_copy_only_GiB_per_s"] = round(w.value_bytes * reps / 2**30 / (time.perf_counter() - t0), 3)
+    res["roots_match_device_build"] = ok
+    res["note"] = "pinned host arena -> 2-slot device ring (256 MiB chunks, copy/compute overlap) -> digests+roots D2H"
+    return res
 
 
 def perturb_replica(torch, w, n_buckets):
@@ -316,6 +347,8 @@ def main():
             result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_baseline_seconds)
         else:
             result["cpu_baseline"] = None
+        if world == 1 and not args.no_e2e and not args.profile and not c5:
+            result["end_to_end"] = end_to_end(torch, eng, w, B)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

@@ -104,6 +104,13 @@ uint64_t mde_diff_capacity(uint32_t n_buckets_a, uint32_t n_buckets_b); /* max i
 int mde_build(mde_ctx* ctx, const mde_records* rec, const mde_tree_out* out);
 /* Same, device pointers, enqueued on the context stream (inputs resident in HBM). */
 int mde_build_async(mde_ctx* ctx, const mde_records* rec, const mde_tree_out* out);
+/* Host ingest path: same contract as mde_build, but the arena is
+ * streamed to the device in chunks of whole partitions (about chunk_bytes each; 0 = 256 MiB)
+ * through a two-slot device ring -- the copy of chunk k+1 overlaps the build of chunk k on a
+ * second stream -- so device memory stays bounded and arenas larger than HBM work. Pass pinned
+ * host memory (hipHostMalloc / hipHostRegister) for the copies to be asynchronous. */
+int mde_build_streamed(mde_ctx* ctx, const mde_records* rec, const mde_tree_out* out,
+                       uint64_t chunk_bytes);
 /* The two stages of mde_build_async, for stage timing: bucket byte-sum kernel, then the
  * digest/size/tree kernel. mde_build_async == mde_digest_async + mde_tree_async. */
 int mde_digest_async(mde_ctx* ctx, const mde_records* rec);

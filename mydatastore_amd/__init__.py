@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "mde_abi_version", "mde_strerror", "mde_create", "mde_destroy", "mde_last_error",
     "mde_set_stream", "mde_use_own_stream", "mde_set_tuning", "mde_get_stream", "mde_synchronize", "mde_device_info", "mde_tree_depth",
     "mde_tree_internal_nodes", "mde_diff_capacity", "mde_build", "mde_build_async",
+    "mde_build_streamed",
     "mde_digest_async", "mde_tree_async", "mde_tree_from_digests", "mde_tree_from_digests_async",
     "mde_decode_bucket_hashes", "mde_diff", "mde_diff_async", "mde_diff_digests", "mde_tag_keys_async", "mde_tag_keys",
     "mde_extract", "mde_extract_async", "mde_synth_tags_async", "mde_synth_values_async", "mde_dev_alloc", "mde_dev_free",
@@ -95,6 +96,7 @@ def load_library() -> C.CDLL:
         "mde_diff_capacity": (u64, [u32, u32]),
         "mde_build": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
         "mde_build_async": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
+        "mde_build_streamed": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), u64]),
         "mde_digest_async": (C.c_int, [vp, C.POINTER(Records)]),
         "mde_tree_async": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
         "mde_tree_from_digests": (C.c_int, [vp, u32, u32, vp, vp, vp]),
@@ -235,6 +237,26 @@ class Engine:
         }
         to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
         self._check(self.lib.mde_build(self.ctx, C.byref(rec), C.byref(to)))
+        return out
+
+    def build_streamed(self, values, seg_rec, n_partitions, n_buckets, value_stride=0,
+                       value_off=None, chunk_bytes=0, want_nodes=True):
+        """mde_build_streamed: host arena streamed through a two-slot device ring. `values` may
+        be a numpy array or a (pinned) CPU torch tensor."""
+        P, B = n_partitions, n_buckets
+        seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
+        if value_off is not None:
+            value_off = np.ascontiguousarray(value_off, dtype=np.uint64)
+        nbytes = _nbytes(values)
+        n_rec = (value_off.size - 1) if value_off is not None else (nbytes // value_stride if value_stride else 0)
+        rec = Records(_ptr(values), nbytes, value_stride, 0, _ptr(value_off), n_rec, P, B, _ptr(seg_rec))
+        out = {
+            "digest": np.zeros(P * B, np.uint64), "size": np.zeros(P * B, np.int32),
+            "items": np.zeros(P, np.int32), "root": np.zeros(P * 32, np.uint8),
+            "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
+        }
+        to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
+        self._check(self.lib.mde_build_streamed(self.ctx, C.byref(rec), C.byref(to), chunk_bytes))
         return out
 
     def build_async(self, rec: Records, out: TreeOut):

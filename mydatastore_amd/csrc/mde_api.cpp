@@ -11,10 +11,12 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "mde_internal.hpp"
 
@@ -42,6 +44,10 @@ struct mde_ctx {
   Buf stage[16];
   Buf nodes_scratch;
   Buf extract_scratch;
+  // Host-ingest ring (mde_build_streamed): two slots of values / value_off / seg_rec.
+  Buf ring_vals[2], ring_voff[2], ring_seg[2];
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t ev_loaded[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -178,6 +184,27 @@ int digest_async(mde_ctx* c, const mde_records* r) {
   return MDE_OK;
 }
 
+// Digest launch for a chunk whose values pointer is biased (mde_build_streamed): positions are
+// global byte offsets, `end` is the chunk's end position, and the arena range actually read is
+// [segpos(first bucket), end) -- inside the slot.
+int digest_async_biased(mde_ctx* c, const mde_records* r, uint64_t end_pos, uint64_t span) {
+  const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
+  int rc = ensure_sums(c, S);
+  if (rc) return rc;
+  if (S == 0 || r->n_records == 0) return MDE_OK;
+  mde::DigestLaunch a{};
+  a.seg = seg_desc(r);
+  a.seg.end = a.seg.shift + end_pos;
+  a.sums = c->sums;
+  if (!c->digest_blocks_per_cu)
+    c->digest_blocks_per_cu = mde::bucket_digest_blocks_per_cu(c->digest_variant, c->digest_cap);
+  a.variant = c->digest_variant;
+  // plan over the bytes this chunk actually covers (span is known on the host)
+  mde::plan_bucket_digest(span + 16, c->cus, c->digest_blocks_per_cu, &a.wave_bytes, &a.n_waves);
+  MDE_HIP(c, mde::launch_bucket_digest(a, c->stream));
+  return MDE_OK;
+}
+
 int tree_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
   const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
@@ -306,6 +333,13 @@ void mde_destroy(mde_ctx* c) {
       if (b.p) (void)hipFree(b.p);
     if (c->nodes_scratch.p) (void)hipFree(c->nodes_scratch.p);
     if (c->extract_scratch.p) (void)hipFree(c->extract_scratch.p);
+    for (int i = 0; i < 2; i++) {
+      for (auto* b : {&c->ring_vals[i], &c->ring_voff[i], &c->ring_seg[i]})
+        if (b->p) (void)hipFree(b->p);
+      if (c->ev_loaded[i]) (void)hipEventDestroy(c->ev_loaded[i]);
+      if (c->ev_done[i]) (void)hipEventDestroy(c->ev_done[i]);
+    }
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   }
   delete c;
@@ -419,6 +453,95 @@ int mde_build(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   if (o->items) MDE_HIP(c, hipMemcpyAsync(o->items, dout.items, P * 4, hipMemcpyDeviceToHost, c->stream));
   MDE_HIP(c, hipMemcpyAsync(o->root, dout.root, P * 32, hipMemcpyDeviceToHost, c->stream));
   if (o->nodes) MDE_HIP(c, hipMemcpyAsync(o->nodes, dout.nodes, P * NI * 32, hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  return MDE_OK;
+}
+
+int mde_build_streamed(mde_ctx* c, const mde_records* r, const mde_tree_out* o, uint64_t chunk_bytes) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  int rc = check_records(c, r);
+  if (rc) return rc;
+  if ((rc = check_host_records(c, r))) return rc;
+  if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
+  if (!chunk_bytes) chunk_bytes = 256ull << 20;
+  if (!c->copy_stream) {
+    MDE_HIP(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; i++) {
+      MDE_HIP(c, hipEventCreateWithFlags(&c->ev_loaded[i], hipEventDisableTiming));
+      MDE_HIP(c, hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming));
+    }
+  }
+  const uint32_t P = r->n_partitions, B = r->n_buckets;
+  const uint64_t NI = mde::tree_internal(B);
+  auto pos = [&](uint64_t rr) { return r->value_stride ? rr * r->value_stride : r->value_off[rr]; };
+  // Chunks of whole partitions, ~chunk_bytes each.
+  std::vector<uint32_t> cuts{0};
+  uint64_t max_bytes = 0, max_recs = 0, max_parts = 0;
+  for (uint32_t p = 0; p < P;) {
+    const uint64_t b0 = pos(r->seg_rec[(uint64_t)p * B]);
+    uint32_t q = p + 1;
+    while (q < P && pos(r->seg_rec[(uint64_t)(q + 1) * B]) - b0 <= chunk_bytes) q++;
+    cuts.push_back(q);
+    max_bytes = std::max(max_bytes, pos(r->seg_rec[(uint64_t)q * B]) - b0);
+    max_recs = std::max(max_recs, r->seg_rec[(uint64_t)q * B] - r->seg_rec[(uint64_t)p * B]);
+    max_parts = std::max<uint64_t>(max_parts, q - p);
+    p = q;
+  }
+  for (int i = 0; i < 2; i++) {
+    if ((rc = ensure_buf(c, c->ring_vals[i], max_bytes + 32))) return rc;
+    if ((rc = ensure_buf(c, c->ring_seg[i], (max_parts * B + 1) * 8))) return rc;
+    if (!r->value_stride && (rc = ensure_buf(c, c->ring_voff[i], (max_recs + 1) * 8))) return rc;
+  }
+  // Device outputs for the whole build (host copies at the end).
+  const uint64_t S = (uint64_t)P * B;
+  const uint64_t osz[5] = {S * 8, S * 4, (uint64_t)P * 4, (uint64_t)P * 32, o->nodes ? P * NI * 32 : 0};
+  for (int i = 0; i < 5; i++)
+    if ((rc = ensure_buf(c, c->stage[11 + i], osz[i]))) return rc;
+  uint64_t* d_digest = static_cast<uint64_t*>(c->stage[11].p);
+  int32_t* d_size = static_cast<int32_t*>(c->stage[12].p);
+  int32_t* d_items = static_cast<int32_t*>(c->stage[13].p);
+  uint8_t* d_root = static_cast<uint8_t*>(c->stage[14].p);
+  uint8_t* d_nodes = o->nodes ? static_cast<uint8_t*>(c->stage[15].p) : nullptr;
+  MDE_HIP(c, hipEventRecord(c->ev_done[0], c->stream));
+  MDE_HIP(c, hipEventRecord(c->ev_done[1], c->stream));
+  for (size_t k = 0; k + 1 < cuts.size(); k++) {
+    const int slot = (int)(k & 1);
+    const uint32_t p0 = cuts[k], p1 = cuts[k + 1];
+    const uint64_t r0 = r->seg_rec[(uint64_t)p0 * B], r1 = r->seg_rec[(uint64_t)p1 * B];
+    const uint64_t byte0 = pos(r0), byte1 = pos(r1);
+    uint8_t* vslot = static_cast<uint8_t*>(c->ring_vals[slot].p);
+    // copy stream: wait until the build two chunks back released this slot, then load
+    MDE_HIP(c, hipStreamWaitEvent(c->copy_stream, c->ev_done[slot], 0));
+    if (byte1 > byte0)
+      MDE_HIP(c, hipMemcpyAsync(vslot + (byte0 & 15), r->values + byte0, byte1 - byte0,
+                                hipMemcpyHostToDevice, c->copy_stream));
+    MDE_HIP(c, hipMemcpyAsync(c->ring_seg[slot].p, r->seg_rec + (uint64_t)p0 * B,
+                              ((uint64_t)(p1 - p0) * B + 1) * 8, hipMemcpyHostToDevice, c->copy_stream));
+    if (!r->value_stride)
+      MDE_HIP(c, hipMemcpyAsync(c->ring_voff[slot].p, r->value_off + r0, (r1 - r0 + 1) * 8,
+                                hipMemcpyHostToDevice, c->copy_stream));
+    MDE_HIP(c, hipEventRecord(c->ev_loaded[slot], c->copy_stream));
+    // compute stream: build the chunk. Record indices stay global; the value and value_off
+    // pointers are biased so that global offsets land in the slot (never dereferenced outside).
+    MDE_HIP(c, hipStreamWaitEvent(c->stream, c->ev_loaded[slot], 0));
+    mde_records cr = *r;
+    cr.values = vslot - (byte0 & ~uint64_t(15));
+    cr.values_bytes = byte1 - (byte0 & ~uint64_t(15));
+    cr.value_off = r->value_stride ? nullptr : static_cast<const uint64_t*>(c->ring_voff[slot].p) - r0;
+    cr.n_partitions = p1 - p0;
+    cr.seg_rec = static_cast<const uint64_t*>(c->ring_seg[slot].p);
+    mde_tree_out co{d_digest + (uint64_t)p0 * B, d_size + (uint64_t)p0 * B, d_items + p0,
+                    d_root + (uint64_t)p0 * 32, d_nodes ? d_nodes + (uint64_t)p0 * NI * 32 : nullptr};
+    if (byte1 > byte0 && (rc = digest_async_biased(c, &cr, byte1, byte1 - byte0))) return rc;
+    if ((rc = tree_async(c, &cr, &co))) return rc;
+    MDE_HIP(c, hipEventRecord(c->ev_done[slot], c->stream));
+  }
+  if (o->digest) MDE_HIP(c, hipMemcpyAsync(o->digest, d_digest, S * 8, hipMemcpyDeviceToHost, c->stream));
+  if (o->size) MDE_HIP(c, hipMemcpyAsync(o->size, d_size, S * 4, hipMemcpyDeviceToHost, c->stream));
+  if (o->items) MDE_HIP(c, hipMemcpyAsync(o->items, d_items, (uint64_t)P * 4, hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(o->root, d_root, (uint64_t)P * 32, hipMemcpyDeviceToHost, c->stream));
+  if (o->nodes) MDE_HIP(c, hipMemcpyAsync(o->nodes, d_nodes, P * NI * 32, hipMemcpyDeviceToHost, c->stream));
   MDE_HIP(c, hipStreamSynchronize(c->stream));
   return MDE_OK;
 }
