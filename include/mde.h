@@ -70,7 +70,8 @@ typedef struct mde_records {
 typedef struct mde_tree_out {
   uint64_t* digest; /* [P*B] CustomHash value of each bucket, in [0, 999999) */
   int32_t* size;    /* [P*B] MerkleBucket.size (record count, int32) */
-  int32_t* items;   /* [P]   EpochTreeObject.items = sum of sizes (int32, wraps like Go) */
+  int32_t* items;   /* [P]   EpochTreeObject.items: sum of sizes over tree.Leafs -- the duplicate
+                       leaf of an odd B counts twice (main/merkle_tree.go:122-134); int32 wrap */
   uint8_t* root;    /* [P*32] tree.MerkleRoot() */
   uint8_t* nodes;   /* [P*mde_tree_internal_nodes(B)*32] internal node hashes, level 1 .. root */
 } mde_tree_out;
@@ -162,6 +163,37 @@ int mde_extract_async(mde_ctx* ctx, const mde_records* rec, const int32_t* ids, 
 int mde_extract(mde_ctx* ctx, const mde_records* rec, const int32_t* ids, uint64_t ids_stride,
                 const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
                 uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap);
+
+/* EpochTreeObject wire bytes (datap/data.proto:60-68), exactly as proto.Marshal emits them for
+ * MerkleTreeToPartitionEpochObject's object (main/merkle_tree.go:118-138, main/manager.go:1045):
+ * leaves follow tree.Leafs (an odd B repeats the last bucket), zero scalars omitted, sizes packed.
+ * Object i is written at out + i*out_stride (out_stride >= mde_epoch_tree_object_max_bytes(B)),
+ * its length in out_len[i]. partition/valid/items may be NULL (0 / false / the tree.Leafs sum). */
+uint64_t mde_epoch_tree_object_max_bytes(uint32_t n_buckets);
+int mde_encode_epoch_tree_objects_async(mde_ctx* ctx, uint32_t n, uint32_t n_buckets,
+                                        const int32_t* partition, int64_t lower_epoch,
+                                        int64_t upper_epoch, const uint64_t* digest,
+                                        const int32_t* size, const uint8_t* valid,
+                                        const int32_t* items, uint8_t* out, uint64_t out_stride,
+                                        uint32_t* out_len);
+int mde_encode_epoch_tree_objects(mde_ctx* ctx, uint32_t n, uint32_t n_buckets,
+                                  const int32_t* partition, int64_t lower_epoch, int64_t upper_epoch,
+                                  const uint64_t* digest, const int32_t* size, const uint8_t* valid,
+                                  const int32_t* items, uint8_t* out, uint64_t out_stride,
+                                  uint32_t* out_len);
+/* Decode n objects (object i = bytes[off[i] .. off[i+1])) into up to `cap` buckets each:
+ * n_buckets[i] = number of bucket hashes (the tree's leaf count for EpochTreeObjectToMerkleTree),
+ * or MDE_E_DECODE (malformed, or a bucket hash that is not 8 bytes) / MDE_E_CAPACITY. Missing
+ * sizes read as 0 (main/merkle_tree.go:147-152). Any output except n_buckets may be NULL. */
+int mde_decode_epoch_tree_objects_async(mde_ctx* ctx, uint32_t n, const uint8_t* bytes,
+                                        const uint64_t* off, uint32_t cap, int32_t* partition,
+                                        int64_t* lower_epoch, int64_t* upper_epoch,
+                                        uint64_t* digest, int32_t* size, uint8_t* valid,
+                                        int32_t* items, int32_t* n_buckets);
+int mde_decode_epoch_tree_objects(mde_ctx* ctx, uint32_t n, const uint8_t* bytes,
+                                  const uint64_t* off, uint32_t cap, int32_t* partition,
+                                  int64_t* lower_epoch, int64_t* upper_epoch, uint64_t* digest,
+                                  int32_t* size, uint8_t* valid, int32_t* items, int32_t* n_buckets);
 
 /* Write-time tagging of raw keys (device): bucket = BE64(SHA256(key)[:8]) % n_buckets
  * (main/manager.go:773-778), partition = XXH64(key, 0) % n_partitions (hashring.go:108-110).

@@ -33,7 +33,9 @@ EXPORTED_SYMBOLS = (
     "mde_build_streamed",
     "mde_digest_async", "mde_tree_async", "mde_tree_from_digests", "mde_tree_from_digests_async",
     "mde_decode_bucket_hashes", "mde_diff", "mde_diff_async", "mde_diff_digests", "mde_tag_keys_async", "mde_tag_keys",
-    "mde_extract", "mde_extract_async", "mde_synth_tags_async", "mde_synth_values_async", "mde_dev_alloc", "mde_dev_free",
+    "mde_extract", "mde_extract_async", "mde_epoch_tree_object_max_bytes",
+    "mde_encode_epoch_tree_objects", "mde_encode_epoch_tree_objects_async",
+    "mde_decode_epoch_tree_objects", "mde_decode_epoch_tree_objects_async", "mde_synth_tags_async", "mde_synth_values_async", "mde_dev_alloc", "mde_dev_free",
     "mde_memcpy_h2d", "mde_memcpy_d2h",
 )
 
@@ -109,6 +111,11 @@ def load_library() -> C.CDLL:
         "mde_tag_keys": (C.c_int, [vp, vp, vp, u64, u32, u32, vp, vp]),
         "mde_extract": (C.c_int, [vp, C.POINTER(Records), vp, u64, vp, vp, vp, u64, vp, vp, u64]),
         "mde_extract_async": (C.c_int, [vp, C.POINTER(Records), vp, u64, vp, vp, vp, u64, vp, vp, u64, vp]),
+        "mde_epoch_tree_object_max_bytes": (u64, [u32]),
+        "mde_encode_epoch_tree_objects": (C.c_int, [vp, u32, u32, vp, C.c_int64, C.c_int64, vp, vp, vp, vp, vp, u64, vp]),
+        "mde_encode_epoch_tree_objects_async": (C.c_int, [vp, u32, u32, vp, C.c_int64, C.c_int64, vp, vp, vp, vp, vp, u64, vp]),
+        "mde_decode_epoch_tree_objects": (C.c_int, [vp, u32, vp, vp, u32, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "mde_decode_epoch_tree_objects_async": (C.c_int, [vp, u32, vp, vp, u32, vp, vp, vp, vp, vp, vp, vp, vp]),
         "mde_synth_tags_async": (C.c_int, [vp, vp, u64, u32, u32, C.c_int, u64, vp, vp]),
         "mde_synth_values_async": (C.c_int, [vp, vp, vp, u64, u32, u64]),
         "mde_dev_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
@@ -348,6 +355,51 @@ class Engine:
                                                _ptr(counts), _ptr(part_off), _ptr(out_rec), rec_cap,
                                                _ptr(out_values), _ptr(out_value_off), bytes_cap,
                                                _ptr(status)))
+
+    # -- EpochTreeObject wire bytes -----------------------------------------------------------
+    def encode_objects(self, n_buckets, digest, size, partition=None, lower=0, upper=0, valid=None,
+                       items=None):
+        """proto.Marshal(EpochTreeObject) for each of the n trees: list of bytes objects."""
+        B = n_buckets
+        digest = np.ascontiguousarray(digest, dtype=np.uint64)
+        size = np.ascontiguousarray(size, dtype=np.int32)
+        n = digest.size // B
+        stride = int(self.lib.mde_epoch_tree_object_max_bytes(B))
+        out = np.zeros(n * stride, np.uint8)
+        ln = np.zeros(n, np.uint32)
+        part = None if partition is None else np.ascontiguousarray(partition, dtype=np.int32)
+        val = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
+        it = None if items is None else np.ascontiguousarray(items, dtype=np.int32)
+        self._check(self.lib.mde_encode_epoch_tree_objects(self.ctx, n, B, _ptr(part), lower, upper,
+                                                           _ptr(digest), _ptr(size), _ptr(val), _ptr(it),
+                                                           _ptr(out), stride, _ptr(ln)))
+        return [out[i * stride:i * stride + int(ln[i])].tobytes() for i in range(n)]
+
+    def decode_objects(self, objs, cap):
+        """Decode EpochTreeObject bytes: list of dicts (or an MDE_E_* code per object)."""
+        n = len(objs)
+        off = np.zeros(n + 1, np.uint64)
+        off[1:] = np.cumsum([len(o) for o in objs])
+        blob = np.frombuffer(b"".join(objs) or b"\0", dtype=np.uint8).copy()
+        o = {"partition": np.zeros(n, np.int32), "lower": np.zeros(n, np.int64),
+             "upper": np.zeros(n, np.int64), "digest": np.zeros(n * cap, np.uint64),
+             "size": np.zeros(n * cap, np.int32), "valid": np.zeros(n, np.uint8),
+             "items": np.zeros(n, np.int32), "n_buckets": np.zeros(n, np.int32)}
+        self._check(self.lib.mde_decode_epoch_tree_objects(
+            self.ctx, n, _ptr(blob), _ptr(off), cap, *(_ptr(o[k]) for k in (
+                "partition", "lower", "upper", "digest", "size", "valid", "items", "n_buckets"))))
+        res = []
+        for i in range(n):
+            nb = int(o["n_buckets"][i])
+            if nb < 0:
+                res.append(nb)
+                continue
+            res.append({"partition": int(o["partition"][i]), "lower": int(o["lower"][i]),
+                        "upper": int(o["upper"][i]), "valid": bool(o["valid"][i]),
+                        "items": int(o["items"][i]),
+                        "digest": o["digest"][i * cap:i * cap + nb].tolist(),
+                        "size": o["size"][i * cap:i * cap + nb].tolist()})
+        return res
 
     # -- tagging / synthetic workload ---------------------------------------------------------
     def tag_keys(self, keys, n_buckets: int, n_partitions: int):

@@ -744,6 +744,119 @@ int mde_extract(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t i
   return MDE_OK;
 }
 
+uint64_t mde_epoch_tree_object_max_bytes(uint32_t B) { return B ? mde::wire_max_bytes(B) : 0; }
+
+int mde_encode_epoch_tree_objects_async(mde_ctx* c, uint32_t n, uint32_t B, const int32_t* partition,
+                                        int64_t lower, int64_t upper, const uint64_t* digest,
+                                        const int32_t* size, const uint8_t* valid, const int32_t* items,
+                                        uint8_t* out, uint64_t out_stride, uint32_t* out_len) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (!B || !digest || !size || !out || !out_len) return set_err(c, MDE_E_INVAL, "bad encode arguments");
+  if (out_stride < mde::wire_max_bytes(B)) return set_err(c, MDE_E_CAPACITY, "out_stride too small");
+  mde::WireEncodeLaunch a{n, B, partition, lower, upper, digest, size, valid, items, out, out_stride, out_len};
+  MDE_HIP(c, mde::launch_wire_encode(a, c->stream));
+  return MDE_OK;
+}
+
+int mde_encode_epoch_tree_objects(mde_ctx* c, uint32_t n, uint32_t B, const int32_t* partition,
+                                  int64_t lower, int64_t upper, const uint64_t* digest, const int32_t* size,
+                                  const uint8_t* valid, const int32_t* items, uint8_t* out,
+                                  uint64_t out_stride, uint32_t* out_len) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (!B || !digest || !size || !out || !out_len) return set_err(c, MDE_E_INVAL, "bad encode arguments");
+  if (out_stride < mde::wire_max_bytes(B)) return set_err(c, MDE_E_CAPACITY, "out_stride too small");
+  const uint64_t N = n;
+  const uint64_t sz[7] = {N * 4, N * B * 8, N * B * 4, N, N * 4, N * out_stride, N * 4};
+  int rc;
+  for (int i = 0; i < 7; i++)
+    if ((rc = ensure_buf(c, c->stage[i], sz[i]))) return rc;
+  auto up = [&](int i, const void* src) -> int {
+    if (!src) return MDE_OK;
+    MDE_HIP(c, hipMemcpyAsync(c->stage[i].p, src, sz[i], hipMemcpyHostToDevice, c->stream));
+    return MDE_OK;
+  };
+  if ((rc = up(0, partition)) || (rc = up(1, digest)) || (rc = up(2, size)) || (rc = up(3, valid)) ||
+      (rc = up(4, items)))
+    return rc;
+  mde::WireEncodeLaunch a{n,
+                          B,
+                          partition ? static_cast<const int32_t*>(c->stage[0].p) : nullptr,
+                          lower,
+                          upper,
+                          static_cast<const uint64_t*>(c->stage[1].p),
+                          static_cast<const int32_t*>(c->stage[2].p),
+                          valid ? static_cast<const uint8_t*>(c->stage[3].p) : nullptr,
+                          items ? static_cast<const int32_t*>(c->stage[4].p) : nullptr,
+                          static_cast<uint8_t*>(c->stage[5].p),
+                          out_stride,
+                          static_cast<uint32_t*>(c->stage[6].p)};
+  MDE_HIP(c, mde::launch_wire_encode(a, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(out, c->stage[5].p, sz[5], hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(out_len, c->stage[6].p, sz[6], hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  return MDE_OK;
+}
+
+int mde_decode_epoch_tree_objects_async(mde_ctx* c, uint32_t n, const uint8_t* bytes, const uint64_t* off,
+                                        uint32_t cap, int32_t* partition, int64_t* lower, int64_t* upper,
+                                        uint64_t* digest, int32_t* size, uint8_t* valid, int32_t* items,
+                                        int32_t* n_buckets) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (!off || !digest || !size || !n_buckets || (n && !bytes))
+    return set_err(c, MDE_E_INVAL, "bad decode arguments");
+  mde::WireDecodeLaunch a{n, bytes, off, cap, partition, lower, upper, digest, size, valid, items, n_buckets};
+  MDE_HIP(c, mde::launch_wire_decode(a, c->stream));
+  return MDE_OK;
+}
+
+int mde_decode_epoch_tree_objects(mde_ctx* c, uint32_t n, const uint8_t* bytes, const uint64_t* off,
+                                  uint32_t cap, int32_t* partition, int64_t* lower, int64_t* upper,
+                                  uint64_t* digest, int32_t* size, uint8_t* valid, int32_t* items,
+                                  int32_t* n_buckets) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (!off || !digest || !size || !n_buckets || (n && !bytes))
+    return set_err(c, MDE_E_INVAL, "bad decode arguments");
+  for (uint32_t i = 0; i < n; i++)
+    if (off[i] > off[i + 1]) return set_err(c, MDE_E_INVAL, "off not nondecreasing");
+  const uint64_t N = n, nbytes = off[n] - off[0];
+  const uint64_t sz[11] = {nbytes + 1, (N + 1) * 8, N * 4, N * 8, N * 8, N * cap * 8, N * cap * 4, N, N * 4, N * 4, 0};
+  int rc;
+  for (int i = 0; i < 10; i++)
+    if ((rc = ensure_buf(c, c->stage[i], sz[i]))) return rc;
+  std::vector<uint64_t> rel(N + 1);
+  for (uint64_t i = 0; i <= N; i++) rel[i] = off[i] - off[0];
+  if (nbytes) MDE_HIP(c, hipMemcpyAsync(c->stage[0].p, bytes + off[0], nbytes, hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(c->stage[1].p, rel.data(), (N + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  auto dp = [&](int i) { return c->stage[i].p; };
+  mde::WireDecodeLaunch a{n,
+                          static_cast<const uint8_t*>(dp(0)),
+                          static_cast<const uint64_t*>(dp(1)),
+                          cap,
+                          static_cast<int32_t*>(dp(2)),
+                          static_cast<int64_t*>(dp(3)),
+                          static_cast<int64_t*>(dp(4)),
+                          static_cast<uint64_t*>(dp(5)),
+                          static_cast<int32_t*>(dp(6)),
+                          static_cast<uint8_t*>(dp(7)),
+                          static_cast<int32_t*>(dp(8)),
+                          static_cast<int32_t*>(dp(9))};
+  MDE_HIP(c, mde::launch_wire_decode(a, c->stream));
+  auto down = [&](void* dst, int i) -> int {
+    if (!dst) return MDE_OK;
+    MDE_HIP(c, hipMemcpyAsync(dst, dp(i), sz[i], hipMemcpyDeviceToHost, c->stream));
+    return MDE_OK;
+  };
+  if ((rc = down(partition, 2)) || (rc = down(lower, 3)) || (rc = down(upper, 4)) || (rc = down(digest, 5)) ||
+      (rc = down(size, 6)) || (rc = down(valid, 7)) || (rc = down(items, 8)) || (rc = down(n_buckets, 9)))
+    return rc;
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  return MDE_OK;
+}
+
 int mde_tag_keys_async(mde_ctx* c, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
                        uint32_t B, uint32_t P, uint32_t* bucket, uint32_t* partition) {
   if (!c) return MDE_E_INVAL;

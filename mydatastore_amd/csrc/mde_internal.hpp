@@ -93,6 +93,36 @@ struct ExtractLaunch {
 constexpr uint32_t kExtractMaxBuckets = 1u << 16;
 hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st);
 
+struct WireEncodeLaunch {
+  uint32_t n, B;
+  const int32_t* partition;  // [n] (may be null: 0)
+  int64_t lower, upper;
+  const uint64_t* digest;    // [n*B]
+  const int32_t* size;       // [n*B]
+  const uint8_t* valid;      // [n] (may be null: false)
+  const int32_t* items;      // [n] (may be null: sum over tree.Leafs)
+  uint8_t* out;              // [n*out_stride]
+  uint64_t out_stride;
+  uint32_t* out_len;         // [n]
+};
+struct WireDecodeLaunch {
+  uint32_t n;
+  const uint8_t* bytes;
+  const uint64_t* off;       // [n+1]
+  uint32_t cap;              // bucket capacity per object
+  int32_t* partition;
+  int64_t* lower;
+  int64_t* upper;
+  uint64_t* digest;          // [n*cap]
+  int32_t* size;             // [n*cap]
+  uint8_t* valid;
+  int32_t* items;
+  int32_t* n_buckets;        // [n] bucket count, or MDE_E_DECODE / MDE_E_CAPACITY
+};
+inline uint64_t wire_max_bytes(uint32_t B) { return 57 + 20ull * (B + (B & 1u)); }
+hipError_t launch_wire_encode(const WireEncodeLaunch& a, hipStream_t st);
+hipError_t launch_wire_decode(const WireDecodeLaunch& a, hipStream_t st);
+
 hipError_t launch_tag_keys(const uint8_t* keys, const uint64_t* key_off, uint64_t n, uint32_t B,
                            uint32_t P, uint32_t* bucket, uint32_t* partition, hipStream_t st);
 hipError_t launch_synth_tags(const uint64_t* gids, uint64_t n, uint32_t P, uint32_t B, int mode,

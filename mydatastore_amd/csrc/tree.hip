@@ -79,6 +79,8 @@ __global__ __launch_bounds__(256) void tree_kernel(TreeLaunch a, uint32_t G, uin
       const uint32_t bl = 2 * j, br = (2 * j + 1 < B) ? 2 * j + 1 : 2 * j;
       const uint64_t dl = leaf(a, s0 + bl, items);
       const uint64_t dr = (br != bl) ? leaf(a, s0 + br, items) : dl;
+      if (br == bl && a.seg_rec)  // odd B: the duplicate leaf's size counts again (tree.Leafs walk)
+        items += (uint32_t)(a.seg_rec[s0 + bl + 1] - a.seg_rec[s0 + bl]);
       uint32_t st[8];
       sha256_leaf_pair(dl, dr, st);
       store_node(buf0 + (uint64_t)j * 8, st);

@@ -207,6 +207,7 @@ static void digests_partition(const uint8_t* values, uint32_t stride, const uint
     digest[s] = (uint64_t)value;
     size[s] = sz;
     it += sz;
+    if (b == n_buckets - 1 && (n_buckets & 1)) it += sz;  /* tree.Leafs includes the dup leaf */
   }
   if (items) items[p] = it;
 }

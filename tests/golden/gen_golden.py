@@ -121,7 +121,9 @@ def synth_case(name, P, B, n, value_len, part_mode, var_len=False, seed=O.SYNTH_
         levels = O.tree_levels_from_digests(d)
         roots.append(_hex(levels[-1][0]))
         node_sha.append(hashlib.sha256(O.internal_nodes_blob(d)).hexdigest())
-        items.append(int(np.int64(size[p * B:(p + 1) * B].sum())))
+        # EpochTreeObject.items walks tree.Leafs: an odd B counts the duplicate leaf twice
+        leaf_sizes = [int(x) for x in size[p * B:(p + 1) * B]] + ([int(size[p * B + B - 1])] if B % 2 else [])
+        items.append(sum(leaf_sizes))
     # cross-check the array form against the object form (RawPartitionMerkleTree semantics)
     for p in range(min(P, 2)):
         bl = [O.MerkleBucket(b, O.CustomHash()) for b in range(B)]

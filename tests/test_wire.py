@@ -1,0 +1,106 @@
+"""EpochTreeObject wire bytes: device encoder/decoder (mydatastore_amd/csrc/wire.hip) against the
+official protobuf runtime (oracle/wire_pb.py)."""
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from oracle import wire_pb
+from tests.datasets import synth_arrays
+
+REF_PROTO = Path("/root/reference/datap/data.proto")
+
+
+def test_descriptor_matches_reference_schema():
+    if not REF_PROTO.exists():
+        pytest.skip("reference not mounted (GPU box)")
+    text = REF_PROTO.read_text()
+    body = re.search(r"message EpochTreeObject\s*\{(.*?)\}", text, re.S).group(1)
+    fields = re.findall(r"(repeated\s+)?(\w+)\s+(\w+)\s*=\s*(\d+)\s*;", body)
+    got = [(name, int(num), "TYPE_" + typ.upper(), bool(rep)) for rep, typ, name, num in fields]
+    assert got == wire_pb.FIELDS
+
+
+def test_oracle_roundtrip_testmerkletreeraw(golden):
+    fix = golden("testmerkletreeraw_n100.json")
+    tr = fix["trees"]["0_3"]
+    b = wire_pb.marshal(0, 0, 3, tr["digests"], tr["sizes"])
+    m = wire_pb.unmarshal(b)
+    assert [x.hex() for x in m.buckets] == tr["object_buckets"] and m.items == tr["items"]
+    assert b[:2] == bytes([0x18, 0x03])  # partition 0 and lower_epoch 0 omitted (proto3)
+
+
+@pytest.mark.gpu
+def test_encode_matches_protobuf(engine, golden, coracle):
+    rng = np.random.default_rng(31)
+    for case in golden("synth_cases.json"):
+        P, B = case["P"], case["B"]
+        dg = np.array(case["digest"], np.uint64)
+        sz = np.array(case["size"], np.int32)
+        parts = np.arange(P, dtype=np.int32) * 3 - 2       # includes 0 and a negative id
+        valid = (np.arange(P) % 2).astype(np.uint8)
+        got = engine.encode_objects(B, dg, sz, parts, 7, 8, valid)
+        for p in range(P):
+            want = wire_pb.marshal(int(parts[p]), 7, 8, case["digest"][p * B:(p + 1) * B],
+                                   case["size"][p * B:(p + 1) * B], bool(valid[p]))
+            assert got[p] == want, (case["name"], p)
+            assert wire_pb.unmarshal(got[p]).items == case["items"][p]
+    # extremes: negative sizes/items (10-byte varints), int64 epochs, B = 1
+    for B in (1, 2, 3, 64, 1000):
+        dg = rng.integers(0, 2**64 - 1, 2 * B, dtype=np.uint64)
+        sz = rng.integers(-2**31, 2**31 - 1, 2 * B, dtype=np.int64).astype(np.int32)
+        items = np.array([-7, 2**31 - 1], np.int32)
+        got = engine.encode_objects(B, dg, sz, np.array([-1, 2**31 - 1], np.int32), -(2**40), 2**62,
+                                    None, items)
+        for t in range(2):
+            want = wire_pb.marshal([-1, 2**31 - 1][t], -(2**40), 2**62, dg[t * B:(t + 1) * B].tolist(),
+                                   sz[t * B:(t + 1) * B].tolist(), False, int(items[t]))
+            assert got[t] == want, B
+
+
+@pytest.mark.gpu
+def test_decode_matches_protobuf(engine):
+    import mydatastore_amd as mde
+    rng = np.random.default_rng(32)
+    cls = wire_pb.epoch_tree_object_class()
+    objs, exp = [], []
+    for B in (1, 2, 5, 30, 64, 200):
+        d = rng.integers(0, 999999, B).tolist()
+        s = rng.integers(0, 500, B).tolist()
+        b = wire_pb.marshal(int(rng.integers(-3, 9)), 4, 5, d, s, bool(B % 2), None)
+        objs.append(b)
+        exp.append(wire_pb.unmarshal(b))
+    # sizes shorter than buckets (read as 0), unknown fields, fields out of order, unpacked sizes
+    m = cls(partition=9, buckets=[O.encode_int64_to_bytes(5)] * 4, buckets_size=[1, 2])
+    odd = m.SerializeToString() + bytes([0x48, 0x05, 0x52, 0x02, 0xAA, 0xBB])  # fields 9 and 10
+    odd = bytes([0x38, 0x07]) + odd + bytes([0x28, 0x0B])  # items first; an unpacked size element
+    objs.append(odd)
+    got = engine.decode_objects(objs, cap=256)
+    for g, e in zip(got[:-1], exp):
+        assert g["partition"] == e.partition and g["lower"] == e.lower_epoch and g["upper"] == e.upper_epoch
+        assert g["valid"] == e.valid and g["items"] == e.items
+        assert g["digest"] == [int.from_bytes(x, "little") for x in e.buckets]
+        assert g["size"] == list(e.buckets_size)
+    assert got[-1]["partition"] == 9 and got[-1]["items"] == 7
+    assert got[-1]["digest"] == [5] * 4 and got[-1]["size"] == [1, 2, 11, 0]
+    # a 7-byte bucket hash (DecodeBytesToInt64 error), truncation, capacity
+    bad = cls(buckets=[b"\0" * 7]).SerializeToString()
+    trunc = objs[3][:-3]
+    res = engine.decode_objects([bad, trunc], cap=256)
+    assert res[0] == mde.MDE_E_DECODE and res[1] == mde.MDE_E_DECODE
+    assert engine.decode_objects([objs[5]], cap=8)[0] == mde.MDE_E_CAPACITY
+
+
+@pytest.mark.gpu
+def test_wire_roundtrip_rebuilds_same_tree(engine, golden, coracle):
+    """Peer path: encode -> decode -> EpochTreeObjectToMerkleTree on device == original root."""
+    case = next(c for c in golden("synth_cases.json") if c["name"] == "b64_1k")
+    P, B = case["P"], case["B"]
+    objs = engine.encode_objects(B, np.array(case["digest"], np.uint64), np.array(case["size"], np.int32),
+                                 np.arange(P, dtype=np.int32), 1, 2)
+    dec = engine.decode_objects(objs, cap=B)
+    d = np.array([x for o in dec for x in o["digest"]], np.uint64)
+    roots, _ = engine.tree_from_digests(d, B)
+    assert [roots[32 * p:32 * p + 32].tobytes().hex() for p in range(P)] == case["root"]
