@@ -87,7 +87,7 @@ def test_decode_matches_protobuf(engine):
     assert got[-1]["digest"] == [5] * 4 and got[-1]["size"] == [1, 2, 11, 0]
     # a 7-byte bucket hash (DecodeBytesToInt64 error), truncation, capacity
     bad = cls(buckets=[b"\0" * 7]).SerializeToString()
-    trunc = objs[3][:-3]
+    trunc = objs[3][:-1]  # cuts the trailing items varint mid-field
     res = engine.decode_objects([bad, trunc], cap=256)
     assert res[0] == mde.MDE_E_DECODE and res[1] == mde.MDE_E_DECODE
     assert engine.decode_objects([objs[5]], cap=8)[0] == mde.MDE_E_CAPACITY
