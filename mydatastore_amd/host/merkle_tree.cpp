@@ -143,6 +143,63 @@ Error DifferentMerkleTreeBuckets(Engine& eng, const MerkleTree& t1, const Merkle
   return "";
 }
 
+Error MarshalEpochTreeObject(Engine& eng, const EpochTreeObject& obj, Bytes* out) {
+  const uint32_t L = (uint32_t)obj.Buckets.size();
+  if (L == 0) return "cannot marshal an object without buckets";  // no tree has zero leaves
+  std::vector<uint64_t> digest(L);
+  std::vector<int32_t> size(L, 0);
+  for (uint32_t i = 0; i < L; i++) {
+    int64_t v;
+    Error e = DecodeBytesToInt64(obj.Buckets[i], &v);
+    if (!e.empty()) return e;
+    digest[i] = (uint64_t)v;
+    if (i < obj.BucketsSize.size()) size[i] = obj.BucketsSize[i];
+  }
+  // The object holds tree.Leafs, whose count is always even (merkletree duplicates the last leaf
+  // of an odd B), so its L leaves are encoded as B = L buckets with no further duplicate.
+  const uint8_t valid = obj.Valid ? 1 : 0;
+  const int32_t part = obj.Partition, items = obj.Items;
+  const uint32_t B = L;
+  if (L % 2 == 1) return "EpochTreeObject with an odd leaf count cannot come from a merkletree";
+  const uint64_t stride = mde_epoch_tree_object_max_bytes(B);
+  Bytes buf(stride);
+  uint32_t len = 0;
+  int rc = mde_encode_epoch_tree_objects(eng.ctx(), 1, B, &part, obj.LowerEpoch, obj.UpperEpoch,
+                                         digest.data(), size.data(), &valid, &items, buf.data(),
+                                         stride, &len);
+  if (rc != MDE_OK) return eng.error(rc);
+  buf.resize(len);
+  *out = std::move(buf);
+  return "";
+}
+
+Error UnmarshalEpochTreeObject(Engine& eng, const Bytes& data, EpochTreeObject* out) {
+  const uint64_t off[2] = {0, data.size()};
+  const uint32_t cap = (uint32_t)(data.size() / 10 + 1);
+  std::vector<uint64_t> digest(cap);
+  std::vector<int32_t> size(cap);
+  int32_t part = 0, items = 0, nb = 0;
+  int64_t lo = 0, hi = 0;
+  uint8_t valid = 0;
+  const uint8_t dummy = 0;
+  int rc = mde_decode_epoch_tree_objects(eng.ctx(), 1, data.empty() ? &dummy : data.data(), off, cap,
+                                         &part, &lo, &hi, digest.data(), size.data(), &valid, &items, &nb);
+  if (rc != MDE_OK) return eng.error(rc);
+  if (nb < 0) return std::string("proto: cannot parse EpochTreeObject: ") + mde_strerror(nb);
+  EpochTreeObject o;
+  o.Partition = part;
+  o.LowerEpoch = lo;
+  o.UpperEpoch = hi;
+  o.Valid = valid != 0;
+  o.Items = items;
+  for (int32_t i = 0; i < nb; i++) {
+    o.Buckets.push_back(EncodeInt64ToBytes((int64_t)digest[i]));
+    o.BucketsSize.push_back(size[i]);
+  }
+  *out = std::move(o);
+  return "";
+}
+
 // ---------------------------------------------------------------- index keys
 Error Index::Build(std::string* out) const {
   std::string s;

@@ -118,6 +118,10 @@ struct EpochTreeObject {
   int32_t Items = 0;
 };
 
+// proto.Marshal / proto.Unmarshal of the object (main/manager.go:1045,1025), on the device.
+Error MarshalEpochTreeObject(Engine& eng, const EpochTreeObject& obj, Bytes* out);
+Error UnmarshalEpochTreeObject(Engine& eng, const Bytes& data, EpochTreeObject* out);
+
 Error MerkleTreeToPartitionEpochObject(const MerkleTree& tree, int partitionId, int64_t lowerEpoch,
                                        int64_t upperEpoch, EpochTreeObject* out);
 Error EpochTreeObjectToMerkleTree(Engine& eng, const EpochTreeObject& obj, MerkleTree* out);

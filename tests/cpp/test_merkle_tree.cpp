@@ -104,7 +104,16 @@ static void TestMerkleTreeRaw(Engine& eng, int writeValuesNum) {
   CHECK(!diff5.empty(), "there should be a diff");
   CHECK(diff3 == diff5, "diff vs the round-tripped tree equals diff vs the tree");
 
+  // proto.Marshal / Unmarshal round trip on the device (main/manager.go:1045, :1025)
+  Bytes wire1;
+  CHECK_OK(MarshalEpochTreeObject(eng, obj1, &wire1));
+  EpochTreeObject back;
+  CHECK_OK(UnmarshalEpochTreeObject(eng, wire1, &back));
+  CHECK(back.Buckets == obj1.Buckets && back.BucketsSize == obj1.BucketsSize && back.Items == obj1.Items &&
+            back.LowerEpoch == 0 && back.UpperEpoch == 3 && !back.Valid, "wire round trip");
+
   const std::string n = std::to_string(writeValuesNum);
+  std::printf("WIRE n%s_0_3 %s\n", n.c_str(), hex(wire1).c_str());
   std::printf("ROOT n%s_0_3 %s\nROOT n%s_1_3 %s\nROOT n%s_2_3 %s\nDIFF n%s_t1_t3 %s\nITEMS n%s_0_3 %d\n",
               n.c_str(), hex(tree1.MerkleRoot()).c_str(), n.c_str(), hex(tree2.MerkleRoot()).c_str(),
               n.c_str(), hex(tree3.MerkleRoot()).c_str(), n.c_str(), ids(diff3).c_str(), n.c_str(),

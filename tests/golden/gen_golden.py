@@ -19,6 +19,7 @@ import numpy as np
 HERE = Path(__file__).resolve().parent
 sys.path.insert(0, str(HERE.parents[1]))
 from oracle import oracle as O  # noqa: E402
+from oracle import wire_pb  # noqa: E402
 
 
 def _hex(b: bytes) -> str:
@@ -49,6 +50,11 @@ def testmerkletreeraw(n: int, n_buckets: int = 30) -> dict:
             "root": _hex(t.merkle_root()),
             "nodes": _hex(O.internal_nodes_blob([leaf.c.hasher.hash() for leaf in t.leafs[:n_buckets]])),
             "object_buckets": [_hex(b) for b in obj.buckets],
+            # proto.Marshal(obj) (main/manager.go:1045) via the protobuf runtime
+            "wire": _hex(wire_pb.epoch_tree_object_class()(
+                partition=obj.partition, lower_epoch=obj.lower_epoch, upper_epoch=obj.upper_epoch,
+                buckets=obj.buckets, buckets_size=obj.buckets_size, valid=obj.valid,
+                items=obj.items).SerializeToString()),
         }
     t1, t2, t3 = (m.raw_partition_merkle_tree(0, lo, 3) for lo in (0, 1, 2))
     st1 = O.epoch_tree_object_to_merkle_tree(O.merkle_tree_to_partition_epoch_object(t1, 0, 0, 3))
