@@ -50,13 +50,16 @@ class RootGather:
                      for _ in range(nbuf)]
 
     def gather(self, roots, buf: int = 0):
-        """roots: this rank's [n_local * 32] uint8 tensor. Enqueued on the current stream."""
+        """roots: this rank's [n_local * width] uint8 tensor. Enqueued on the current stream."""
+        import torch
         import torch.distributed as dist
         n = roots.numel()
         self.send[buf][:n].copy_(roots, non_blocking=True)
-        if dist.get_backend() == "gloo":
-            parts = list(self.recv[buf].view(self.world, -1).unbind(0))
-            dist.all_gather(parts, self.send[buf])
+        if dist.get_backend() == "gloo":  # CPU tests / single-GPU rehearsal: stage through host
+            send = self.send[buf].cpu()
+            parts = [t.cpu() for t in self.recv[buf].view(self.world, -1).unbind(0)]
+            dist.all_gather(parts, send)
+            self.recv[buf].copy_(torch.cat(parts))
         else:
             dist.all_gather_into_tensor(self.recv[buf], self.send[buf])
         return self.recv[buf]
