@@ -54,6 +54,11 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 logic on one GPU: ranks share cuda:0, gloo gather (not a measurement)")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="build only rank 0's shard of an N-GPU run on this GPU (no process group); "
+                         "a per-GPU prediction, reported as such, never the N-GPU value")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="run each build's tree kernel on the main stream (no overlap with the next build)")
     ap.add_argument("--tuning", default="", help="digest kernel 'variant,workgroups_per_cu' (A/B only)")
     return ap.parse_args()
 
@@ -197,11 +202,27 @@ def main():
     if args.tuning:
         eng.set_tuning(*map(int, args.tuning.split(",")))
     kpp = -(-n_keys // P)
+    shard_world = args.simulate_world if (args.simulate_world and world == 1) else world
     w = make_workload(eng, n_partitions=P, n_buckets=B, value_len=V, part_mode=mode,
-                      keys_per_partition=kpp, n_keys=n_keys, rank=rank, world=world)
+                      keys_per_partition=kpp, n_keys=n_keys, rank=rank, world=shard_world)
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
     Pl = w.n_partitions
+    # Build pipelining: two engine contexts (each with its own byte-sum scratch) alternate
+    # builds. A build's digest kernel runs on the main stream, its tree kernel on `tstream`, so
+    # build i's latency-bound tree (11 dependent SHA-256 compressions) overlaps build i+1's HBM
+    # streaming instead of serializing behind it. Every build still runs both kernels in full.
+    pipeline = not args.no_pipeline and not c5
+    engines = [eng]
+    tstream = None
+    if pipeline:
+        e2 = mde.Engine(local_rank)
+        if args.tuning:
+            e2.set_tuning(*map(int, args.tuning.split(",")))
+        engines.append(e2)
+        tstream = torch.cuda.Stream(dev)
+    ev_digested = [torch.cuda.Event() for _ in range(2)]
+    ev_treed = [torch.cuda.Event() for _ in range(2)]
 
     # Config 5: replica B, diff and extract buffers (both replicas of a partition on one GPU).
     if c5:
@@ -235,14 +256,33 @@ def main():
         i = n_step[0] % 2
         n_step[0] += 1
         o, to = outs[i]
-        if world > 1:
+        if world > 1 and not pipeline:
             stream.wait_event(ev_gathered[i])
-        if ev_a is not None:
-            ev_a.record(stream)
-        w.digest_async()
-        if ev_b is not None:
-            ev_b.record(stream)
-        w.tree_async(to)
+        if pipeline:
+            e = engines[i]
+            stream.wait_event(ev_treed[i])          # this context's sums are free again
+            e.set_stream(stream.cuda_stream)
+            if ev_a is not None:
+                ev_a.record(stream)
+            e.digest_async(w.rec)
+            if ev_b is not None:
+                ev_b.record(stream)
+            ev_digested[i].record(stream)
+            tstream.wait_event(ev_digested[i])
+            if world > 1:
+                tstream.wait_event(ev_gathered[i])  # output set i no longer read by its gather
+            e.set_stream(tstream.cuda_stream)
+            e.tree_async(w.rec, to)
+            ev_treed[i].record(tstream)
+            build_stream = tstream
+        else:
+            if ev_a is not None:
+                ev_a.record(stream)
+            w.digest_async()
+            if ev_b is not None:
+                ev_b.record(stream)
+            w.tree_async(to)
+            build_stream = stream
         roots = o["root"]
         if c5:
             ob, tob = outs_b[i]
@@ -253,17 +293,24 @@ def main():
                               out_voff, bytes_cap, status)
             roots = torch.cat([o["root"], ob["root"]]) if world > 1 else None
         if world > 1:
-            ev_built[i].record(stream)
+            ev_built[i].record(build_stream)
             side.wait_event(ev_built[i])
             with torch.cuda.stream(side):
                 gather.gather(roots, i)
                 ev_gathered[i].record(side)
 
+    def join():  # everything issued so far, on the main stream
+        if pipeline:
+            stream.wait_event(ev_treed[0])
+            stream.wait_event(ev_treed[1])
+
     # parity gate on this rank's workload before timing: tree(digests) == device roots; for C5 the
     # diff of every partition is exactly its perturbed bucket and the extract returns exactly
     # that bucket's records of replica B.
     step()
+    join()
     torch.cuda.synchronize(dev)
+    eng.set_stream(stream.cuda_stream)
     root_ref, _ = eng.tree_from_digests(w.out["digest"].cpu().numpy().view(np.uint64), B)
     parity = {"tree_of_device_digests_equals_device_roots":
               bool(np.array_equal(root_ref, w.out["root"].cpu().numpy()))}
@@ -304,6 +351,7 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    eng.set_stream(stream.cuda_stream)
     ms = (t1 - t0) * 1e3 / args.steps
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     hashed = w.value_bytes * (2 if c5 else 1)
@@ -349,6 +397,9 @@ def main():
                          "kernel_ms": round(kern_ms, 5),
                          "algorithmic_bytes_per_launch": local_bytes},
             "parity": parity,
+            "simulated_shard_of_world": shard_world if shard_world != world else None,
+            "pipeline": ("2 contexts alternate builds; each build's tree kernel runs on a second "
+                         "stream, overlapping the next build's digest kernel") if pipeline else None,
         }
         if world == 1 and not args.no_cpu_baseline and not args.profile:
             result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_baseline_seconds)

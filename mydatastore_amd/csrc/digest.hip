@@ -95,9 +95,12 @@ __device__ __forceinline__ void load_step(u32x4 (&v)[U], const u32x4* src, uint6
 
 // U = 16-byte loads per lane per step (step = U KiB per wave); NT = nontemporal loads;
 // PIPE = issue the next step's loads before reducing the current one (register double buffer).
-template <int U, bool NT, bool PIPE>
+template <int U, bool NT, bool PIPE, int PRIO = 0>
 __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a) {
   constexpr uint64_t kStep = 1024ull * U;
+  // Streaming waves issue little VALU; when a build's tree kernel (back-to-back SHA-256 VALU)
+  // shares the CU, a raised priority keeps the loads flowing and the SHA waves take the slack.
+  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const int lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
   if (wave >= a.n_waves) return;
@@ -169,7 +172,8 @@ const Variant kVariants[] = {
     {bucket_digest_kernel<8, true, false>, 8},  {bucket_digest_kernel<8, false, false>, 8},
     {bucket_digest_kernel<16, true, false>, 16}, {bucket_digest_kernel<4, true, false>, 4},
     {bucket_digest_kernel<4, true, true>, 4},   {bucket_digest_kernel<8, true, true>, 8},
-    {bucket_digest_kernel<16, false, false>, 16},
+    {bucket_digest_kernel<16, false, false>, 16}, {bucket_digest_kernel<4, true, true, 2>, 4},
+    {bucket_digest_kernel<4, true, true, 3>, 4},
 };
 
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));

@@ -21,7 +21,7 @@
 #include "mde_internal.hpp"
 
 // Digest-kernel tuning defaults (tools/digest_sweep.sh, profiles/r01_digest_sweep.json).
-constexpr int kDefaultDigestVariant = 4;  // U=4 nontemporal, register-prefetched
+constexpr int kDefaultDigestVariant = 7;  // U=4 nontemporal, register-prefetched, s_setprio 2
 constexpr int kDefaultDigestCap = 2;      // 2 workgroups (8 waves) per CU
 
 struct mde_ctx {
