@@ -91,9 +91,10 @@ int mde_use_own_stream(mde_ctx* ctx);
 void* mde_get_stream(mde_ctx* ctx);
 int mde_synchronize(mde_ctx* ctx);
 int mde_device_info(mde_ctx* ctx, int* cu_count, char* arch_name, int arch_cap);
-/* Tuning hook for benchmarks: digest-kernel variant and resident workgroups per CU (-1 = the
- * built-in defaults). Results are identical for every setting; only speed changes. */
-int mde_set_tuning(mde_ctx* ctx, int digest_variant, int digest_blocks_per_cu);
+/* Tuning hook for benchmarks: digest-kernel variant, resident workgroups per CU, and grid
+ * oversubscription (-1 = the built-in defaults). Results are identical for every setting; only
+ * speed changes. */
+int mde_set_tuning(mde_ctx* ctx, int digest_variant, int digest_blocks_per_cu, int digest_oversub);
 
 /* Tree geometry (merkletree v0.2.0 shape: dup last leaf if odd, self-pair odd levels). */
 uint32_t mde_tree_depth(uint32_t n_buckets);          /* internal levels, root included */

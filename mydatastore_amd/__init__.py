@@ -89,7 +89,7 @@ def load_library() -> C.CDLL:
         "mde_last_error": (C.c_char_p, [vp]),
         "mde_set_stream": (C.c_int, [vp, vp]),
         "mde_use_own_stream": (C.c_int, [vp]),
-        "mde_set_tuning": (C.c_int, [vp, C.c_int, C.c_int]),
+        "mde_set_tuning": (C.c_int, [vp, C.c_int, C.c_int, C.c_int]),
         "mde_get_stream": (vp, [vp]),
         "mde_synchronize": (C.c_int, [vp]),
         "mde_device_info": (C.c_int, [vp, C.POINTER(C.c_int), C.c_char_p, C.c_int]),
@@ -199,8 +199,8 @@ class Engine:
         """Launch on a HIP stream handle (0 = the null stream = torch's default stream)."""
         self._check(self.lib.mde_set_stream(self.ctx, C.c_void_p(int(stream_handle))))
 
-    def set_tuning(self, digest_variant: int = -1, digest_blocks_per_cu: int = -1):
-        self._check(self.lib.mde_set_tuning(self.ctx, digest_variant, digest_blocks_per_cu))
+    def set_tuning(self, digest_variant: int = -1, digest_blocks_per_cu: int = -1, digest_oversub: int = -1):
+        self._check(self.lib.mde_set_tuning(self.ctx, digest_variant, digest_blocks_per_cu, digest_oversub))
 
     def use_own_stream(self):
         self._check(self.lib.mde_use_own_stream(self.ctx))

@@ -195,10 +195,11 @@ int bucket_digest_blocks_per_cu(int v, int cap) {
 
 // One contiguous range per resident wave: every wave of the grid is co-resident and all ranges
 // are equal, so the launch has no tail of late waves.
-void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, uint64_t* wave_bytes,
+void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, int oversub, uint64_t* wave_bytes,
                         uint32_t* n_waves) {
-  const uint64_t target_waves =
-      (uint64_t)(cus > 0 ? cus : 256) * (uint64_t)(blocks_per_cu > 0 ? blocks_per_cu : 4) * (kThreads / 64);
+  const uint64_t target_waves = (uint64_t)(cus > 0 ? cus : 256) *
+                                (uint64_t)(blocks_per_cu > 0 ? blocks_per_cu : 4) * (kThreads / 64) *
+                                (uint64_t)(oversub > 0 ? oversub : 1);
   uint64_t wb = (bytes + target_waves - 1) / target_waves;
   wb = (wb + kMaxStepBytes - 1) / kMaxStepBytes * kMaxStepBytes;
   if (wb < 2 * kMaxStepBytes) wb = 2 * kMaxStepBytes;
@@ -210,7 +211,10 @@ void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, uint64_t* wa
 hipError_t launch_bucket_digest(const DigestLaunch& a, hipStream_t st) {
   if (a.n_waves == 0) return hipSuccess;
   const uint32_t blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);
-  hipLaunchKernelGGL(variant(a.variant).fn, dim3(blocks), dim3(kThreads), 0, st, a);
+  // With an oversubscribed grid, residency is capped by reserving LDS the kernel never touches:
+  // 160 KiB / lds_bytes workgroups fit per CU, and the dispatcher hands the remaining workgroups
+  // to whichever CU frees a slot first (load balance around CUs slowed by co-running kernels).
+  hipLaunchKernelGGL(variant(a.variant).fn, dim3(blocks), dim3(kThreads), a.lds_bytes, st, a);
   return hipGetLastError();
 }
 

@@ -23,6 +23,7 @@
 // Digest-kernel tuning defaults (tools/digest_sweep.sh, profiles/r01_digest_sweep.json).
 constexpr int kDefaultDigestVariant = 7;  // U=4 nontemporal, register-prefetched, s_setprio 2
 constexpr int kDefaultDigestCap = 2;      // 2 workgroups (8 waves) per CU
+constexpr int kDefaultDigestOversub = 1;  // grid = resident slots x oversub
 
 struct mde_ctx {
   int device = 0;
@@ -30,6 +31,7 @@ struct mde_ctx {
   int digest_blocks_per_cu = 0;  // resident workgroups per CU for the digest kernel (queried)
   int digest_variant = kDefaultDigestVariant;
   int digest_cap = kDefaultDigestCap;
+  int digest_oversub = kDefaultDigestOversub;
   char arch[64] = {0};
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
@@ -146,6 +148,12 @@ mde::SegDesc seg_desc(const mde_records* r) {
   return d;
 }
 
+void plan_digest(mde_ctx* c, uint64_t bytes, mde::DigestLaunch* a) {
+  mde::plan_bucket_digest(bytes, c->cus, c->digest_blocks_per_cu, c->digest_oversub, &a->wave_bytes,
+                          &a->n_waves);
+  a->lds_bytes = c->digest_oversub > 1 ? (uint32_t)((160u * 1024u) / (uint32_t)c->digest_blocks_per_cu) & ~255u : 0u;
+}
+
 // Full validation of host-resident inputs (mde_build): the device API trusts its inputs but the
 // kernels clamp every index, so bad device input gives wrong digests, never a fault.
 int check_host_records(mde_ctx* c, const mde_records* r) {
@@ -178,8 +186,7 @@ int digest_async(mde_ctx* c, const mde_records* r) {
   if (!c->digest_blocks_per_cu)
     c->digest_blocks_per_cu = mde::bucket_digest_blocks_per_cu(c->digest_variant, c->digest_cap);
   a.variant = c->digest_variant;
-  mde::plan_bucket_digest(r->values_bytes + a.seg.shift, c->cus, c->digest_blocks_per_cu,
-                          &a.wave_bytes, &a.n_waves);
+  plan_digest(c, r->values_bytes + a.seg.shift, &a);
   MDE_HIP(c, mde::launch_bucket_digest(a, c->stream));
   return MDE_OK;
 }
@@ -200,7 +207,7 @@ int digest_async_biased(mde_ctx* c, const mde_records* r, uint64_t end_pos, uint
     c->digest_blocks_per_cu = mde::bucket_digest_blocks_per_cu(c->digest_variant, c->digest_cap);
   a.variant = c->digest_variant;
   // plan over the bytes this chunk actually covers (span is known on the host)
-  mde::plan_bucket_digest(span + 16, c->cus, c->digest_blocks_per_cu, &a.wave_bytes, &a.n_waves);
+  plan_digest(c, span + 16, &a);
   MDE_HIP(c, mde::launch_bucket_digest(a, c->stream));
   return MDE_OK;
 }
@@ -347,13 +354,14 @@ void mde_destroy(mde_ctx* c) {
 
 const char* mde_last_error(mde_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
-int mde_set_tuning(mde_ctx* c, int digest_variant, int digest_blocks_per_cu) {
+int mde_set_tuning(mde_ctx* c, int digest_variant, int digest_blocks_per_cu, int digest_oversub) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
   if (digest_variant >= mde::bucket_digest_variants())
     return set_err(c, MDE_E_INVAL, "digest variant %d out of range", digest_variant);
   c->digest_variant = digest_variant < 0 ? kDefaultDigestVariant : digest_variant;
   c->digest_cap = digest_blocks_per_cu < 0 ? kDefaultDigestCap : digest_blocks_per_cu;
+  c->digest_oversub = digest_oversub < 0 ? kDefaultDigestOversub : (digest_oversub ? digest_oversub : 1);
   c->digest_blocks_per_cu = 0;  // re-query
   return MDE_OK;
 }

@@ -37,10 +37,11 @@ struct DigestLaunch {
   uint64_t wave_bytes;        // contiguous bytes per wave (multiple of the 16 KiB max step)
   uint32_t n_waves;
   int variant;                // kernel variant (unroll / load policy), see digest.hip
+  uint32_t lds_bytes;         // residency cap for oversubscribed grids (0 = none)
 };
 hipError_t launch_bucket_digest(const DigestLaunch& a, hipStream_t st);
 // Waves and wave range for an arena of `bytes` on a device with `cus` CUs.
-void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, uint64_t* wave_bytes,
+void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, int oversub, uint64_t* wave_bytes,
                         uint32_t* n_waves);
 int bucket_digest_blocks_per_cu(int variant, int cap);
 int bucket_digest_variants();
