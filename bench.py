@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 logic on one GPU: ranks share cuda:0, gloo gather (not a measurement)")
+    ap.add_argument("--layout", default="a", choices=["a", "b"],
+                    help="a: records sorted by (partition, bucket); b: grouped by partition in arrival "
+                         "order with per-record bucket tags (binned on device)")
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="build only rank 0's shard of an N-GPU run on this GPU (no process group); "
                          "a per-GPU prediction, reported as such, never the N-GPU value")
@@ -203,8 +206,11 @@ def main():
         eng.set_tuning(*map(int, args.tuning.split(",")))
     kpp = -(-n_keys // P)
     shard_world = args.simulate_world if (args.simulate_world and world == 1) else world
+    if c5 and args.layout != "a":
+        raise SystemExit("--config c5 uses layout a (the extract gathers bucket runs)")
     w = make_workload(eng, n_partitions=P, n_buckets=B, value_len=V, part_mode=mode,
-                      keys_per_partition=kpp, n_keys=n_keys, rank=rank, world=shard_world)
+                      keys_per_partition=kpp, n_keys=n_keys, rank=rank, world=shard_world,
+                      layout=args.layout)
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
     Pl = w.n_partitions
@@ -385,15 +391,18 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (device-generated splitmix64 values, 'k%016x' keys, SHA-256 bucket tags)",
-            "config": {"workload": desc, "n_keys": n_keys, "value_len": V, "n_partitions": P,
+            "config": {"workload": desc, "layout": "A (sorted by partition, bucket)" if args.layout == "a"
+                       else "B (arrival order + bucket tags, binned on device)", "n_keys": n_keys, "value_len": V, "n_partitions": P,
                        "n_buckets": B, "bytes_hashed_per_step": total_bytes,
                        "partitions_per_gpu": Pl, "parallelism": f"partition-shard x{world}",
                        "root_gather": ("rccl all_gather_into_tensor of ceil(P/N) x 32 B slabs on a side "
                                        "stream, overlapped with the next build") if world > 1 else None},
-            "roofline": {"bound": "hbm", "kernel": "bucket_digest_kernel",
+            "roofline": {"bound": "hbm",
+                         "kernel": "bucket_digest_kernel" if args.layout == "a" else "tagged_digest_kernel",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic("c4" if c5 else args.config, local_bytes),
+                         "traffic": pmc_traffic(("c4" if c5 else args.config) + ("" if args.layout == "a" else "_b"),
+                                                local_bytes),
                          "kernel_ms": round(kern_ms, 5),
                          "algorithmic_bytes_per_launch": local_bytes},
             "parity": parity,
@@ -405,7 +414,7 @@ def main():
             result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_baseline_seconds)
         else:
             result["cpu_baseline"] = None
-        if world == 1 and not args.no_e2e and not args.profile and not c5:
+        if world == 1 and not args.no_e2e and not args.profile and not c5 and args.layout == "a":
             result["end_to_end"] = end_to_end(torch, eng, w, B)
         print(json.dumps(result), flush=True)
     if world > 1:

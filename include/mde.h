@@ -58,13 +58,21 @@ typedef struct mde_records {
   const uint8_t* values;     /* value arena: the bytes CustomHash.Add consumes */
   uint64_t values_bytes;     /* arena size in bytes */
   uint32_t value_stride;     /* > 0: record r = values[r*stride, (r+1)*stride) */
-  uint32_t reserved0;
+  uint32_t layout;           /* MDE_LAYOUT_SORTED (A) or MDE_LAYOUT_TAGGED (B) */
   const uint64_t* value_off; /* value_stride == 0: [n_records+1] byte offsets into values */
   uint64_t n_records;
   uint32_t n_partitions;
   uint32_t n_buckets;        /* PartitionBuckets (config/config.go:20); any value >= 1 */
-  const uint64_t* seg_rec;   /* [n_partitions*n_buckets + 1], nondecreasing, <= n_records */
+  const uint64_t* seg_rec;   /* layout A: [n_partitions*n_buckets + 1], nondecreasing, <= n_records */
+  /* Layout B: records grouped by partition in arrival order, each with its bucket tag (the
+   * getKeyBucket value, main/manager.go:773-778); the engine bins them into buckets itself.
+   * Fixed-length values (value_stride > 0), n_buckets <= 65536. */
+  const uint16_t* bucket_tag; /* [n_records] */
+  const uint64_t* part_rec;   /* [n_partitions + 1] record ranges, nondecreasing, <= n_records */
 } mde_records;
+
+#define MDE_LAYOUT_SORTED 0u /* layout A: sorted by (partition, bucket); seg_rec */
+#define MDE_LAYOUT_TAGGED 1u /* layout B: grouped by partition; bucket_tag + part_rec */
 
 /* Per-partition results. Any pointer may be NULL except root. */
 typedef struct mde_tree_out {

@@ -24,6 +24,8 @@ MDE_E_TREE = -4
 MDE_E_CAPACITY = -5
 MDE_E_DECODE = -6
 HASH_MOD = 999999
+LAYOUT_SORTED = 0  # layout A: sorted by (partition, bucket), seg_rec
+LAYOUT_TAGGED = 1  # layout B: grouped by partition, per-record bucket tags
 
 # Every symbol include/mde.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
@@ -50,8 +52,9 @@ class Records(C.Structure):
     """struct mde_records (include/mde.h)."""
     _fields_ = [
         ("values", C.c_void_p), ("values_bytes", C.c_uint64), ("value_stride", C.c_uint32),
-        ("reserved0", C.c_uint32), ("value_off", C.c_void_p), ("n_records", C.c_uint64),
+        ("layout", C.c_uint32), ("value_off", C.c_void_p), ("n_records", C.c_uint64),
         ("n_partitions", C.c_uint32), ("n_buckets", C.c_uint32), ("seg_rec", C.c_void_p),
+        ("bucket_tag", C.c_void_p), ("part_rec", C.c_void_p),
     ]
 
 
@@ -264,6 +267,24 @@ class Engine:
         }
         to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
         self._check(self.lib.mde_build_streamed(self.ctx, C.byref(rec), C.byref(to), chunk_bytes))
+        return out
+
+    def build_tagged(self, values: np.ndarray, part_rec: np.ndarray, bucket_tag: np.ndarray,
+                     n_partitions: int, n_buckets: int, value_stride: int, want_nodes=True):
+        """Layout B build: records grouped by partition in arrival order + bucket tags."""
+        P, B = n_partitions, n_buckets
+        values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)
+        part_rec = np.ascontiguousarray(part_rec, dtype=np.uint64)
+        tags = np.ascontiguousarray(bucket_tag, dtype=np.uint16)
+        rec = Records(_ptr(values), values.nbytes, value_stride, LAYOUT_TAGGED, 0,
+                      values.size // value_stride, P, B, 0, _ptr(tags), _ptr(part_rec))
+        out = {
+            "digest": np.zeros(P * B, np.uint64), "size": np.zeros(P * B, np.int32),
+            "items": np.zeros(P, np.int32), "root": np.zeros(P * 32, np.uint8),
+            "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
+        }
+        to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
+        self._check(self.lib.mde_build(self.ctx, C.byref(rec), C.byref(to)))
         return out
 
     def build_async(self, rec: Records, out: TreeOut):

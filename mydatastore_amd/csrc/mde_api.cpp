@@ -39,6 +39,7 @@ struct mde_ctx {
   std::string err;
   // Byte-sum accumulators: zero between builds (the tree kernel clears what it reads).
   unsigned long long* sums = nullptr;
+  uint32_t* counts = nullptr;  // layout-B record counts, same lifecycle as sums
   uint64_t sums_cap = 0;
   bool sums_dirty = false;
   // Host-API staging (device) and a scratch node array for B > kTreeLdsMaxBuckets.
@@ -96,11 +97,15 @@ int ensure_sums(mde_ctx* c, uint64_t S) {
     if (c->sums) {
       MDE_HIP(c, hipStreamSynchronize(c->stream));
       MDE_HIP(c, hipFree(c->sums));
+      MDE_HIP(c, hipFree(c->counts));
       c->sums = nullptr;
+      c->counts = nullptr;
     }
     uint64_t cap = S < 1024 ? 1024 : S;
-    if (hipMalloc(&c->sums, cap * 8) != hipSuccess) {
+    if (hipMalloc(&c->sums, cap * 8) != hipSuccess || hipMalloc(&c->counts, cap * 4) != hipSuccess) {
+      if (c->sums) (void)hipFree(c->sums);
       c->sums = nullptr;
+      c->counts = nullptr;
       c->sums_cap = 0;
       return set_err(c, MDE_E_NOMEM, "sums allocation failed");
     }
@@ -109,6 +114,7 @@ int ensure_sums(mde_ctx* c, uint64_t S) {
   }
   if (c->sums_dirty) {
     MDE_HIP(c, hipMemsetAsync(c->sums, 0, c->sums_cap * 8, c->stream));
+    MDE_HIP(c, hipMemsetAsync(c->counts, 0, c->sums_cap * 4, c->stream));
     c->sums_dirty = false;
   }
   return MDE_OK;
@@ -123,7 +129,14 @@ struct Guard {
 int check_records(mde_ctx* c, const mde_records* r) {
   if (!r) return set_err(c, MDE_E_INVAL, "records is NULL");
   if (r->n_buckets == 0) return set_err(c, MDE_E_INVAL, "n_buckets must be >= 1");
-  if (!r->seg_rec) return set_err(c, MDE_E_INVAL, "seg_rec is NULL");
+  if (r->layout > MDE_LAYOUT_TAGGED) return set_err(c, MDE_E_INVAL, "unknown layout %u", r->layout);
+  if (r->layout == MDE_LAYOUT_TAGGED) {
+    if (!r->part_rec || (!r->bucket_tag && r->n_records)) return set_err(c, MDE_E_INVAL, "layout B needs part_rec and bucket_tag");
+    if (!r->value_stride) return set_err(c, MDE_E_INVAL, "layout B needs fixed-length values");
+    if (r->n_buckets > 65536) return set_err(c, MDE_E_INVAL, "layout B supports n_buckets <= 65536");
+  } else if (!r->seg_rec) {
+    return set_err(c, MDE_E_INVAL, "seg_rec is NULL");
+  }
   if ((uint64_t)r->n_partitions * r->n_buckets > 0xffffffffull)
     return set_err(c, MDE_E_INVAL, "n_partitions * n_buckets exceeds 2^32");
   if (r->value_stride == 0 && !r->value_off && r->n_records)
@@ -157,6 +170,14 @@ void plan_digest(mde_ctx* c, uint64_t bytes, mde::DigestLaunch* a) {
 // Full validation of host-resident inputs (mde_build): the device API trusts its inputs but the
 // kernels clamp every index, so bad device input gives wrong digests, never a fault.
 int check_host_records(mde_ctx* c, const mde_records* r) {
+  if (r->layout == MDE_LAYOUT_TAGGED) {
+    for (uint32_t p = 0; p < r->n_partitions; p++)
+      if (r->part_rec[p] > r->part_rec[p + 1]) return set_err(c, MDE_E_INVAL, "part_rec not nondecreasing");
+    if (r->part_rec[r->n_partitions] > r->n_records) return set_err(c, MDE_E_INVAL, "part_rec exceeds n_records");
+    for (uint64_t i = r->part_rec[0]; i < r->part_rec[r->n_partitions]; i++)
+      if (r->bucket_tag[i] >= r->n_buckets) return set_err(c, MDE_E_INVAL, "bucket_tag[%llu] out of range", (unsigned long long)i);
+    return MDE_OK;
+  }
   const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
   for (uint64_t s = 0; s < S; s++)
     if (r->seg_rec[s] > r->seg_rec[s + 1])
@@ -175,11 +196,30 @@ int check_host_records(mde_ctx* c, const mde_records* r) {
   return MDE_OK;
 }
 
+int tagged_async(mde_ctx* c, const mde_records* r) {
+  mde::TaggedLaunch t{};
+  const uintptr_t v = reinterpret_cast<uintptr_t>(r->values);
+  t.base = reinterpret_cast<const uint8_t*>(v & ~uintptr_t(15));
+  t.shift = v & 15u;
+  t.stride = r->value_stride;
+  t.inv_stride = 1.0 / (double)r->value_stride;
+  t.part_rec = r->part_rec;
+  t.tag = r->bucket_tag;
+  t.P = r->n_partitions;
+  t.B = r->n_buckets;
+  t.sums = c->sums;
+  t.counts = c->counts;
+  mde::plan_tagged(r->values_bytes + t.shift, c->cus, 2, &t.wave_bytes, &t.n_waves);
+  MDE_HIP(c, mde::launch_tagged_digest(t, c->stream));
+  return MDE_OK;
+}
+
 int digest_async(mde_ctx* c, const mde_records* r) {
   const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
   int rc = ensure_sums(c, S);
   if (rc) return rc;
   if (S == 0 || r->n_records == 0 || r->values_bytes == 0) return MDE_OK;
+  if (r->layout == MDE_LAYOUT_TAGGED) return tagged_async(c, r);
   mde::DigestLaunch a{};
   a.seg = seg_desc(r);
   a.sums = c->sums;
@@ -222,7 +262,9 @@ int tree_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   t.B = r->n_buckets;
   t.sums_in = c->sums;
   t.sums_clear = c->sums;
-  t.seg_rec = r->seg_rec;
+  const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
+  t.seg_rec = tagged ? nullptr : r->seg_rec;
+  t.counts_in = tagged ? c->counts : nullptr;
   t.digest_out = o->digest;
   t.size_out = o->size;
   t.items_out = o->items;
@@ -241,6 +283,7 @@ int tree_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
 int extract_async(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t ids_stride,
                   const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
                   uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap, int32_t* status) {
+  if (r->layout != MDE_LAYOUT_SORTED) return set_err(c, MDE_E_INVAL, "extract takes layout A");
   if (r->n_buckets > mde::kExtractMaxBuckets)
     return set_err(c, MDE_E_INVAL, "extract supports n_buckets <= %u", mde::kExtractMaxBuckets);
   if (!ids || !counts || !part_off || !out_rec || !status || (out_values && !r->values))
@@ -336,6 +379,7 @@ void mde_destroy(mde_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->sums) (void)hipFree(c->sums);
+    if (c->counts) (void)hipFree(c->counts);
     for (auto& b : c->stage)
       if (b.p) (void)hipFree(b.p);
     if (c->nodes_scratch.p) (void)hipFree(c->nodes_scratch.p);
@@ -436,21 +480,26 @@ int mde_build(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   if ((rc = check_host_records(c, r))) return rc;
   if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
   const uint64_t P = r->n_partitions, S = P * r->n_buckets, NI = mde::tree_internal(r->n_buckets);
+  const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
   const uint64_t nvo = r->value_stride ? 0 : (r->n_records + 1);
-  const uint64_t sizes[9] = {r->values_bytes, nvo * 8, (S + 1) * 8, S * 8, S * 4, P * 4, P * 32,
-                             o->nodes ? P * NI * 32 : 0, 0};
-  for (int i = 0; i < 8; i++)
+  const uint64_t sizes[10] = {r->values_bytes, nvo * 8, tagged ? (P + 1) * 8 : (S + 1) * 8, S * 8, S * 4, P * 4,
+                              P * 32, o->nodes ? P * NI * 32 : 0, tagged ? r->n_records * 2 : 0, 0};
+  for (int i = 0; i < 9; i++)
     if ((rc = ensure_buf(c, c->stage[i], sizes[i]))) return rc;
   auto dp = [&](int i) { return c->stage[i].p; };
   if (r->values_bytes)
     MDE_HIP(c, hipMemcpyAsync(dp(0), r->values, r->values_bytes, hipMemcpyHostToDevice, c->stream));
   if (nvo)
     MDE_HIP(c, hipMemcpyAsync(dp(1), r->value_off, nvo * 8, hipMemcpyHostToDevice, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(dp(2), r->seg_rec, (S + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(dp(2), tagged ? r->part_rec : r->seg_rec, sizes[2], hipMemcpyHostToDevice, c->stream));
+  if (tagged && r->n_records)
+    MDE_HIP(c, hipMemcpyAsync(dp(8), r->bucket_tag, sizes[8], hipMemcpyHostToDevice, c->stream));
   mde_records dr = *r;
   dr.values = static_cast<const uint8_t*>(dp(0));
   dr.value_off = nvo ? static_cast<const uint64_t*>(dp(1)) : nullptr;
-  dr.seg_rec = static_cast<const uint64_t*>(dp(2));
+  dr.seg_rec = tagged ? nullptr : static_cast<const uint64_t*>(dp(2));
+  dr.part_rec = tagged ? static_cast<const uint64_t*>(dp(2)) : nullptr;
+  dr.bucket_tag = tagged ? static_cast<const uint16_t*>(dp(8)) : nullptr;
   mde_tree_out dout{static_cast<uint64_t*>(dp(3)), static_cast<int32_t*>(dp(4)),
                     static_cast<int32_t*>(dp(5)), static_cast<uint8_t*>(dp(6)),
                     o->nodes ? static_cast<uint8_t*>(dp(7)) : nullptr};
@@ -470,6 +519,7 @@ int mde_build_streamed(mde_ctx* c, const mde_records* r, const mde_tree_out* o, 
   Guard g(c);
   int rc = check_records(c, r);
   if (rc) return rc;
+  if (r->layout != MDE_LAYOUT_SORTED) return set_err(c, MDE_E_INVAL, "mde_build_streamed takes layout A");
   if ((rc = check_host_records(c, r))) return rc;
   if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
   if (!chunk_bytes) chunk_bytes = 256ull << 20;

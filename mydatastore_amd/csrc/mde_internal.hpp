@@ -46,12 +46,31 @@ void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, int oversub,
 int bucket_digest_blocks_per_cu(int variant, int cap);
 int bucket_digest_variants();
 
+struct TaggedLaunch {
+  const uint8_t* base;        // values rounded down to 16 B
+  uint64_t shift;             // values - base
+  uint32_t stride;            // fixed value length (> 0)
+  double inv_stride;
+  const uint64_t* part_rec;   // [P+1] record ranges of the partitions
+  const uint16_t* tag;        // [n_records] bucket of each record
+  uint32_t P, B;
+  unsigned long long* sums;   // [P*B]
+  uint32_t* counts;           // [P*B]
+  uint64_t wave_bytes;
+  uint32_t n_waves;
+  int use_lds;
+};
+constexpr uint32_t kTaggedLdsMaxBuckets = 1024;
+void plan_tagged(uint64_t bytes, int cus, int blocks_per_cu, uint64_t* wave_bytes, uint32_t* n_waves);
+hipError_t launch_tagged_digest(TaggedLaunch& a, hipStream_t st);
+
 struct TreeLaunch {
   uint32_t P, B;
   const unsigned long long* sums_in;  // [P*B] byte sums (digest = sum % 999999), or
   const uint64_t* digest_in;          // [P*B] digests (tree-from-digests mode)
   unsigned long long* sums_clear;     // zeroed after read (may be null)
   const uint64_t* seg_rec;            // [P*B+1] for sizes (may be null)
+  uint32_t* counts_in;                // [P*B] sizes when seg_rec is null (layout B); cleared
   uint64_t* digest_out;               // [P*B] (may be null)
   int32_t* size_out;                  // [P*B]
   int32_t* items_out;                 // [P]

@@ -32,7 +32,7 @@ __device__ __forceinline__ void store_node(uint32_t* dst, const uint32_t st[8]) 
 }
 
 // Leaf b of partition p: digest, and (when building from byte sums) its size/digest outputs.
-__device__ __forceinline__ uint64_t leaf(const TreeLaunch& a, uint64_t s, uint32_t& items) {
+__device__ __forceinline__ uint64_t leaf(const TreeLaunch& a, uint64_t s, uint32_t& items, uint32_t& sz_out) {
   uint64_t v;
   if (a.sums_in) {
     v = (uint64_t)(a.sums_in[s] % kHashMod);
@@ -41,10 +41,17 @@ __device__ __forceinline__ uint64_t leaf(const TreeLaunch& a, uint64_t s, uint32
     v = a.digest_in[s];
   }
   if (a.digest_out) a.digest_out[s] = v;
-  if (a.seg_rec) {
-    const uint32_t sz = (uint32_t)(a.seg_rec[s + 1] - a.seg_rec[s]);  // int32 wrap like Go
+  if (a.seg_rec || a.counts_in) {
+    uint32_t sz;  // int32 wrap like Go
+    if (a.seg_rec) {
+      sz = (uint32_t)(a.seg_rec[s + 1] - a.seg_rec[s]);
+    } else {
+      sz = a.counts_in[s];
+      a.counts_in[s] = 0u;
+    }
     if (a.size_out) a.size_out[s] = (int32_t)sz;
     items += sz;
+    sz_out = sz;
   }
   return v;
 }
@@ -77,10 +84,10 @@ __global__ __launch_bounds__(256) void tree_kernel(TreeLaunch a, uint32_t G, uin
   if (live) {
     for (uint32_t j = tid; j < n1; j += G) {
       const uint32_t bl = 2 * j, br = (2 * j + 1 < B) ? 2 * j + 1 : 2 * j;
-      const uint64_t dl = leaf(a, s0 + bl, items);
-      const uint64_t dr = (br != bl) ? leaf(a, s0 + br, items) : dl;
-      if (br == bl && a.seg_rec)  // odd B: the duplicate leaf's size counts again (tree.Leafs walk)
-        items += (uint32_t)(a.seg_rec[s0 + bl + 1] - a.seg_rec[s0 + bl]);
+      uint32_t szl = 0, szr = 0;
+      const uint64_t dl = leaf(a, s0 + bl, items, szl);
+      const uint64_t dr = (br != bl) ? leaf(a, s0 + br, items, szr) : dl;
+      if (br == bl) items += szl;  // odd B: the duplicate leaf's size counts again (tree.Leafs walk)
       uint32_t st[8];
       sha256_leaf_pair(dl, dr, st);
       store_node(buf0 + (uint64_t)j * 8, st);

@@ -31,14 +31,22 @@ class Workload:
     n_records: int
     value_len: int
     partition_ids: np.ndarray  # global partition id of each local partition
+    bucket_tag: "object" = None  # layout B: torch.int16 [n] bucket of each record
+    part_rec: "object" = None    # layout B: torch.int64 [P+1]
 
     def __post_init__(self):
         import torch
         P, B, dev = self.n_partitions, self.n_buckets, self.values.device
         self.n_int = mde.tree_internal_nodes(B)
-        self.rec = mde.Records(self.values.data_ptr() if self.values.numel() else 0,
-                               self.values.numel(), self.value_len, 0, 0, self.n_records, P, B,
-                               self.seg_rec.data_ptr())
+        if self.bucket_tag is not None:
+            self.rec = mde.Records(self.values.data_ptr() if self.values.numel() else 0,
+                                   self.values.numel(), self.value_len, mde.LAYOUT_TAGGED, 0,
+                                   self.n_records, P, B, 0, self.bucket_tag.data_ptr(),
+                                   self.part_rec.data_ptr())
+        else:
+            self.rec = mde.Records(self.values.data_ptr() if self.values.numel() else 0,
+                                   self.values.numel(), self.value_len, mde.LAYOUT_SORTED, 0,
+                                   self.n_records, P, B, self.seg_rec.data_ptr())
 
         def outs():
             o = {"digest": torch.zeros(P * B, dtype=torch.int64, device=dev),
@@ -88,7 +96,9 @@ class Workload:
 def make_workload(engine: "mde.Engine", n_partitions: int, n_buckets: int, value_len: int,
                   part_mode: str = "block", keys_per_partition: int = 0, n_keys: int = 0,
                   rank: int = 0, world: int = 1, seed: int = SYNTH_SEED,
-                  device: str = "cuda") -> Workload:
+                  device: str = "cuda", layout: str = "a") -> Workload:
+    """layout "a": records sorted by (partition, bucket) + seg_rec; layout "b": records grouped by
+    partition in arrival (gid) order + per-record bucket tags + part_rec."""
     import torch
     if not n_keys:
         n_keys = n_partitions * keys_per_partition
@@ -106,17 +116,24 @@ def make_workload(engine: "mde.Engine", n_partitions: int, n_buckets: int, value
     engine.synth_tags_async(gids, n, n_partitions, n_buckets, _MODES[part_mode],
                             max(keys_per_partition, 1), part, bkt)
     local = part.to(torch.int64) // world   # partition p lives on rank p % world at slot p // world
-    comp = local * n_buckets + bkt.to(torch.int64)
-    del part, bkt
+    if layout == "b":
+        comp = local
+    else:
+        comp = local * n_buckets + bkt.to(torch.int64)
+    del part
     comp_sorted, order = torch.sort(comp, stable=True)
-    counts = torch.bincount(comp_sorted, minlength=P * n_buckets)
+    nseg = P if layout == "b" else P * n_buckets
+    counts = torch.bincount(comp_sorted, minlength=nseg)
     del comp, comp_sorted
-    seg_rec = torch.zeros(P * n_buckets + 1, dtype=torch.int64, device=dev)
+    seg_rec = torch.zeros(nseg + 1, dtype=torch.int64, device=dev)
     seg_rec[1:] = torch.cumsum(counts, 0)
     sorted_gids = gids[order].contiguous()
-    del order, gids, counts
+    tags = bkt[order].to(torch.int16).contiguous() if layout == "b" else None
+    del order, gids, counts, bkt
     values = torch.empty(n * value_len, dtype=torch.uint8, device=dev)
     engine.synth_values_async(values, sorted_gids, n, value_len, seed)
     torch.cuda.synchronize(dev)
     del sorted_gids
+    if layout == "b":
+        return Workload(engine, values, None, P, n_buckets, n, value_len, pids, tags, seg_rec)
     return Workload(engine, values, seg_rec, P, n_buckets, n, value_len, pids)
