@@ -14,6 +14,9 @@
  *   DifferentMerkleTreeBuckets(tree1, tree2)                         main/merkle_tree.go:159-216
  *       -> mde_diff / mde_diff_async
  *
+ * and their caller's decision step, Manager.VerifyEpoch (main/manager.go:998-1118: build ->
+ * persist -> decode peer objects -> diff -> valid / diffSet) -> mde_verify_epochs / _async.
+ *
  * plus the write-time tagging the records carry (main/manager.go:773-778 getKeyBucket,
  * hashring/hashring.go:108-110 FindPartitionID) -> mde_tag_keys_async.
  *
@@ -203,6 +206,42 @@ int mde_decode_epoch_tree_objects(mde_ctx* ctx, uint32_t n, const uint8_t* bytes
                                   const uint64_t* off, uint32_t cap, int32_t* partition,
                                   int64_t* lower_epoch, int64_t* upper_epoch, uint64_t* digest,
                                   int32_t* size, uint8_t* valid, int32_t* items, int32_t* n_buckets);
+
+/* Manager.VerifyEpoch (main/manager.go:1036-1118) for n_partitions partitions of epoch E, given
+ * this node's trees (digest/size/nodes from mde_build with the nodes output, n_buckets each) and
+ * n_peers peer EpochTreeObject wire objects per partition (what EpochTreeObjectRequest returned):
+ * object (p, r) = peer_bytes[peer_off[p*n_peers+r] .. peer_off[p*n_peers+r+1]); an empty range is
+ * an absent peer. Each peer object is decoded and rebuilt (EpochTreeObjectToMerkleTree) and diffed
+ * against the local tree (DifferentMerkleTreeBuckets(myTree, otherTree)); a peer whose object or
+ * diff fails is skipped, as the reference does (logrus.Error; continue).
+ * Outputs per partition p:
+ *   valid[p]       = validCount >= replica_count || a non-empty diff against a Valid peer object
+ *   valid_count[p] = number of peers whose diff is empty
+ *   diff_ids[p*n_buckets ..], diff_count[p] = diffSet (utils.Int32Set of every successful diff),
+ *                    ascending -- the bucket list PoliteStreamRequest asks for when !valid
+ *   peer_status[p*n_peers+r] (optional) = the peer's diff length, MDE_E_DECODE (no tree from the
+ *                    object) or MDE_E_TREE (DifferentMerkleTreeBuckets error)
+ *   object_out (optional) = the EpochTreeObject VerifyEpoch persists for index
+ *                    epochtree_{p}_{E}: MerkleTreeToPartitionEpochObject(myTree, p, E, E+1) with
+ *                    Valid = valid[p], at object_out + p*object_stride (length object_len[p]).
+ * partition may be NULL (0). n_buckets <= 65536. A peer object with more than
+ * mde_verify_peer_capacity(n_buckets) buckets builds a deeper tree, which the reference's diff
+ * always rejects; it is reported as MDE_E_TREE without being rebuilt. */
+uint32_t mde_verify_peer_capacity(uint32_t n_buckets);
+int mde_verify_epochs_async(mde_ctx* ctx, uint32_t n_partitions, uint32_t n_buckets,
+                            const int32_t* partition, int64_t epoch, const uint64_t* digest,
+                            const int32_t* size, const uint8_t* nodes, uint32_t n_peers,
+                            const uint8_t* peer_bytes, const uint64_t* peer_off,
+                            uint32_t replica_count, uint8_t* valid, int32_t* valid_count,
+                            int32_t* diff_ids, int32_t* diff_count, int32_t* peer_status,
+                            uint8_t* object_out, uint64_t object_stride, uint32_t* object_len);
+int mde_verify_epochs(mde_ctx* ctx, uint32_t n_partitions, uint32_t n_buckets,
+                      const int32_t* partition, int64_t epoch, const uint64_t* digest,
+                      const int32_t* size, const uint8_t* nodes, uint32_t n_peers,
+                      const uint8_t* peer_bytes, const uint64_t* peer_off, uint32_t replica_count,
+                      uint8_t* valid, int32_t* valid_count, int32_t* diff_ids, int32_t* diff_count,
+                      int32_t* peer_status, uint8_t* object_out, uint64_t object_stride,
+                      uint32_t* object_len);
 
 /* Write-time tagging of raw keys (device): bucket = BE64(SHA256(key)[:8]) % n_buckets
  * (main/manager.go:773-778), partition = XXH64(key, 0) % n_partitions (hashring.go:108-110).

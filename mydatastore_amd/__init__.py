@@ -38,7 +38,8 @@ EXPORTED_SYMBOLS = (
     "mde_extract", "mde_extract_async", "mde_epoch_tree_object_max_bytes",
     "mde_encode_epoch_tree_objects", "mde_encode_epoch_tree_objects_async",
     "mde_decode_epoch_tree_objects", "mde_decode_epoch_tree_objects_async", "mde_synth_tags_async", "mde_synth_values_async", "mde_dev_alloc", "mde_dev_free",
-    "mde_memcpy_h2d", "mde_memcpy_d2h",
+    "mde_memcpy_h2d", "mde_memcpy_d2h", "mde_verify_peer_capacity", "mde_verify_epochs",
+    "mde_verify_epochs_async",
 )
 
 
@@ -119,6 +120,11 @@ def load_library() -> C.CDLL:
         "mde_encode_epoch_tree_objects_async": (C.c_int, [vp, u32, u32, vp, C.c_int64, C.c_int64, vp, vp, vp, vp, vp, u64, vp]),
         "mde_decode_epoch_tree_objects": (C.c_int, [vp, u32, vp, vp, u32, vp, vp, vp, vp, vp, vp, vp, vp]),
         "mde_decode_epoch_tree_objects_async": (C.c_int, [vp, u32, vp, vp, u32, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "mde_verify_peer_capacity": (u32, [u32]),
+        "mde_verify_epochs": (C.c_int, [vp, u32, u32, vp, C.c_int64, vp, vp, vp, u32, vp, vp, u32,
+                                        vp, vp, vp, vp, vp, vp, u64, vp]),
+        "mde_verify_epochs_async": (C.c_int, [vp, u32, u32, vp, C.c_int64, vp, vp, vp, u32, vp, vp,
+                                              u32, vp, vp, vp, vp, vp, vp, u64, vp]),
         "mde_synth_tags_async": (C.c_int, [vp, vp, u64, u32, u32, C.c_int, u64, vp, vp]),
         "mde_synth_values_async": (C.c_int, [vp, vp, vp, u64, u32, u64]),
         "mde_dev_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
@@ -421,6 +427,57 @@ class Engine:
                         "digest": o["digest"][i * cap:i * cap + nb].tolist(),
                         "size": o["size"][i * cap:i * cap + nb].tolist()})
         return res
+
+    # -- VerifyEpoch decision step ------------------------------------------------------------
+    def verify_epochs(self, n_buckets, digest, size, nodes, peer_objects, replica_count, epoch,
+                      partition=None, want_objects=True):
+        """Manager.VerifyEpoch over P partitions (mde_verify_epochs). ``peer_objects[p]`` is the
+        list of peer EpochTreeObject wire bytes for partition p (None = absent peer); every
+        partition must list the same number of peers. Returns a dict with valid, valid_count,
+        diff (ascending Int32Set per partition), peer_status ([P][R]) and objects (the persisted
+        EpochTreeObject bytes per partition)."""
+        B = n_buckets
+        digest = np.ascontiguousarray(digest, dtype=np.uint64).reshape(-1)
+        size = np.ascontiguousarray(size, dtype=np.int32).reshape(-1)
+        nodes = np.ascontiguousarray(nodes, dtype=np.uint8).reshape(-1)
+        P = digest.size // B
+        R = len(peer_objects[0]) if P else 0
+        if any(len(x) != R for x in peer_objects):
+            raise ValueError("every partition needs the same number of peer slots")
+        flat = [o or b"" for row in peer_objects for o in row]
+        off = np.zeros(len(flat) + 1, np.uint64)
+        off[1:] = np.cumsum([len(o) for o in flat])
+        blob = np.frombuffer(b"".join(flat) or b"\0", dtype=np.uint8).copy()
+        part = None if partition is None else np.ascontiguousarray(partition, dtype=np.int32)
+        valid = np.zeros(P, np.uint8)
+        vcount = np.zeros(P, np.int32)
+        ids = np.zeros(P * B, np.int32)
+        dcount = np.zeros(P, np.int32)
+        status = np.zeros(max(P * R, 1), np.int32)
+        stride = int(self.lib.mde_epoch_tree_object_max_bytes(B)) if want_objects else 0
+        objs = np.zeros(max(P * stride, 1), np.uint8) if want_objects else None
+        olen = np.zeros(P, np.uint32) if want_objects else None
+        self._check(self.lib.mde_verify_epochs(
+            self.ctx, P, B, _ptr(part), epoch, _ptr(digest), _ptr(size), _ptr(nodes), R, _ptr(blob),
+            _ptr(off), replica_count, _ptr(valid), _ptr(vcount), _ptr(ids), _ptr(dcount),
+            _ptr(status), _ptr(objs), stride, _ptr(olen)))
+        return {
+            "valid": [bool(v) for v in valid], "valid_count": vcount.tolist(),
+            "diff": [ids[p * B:p * B + int(dcount[p])].tolist() for p in range(P)],
+            "peer_status": [status[p * R:(p + 1) * R].tolist() for p in range(P)],
+            "objects": ([objs[p * stride:p * stride + int(olen[p])].tobytes() for p in range(P)]
+                        if want_objects else None),
+        }
+
+    def verify_epochs_async(self, n_partitions, n_buckets, partition, epoch, digest, size, nodes,
+                            n_peers, peer_bytes, peer_off, replica_count, valid, valid_count,
+                            diff_ids, diff_count, peer_status=None, object_out=None,
+                            object_stride=0, object_len=None):
+        self._check(self.lib.mde_verify_epochs_async(
+            self.ctx, n_partitions, n_buckets, _ptr(partition), epoch, _ptr(digest), _ptr(size),
+            _ptr(nodes), n_peers, _ptr(peer_bytes), _ptr(peer_off), replica_count, _ptr(valid),
+            _ptr(valid_count), _ptr(diff_ids), _ptr(diff_count), _ptr(peer_status),
+            _ptr(object_out), object_stride, _ptr(object_len)))
 
     # -- tagging / synthetic workload ---------------------------------------------------------
     def tag_keys(self, keys, n_buckets: int, n_partitions: int):

@@ -42,6 +42,13 @@ __device__ void make_shape(uint32_t B, Shape& s) {
   s.L = lv + 1;
 }
 
+__device__ __forceinline__ uint64_t internal_nodes(uint32_t B) {
+  uint32_t n = B + (B & 1u);
+  uint64_t t = 0;
+  while (n > 1) { n = (n + 1) / 2; t += n; }
+  return t;
+}
+
 // Compare node (level la, index ia) of tree A with (lb, ib) of tree B. Leaves are 8-byte LE
 // digests, inner nodes 32-byte hashes; different lengths never compare equal (bytes.Equal).
 __device__ __forceinline__ bool differs(uint32_t la, uint32_t ia, const Shape& sa, uint32_t Ba,
@@ -61,17 +68,27 @@ __global__ __launch_bounds__(kThreads) void diff_kernel(DiffLaunch a) {
   __shared__ uint32_t wave_tot[kThreads / 64];
   __shared__ uint32_t err;
   const uint32_t pr = blockIdx.x;
+  // Verify mode: the peer tree's own bucket count; a peer object that gave no tree is reported,
+  // not diffed (uniform across the block, so the early return is safe).
+  const int32_t bt = a.nb_in ? a.nb_in[pr] : (int32_t)a.Bb;
+  if (bt <= 0 || (uint32_t)bt > a.Bb) {
+    // capacity: more leaves than fit the local depth -> the DFS would fail (MDE_E_TREE)
+    if (threadIdx.x == 0) a.out_count[pr] = bt == -5 ? -4 : -6;
+    return;
+  }
+  const uint32_t Bb = (uint32_t)bt;
+  const uint32_t ai = a.a_div ? pr / a.a_div : pr;
   if (threadIdx.x == 0) {
     make_shape(a.Ba, sa);
-    make_shape(a.Bb, sb);
+    make_shape(Bb, sb);
     err = 0;
   }
   __syncthreads();
-  const uint64_t nia = sa.L > 1 ? sa.off[sa.L - 1] + 1 : 0;  // internal nodes per tree
-  const uint64_t nib = sb.L > 1 ? sb.off[sb.L - 1] + 1 : 0;
-  const uint64_t* da = a.da + (uint64_t)pr * a.Ba;
+  const uint64_t nia = internal_nodes(a.Ba);  // node stride per tree
+  const uint64_t nib = internal_nodes(a.Bb);
+  const uint64_t* da = a.da + (uint64_t)ai * a.Ba;
   const uint64_t* db = a.db + (uint64_t)pr * a.Bb;
-  const uint8_t* na = a.na + (uint64_t)pr * nia * 32;
+  const uint8_t* na = a.na + (uint64_t)ai * nia * 32;
   const uint8_t* nb = a.nb + (uint64_t)pr * nib * 32;
   int32_t* out = a.out_ids + (uint64_t)pr * a.out_stride;
 
@@ -90,7 +107,7 @@ __global__ __launch_bounds__(kThreads) void diff_kernel(DiffLaunch a) {
       bool alive = true;
       for (uint32_t d = 0; d <= Dm; d++) {
         const uint32_t la = Da - d, lb = Db - d;
-        if (!differs(la, ia, sa, a.Ba, da, na, lb, ib, sb, a.Bb, db, nb)) { alive = false; break; }
+        if (!differs(la, ia, sa, a.Ba, da, na, lb, ib, sb, Bb, db, nb)) { alive = false; break; }
         if (d == Dm) break;
         const uint32_t bit = (uint32_t)(v >> (Dm - 1 - d)) & 1u;
         const uint32_t ca = 2 * ia + bit, cb = 2 * ib + bit;
@@ -101,7 +118,7 @@ __global__ __launch_bounds__(kThreads) void diff_kernel(DiffLaunch a) {
         if (Da != Db) {
           atomicOr(&err, 1u);  // leaf vs inner node: nil child / missing content
         } else {
-          const uint32_t ida = min(ia, a.Ba - 1), idb = min(ib, a.Bb - 1);
+          const uint32_t ida = min(ia, a.Ba - 1), idb = min(ib, Bb - 1);
           if (ida != idb) atomicOr(&err, 1u);  // "bucketIds dont match"
           emit = true;
           id = (int32_t)ida;

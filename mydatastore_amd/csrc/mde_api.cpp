@@ -47,6 +47,7 @@ struct mde_ctx {
   Buf stage[16];
   Buf nodes_scratch;
   Buf extract_scratch;
+  Buf verify_scratch;
   // Host-ingest ring (mde_build_streamed): two slots of values / value_off / seg_rec.
   Buf ring_vals[2], ring_voff[2], ring_seg[2];
   hipStream_t copy_stream = nullptr;
@@ -384,6 +385,7 @@ void mde_destroy(mde_ctx* c) {
       if (b.p) (void)hipFree(b.p);
     if (c->nodes_scratch.p) (void)hipFree(c->nodes_scratch.p);
     if (c->extract_scratch.p) (void)hipFree(c->extract_scratch.p);
+    if (c->verify_scratch.p) (void)hipFree(c->verify_scratch.p);
     for (int i = 0; i < 2; i++) {
       for (auto* b : {&c->ring_vals[i], &c->ring_voff[i], &c->ring_seg[i]})
         if (b->p) (void)hipFree(b->p);
@@ -911,6 +913,141 @@ int mde_decode_epoch_tree_objects(mde_ctx* c, uint32_t n, const uint8_t* bytes, 
   if ((rc = down(partition, 2)) || (rc = down(lower, 3)) || (rc = down(upper, 4)) || (rc = down(digest, 5)) ||
       (rc = down(size, 6)) || (rc = down(valid, 7)) || (rc = down(items, 8)) || (rc = down(n_buckets, 9)))
     return rc;
+  MDE_HIP(c, hipStreamSynchronize(c->stream));
+  return MDE_OK;
+}
+
+uint32_t mde_verify_peer_capacity(uint32_t B) {
+  if (!B) return 0;
+  const uint32_t d = mde_tree_depth(B);
+  return d >= 31 ? 0u : (1u << d);
+}
+
+namespace {
+
+// Manager.VerifyEpoch, device pointers (see include/mde.h). Peer object (p, r) is
+// peer_bytes[peer_off[p*R+r] .. peer_off[p*R+r+1]); an empty range is an absent peer (an empty
+// object gives no tree, exactly like a missing one contributes nothing).
+int verify_async(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, int64_t epoch,
+                 const uint64_t* digest, const int32_t* size, const uint8_t* nodes, uint32_t R,
+                 const uint8_t* peer_bytes, const uint64_t* peer_off, uint32_t replica_count,
+                 uint8_t* valid, int32_t* valid_count, int32_t* diff_ids, int32_t* diff_count,
+                 int32_t* peer_status, uint8_t* object_out, uint64_t object_stride, uint32_t* object_len) {
+  if (!B || B > mde::kVerifyMaxBuckets || !digest || !nodes || !valid || !valid_count || !diff_ids ||
+      !diff_count || (R && (!peer_off || !peer_bytes)) || (object_out && (!size || !object_len)))
+    return set_err(c, MDE_E_INVAL, "bad verify arguments");
+  if (object_out && object_stride < mde::wire_max_bytes(B))
+    return set_err(c, MDE_E_CAPACITY, "object_stride too small");
+  if (!P) return MDE_OK;
+  const uint64_t T = (uint64_t)P * R;
+  const uint32_t cap = mde_verify_peer_capacity(B);
+  if (!cap) return set_err(c, MDE_E_INVAL, "n_buckets too large");
+  const uint64_t NI = mde::tree_internal(cap), idcap = mde_diff_capacity(B, cap);
+  // scratch: digests, sizes, bucket counts, valid flags, nodes, roots, diff ids, statuses
+  const uint64_t part[8] = {T * cap * 8, T * cap * 4, T * 4, T, T * NI * 32, T * 32, T * idcap * 4, T * 4};
+  uint64_t off[9] = {0};
+  for (int i = 0; i < 8; i++) off[i + 1] = off[i] + ((part[i] + 255) & ~255ull);
+  int rc = ensure_buf(c, c->verify_scratch, off[8]);
+  if (rc) return rc;
+  uint8_t* base = static_cast<uint8_t*>(c->verify_scratch.p);
+  auto at = [&](int i) { return static_cast<void*>(base + off[i]); };
+  uint64_t* pd = static_cast<uint64_t*>(at(0));
+  int32_t* nbk = static_cast<int32_t*>(at(2));
+  uint8_t* pvalid = static_cast<uint8_t*>(at(3));
+  uint8_t* pnodes = static_cast<uint8_t*>(at(4));
+  int32_t* pids = static_cast<int32_t*>(at(6));
+  int32_t* pst = peer_status ? peer_status : static_cast<int32_t*>(at(7));
+  if (T) {
+    // EpochTreeObjectToMerkleTree: decode (>cap buckets can only diff with an error: deeper tree)
+    mde::WireDecodeLaunch d{(uint32_t)T, peer_bytes, peer_off, cap, nullptr, nullptr, nullptr, pd,
+                            static_cast<int32_t*>(at(1)), pvalid, nullptr, nbk};
+    MDE_HIP(c, mde::launch_wire_decode(d, c->stream));
+    mde::TreeLaunch t{};
+    t.P = (uint32_t)T;
+    t.B = cap;
+    t.digest_in = pd;
+    t.root_out = static_cast<uint8_t*>(at(5));
+    t.nodes_out = pnodes;
+    t.n_int = NI;
+    t.n_in = nbk;
+    MDE_HIP(c, mde::launch_tree(t, c->stream));
+    // DifferentMerkleTreeBuckets(myTree, otherTree)
+    mde::DiffLaunch df{(uint32_t)T, B, cap, digest, nodes, pd, pnodes, pids, idcap, pst, R, nbk};
+    MDE_HIP(c, mde::launch_diff(df, c->stream));
+  }
+  mde::VerifyLaunch v{P, R, B, pst, pids, idcap, pvalid, replica_count, valid, valid_count, diff_ids, diff_count};
+  MDE_HIP(c, mde::launch_verify(v, c->stream));
+  if (object_out) {
+    // the object VerifyEpoch persists: MerkleTreeToPartitionEpochObject(myTree, p, E, E+1) with Valid
+    mde::WireEncodeLaunch e{P, B, partition, epoch, epoch + 1, digest, size, valid, nullptr,
+                            object_out, object_stride, object_len};
+    MDE_HIP(c, mde::launch_wire_encode(e, c->stream));
+  }
+  return MDE_OK;
+}
+
+}  // namespace
+
+int mde_verify_epochs_async(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, int64_t epoch,
+                            const uint64_t* digest, const int32_t* size, const uint8_t* nodes, uint32_t R,
+                            const uint8_t* peer_bytes, const uint64_t* peer_off, uint32_t replica_count,
+                            uint8_t* valid, int32_t* valid_count, int32_t* diff_ids, int32_t* diff_count,
+                            int32_t* peer_status, uint8_t* object_out, uint64_t object_stride,
+                            uint32_t* object_len) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  return verify_async(c, P, B, partition, epoch, digest, size, nodes, R, peer_bytes, peer_off, replica_count,
+                      valid, valid_count, diff_ids, diff_count, peer_status, object_out, object_stride,
+                      object_len);
+}
+
+int mde_verify_epochs(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, int64_t epoch,
+                      const uint64_t* digest, const int32_t* size, const uint8_t* nodes, uint32_t R,
+                      const uint8_t* peer_bytes, const uint64_t* peer_off, uint32_t replica_count,
+                      uint8_t* valid, int32_t* valid_count, int32_t* diff_ids, int32_t* diff_count,
+                      int32_t* peer_status, uint8_t* object_out, uint64_t object_stride, uint32_t* object_len) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (!B || !digest || !nodes || !valid || !valid_count || !diff_ids || !diff_count ||
+      (R && P && !peer_off) || (object_out && (!size || !object_len)))
+    return set_err(c, MDE_E_INVAL, "bad verify arguments");
+  const uint64_t N = P, T = N * R, NI = mde::tree_internal(B);
+  for (uint64_t i = 0; i < T; i++)
+    if (peer_off[i] > peer_off[i + 1]) return set_err(c, MDE_E_INVAL, "peer_off not nondecreasing");
+  const uint64_t nbytes = T ? peer_off[T] - peer_off[0] : 0;
+  if (nbytes && !peer_bytes) return set_err(c, MDE_E_INVAL, "peer_bytes is NULL");
+  const uint64_t ostride = object_out ? object_stride : 0;
+  const uint64_t sz[14] = {N * 4, N * B * 8, N * B * 4, N * NI * 32, nbytes + 1, (T + 1) * 8,
+                           N, N * 4, N * B * 4, N * 4, T * 4, N * ostride, N * 4, 0};
+  int rc;
+  for (int i = 0; i < 13; i++)
+    if ((rc = ensure_buf(c, c->stage[i], sz[i]))) return rc;
+  auto dp = [&](int i) { return c->stage[i].p; };
+  std::vector<uint64_t> rel(T + 1, 0);
+  for (uint64_t i = 0; i <= T && T; i++) rel[i] = peer_off[i] - peer_off[0];
+  if (partition) MDE_HIP(c, hipMemcpyAsync(dp(0), partition, sz[0], hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(dp(1), digest, sz[1], hipMemcpyHostToDevice, c->stream));
+  if (size) MDE_HIP(c, hipMemcpyAsync(dp(2), size, sz[2], hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(dp(3), nodes, sz[3], hipMemcpyHostToDevice, c->stream));
+  if (nbytes) MDE_HIP(c, hipMemcpyAsync(dp(4), peer_bytes + peer_off[0], nbytes, hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(dp(5), rel.data(), (T + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  rc = verify_async(c, P, B, partition ? static_cast<const int32_t*>(dp(0)) : nullptr, epoch,
+                    static_cast<const uint64_t*>(dp(1)), size ? static_cast<const int32_t*>(dp(2)) : nullptr,
+                    static_cast<const uint8_t*>(dp(3)), R, static_cast<const uint8_t*>(dp(4)),
+                    static_cast<const uint64_t*>(dp(5)), replica_count, static_cast<uint8_t*>(dp(6)),
+                    static_cast<int32_t*>(dp(7)), static_cast<int32_t*>(dp(8)), static_cast<int32_t*>(dp(9)),
+                    static_cast<int32_t*>(dp(10)), object_out ? static_cast<uint8_t*>(dp(11)) : nullptr,
+                    ostride, object_out ? static_cast<uint32_t*>(dp(12)) : nullptr);
+  if (rc) return rc;
+  MDE_HIP(c, hipMemcpyAsync(valid, dp(6), sz[6], hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(valid_count, dp(7), sz[7], hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(diff_ids, dp(8), sz[8], hipMemcpyDeviceToHost, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(diff_count, dp(9), sz[9], hipMemcpyDeviceToHost, c->stream));
+  if (peer_status && T) MDE_HIP(c, hipMemcpyAsync(peer_status, dp(10), sz[10], hipMemcpyDeviceToHost, c->stream));
+  if (object_out) {
+    MDE_HIP(c, hipMemcpyAsync(object_out, dp(11), sz[11], hipMemcpyDeviceToHost, c->stream));
+    MDE_HIP(c, hipMemcpyAsync(object_len, dp(12), sz[12], hipMemcpyDeviceToHost, c->stream));
+  }
   MDE_HIP(c, hipStreamSynchronize(c->stream));
   return MDE_OK;
 }

@@ -77,6 +77,10 @@ struct TreeLaunch {
   uint8_t* root_out;                  // [P*32]
   uint8_t* nodes_out;                 // [P*n_int*32]; required when B > kTreeLdsMaxBuckets
   uint64_t n_int;
+  // Tree-from-digests with a per-tree bucket count (decoded peer objects): tree p has
+  // n_in[p] <= B buckets at digest_in + p*B (n_in[p] <= 0: no tree, nothing written); its nodes
+  // use its own shape at stride n_int (= tree_internal(B)). Null: every tree has B buckets.
+  const int32_t* n_in;
 };
 constexpr uint32_t kTreeLdsMaxBuckets = 4096;
 hipError_t launch_tree(const TreeLaunch& a, hipStream_t st);
@@ -91,6 +95,12 @@ struct DiffLaunch {
   int32_t* out_ids;
   uint64_t out_stride;
   int32_t* out_count;
+  // Verify mode (all zero/null for plain pairwise diffs): pair i compares A tree i / a_div with
+  // B tree i, whose bucket count is nb_in[i] (<= Bb; <= 0 means the peer tree could not be built:
+  // out_count[i] = nb_in[i] or MDE_E_DECODE); B trees sit at stride Bb digests and
+  // tree_internal(Bb) nodes, each laid out by its own shape.
+  uint32_t a_div;
+  const int32_t* nb_in;
 };
 hipError_t launch_diff(const DiffLaunch& a, hipStream_t st);
 
@@ -142,6 +152,22 @@ struct WireDecodeLaunch {
 inline uint64_t wire_max_bytes(uint32_t B) { return 57 + 20ull * (B + (B & 1u)); }
 hipError_t launch_wire_encode(const WireEncodeLaunch& a, hipStream_t st);
 hipError_t launch_wire_decode(const WireDecodeLaunch& a, hipStream_t st);
+
+// VerifyEpoch's per-partition fold over its R peer diffs (main/manager.go:1072-1103).
+struct VerifyLaunch {
+  uint32_t P, R, B;
+  const int32_t* peer_status;  // [P*R] diff length (>= 0) or a skipped peer (< 0)
+  const int32_t* peer_ids;     // [P*R*ids_stride] diff ids
+  uint64_t ids_stride;
+  const uint8_t* peer_valid;   // [P*R] decoded EpochTreeObject.valid
+  uint32_t replica_count;
+  uint8_t* valid;              // [P]
+  int32_t* valid_count;        // [P]
+  int32_t* diff_ids;           // [P*B] ascending, de-duplicated (utils.Int32Set)
+  int32_t* diff_count;         // [P]
+};
+constexpr uint32_t kVerifyMaxBuckets = 1u << 16;
+hipError_t launch_verify(const VerifyLaunch& a, hipStream_t st);
 
 hipError_t launch_tag_keys(const uint8_t* keys, const uint64_t* key_off, uint64_t n, uint32_t B,
                            uint32_t P, uint32_t* bucket, uint32_t* partition, hipStream_t st);

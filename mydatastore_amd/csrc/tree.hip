@@ -65,17 +65,21 @@ __global__ __launch_bounds__(256) void tree_kernel(TreeLaunch a, uint32_t G, uin
   const uint32_t groups = blockDim.x / G;
   const uint32_t gi = threadIdx.x / G, tid = threadIdx.x % G;
   const uint32_t p = blockIdx.x * groups + gi;
-  const bool live = p < a.P;
-  const uint32_t B = a.B;
+  // Every group runs the level loop of the widest tree (a.B) so that __syncthreads() stays
+  // uniform; a group whose own tree (n_in) is narrower idles once it reaches its root.
+  const int32_t bt = (a.n_in && p < a.P) ? a.n_in[p] : (int32_t)a.B;
+  const bool live = p < a.P && bt > 0 && (uint32_t)bt <= a.B;
+  const uint32_t B = live ? (uint32_t)bt : a.B;
   const uint32_t n1 = (B + 1) / 2;  // level-1 nodes (leaf count incl. dup / 2)
-  const uint64_t s0 = (uint64_t)p * B;
+  const uint32_t n1_max = (a.B + 1) / 2;
+  const uint64_t s0 = (uint64_t)p * a.B;
   uint32_t* node_base = (a.nodes_out && live)
                             ? reinterpret_cast<uint32_t*>(a.nodes_out + (uint64_t)p * a.n_int * 32)
                             : nullptr;
   uint32_t* region = lds + (uint64_t)gi * lds_words;
   uint32_t* counter = region;  // region[0]: items accumulator
   uint32_t* buf0 = kLds ? region + 4 : node_base;
-  uint32_t* buf1 = kLds ? region + 4 + (uint64_t)n1 * 8 : nullptr;
+  uint32_t* buf1 = kLds ? region + 4 + (uint64_t)n1_max * 8 : nullptr;
   if (tid == 0) counter[0] = 0;
   __syncthreads();
 
@@ -97,12 +101,15 @@ __global__ __launch_bounds__(256) void tree_kernel(TreeLaunch a, uint32_t G, uin
   if (items) atomicAdd(counter, items);
 
   // Upper levels.
+  uint32_t n_max = n1_max;
   uint32_t n = n1;
   uint64_t level_off = 0;  // node index of the current level's first node in node_base
   uint32_t* cur = buf0;
   uint32_t* nxt = kLds ? buf1 : (node_base ? node_base + (uint64_t)n1 * 8 : nullptr);
-  while (n > 1) {
+  while (n_max > 1) {
     __syncthreads();
+    n_max = (n_max + 1) / 2;
+    if (n <= 1) continue;  // this group's tree is complete
     const uint32_t m = (n + 1) / 2;
     if (live) {
       for (uint32_t j = tid; j < m; j += G) {

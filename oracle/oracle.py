@@ -375,6 +375,62 @@ class Manager:
 
 
 # ---------------------------------------------------------------------------------------------
+# main/manager.go:1036-1118 -- VerifyEpoch's decision step
+# ---------------------------------------------------------------------------------------------
+VERIFY_DECODE = "decode"  # EpochTreeObjectToMerkleTree (or proto.Unmarshal) failed
+VERIFY_TREE = "tree"      # DifferentMerkleTreeBuckets returned an error
+
+
+def tree_from_digests(digests: Sequence[int], sizes: Optional[Sequence[int]] = None) -> MerkleTree:
+    """RawPartitionMerkleTree's tree for given bucket digests/sizes (bucket i -> id i)."""
+    sizes = list(sizes) if sizes is not None else [0] * len(digests)
+    return new_tree([MerkleBucket(bucket_id=i, hasher=CustomHash(int(d)), size=int(sizes[i]))
+                     for i, d in enumerate(digests)])
+
+
+def verify_epoch(my_tree: MerkleTree, partition_id: int, epoch: int,
+                 peer_objects: Sequence[Optional[bytes]], replica_count: int):
+    """Manager.VerifyEpoch (main/manager.go:1036-1118) after the peer fetch: the local object
+    (:1041), each peer object -> tree (:1076) -> diff against my tree (:1081), peers whose object
+    or diff fails are skipped (:1077-1084), diffSet = Int32Set of all successful diffs (:1086),
+    validCount / validDiff (:1088-1097), valid = validCount >= ReplicaCount || validDiff (:1100).
+    A missing peer (None) contributes nothing, like an object that yields no tree.
+    Returns dict(valid, valid_count, diff (sorted set), status (per peer: diff length or
+    VERIFY_DECODE / VERIFY_TREE), object (the persisted EpochTreeObject wire bytes))."""
+    from oracle import wire_pb
+
+    obj = merkle_tree_to_partition_epoch_object(my_tree, partition_id, epoch, epoch + 1)
+    valid_count, valid_diff, diff_set, status = 0, False, set(), []
+    for raw in peer_objects:
+        try:
+            m = wire_pb.unmarshal(raw or b"")
+            other = epoch_tree_object_to_merkle_tree(EpochTreeObject(
+                partition=m.partition, lower_epoch=m.lower_epoch, upper_epoch=m.upper_epoch,
+                buckets=list(m.buckets), buckets_size=list(m.buckets_size), valid=m.valid,
+                items=m.items))
+        except Exception:  # MerkleError / DecodeError: logrus.Error; continue
+            status.append(VERIFY_DECODE)
+            continue
+        try:
+            diff = different_merkle_tree_buckets(my_tree, other)
+        except MerkleError:
+            status.append(VERIFY_TREE)
+            continue
+        diff_set.update(diff)
+        if not diff:
+            valid_count += 1
+        elif m.valid:
+            valid_diff = True
+        status.append(len(diff))
+    valid = valid_count >= replica_count or valid_diff
+    digests = [decode_bytes_to_int64(h) for h in obj.buckets]
+    wire = wire_pb.marshal(partition_id, epoch, epoch + 1, digests, obj.buckets_size, valid=valid,
+                           items=obj.items)
+    return {"valid": valid, "valid_count": valid_count, "diff": sorted(diff_set), "status": status,
+            "object": wire}
+
+
+# ---------------------------------------------------------------------------------------------
 # Array form used to check the device engine (same semantics as above, flat layout)
 # ---------------------------------------------------------------------------------------------
 def level_sizes(n_buckets: int) -> List[int]:
