@@ -133,7 +133,8 @@ int check_records(mde_ctx* c, const mde_records* r) {
   if (r->layout > MDE_LAYOUT_TAGGED) return set_err(c, MDE_E_INVAL, "unknown layout %u", r->layout);
   if (r->layout == MDE_LAYOUT_TAGGED) {
     if (!r->part_rec || (!r->bucket_tag && r->n_records)) return set_err(c, MDE_E_INVAL, "layout B needs part_rec and bucket_tag");
-    if (!r->value_stride) return set_err(c, MDE_E_INVAL, "layout B needs fixed-length values");
+    if (!r->value_stride || r->value_stride > (1u << 30))
+      return set_err(c, MDE_E_INVAL, "layout B needs fixed-length values of 1 B .. 1 GiB");
     if (r->n_buckets > 65536) return set_err(c, MDE_E_INVAL, "layout B supports n_buckets <= 65536");
   } else if (!r->seg_rec) {
     return set_err(c, MDE_E_INVAL, "seg_rec is NULL");
@@ -210,7 +211,7 @@ int tagged_async(mde_ctx* c, const mde_records* r) {
   t.B = r->n_buckets;
   t.sums = c->sums;
   t.counts = c->counts;
-  mde::plan_tagged(r->values_bytes + t.shift, c->cus, 2, &t.wave_bytes, &t.n_waves);
+  mde::plan_tagged(r->values_bytes + t.shift, c->cus, 8, &t.wave_bytes, &t.n_waves);
   MDE_HIP(c, mde::launch_tagged_digest(t, c->stream));
   return MDE_OK;
 }

@@ -58,10 +58,12 @@ struct TaggedLaunch {
   uint32_t* counts;           // [P*B]
   uint64_t wave_bytes;
   uint32_t n_waves;
-  int use_lds;
+  int use_lds;                // set by the launcher: B <= kTaggedLdsMaxBuckets
+  uint32_t lrep;              // set by the launcher: LDS bin slots per bucket (power of two)
+  float inv_stride_f;         // set by the launcher
 };
-constexpr uint32_t kTaggedLdsMaxBuckets = 1024;
-void plan_tagged(uint64_t bytes, int cus, int blocks_per_cu, uint64_t* wave_bytes, uint32_t* n_waves);
+constexpr uint32_t kTaggedLdsMaxBuckets = 4096;
+void plan_tagged(uint64_t bytes, int cus, int waves_per_cu, uint64_t* wave_bytes, uint32_t* n_waves);
 hipError_t launch_tagged_digest(TaggedLaunch& a, hipStream_t st);
 
 struct TreeLaunch {

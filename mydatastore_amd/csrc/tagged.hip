@@ -3,24 +3,30 @@
 //
 // Reference: the bucket of a record is fixed at write time (Manager.getKeyBucket,
 // main/manager.go:773-778) and the build folds CustomHash.Add over each bucket's records
-// (main/merkle_tree.go:90-113). Layout A needs the records sorted by bucket; layout B hashes them
-// into the B leaf buckets inside the kernel:
-//   * equal contiguous byte ranges per wave (one per resident wave), 16-byte nontemporal loads;
-//   * each lane byte-sums (v_sad_u8) the part of its 16 bytes that belongs to the first record
-//     it touches; a record spilling into the vector's tail goes straight to its bin;
-//   * records are contiguous runs of lanes, so a key-segmented inclusive scan over the wave
-//     (6 shuffle steps) leaves each run's total on its last lane, which does ONE LDS atomic into
-//     the wave's private bucket bins (u64 byte sum + u32 record count per bucket);
-//   * when the wave passes a partition boundary it flushes its bins to global u64/u32 atomics
-//     (B per partition per wave) and clears them. B > 1024 bins skip LDS and add globally.
-// Fixed-length values only (value_stride > 0).
+// (main/merkle_tree.go:90-113). Layout A needs the records sorted by bucket; layout B bins them
+// into the B leaf buckets inside the kernel, so the unit of work is a record, not a bucket:
+//   * equal contiguous byte ranges per wave (one per resident wave), 16-byte nontemporal loads,
+//     the next step's loads issued before the current step is reduced (register double buffer);
+//   * each lane byte-sums (v_sad_u8) the part of its 16 bytes that belongs to each record it
+//     touches (one record unless a boundary falls inside the vector) -- the record index comes
+//     from a float reciprocal of the wave-relative offset, corrected to exact;
+//   * no cross-lane reduction per record: every lane owns a private slot in the wave's LDS bins
+//     (sum bins laid out [bucket][lane slot], u32) and adds its partial sum to
+//     bins[tag(record)][slot] with one conflict-free ds_add; the lane holding a record's first
+//     byte adds 1 to that bucket's record count;
+//   * when the wave leaves a partition it folds the lane slots of each bucket (rotated so the 64
+//     lanes hit 64 banks), adds them to the global u64 sums / u32 counts and clears the bins.
+// Slots per bucket: 64 up to B = 64, halving as B doubles (<= 32 KiB of bins per wave); lanes
+// sharing a slot serialize on the LDS atomic. B > 4096 adds straight to global memory.
+// Exactness: a wave covers <= 8 MiB, so any u32 slot holds <= 255 * 8 MiB < 2^32.
+// Fixed-length values only (0 < value_stride <= 2^30).
 #include "mde_device.hpp"
 #include "mde_internal.hpp"
 
 namespace mde {
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 128;  // 2 waves: 4 workgroups per CU fit their LDS bins
 constexpr int kU = 4;                       // 16-byte loads per lane per step
 constexpr uint64_t kStep = 1024ull * kU;    // 4 KiB per wave step
 
@@ -30,22 +36,23 @@ __device__ __forceinline__ uint32_t byte_mask(int lo, int hi) {
   return hi > lo ? (mh & ~ml) : 0u;
 }
 
-__device__ __forceinline__ uint32_t masked_sum16(u32x4 v, int64_t a, int64_t b) {
-  const int ia = (int)min<int64_t>(max<int64_t>(a, 0), 16);
-  const int ib = (int)min<int64_t>(max<int64_t>(b, 0), 16);
+// Byte sum of bytes [a, b) of the 16-byte vector v (0 <= a <= b <= 16).
+__device__ __forceinline__ uint32_t masked_sum16(u32x4 v, int a, int b) {
   uint32_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const int lo = min(max(ia - 4 * k, 0), 4), hi = min(max(ib - 4 * k, 0), 4);
+    const int lo = min(max(a - 4 * k, 0), 4), hi = min(max(b - 4 * k, 0), 4);
     acc = __builtin_amdgcn_sad_u8(v[k] & byte_mask(lo, hi), 0u, acc);
   }
   return acc;
 }
 
-struct Bins {
-  unsigned long long* sum;  // LDS, B entries (nullptr: global only)
-  uint32_t* cnt;
-};
+__device__ __forceinline__ uint32_t full_sum16(u32x4 v) {
+  uint32_t acc = __builtin_amdgcn_sad_u8(v[0], 0u, 0u);
+  acc = __builtin_amdgcn_sad_u8(v[1], 0u, acc);
+  acc = __builtin_amdgcn_sad_u8(v[2], 0u, acc);
+  return __builtin_amdgcn_sad_u8(v[3], 0u, acc);
+}
 
 // Partition of record r (linear walk from q; only taken for records past the wave's partition).
 __device__ __forceinline__ uint32_t part_of(const TaggedLaunch& a, uint64_t r, uint32_t q) {
@@ -53,43 +60,50 @@ __device__ __forceinline__ uint32_t part_of(const TaggedLaunch& a, uint64_t r, u
   return q;
 }
 
-__device__ __forceinline__ void add_bin(const TaggedLaunch& a, const Bins& bins, uint32_t q,
-                                        uint64_t q_end, uint64_t r, uint32_t s, uint32_t c) {
-  if (!s && !c) return;
-  const uint32_t b = a.tag[r];
-  if (bins.sum && r < q_end) {
-    if (s) atomicAdd(bins.sum + b, (unsigned long long)s);
-    if (c) atomicAdd(bins.cnt + b, c);
-  } else {
-    const uint64_t idx = (uint64_t)part_of(a, r, q) * a.B + b;
-    if (s) atomicAdd(a.sums + idx, (unsigned long long)s);
-    if (c) atomicAdd(a.counts + idx, c);
+struct WaveBins {
+  uint32_t* sum;  // [B][lrep] (nullptr: global only)
+  uint32_t* cnt;  // [B]
+};
+
+__device__ void flush_bins(const TaggedLaunch& a, const WaveBins& w, uint32_t q, int lane) {
+  if (!w.sum) return;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint32_t L = a.lrep;
+  for (uint32_t b = lane; b < a.B; b += 64) {
+    uint32_t* row = w.sum + (uint64_t)b * L;
+    unsigned long long s = 0;
+    for (uint32_t j = 0; j < L; j++) {
+      const uint32_t k = (j + (uint32_t)lane) & (L - 1);  // rotate: lanes hit different banks
+      s += row[k];
+      row[k] = 0;
+    }
+    const uint32_t c = w.cnt[b];
+    w.cnt[b] = 0;
+    if (s) atomicAdd(a.sums + (uint64_t)q * a.B + b, s);
+    if (c) atomicAdd(a.counts + (uint64_t)q * a.B + b, c);
   }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
-__device__ void flush_bins(const TaggedLaunch& a, const Bins& bins, uint32_t q, int lane) {
-  if (!bins.sum) return;
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  for (uint32_t j = lane; j < a.B; j += 64) {
-    const unsigned long long s = bins.sum[j];
-    const uint32_t c = bins.cnt[j];
-    if (s) atomicAdd(a.sums + (uint64_t)q * a.B + j, s);
-    if (c) atomicAdd(a.counts + (uint64_t)q * a.B + j, c);
-    bins.sum[j] = 0;
-    bins.cnt[j] = 0;
+__device__ __forceinline__ void load_step(u32x4 (&v)[kU], const u32x4* lane_base, uint64_t p,
+                                          uint64_t end, int lane) {
+#pragma unroll
+  for (int u = 0; u < kU; u++) {
+    const uint64_t x = p + (uint64_t)u * 1024u + (uint64_t)lane * 16u;
+    v[u] = x < end ? __builtin_nontemporal_load(lane_base + (p >> 4) + u * 64) : u32x4{0u, 0u, 0u, 0u};
   }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
 __global__ __launch_bounds__(kThreads) void tagged_digest_kernel(TaggedLaunch a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  Bins bins{nullptr, nullptr};
+  const uint32_t L = a.lrep;
+  WaveBins w{nullptr, nullptr};
   if (a.use_lds) {
-    bins.sum = reinterpret_cast<unsigned long long*>(smem) + (uint64_t)wid * a.B;
-    bins.cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned long long*>(smem) + 4ull * a.B) +
-               (uint64_t)wid * a.B;
-    for (uint32_t j = lane; j < a.B; j += 64) { bins.sum[j] = 0; bins.cnt[j] = 0; }
+    const uint64_t words = (uint64_t)a.B * L + a.B;
+    w.sum = smem + (uint64_t)wid * words;
+    w.cnt = w.sum + (uint64_t)a.B * L;
+    for (uint64_t j = lane; j < words; j += 64) w.sum[j] = 0;
   }
   const uint32_t wave = blockIdx.x * (kThreads / 64) + wid;
   if (wave >= a.n_waves) return;
@@ -100,88 +114,137 @@ __global__ __launch_bounds__(kThreads) void tagged_digest_kernel(TaggedLaunch a)
   const uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
   if (beg >= last) return;
   const uint64_t end = min(beg + a.wave_bytes, last);
-  auto rec_of = [&](uint64_t pos) -> uint64_t {  // record containing byte position pos
-    const uint64_t rel = pos - a.shift;
-    uint64_t r = (uint64_t)((double)rel * a.inv_stride);
-    while (r * V > rel) r--;
-    while ((r + 1) * V <= rel) r++;
-    return r;
+  const uint64_t start = max(beg, valid_lo);
+  // The wave's first record (exact, double reciprocal), then wave-relative offsets (< 2^24 + V)
+  // divide in float with a one-step correction.
+  uint64_t r0;
+  {
+    const uint64_t rel = start - a.shift;
+    r0 = (uint64_t)((double)rel * a.inv_stride);
+    while (r0 * V > rel) r0--;
+    while ((r0 + 1) * V <= rel) r0++;
+  }
+  const uint64_t pos0 = a.shift + r0 * V;
+  auto rec_at = [&](uint64_t pos) -> uint64_t {
+    const uint32_t rel = (uint32_t)(pos - pos0);
+    uint32_t q = (uint32_t)((float)rel * a.inv_stride_f);
+    while ((uint64_t)q * V > rel) q--;
+    while ((uint64_t)(q + 1) * V <= rel) q++;
+    return r0 + q;
   };
-  // partition of the wave's first byte (64-ary search over part_rec)
-  uint64_t r_first = rec_of(max(beg, valid_lo));
+  // partition of the wave's first record (64-ary search over part_rec)
   uint32_t q = 0;
   {
     uint32_t lo = 0, hi = a.P;
     while (hi - lo > 1) {
       const uint32_t n = hi - lo, step = (n + 63u) / 64u;
       const uint32_t idx = lo + (uint32_t)lane * step;
-      const int c = __popcll(__ballot(idx < hi && a.part_rec[idx] <= r_first));
+      const int c = __popcll(__ballot(idx < hi && a.part_rec[idx] <= r0));
       if (c == 0) break;
       lo = lo + (uint32_t)(c - 1) * step;
       hi = min(lo + step, hi);
     }
     q = lo;
-    while (q + 1 < a.P && a.part_rec[q + 1] <= r_first) q++;  // skip empty partitions
+    while (q + 1 < a.P && a.part_rec[q + 1] <= r0) q++;  // skip empty partitions
   }
   uint64_t q_end = a.part_rec[q + 1];  // first record past partition q
   const u32x4* lane_base = reinterpret_cast<const u32x4*>(a.base) + lane;
+  const uint32_t slot = (uint32_t)lane & (L - 1);
 
+  // Tags travel with the data: the loads of a step also fetch the tags of its first 64 records
+  // (one coalesced u16 per lane), read back with a lane shuffle. A tag load issued next to the
+  // record's own use would make the wait for it (vmcnt counts in order) also wait for the
+  // prefetched next step.
+  const bool straddles = ((V | a.shift) & 15u) != 0;  // record boundaries inside a 16-byte vector
+  const uint32_t vsh = V >= 64 && (V & (V - 1)) == 0 ? (uint32_t)__builtin_ctzll(V) : 0u;
+  const uint32_t vmask = (uint32_t)V - 1u;
+  const bool fast_ok = vsh != 0 && !straddles && w.sum != nullptr && start == beg;
+  const uint64_t r_last = r_hi - 1;
+  auto load_tags = [&](uint64_t p, uint64_t& r_first) -> uint32_t {
+    r_first = rec_at(max(p, start));
+    return a.tag[min(r_first + (uint64_t)lane, r_last)];
+  };
+  u32x4 cur[kU], nxt[kU];
+  uint64_t cur_r0 = 0, nxt_r0 = 0;
+  uint32_t cur_tags = load_tags(beg, cur_r0), nxt_tags = 0;
+  load_step(cur, lane_base, beg, end, lane);
   for (uint64_t p = beg; p < end; p += kStep) {
-    u32x4 v[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const uint64_t x = p + (uint64_t)u * 1024u + (uint64_t)lane * 16u;
-      v[u] = x < end ? __builtin_nontemporal_load(lane_base + (p >> 4) + u * 64) : u32x4{0u, 0u, 0u, 0u};
+    const uint64_t pn = p + kStep;
+    if (pn < end) {
+      nxt_tags = load_tags(pn, nxt_r0);
+      load_step(nxt, lane_base, pn, end, lane);
     }
+    // Fast step (wave-uniform): power-of-two records of >= 64 B on 16-byte boundaries, the whole
+    // step inside [start, end) and inside partition q. Every vector then lies in one record, the
+    // record index is a shift, and a step holds <= 64 records (tags by shuffle): per vector 4
+    // v_sad_u8 + one ds_add, in 32-bit arithmetic.
+    if (fast_ok && pn <= end && r0 + ((pn - 1 - pos0) >> vsh) < q_end) {
+      const uint32_t xr0 = (uint32_t)(p - pos0) + (uint32_t)lane * 16u;
+      const uint32_t k0 = (uint32_t)(cur_r0 - r0);
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const uint32_t xr = xr0 + (uint32_t)u * 1024u;
+        const uint32_t k = (xr >> vsh) - k0;  // < 64
+        const uint32_t b = min((uint32_t)__shfl((int)cur_tags, (int)k), a.B - 1);
+        atomicAdd(w.sum + b * L + slot, full_sum16(cur[u]));
+        if ((xr & vmask) == 0) atomicAdd(w.cnt + b, 1u);
+      }
+    } else {
 #pragma unroll
     for (int u = 0; u < kU; u++) {
       const uint64_t x = p + (uint64_t)u * 1024u + (uint64_t)lane * 16u;
-      const uint64_t lo = max(x, max(beg, valid_lo)), hi = min(x + 16, end);
-      uint32_t key = 0xffffffffu, s_a = 0;
-      if (lo < hi) {
-        const uint64_t ra = rec_of(lo), rb = rec_of(hi - 1);
-        const uint64_t ra_end = a.shift + (ra + 1) * V;
-        s_a = masked_sum16(v[u], (int64_t)lo - (int64_t)x, (int64_t)min(hi, ra_end) - (int64_t)x);
-        key = (uint32_t)(ra - r_first);
-        // records starting inside [lo, hi) are counted here; tail records are summed here
-        if (a.shift + ra * V >= lo) add_bin(a, bins, q, q_end, ra, 0u, 1u);
-        for (uint64_t r = ra + 1; r <= rb; r++) {
-          const uint64_t rs = a.shift + r * V, re = rs + V;
-          const uint32_t s = masked_sum16(v[u], (int64_t)rs - (int64_t)x, (int64_t)min(hi, re) - (int64_t)x);
-          add_bin(a, bins, q, q_end, r, s, 1u);
+      const uint64_t lo = max(x, start), hi = min(x + 16, end);
+      const bool act = lo < hi;
+      uint64_t r = rec_at(act ? lo : start);
+      const uint32_t k = (uint32_t)min<uint64_t>(r - cur_r0, 64);  // r >= cur_r0 for active lanes
+      // shuffles stay outside divergent code (bpermute reads inactive lanes as 0)
+      const uint32_t t0 = (uint32_t)__shfl((int)cur_tags, (int)min(k, 63u));
+      const uint32_t t1 = straddles ? (uint32_t)__shfl((int)cur_tags, (int)min(k + 1, 63u)) : 0u;
+      if (!act) continue;
+      uint64_t rs = a.shift + r * V;
+      for (uint32_t j = 0;; j++, r++) {  // one record unless a boundary falls inside
+        const uint64_t c0 = j ? rs : lo;
+        if (c0 >= hi) break;
+        const uint64_t re = rs + V, c1 = min(hi, re);
+        const uint32_t s = (c0 == x && c1 == x + 16) ? full_sum16(cur[u])
+                                                      : masked_sum16(cur[u], (int)(c0 - x), (int)(c1 - x));
+        const uint32_t cnt = rs >= lo ? 1u : 0u;  // this lane holds the record's first byte
+        const uint32_t tg = (j == 0 && k < 64) ? t0 : (j == 1 && k + 1 < 64) ? t1 : (uint32_t)a.tag[r];
+        const uint32_t b = min(tg, a.B - 1);  // bad tags never fault (the host API rejects them)
+        if (w.sum && r < q_end) {
+          if (s) atomicAdd(w.sum + (uint64_t)b * L + slot, s);
+          if (cnt) atomicAdd(w.cnt + b, 1u);
+        } else {
+          const uint64_t idx = (uint64_t)part_of(a, r, q) * a.B + b;
+          if (s) atomicAdd(a.sums + idx, (unsigned long long)s);
+          if (cnt) atomicAdd(a.counts + idx, 1u);
         }
+        rs = re;
       }
-      // key-segmented inclusive scan: runs of equal keys are contiguous lanes
-      uint32_t tot = s_a;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t ot = __shfl_up(tot, o), ok = __shfl_up(key, o);
-        if (lane >= o && ok == key) tot += ot;
-      }
-      const uint32_t next_key = __shfl_down(key, 1);
-      const bool tail = lane == 63 || next_key != key;
-      if (tail && key != 0xffffffffu) add_bin(a, bins, q, q_end, r_first + key, tot, 0u);
+    }
     }
     // leave partitions the next step no longer touches
-    const uint64_t pn = p + kStep;
     while (q + 1 < a.P && pn < end && a.shift + q_end * V <= pn) {
-      flush_bins(a, bins, q, lane);
+      flush_bins(a, w, q, lane);
       q++;
       q_end = a.part_rec[q + 1];
     }
+#pragma unroll
+    for (int u = 0; u < kU; u++) cur[u] = nxt[u];
+    cur_tags = nxt_tags;
+    cur_r0 = nxt_r0;
   }
-  flush_bins(a, bins, q, lane);
+  flush_bins(a, w, q, lane);
 }
 
 }  // namespace
 
-void plan_tagged(uint64_t bytes, int cus, int blocks_per_cu, uint64_t* wave_bytes, uint32_t* n_waves) {
-  const uint64_t target = (uint64_t)(cus > 0 ? cus : 256) * (uint64_t)(blocks_per_cu > 0 ? blocks_per_cu : 2) *
-                          (kThreads / 64);
+void plan_tagged(uint64_t bytes, int cus, int waves_per_cu, uint64_t* wave_bytes, uint32_t* n_waves) {
+  const uint64_t target = (uint64_t)(cus > 0 ? cus : 256) * (uint64_t)(waves_per_cu > 0 ? waves_per_cu : 8);
   uint64_t wb = (bytes + target - 1) / target;
   wb = (wb + kStep - 1) / kStep * kStep;
   if (wb < 2 * kStep) wb = 2 * kStep;
-  if (wb > (8ull << 20)) wb = 8ull << 20;
+  if (wb > (8ull << 20)) wb = 8ull << 20;  // u32 bin slots stay exact; float offsets stay < 2^24
   *wave_bytes = wb;
   *n_waves = (uint32_t)((bytes + 16 + wb - 1) / wb);
 }
@@ -189,7 +252,12 @@ void plan_tagged(uint64_t bytes, int cus, int blocks_per_cu, uint64_t* wave_byte
 hipError_t launch_tagged_digest(TaggedLaunch& a, hipStream_t st) {
   if (a.n_waves == 0) return hipSuccess;
   a.use_lds = a.B <= kTaggedLdsMaxBuckets ? 1 : 0;
-  const size_t lds = a.use_lds ? (size_t)(kThreads / 64) * a.B * 12 : 0;
+  // bins of one workgroup <= 64 KiB: (kThreads/64) * B * (L + 1) * 4 bytes
+  uint32_t L = 64;
+  while (L > 1 && (uint64_t)a.B * (L + 1) * (kThreads / 64) * 4 > 65536) L >>= 1;
+  a.lrep = L;
+  a.inv_stride_f = 1.0f / (float)a.stride;
+  const size_t lds = a.use_lds ? (size_t)(kThreads / 64) * ((size_t)a.B * L + a.B) * 4 : 0;
   const uint32_t blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);
   hipLaunchKernelGGL(tagged_digest_kernel, dim3(blocks), dim3(kThreads), lds, st, a);
   return hipGetLastError();

@@ -2,6 +2,8 @@
 // by the engine (libmde.so).
 #include "merkle_tree.hpp"
 
+#include <algorithm>
+
 #include <cstdio>
 #include <cstring>
 
@@ -405,6 +407,91 @@ Error Manager::RawPartitionMerkleTrees(const std::vector<int>& partitionIds, int
         std::vector<uint64_t>(digest.begin() + (size_t)i * B, digest.begin() + (size_t)(i + 1) * B),
         std::vector<int32_t>(size.begin() + (size_t)i * B, size.begin() + (size_t)(i + 1) * B),
         Bytes(nodes.begin() + (size_t)i * NI * 32, nodes.begin() + (size_t)(i + 1) * NI * 32)));
+  }
+  return "";
+}
+
+Error Manager::VerifyEpoch(int PartitionId, int64_t Epoch, const std::vector<Bytes>& peerObjects,
+                           int replicaCount, VerifyResult* out) {
+  std::vector<VerifyResult> res;
+  std::vector<Error> errs;
+  Error e = VerifyEpochs({PartitionId}, Epoch, {peerObjects}, replicaCount, &res, &errs);
+  if (!e.empty()) return e;
+  *out = res[0];
+  return errs[0];
+}
+
+Error Manager::VerifyEpochs(const std::vector<int>& partitionIds, int64_t Epoch,
+                            const std::vector<std::vector<Bytes>>& peerObjects, int replicaCount,
+                            std::vector<VerifyResult>* out, std::vector<Error>* errs) {
+  const size_t N = partitionIds.size();
+  if (peerObjects.size() != N) return "one peer list per partition";
+  out->assign(N, VerifyResult{});
+  errs->assign(N, "");
+  if (Epoch < 0) return "";  // :1006-1008
+  // Early return when the stored object is already valid (:1015-1027).
+  std::vector<int> todo_parts;
+  std::vector<size_t> todo;
+  std::vector<std::string> index(N);
+  for (size_t i = 0; i < N; i++) {
+    Error e = BuildEpochTreeObjectIndex(partitionIds[i], Epoch, &index[i]);
+    if (!e.empty()) return e;
+    Bytes stored;
+    EpochTreeObject obj;
+    if (db_.Get(index[i], &stored) && UnmarshalEpochTreeObject(eng_, stored, &obj).empty() && obj.Valid) {
+      (*out)[i].Valid = (*out)[i].AlreadyValid = true;
+      continue;
+    }
+    todo.push_back(i);
+    todo_parts.push_back(partitionIds[i]);
+  }
+  if (todo.empty()) return "";
+  // myTree = RawPartitionMerkleTree(p, E, E+1) for every partition at once (:1036).
+  std::vector<MerkleTree> trees;
+  Error e = RawPartitionMerkleTrees(todo_parts, Epoch, Epoch + 1, &trees);
+  if (!e.empty()) return e;
+  const uint32_t P = (uint32_t)todo.size(), B = (uint32_t)partitionBuckets_;
+  const uint64_t NI = mde_tree_internal_nodes(B);
+  size_t R = 0;
+  for (size_t i : todo) R = std::max(R, peerObjects[i].size());
+  std::vector<uint64_t> digest((size_t)P * B);
+  std::vector<int32_t> size((size_t)P * B), part(P);
+  Bytes nodes((size_t)P * NI * 32), blob;
+  std::vector<uint64_t> off{0};
+  for (uint32_t k = 0; k < P; k++) {
+    const MerkleTree& t = trees[k];
+    std::copy(t.digests().begin(), t.digests().end(), digest.begin() + (size_t)k * B);
+    for (uint32_t b = 0; b < B; b++) size[(size_t)k * B + b] = t.Leafs[b]->C->size;
+    std::copy(t.nodes().begin(), t.nodes().end(), nodes.begin() + (size_t)k * NI * 32);
+    part[k] = todo_parts[k];
+    const std::vector<Bytes>& peers = peerObjects[todo[k]];
+    for (size_t r = 0; r < R; r++) {  // a missing peer is an empty object: it yields no tree
+      if (r < peers.size()) blob.insert(blob.end(), peers[r].begin(), peers[r].end());
+      off.push_back(blob.size());
+    }
+  }
+  std::vector<uint8_t> valid(P);
+  std::vector<int32_t> vcount(P), ids((size_t)P * B), dcount(P), status((size_t)P * R + 1);
+  const uint64_t stride = mde_epoch_tree_object_max_bytes(B);
+  Bytes objs((size_t)P * stride);
+  std::vector<uint32_t> olen(P);
+  int rc = mde_verify_epochs(eng_.ctx(), P, B, part.data(), Epoch, digest.data(), size.data(), nodes.data(),
+                             (uint32_t)R, blob.data(), off.data(), (uint32_t)replicaCount, valid.data(),
+                             vcount.data(), ids.data(), dcount.data(), status.data(), objs.data(), stride,
+                             olen.data());
+  if (rc != MDE_OK) return eng_.error(rc);
+  for (uint32_t k = 0; k < P; k++) {
+    VerifyResult& v = (*out)[todo[k]];
+    v.Valid = valid[k] != 0;
+    v.ValidCount = vcount[k];
+    v.Trees = (int)peerObjects[todo[k]].size();
+    v.DiffSet.assign(ids.begin() + (size_t)k * B, ids.begin() + (size_t)k * B + dcount[k]);
+    // persist the epoch object (:1049, :1102): Valid set when verified
+    db_.Put(index[todo[k]], Bytes(objs.begin() + (size_t)k * stride, objs.begin() + (size_t)k * stride + olen[k]));
+    if (!v.Valid)
+      (*errs)[todo[k]] = "validCount= " + std::to_string(v.ValidCount) + "<" + std::to_string(replicaCount) +
+                         " Epoch " + std::to_string(Epoch) + " trees " + std::to_string(v.Trees) +
+                         " diffSet= " + std::to_string(v.DiffSet.size());
   }
   return "";
 }

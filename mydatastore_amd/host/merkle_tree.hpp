@@ -11,6 +11,7 @@
 //   MerkleTreeToPartitionEpochObject  main/merkle_tree.go:118-138  (leaf walk, host)
 //   EpochTreeObjectToMerkleTree       main/merkle_tree.go:140-157  -> mde_tree_from_digests
 //   DifferentMerkleTreeBuckets        main/merkle_tree.go:159-216  -> mde_diff
+//   Manager.VerifyEpoch               main/manager.go:998-1118     -> mde_verify_epochs
 //   CustomHash / MerkleBucket         main/merkle_tree.go:21-84
 //   merkletree.MerkleTree / Node      cbergoon/merkletree v0.2.0 (Root, Leafs, MerkleRoot, Left,
 //                                     Right, Hash, C)
@@ -200,6 +201,26 @@ class Manager {
                                 int64_t upperEpoch, std::vector<MerkleTree>* out);
   // Tagging through the engine (getKeyBucket main/manager.go:773-778, FindPartitionID).
   Error KeyTags(const std::string& key, uint64_t* bucket, int* partition);
+
+  // Manager.VerifyEpoch (main/manager.go:998-1118) without the network: peerObjects are the wire
+  // bytes EpochTreeObjectRequest (:729-771) returned for this partition and epoch. Returns nil
+  // when the epoch object is (or already was) valid, else the reference's "validCount= ..." error;
+  // *out carries the decision and diffSet.List() (ascending), the bucket list
+  // PoliteStreamRequest would ask for. The object persisted under epochtree_{p}_{E} is the one the
+  // reference leaves there.
+  struct VerifyResult {
+    bool Valid = false;
+    bool AlreadyValid = false;  // stored object already valid: early return (:1020-1027)
+    int ValidCount = 0;
+    int Trees = 0;              // peer objects considered
+    std::vector<int32_t> DiffSet;
+  };
+  Error VerifyEpoch(int PartitionId, int64_t Epoch, const std::vector<Bytes>& peerObjects, int replicaCount,
+                    VerifyResult* out);
+  // Batched: one build and one verify call for many partitions of the same epoch.
+  Error VerifyEpochs(const std::vector<int>& partitionIds, int64_t Epoch,
+                     const std::vector<std::vector<Bytes>>& peerObjects, int replicaCount,
+                     std::vector<VerifyResult>* out, std::vector<Error>* errs);
 
   MemStorage& db() { return db_; }
   int PartitionBuckets() const { return partitionBuckets_; }

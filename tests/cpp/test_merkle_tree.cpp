@@ -192,6 +192,65 @@ static void TestManagerStorage(Engine& eng, int writeValuesNum) {
   CHECK(!manager.SetValue({"kk", "b", 5, 50}).empty(), "a newer value already exists");
 }
 
+// Manager.VerifyEpoch (main/manager.go:998-1118) with the peer fetch replaced by the objects
+// three replicas would serve: A and B hold the same writes, C misses some and has others.
+// Prints "VERIFY <case> <valid> <validCount> <diffSet>" for tests/test_cpp_port.py to check
+// against the oracle.
+static Bytes EpochObjectBytes(Engine& eng, Manager& m, int p, int64_t e) {
+  MerkleTree t;
+  EpochTreeObject o;
+  Bytes w;
+  CHECK_OK(m.RawPartitionMerkleTree(p, e, e + 1, &t));
+  CHECK_OK(MerkleTreeToPartitionEpochObject(t, p, e, e + 1, &o));
+  CHECK_OK(MarshalEpochTreeObject(eng, o, &w));
+  return w;
+}
+
+static void TestVerifyEpoch(Engine& eng) {
+  Manager a(eng, 1, 16), b(eng, 1, 16), c(eng, 1, 16);
+  for (int i = 0; i < 40; i++) {
+    Value v{"key" + std::to_string(i), "val" + std::to_string(i), 1, i + 1};
+    CHECK_OK(a.SetValue(v));
+    CHECK_OK(b.SetValue(v));
+    if (i < 35) CHECK_OK(c.SetValue(v));
+  }
+  for (int i = 0; i < 3; i++) CHECK_OK(c.SetValue({"other" + std::to_string(i), "x", 1, 100 + i}));
+  const Bytes oa = EpochObjectBytes(eng, a, 0, 1), ob = EpochObjectBytes(eng, b, 0, 1),
+              oc = EpochObjectBytes(eng, c, 0, 1);
+  auto show = [](const char* name, const Manager::VerifyResult& r) {
+    std::printf("VERIFY %s %d %d %s\n", name, r.Valid ? 1 : 0, r.ValidCount, ids(r.DiffSet).c_str());
+  };
+  Manager::VerifyResult r;
+  Error e = a.VerifyEpoch(0, 1, {oa, ob, oc}, 3, &r);  // 2 agreeing trees < ReplicaCount 3
+  CHECK(!e.empty() && !r.Valid && r.ValidCount == 2 && !r.DiffSet.empty(), "not verified");
+  show("a_r3", r);
+  Bytes stored;
+  EpochTreeObject so;
+  std::string idx;
+  CHECK_OK(BuildEpochTreeObjectIndex(0, 1, &idx));
+  CHECK(a.db().Get(idx, &stored), "epoch object persisted");
+  CHECK_OK(UnmarshalEpochTreeObject(eng, stored, &so));
+  CHECK(!so.Valid && so.LowerEpoch == 1 && so.UpperEpoch == 2, "persisted object is not valid");
+  CHECK_OK(a.VerifyEpoch(0, 1, {oa, ob, oc}, 2, &r));  // now enough agreeing trees
+  CHECK(r.Valid && !r.AlreadyValid && r.ValidCount == 2, "verified");
+  show("a_r2", r);
+  CHECK(a.db().Get(idx, &stored), "epoch object persisted");
+  CHECK_OK(UnmarshalEpochTreeObject(eng, stored, &so));
+  CHECK(so.Valid, "persisted object is valid");
+  CHECK_OK(a.VerifyEpoch(0, 1, {}, 3, &r));  // stored object valid: early return
+  CHECK(r.Valid && r.AlreadyValid, "already valid");
+  // C disagrees with a peer object that is marked valid -> validDiff
+  CHECK_OK(c.VerifyEpoch(0, 1, {oc, stored, Bytes{0xff}}, 3, &r));
+  CHECK(r.Valid && r.ValidCount == 1, "valid by a differing valid tree");
+  show("c_vd", r);
+  // batched form over partitions of one epoch (the only partition here, twice)
+  std::vector<Manager::VerifyResult> rs;
+  std::vector<Error> es;
+  CHECK_OK(b.VerifyEpochs({0}, 1, {{oa, oc}}, 2, &rs, &es));
+  CHECK(rs.size() == 1 && !rs[0].Valid && !es[0].empty(), "batched verify");
+  show("b_r2", rs[0]);
+}
+
 int main() {
   Engine eng(0);
   if (!eng.ok()) {
@@ -203,6 +262,7 @@ int main() {
   TestIndexManager();
   TestIndexStorage();
   TestManagerStorage(eng, 100);
+  TestVerifyEpoch(eng);
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);
     return 1;

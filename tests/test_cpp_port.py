@@ -30,3 +30,31 @@ def test_cpp_port_matches_golden(golden):
         assert int(lines[("ITEMS", f"n{n}_0_3")]) == fix["trees"]["0_3"]["items"]
         assert lines[("WIRE", f"n{n}_0_3")] == fix["trees"]["0_3"]["wire"]
     assert "PASS" in r.stdout
+    got = {ln.split()[1]: ln.split()[2:] for ln in r.stdout.splitlines() if ln.startswith("VERIFY")}
+    for name, res in _verify_expected().items():
+        diff = ",".join(map(str, res["diff"]))
+        assert got[name] == [str(int(res["valid"])), str(res["valid_count"])] + ([diff] if diff else []), name
+
+
+def _verify_expected():
+    """The TestVerifyEpoch scenario of tests/cpp/test_merkle_tree.cpp on the oracle."""
+    from oracle import oracle as O
+    from oracle import wire_pb
+    a, b, c = (O.Manager(1, 16) for _ in range(3))
+    for i in range(40):
+        for m in (a, b) + ((c,) if i < 35 else ()):
+            m.set_value(f"key{i}", f"val{i}", 1, i + 1)
+    for i in range(3):
+        c.set_value(f"other{i}", "x", 1, 100 + i)
+    trees = {k: m.raw_partition_merkle_tree(0, 1, 2) for k, m in (("a", a), ("b", b), ("c", c))}
+
+    def wire(t):
+        o = O.merkle_tree_to_partition_epoch_object(t, 0, 1, 2)
+        return wire_pb.marshal(0, 1, 2, [O.decode_bytes_to_int64(h) for h in o.buckets], o.buckets_size)
+
+    oa, ob, oc = (wire(trees[k]) for k in "abc")
+    res = {"a_r3": O.verify_epoch(trees["a"], 0, 1, [oa, ob, oc], 3)}
+    res["a_r2"] = O.verify_epoch(trees["a"], 0, 1, [oa, ob, oc], 2)
+    res["c_vd"] = O.verify_epoch(trees["c"], 0, 1, [oc, res["a_r2"]["object"], b"\xff"], 3)
+    res["b_r2"] = O.verify_epoch(trees["b"], 0, 1, [oa, oc], 2)
+    return res
