@@ -27,8 +27,8 @@ namespace mde {
 namespace {
 
 constexpr int kThreads = 128;  // 2 waves: 4 workgroups per CU fit their LDS bins
-constexpr int kU = 4;                       // 16-byte loads per lane per step
-constexpr uint64_t kStep = 1024ull * kU;    // 4 KiB per wave step
+constexpr int kU = 8;                       // 16-byte loads per lane per step
+constexpr uint64_t kStep = 1024ull * kU;    // 8 KiB per wave step
 
 __device__ __forceinline__ uint32_t byte_mask(int lo, int hi) {
   const uint32_t mh = hi >= 4 ? 0xffffffffu : ((1u << (8 * hi)) - 1u);
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(kThreads) void tagged_digest_kernel(TaggedLaunch a)
   // record's own use would make the wait for it (vmcnt counts in order) also wait for the
   // prefetched next step.
   const bool straddles = ((V | a.shift) & 15u) != 0;  // record boundaries inside a 16-byte vector
-  const uint32_t vsh = V >= 64 && (V & (V - 1)) == 0 ? (uint32_t)__builtin_ctzll(V) : 0u;
+  const uint32_t vsh = V >= kStep / 64 && (V & (V - 1)) == 0 ? (uint32_t)__builtin_ctzll(V) : 0u;
   const uint32_t vmask = (uint32_t)V - 1u;
   const bool fast_ok = vsh != 0 && !straddles && w.sum != nullptr && start == beg;
   const uint64_t r_last = r_hi - 1;
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(kThreads) void tagged_digest_kernel(TaggedLaunch a)
       nxt_tags = load_tags(pn, nxt_r0);
       load_step(nxt, lane_base, pn, end, lane);
     }
-    // Fast step (wave-uniform): power-of-two records of >= 64 B on 16-byte boundaries, the whole
+    // Fast step (wave-uniform): power-of-two records of >= kStep/64 B on 16-byte boundaries, the whole
     // step inside [start, end) and inside partition q. Every vector then lies in one record, the
     // record index is a shift, and a step holds <= 64 records (tags by shuffle): per vector 4
     // v_sad_u8 + one ds_add, in 32-bit arithmetic.
