@@ -243,6 +243,23 @@ int mde_verify_epochs(mde_ctx* ctx, uint32_t n_partitions, uint32_t n_buckets,
                       int32_t* peer_status, uint8_t* object_out, uint64_t object_stride,
                       uint32_t* object_len);
 
+/* Device groups: one process driving G GPUs (a Go node is one process). Partitions are split
+ * into G contiguous blocks, block i built on device i: its records are one contiguous range of
+ * the host arena, so each device receives a single H2D copy, and the shards run concurrently on
+ * one host thread per device. Outputs land in the caller's arrays exactly as one mde_build over
+ * all P partitions would write them (the split never changes a result). The same device may be
+ * listed more than once (several contexts on one GPU). mde_group_ctx gives the per-device
+ * contexts for device-resident (*_async) use, e.g. partition p on device p % G. */
+typedef struct mde_group mde_group;
+int mde_group_create(const int* devices, uint32_t n_devices, mde_group** out);
+void mde_group_destroy(mde_group* group);
+uint32_t mde_group_size(const mde_group* group);
+mde_ctx* mde_group_ctx(mde_group* group, uint32_t i);
+const char* mde_group_last_error(const mde_group* group);
+/* RawPartitionMerkleTree for P partitions over the group (host pointers, synchronous); same
+ * contract as mde_build. */
+int mde_multi_build(mde_group* group, const mde_records* rec, const mde_tree_out* out);
+
 /* Write-time tagging of raw keys (device): bucket = BE64(SHA256(key)[:8]) % n_buckets
  * (main/manager.go:773-778), partition = XXH64(key, 0) % n_partitions (hashring.go:108-110).
  * key i = keys[key_off[i] .. key_off[i+1]). Either output may be NULL. */

@@ -39,7 +39,8 @@ EXPORTED_SYMBOLS = (
     "mde_encode_epoch_tree_objects", "mde_encode_epoch_tree_objects_async",
     "mde_decode_epoch_tree_objects", "mde_decode_epoch_tree_objects_async", "mde_synth_tags_async", "mde_synth_values_async", "mde_dev_alloc", "mde_dev_free",
     "mde_memcpy_h2d", "mde_memcpy_d2h", "mde_verify_peer_capacity", "mde_verify_epochs",
-    "mde_verify_epochs_async",
+    "mde_verify_epochs_async", "mde_group_create", "mde_group_destroy", "mde_group_size",
+    "mde_group_ctx", "mde_group_last_error", "mde_multi_build",
 )
 
 
@@ -125,6 +126,12 @@ def load_library() -> C.CDLL:
                                         vp, vp, vp, vp, vp, vp, u64, vp]),
         "mde_verify_epochs_async": (C.c_int, [vp, u32, u32, vp, C.c_int64, vp, vp, vp, u32, vp, vp,
                                               u32, vp, vp, vp, vp, vp, vp, u64, vp]),
+        "mde_group_create": (C.c_int, [vp, u32, C.POINTER(vp)]),
+        "mde_group_destroy": (None, [vp]),
+        "mde_group_size": (u32, [vp]),
+        "mde_group_ctx": (vp, [vp, u32]),
+        "mde_group_last_error": (C.c_char_p, [vp]),
+        "mde_multi_build": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
         "mde_synth_tags_async": (C.c_int, [vp, vp, u64, u32, u32, C.c_int, u64, vp, vp]),
         "mde_synth_values_async": (C.c_int, [vp, vp, vp, u64, u32, u64]),
         "mde_dev_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
@@ -502,3 +509,59 @@ class Engine:
     def synth_values_async(self, dst, gids, n, value_len, seed):
         self._check(self.lib.mde_synth_values_async(self.ctx, _ptr(dst), _ptr(gids), n, value_len,
                                                     seed))
+
+
+class Group:
+    """mde_group: one process driving several GPUs (contiguous partition blocks per device)."""
+
+    def __init__(self, devices):
+        self.lib = load_library()
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        rc = self.lib.mde_group_create(devs, len(devices), C.byref(h))
+        if rc != MDE_OK:
+            raise MdeError(rc, f"mde_group_create({list(devices)}) failed: {self.lib.mde_strerror(rc).decode()}")
+        self.g = h
+
+    def close(self):
+        if getattr(self, "g", None):
+            self.lib.mde_group_destroy(self.g)
+            self.g = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return int(self.lib.mde_group_size(self.g))
+
+    def build(self, values, n_partitions, n_buckets, value_stride=0, value_off=None, seg_rec=None,
+              part_rec=None, bucket_tag=None, want_nodes=True):
+        """mde_multi_build from host arrays (layout A with seg_rec, or layout B with part_rec +
+        bucket_tag); same outputs as Engine.build."""
+        P, B = n_partitions, n_buckets
+        values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)
+        if value_off is not None:
+            value_off = np.ascontiguousarray(value_off, dtype=np.uint64)
+        n_rec = (value_off.size - 1) if value_off is not None else (values.size // value_stride if value_stride else 0)
+        if part_rec is not None:
+            part_rec = np.ascontiguousarray(part_rec, dtype=np.uint64)
+            bucket_tag = np.ascontiguousarray(bucket_tag, dtype=np.uint16)
+            rec = Records(_ptr(values), values.nbytes, value_stride, LAYOUT_TAGGED, 0, n_rec, P, B, 0,
+                          _ptr(bucket_tag), _ptr(part_rec))
+        else:
+            seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
+            rec = Records(_ptr(values), values.nbytes, value_stride, LAYOUT_SORTED, _ptr(value_off), n_rec, P, B,
+                          _ptr(seg_rec))
+        out = {
+            "digest": np.zeros(P * B, np.uint64), "size": np.zeros(P * B, np.int32),
+            "items": np.zeros(P, np.int32), "root": np.zeros(P * 32, np.uint8),
+            "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
+        }
+        to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
+        rc = self.lib.mde_multi_build(self.g, C.byref(rec), C.byref(to))
+        if rc != MDE_OK:
+            raise MdeError(rc, (self.lib.mde_group_last_error(self.g) or b"").decode())
+        return out

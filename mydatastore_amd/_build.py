@@ -56,7 +56,7 @@ def build_engine(verbose: bool = True) -> Path:
             _run([HIPCC, *HIP_FLAGS, *lang, "-c", src, "-o", obj], verbose)
         objs.append(obj)
     if _stale(LIB, objs):
-        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs], verbose)
+        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-pthread", "-o", LIB, *objs], verbose)
     return LIB
 
 

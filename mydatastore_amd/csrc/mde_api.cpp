@@ -16,6 +16,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mde_internal.hpp"
@@ -1146,3 +1147,114 @@ int mde_memcpy_d2h(mde_ctx* c, void* dst, const void* src, uint64_t bytes) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// Device groups: one process driving G GPUs (mde_multi_build).
+struct mde_group {
+  std::vector<mde_ctx*> ctx;
+  std::string err;
+};
+
+int mde_group_create(const int* devices, uint32_t n, mde_group** out) {
+  if (!out) return MDE_E_INVAL;
+  *out = nullptr;
+  if (!devices || !n) return MDE_E_INVAL;
+  mde_group* g = new (std::nothrow) mde_group();
+  if (!g) return MDE_E_NOMEM;
+  for (uint32_t i = 0; i < n; i++) {
+    mde_ctx* c = nullptr;
+    const int rc = mde_create(devices[i], &c);
+    if (rc != MDE_OK) {
+      mde_group_destroy(g);
+      return rc;
+    }
+    g->ctx.push_back(c);
+  }
+  *out = g;
+  return MDE_OK;
+}
+
+void mde_group_destroy(mde_group* g) {
+  if (!g) return;
+  for (mde_ctx* c : g->ctx) mde_destroy(c);
+  delete g;
+}
+
+uint32_t mde_group_size(const mde_group* g) { return g ? (uint32_t)g->ctx.size() : 0u; }
+
+mde_ctx* mde_group_ctx(mde_group* g, uint32_t i) { return g && i < g->ctx.size() ? g->ctx[i] : nullptr; }
+
+const char* mde_group_last_error(const mde_group* g) { return g ? g->err.c_str() : "null group"; }
+
+int mde_multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o) {
+  if (!g || g->ctx.empty()) return MDE_E_INVAL;
+  g->err.clear();
+  mde_ctx* c0 = g->ctx[0];
+  {
+    Guard gd(c0);
+    int rc = check_records(c0, r);
+    if (!rc) rc = check_host_records(c0, r);
+    if (!rc && (!o || !o->root)) rc = set_err(c0, MDE_E_INVAL, "out/root is NULL");
+    if (rc) {
+      g->err = c0->err;
+      return rc;
+    }
+  }
+  const uint32_t G = (uint32_t)g->ctx.size(), P = r->n_partitions, B = r->n_buckets;
+  const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
+  const uint64_t NI = mde::tree_internal(B);
+  struct Shard {
+    mde_records rec;
+    mde_tree_out out;
+    std::vector<uint64_t> seg, voff;
+    int rc = MDE_OK;
+    bool live = false;
+  };
+  std::vector<Shard> sh(G);
+  for (uint32_t i = 0; i < G; i++) {
+    // contiguous partition blocks: one contiguous record range (and byte range) per device
+    const uint64_t p0 = (uint64_t)P * i / G, p1 = (uint64_t)P * (i + 1) / G;
+    if (p0 == p1) continue;
+    Shard& s = sh[i];
+    s.live = true;
+    s.rec = *r;
+    s.rec.n_partitions = (uint32_t)(p1 - p0);
+    const uint64_t r0 = tagged ? r->part_rec[p0] : r->seg_rec[p0 * B];
+    const uint64_t r1 = tagged ? r->part_rec[p1] : r->seg_rec[p1 * B];
+    const uint64_t b0 = r->value_stride ? r0 * r->value_stride : r->value_off[r0];
+    const uint64_t b1 = r->value_stride ? r1 * r->value_stride : r->value_off[r1];
+    s.rec.values = r->values + b0;
+    s.rec.values_bytes = b1 - b0;
+    s.rec.n_records = r1 - r0;
+    if (tagged) {
+      s.seg.assign(r->part_rec + p0, r->part_rec + p1 + 1);
+      s.rec.part_rec = s.seg.data();
+      s.rec.bucket_tag = r->bucket_tag ? r->bucket_tag + r0 : nullptr;
+    } else {
+      s.seg.assign(r->seg_rec + p0 * B, r->seg_rec + p1 * B + 1);
+      s.rec.seg_rec = s.seg.data();
+    }
+    for (uint64_t& x : s.seg) x -= r0;
+    if (!r->value_stride) {
+      s.voff.assign(r->value_off + r0, r->value_off + r1 + 1);
+      for (uint64_t& x : s.voff) x -= b0;
+      s.rec.value_off = s.voff.data();
+    }
+    s.out.digest = o->digest ? o->digest + p0 * B : nullptr;
+    s.out.size = o->size ? o->size + p0 * B : nullptr;
+    s.out.items = o->items ? o->items + p0 : nullptr;
+    s.out.root = o->root + p0 * 32;
+    s.out.nodes = o->nodes ? o->nodes + p0 * NI * 32 : nullptr;
+  }
+  // one host thread per device: each shard's H2D, build and D2H run concurrently
+  std::vector<std::thread> th;
+  for (uint32_t i = 0; i < G; i++)
+    if (sh[i].live) th.emplace_back([&, i] { sh[i].rc = mde_build(g->ctx[i], &sh[i].rec, &sh[i].out); });
+  for (auto& t : th) t.join();
+  for (uint32_t i = 0; i < G; i++)
+    if (sh[i].rc != MDE_OK) {
+      g->err = "device " + std::to_string(g->ctx[i]->device) + ": " + g->ctx[i]->err;
+      return sh[i].rc;
+    }
+  return MDE_OK;
+}

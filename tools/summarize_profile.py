@@ -2,7 +2,7 @@
 """Summarize a tools/profile.sh run (rocprofv3 CSVs) into profiles/<tag>_<cfg>.json and update
 profiles/pmc_traffic.json, which bench.py reads for roofline.traffic.
 
-    python tools/summarize_profile.py gpurun_out/prof_r01_c4 r01 c4
+    python tools/summarize_profile.py gpurun_out/prof_r01_c4 r01 c4      (label c4_b for --layout b)
 
 HBM bytes per launch = FETCH_SIZE (KiB) x 1024 x 2: on gfx950 FETCH_SIZE reports exactly half of a
 wide coalesced streaming read (MI355X_MICROARCH.md, section HBM).
@@ -23,8 +23,9 @@ def rows(path):
 
 
 def short(name):
-    for k in ("bucket_digest_kernel", "tree_kernel", "diff_kernel", "synth_values_kernel",
-              "synth_tags_kernel", "tag_keys_kernel"):
+    for k in ("bucket_digest_kernel", "tagged_digest_kernel", "tree_kernel", "diff_kernel",
+              "synth_values_kernel", "synth_tags_kernel", "tag_keys_kernel", "verify_kernel",
+              "encode_kernel", "decode_kernel", "extract"):
         if k in name:
             return k
     return name[:60]
@@ -40,16 +41,18 @@ def main(src, tag, cfg):
             "max_ns": float(r["MaxNs"]), "pct": float(r["Percentage"])})
     bench = json.loads((src / "bench_trace.json").read_text())
     alg = bench["roofline"]["algorithmic_bytes_per_launch"]
+    kern = bench["roofline"].get("kernel", "bucket_digest_kernel")
+    out["dominant_kernel"] = kern
     for kind, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         f = src / f"pmc_{kind}" / "run_counter_collection.csv"
         if not f.exists():
             continue
         vals = [float(r["Counter_Value"]) for r in rows(f)
-                if "bucket_digest_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+                if kern in r["Kernel_Name"] and r["Counter_Name"] == counter]
         if vals:
             out[f"digest_{counter}_kib_median"] = statistics.median(vals)
     fk = out.get("digest_FETCH_SIZE_kib_median")
-    dk = out["kernels"].get("bucket_digest_kernel")
+    dk = out["kernels"].get(kern)
     if fk and dk:
         hbm = int(fk * 1024 * 2)
         out["digest_hbm_read_bytes_per_launch"] = hbm
