@@ -163,6 +163,8 @@ int mde_diff_digests(mde_ctx* ctx, uint32_t n_pairs, uint32_t n_buckets_a, const
  * records of the buckets ids[p*ids_stride .. +counts[p]) (duplicates removed -- VerifyEpoch's
  * Int32Set, main/manager.go:1086; counts[p] < 0 extracts nothing), in ascending bucket order and
  * LSM record order. Feed it mde_diff's output directly. n_buckets <= 65536.
+ * Layout B records (MDE_LAYOUT_TAGGED): the same record set, in arrival order (a bucket's records
+ * are not contiguous there).
  * part_off[P+1]: record offsets of each partition in out_rec / out_value_off;
  * out_rec[rec_cap]: source record indices; out_values[bytes_cap] (optional): the value bytes,
  * concatenated; out_value_off[rec_cap+1] (optional): byte offset of each extracted value in

@@ -263,16 +263,23 @@ class Engine:
         return out
 
     def build_streamed(self, values, seg_rec, n_partitions, n_buckets, value_stride=0,
-                       value_off=None, chunk_bytes=0, want_nodes=True):
+                       value_off=None, chunk_bytes=0, want_nodes=True, part_rec=None, bucket_tag=None):
         """mde_build_streamed: host arena streamed through a two-slot device ring. `values` may
-        be a numpy array or a (pinned) CPU torch tensor."""
+        be a numpy array or a (pinned) CPU torch tensor. Layout B: pass part_rec + bucket_tag
+        (seg_rec None)."""
         P, B = n_partitions, n_buckets
-        seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
         if value_off is not None:
             value_off = np.ascontiguousarray(value_off, dtype=np.uint64)
         nbytes = _nbytes(values)
         n_rec = (value_off.size - 1) if value_off is not None else (nbytes // value_stride if value_stride else 0)
-        rec = Records(_ptr(values), nbytes, value_stride, 0, _ptr(value_off), n_rec, P, B, _ptr(seg_rec))
+        if part_rec is not None:
+            part_rec = np.ascontiguousarray(part_rec, dtype=np.uint64)
+            bucket_tag = np.ascontiguousarray(bucket_tag, dtype=np.uint16)
+            rec = Records(_ptr(values), nbytes, value_stride, LAYOUT_TAGGED, 0, n_rec, P, B, 0,
+                          _ptr(bucket_tag), _ptr(part_rec))
+        else:
+            seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
+            rec = Records(_ptr(values), nbytes, value_stride, 0, _ptr(value_off), n_rec, P, B, _ptr(seg_rec))
         out = {
             "digest": np.zeros(P * B, np.uint64), "size": np.zeros(P * B, np.int32),
             "items": np.zeros(P, np.int32), "root": np.zeros(P * 32, np.uint8),
@@ -356,17 +363,24 @@ class Engine:
 
     # -- out-of-sync range extract (StreamBucketsTask) ----------------------------------------
     def extract(self, values, seg_rec, n_partitions, n_buckets, ids, ids_stride, counts,
-                value_stride=0, value_off=None, want_values=True):
-        """Records of the listed buckets per partition (dedup, ascending bucket, LSM order).
+                value_stride=0, value_off=None, want_values=True, part_rec=None, bucket_tag=None):
+        """Records of the listed buckets per partition (dedup; layout A: ascending bucket, LSM
+        order; layout B -- part_rec + bucket_tag instead of seg_rec -- arrival order).
         Returns (part_off, rec_idx, values_bytes, value_off)."""
-        seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
         values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)
         if value_off is not None:
             value_off = np.ascontiguousarray(value_off, dtype=np.uint64)
         n_rec = (value_off.size - 1) if value_off is not None else (
             values.size // value_stride if value_stride else 0)
-        rec = Records(_ptr(values), values.nbytes, value_stride, 0, _ptr(value_off), n_rec,
-                      n_partitions, n_buckets, _ptr(seg_rec))
+        if part_rec is not None:
+            part_rec = np.ascontiguousarray(part_rec, dtype=np.uint64)
+            bucket_tag = np.ascontiguousarray(bucket_tag, dtype=np.uint16)
+            rec = Records(_ptr(values), values.nbytes, value_stride, LAYOUT_TAGGED, 0, n_rec,
+                          n_partitions, n_buckets, 0, _ptr(bucket_tag), _ptr(part_rec))
+        else:
+            seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
+            rec = Records(_ptr(values), values.nbytes, value_stride, 0, _ptr(value_off), n_rec,
+                          n_partitions, n_buckets, _ptr(seg_rec))
         ids = np.ascontiguousarray(ids, dtype=np.int32)
         counts = np.ascontiguousarray(counts, dtype=np.int32)
         rec_cap = max(int(n_rec), 1)

@@ -11,6 +11,11 @@
 // buckets, record/byte totals), scan (one workgroup: exclusive prefix sums + capacity check),
 // copy (one workgroup per partition: record indices, value byte offsets and the value bytes,
 // 16-byte vector copies when source and destination allow it).
+//
+// Layout B (records in write order with bucket tags): the same record set, found by testing every
+// record's tag against the bitmap (a stream compaction over the partition, 2 bytes of tag read
+// per record) and emitted in arrival order -- a bucket's records are not contiguous there, and
+// the reference's order within a bucket is LSM key order, which write order does not carry.
 #include "mde_device.hpp"
 #include "mde_internal.hpp"
 
@@ -41,7 +46,12 @@ __global__ __launch_bounds__(kThreads) void extract_count_kernel(ExtractLaunch a
   if (threadIdx.x == 0) { tot[0] = 0; tot[1] = 0; }
   load_bitmap(a, p, bm);
   unsigned long long nr = 0, nb = 0;
-  for (uint32_t b = threadIdx.x; b < a.B; b += kThreads) {
+  if (a.tag) {  // layout B: test every record's tag
+    for (uint64_t r = a.part_rec[p] + threadIdx.x; r < a.part_rec[p + 1]; r += kThreads)
+      nr += marked(bm, min((uint32_t)a.tag[r], a.B - 1)) ? 1u : 0u;
+    nb = nr * a.stride;
+  }
+  for (uint32_t b = threadIdx.x; b < a.B && !a.tag; b += kThreads) {
     if (!marked(bm, b)) continue;
     const uint32_t s = p * a.B + b;
     nr += a.seg.seg_rec[s + 1] - a.seg.seg_rec[s];
@@ -94,6 +104,57 @@ __global__ __launch_bounds__(kThreads) void extract_scan_kernel(ExtractLaunch a)
     const bool over = carry[0] > a.rec_cap || (a.out_values && carry[1] > a.bytes_cap);
     *a.status = over ? -5 /* MDE_E_CAPACITY */ : 0;
   }
+}
+
+// Layout B copy: chunks of kThreads records in arrival order, a block prefix sum over the
+// "requested" flags places them; each wave then copies the values of every 4th selected record.
+__global__ __launch_bounds__(kThreads) void extract_copy_tagged_kernel(ExtractLaunch a) {
+  __shared__ uint32_t bm[kBitmapWords];
+  __shared__ uint32_t wave_tot[kThreads / 64];
+  __shared__ uint64_t sel[kThreads];
+  const uint32_t p = blockIdx.x;
+  if (*a.status != 0) return;  // capacity exceeded: nothing is written
+  load_bitmap(a, p, bm);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t V = a.stride;
+  uint64_t rb = a.part_off[p];
+  const uint64_t bb0 = a.scratch[2 * (a.P + 1) + p], rb0 = rb;
+  for (uint64_t c0 = a.part_rec[p]; c0 < a.part_rec[p + 1]; c0 += kThreads) {
+    const uint64_t r = c0 + threadIdx.x;
+    const bool m = r < a.part_rec[p + 1] && marked(bm, min((uint32_t)a.tag[r], a.B - 1));
+    const uint64_t bal = __ballot(m);
+    if (lane == 0) wave_tot[wid] = __popcll(bal);
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int w = 0; w < kThreads / 64; w++) {
+      off += w < wid ? wave_tot[w] : 0u;
+      tot += wave_tot[w];
+    }
+    const uint32_t pos = off + __popcll(bal & ((1ull << lane) - 1ull));
+    if (m) {
+      sel[pos] = r;
+      a.out_rec[rb + pos] = r;
+      if (a.out_value_off) a.out_value_off[rb + pos] = bb0 + (rb + pos - rb0) * V;
+    }
+    __syncthreads();
+    if (a.out_values) {
+      for (uint32_t k = wid; k < tot; k += kThreads / 64) {
+        const uint8_t* src = a.values + sel[k] * V;
+        uint8_t* dst = a.out_values + bb0 + (rb + k - rb0) * V;
+        if ((((uintptr_t)src | (uintptr_t)dst | V) & 15u) == 0) {
+          const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+          u32x4* d4 = reinterpret_cast<u32x4*>(dst);
+          for (uint64_t i = lane; i < V / 16; i += 64) d4[i] = __builtin_nontemporal_load(s4 + i);
+        } else {
+          for (uint64_t i = lane; i < V; i += 64) dst[i] = src[i];
+        }
+      }
+    }
+    rb += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && p == a.P - 1 && a.out_value_off)
+    a.out_value_off[a.part_off[a.P]] = a.scratch[2 * (a.P + 1) + a.P];
 }
 
 __global__ __launch_bounds__(kThreads) void extract_copy_kernel(ExtractLaunch a) {
@@ -157,7 +218,10 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
   if (a.P == 0) return hipSuccess;
   hipLaunchKernelGGL(extract_count_kernel, dim3(a.P), dim3(kThreads), 0, st, a);
   hipLaunchKernelGGL(extract_scan_kernel, dim3(1), dim3(kThreads), 0, st, a);
-  hipLaunchKernelGGL(extract_copy_kernel, dim3(a.P), dim3(kThreads), 0, st, a);
+  if (a.tag)
+    hipLaunchKernelGGL(extract_copy_tagged_kernel, dim3(a.P), dim3(kThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL(extract_copy_kernel, dim3(a.P), dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 

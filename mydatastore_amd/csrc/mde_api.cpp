@@ -199,7 +199,9 @@ int check_host_records(mde_ctx* c, const mde_records* r) {
   return MDE_OK;
 }
 
-int tagged_async(mde_ctx* c, const mde_records* r) {
+// span: bytes the records cover (0 = values_bytes); a streamed chunk passes a biased values
+// pointer whose values_bytes includes the bias.
+int tagged_async(mde_ctx* c, const mde_records* r, uint64_t span = 0) {
   mde::TaggedLaunch t{};
   const uintptr_t v = reinterpret_cast<uintptr_t>(r->values);
   t.base = reinterpret_cast<const uint8_t*>(v & ~uintptr_t(15));
@@ -212,7 +214,7 @@ int tagged_async(mde_ctx* c, const mde_records* r) {
   t.B = r->n_buckets;
   t.sums = c->sums;
   t.counts = c->counts;
-  mde::plan_tagged(r->values_bytes + t.shift, c->cus, 8, &t.wave_bytes, &t.n_waves);
+  mde::plan_tagged((span ? span + 16 : r->values_bytes) + t.shift, c->cus, 8, &t.wave_bytes, &t.n_waves);
   MDE_HIP(c, mde::launch_tagged_digest(t, c->stream));
   return MDE_OK;
 }
@@ -242,6 +244,7 @@ int digest_async_biased(mde_ctx* c, const mde_records* r, uint64_t end_pos, uint
   int rc = ensure_sums(c, S);
   if (rc) return rc;
   if (S == 0 || r->n_records == 0) return MDE_OK;
+  if (r->layout == MDE_LAYOUT_TAGGED) return tagged_async(c, r, span);
   mde::DigestLaunch a{};
   a.seg = seg_desc(r);
   a.seg.end = a.seg.shift + end_pos;
@@ -286,7 +289,6 @@ int tree_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
 int extract_async(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t ids_stride,
                   const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
                   uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap, int32_t* status) {
-  if (r->layout != MDE_LAYOUT_SORTED) return set_err(c, MDE_E_INVAL, "extract takes layout A");
   if (r->n_buckets > mde::kExtractMaxBuckets)
     return set_err(c, MDE_E_INVAL, "extract supports n_buckets <= %u", mde::kExtractMaxBuckets);
   if (!ids || !counts || !part_off || !out_rec || !status || (out_values && !r->values))
@@ -294,7 +296,13 @@ int extract_async(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t
   int rc = ensure_buf(c, c->extract_scratch, 3 * ((uint64_t)r->n_partitions + 1) * 8);
   if (rc) return rc;
   mde::ExtractLaunch a{};
-  a.seg = seg_desc(r);
+  if (r->layout == MDE_LAYOUT_TAGGED) {
+    a.tag = r->bucket_tag;
+    a.part_rec = r->part_rec;
+    a.stride = r->value_stride;
+  } else {
+    a.seg = seg_desc(r);
+  }
   a.values = r->values;
   a.P = r->n_partitions;
   a.B = r->n_buckets;
@@ -523,7 +531,6 @@ int mde_build_streamed(mde_ctx* c, const mde_records* r, const mde_tree_out* o, 
   Guard g(c);
   int rc = check_records(c, r);
   if (rc) return rc;
-  if (r->layout != MDE_LAYOUT_SORTED) return set_err(c, MDE_E_INVAL, "mde_build_streamed takes layout A");
   if ((rc = check_host_records(c, r))) return rc;
   if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
   if (!chunk_bytes) chunk_bytes = 256ull << 20;
@@ -535,25 +542,30 @@ int mde_build_streamed(mde_ctx* c, const mde_records* r, const mde_tree_out* o, 
     }
   }
   const uint32_t P = r->n_partitions, B = r->n_buckets;
+  const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
   const uint64_t NI = mde::tree_internal(B);
   auto pos = [&](uint64_t rr) { return r->value_stride ? rr * r->value_stride : r->value_off[rr]; };
+  // first record of partition p (p <= P); layout A: of its first bucket segment
+  auto prec = [&](uint64_t p) { return tagged ? r->part_rec[p] : r->seg_rec[p * B]; };
+  const uint64_t per_part = tagged ? 1 : B;  // index entries per partition
   // Chunks of whole partitions, ~chunk_bytes each.
   std::vector<uint32_t> cuts{0};
   uint64_t max_bytes = 0, max_recs = 0, max_parts = 0;
   for (uint32_t p = 0; p < P;) {
-    const uint64_t b0 = pos(r->seg_rec[(uint64_t)p * B]);
+    const uint64_t b0 = pos(prec(p));
     uint32_t q = p + 1;
-    while (q < P && pos(r->seg_rec[(uint64_t)(q + 1) * B]) - b0 <= chunk_bytes) q++;
+    while (q < P && pos(prec(q + 1)) - b0 <= chunk_bytes) q++;
     cuts.push_back(q);
-    max_bytes = std::max(max_bytes, pos(r->seg_rec[(uint64_t)q * B]) - b0);
-    max_recs = std::max(max_recs, r->seg_rec[(uint64_t)q * B] - r->seg_rec[(uint64_t)p * B]);
+    max_bytes = std::max(max_bytes, pos(prec(q)) - b0);
+    max_recs = std::max(max_recs, prec(q) - prec(p));
     max_parts = std::max<uint64_t>(max_parts, q - p);
     p = q;
   }
   for (int i = 0; i < 2; i++) {
     if ((rc = ensure_buf(c, c->ring_vals[i], max_bytes + 32))) return rc;
-    if ((rc = ensure_buf(c, c->ring_seg[i], (max_parts * B + 1) * 8))) return rc;
+    if ((rc = ensure_buf(c, c->ring_seg[i], (max_parts * per_part + 1) * 8))) return rc;
     if (!r->value_stride && (rc = ensure_buf(c, c->ring_voff[i], (max_recs + 1) * 8))) return rc;
+    if (tagged && (rc = ensure_buf(c, c->ring_voff[i], max_recs * 2 + 16))) return rc;  // tags
   }
   // Device outputs for the whole build (host copies at the end).
   const uint64_t S = (uint64_t)P * B;
@@ -570,7 +582,7 @@ int mde_build_streamed(mde_ctx* c, const mde_records* r, const mde_tree_out* o, 
   for (size_t k = 0; k + 1 < cuts.size(); k++) {
     const int slot = (int)(k & 1);
     const uint32_t p0 = cuts[k], p1 = cuts[k + 1];
-    const uint64_t r0 = r->seg_rec[(uint64_t)p0 * B], r1 = r->seg_rec[(uint64_t)p1 * B];
+    const uint64_t r0 = prec(p0), r1 = prec(p1);
     const uint64_t byte0 = pos(r0), byte1 = pos(r1);
     uint8_t* vslot = static_cast<uint8_t*>(c->ring_vals[slot].p);
     // copy stream: wait until the build two chunks back released this slot, then load
@@ -578,8 +590,11 @@ int mde_build_streamed(mde_ctx* c, const mde_records* r, const mde_tree_out* o, 
     if (byte1 > byte0)
       MDE_HIP(c, hipMemcpyAsync(vslot + (byte0 & 15), r->values + byte0, byte1 - byte0,
                                 hipMemcpyHostToDevice, c->copy_stream));
-    MDE_HIP(c, hipMemcpyAsync(c->ring_seg[slot].p, r->seg_rec + (uint64_t)p0 * B,
-                              ((uint64_t)(p1 - p0) * B + 1) * 8, hipMemcpyHostToDevice, c->copy_stream));
+    MDE_HIP(c, hipMemcpyAsync(c->ring_seg[slot].p, tagged ? r->part_rec + p0 : r->seg_rec + (uint64_t)p0 * B,
+                              ((uint64_t)(p1 - p0) * per_part + 1) * 8, hipMemcpyHostToDevice, c->copy_stream));
+    if (tagged && r1 > r0)
+      MDE_HIP(c, hipMemcpyAsync(c->ring_voff[slot].p, r->bucket_tag + r0, (r1 - r0) * 2, hipMemcpyHostToDevice,
+                                c->copy_stream));
     if (!r->value_stride)
       MDE_HIP(c, hipMemcpyAsync(c->ring_voff[slot].p, r->value_off + r0, (r1 - r0 + 1) * 8,
                                 hipMemcpyHostToDevice, c->copy_stream));
@@ -592,7 +607,12 @@ int mde_build_streamed(mde_ctx* c, const mde_records* r, const mde_tree_out* o, 
     cr.values_bytes = byte1 - (byte0 & ~uint64_t(15));
     cr.value_off = r->value_stride ? nullptr : static_cast<const uint64_t*>(c->ring_voff[slot].p) - r0;
     cr.n_partitions = p1 - p0;
-    cr.seg_rec = static_cast<const uint64_t*>(c->ring_seg[slot].p);
+    if (tagged) {  // part_rec keeps global record indices; the tags pointer is biased like values
+      cr.part_rec = static_cast<const uint64_t*>(c->ring_seg[slot].p);
+      cr.bucket_tag = static_cast<const uint16_t*>(c->ring_voff[slot].p) - r0;
+    } else {
+      cr.seg_rec = static_cast<const uint64_t*>(c->ring_seg[slot].p);
+    }
     mde_tree_out co{d_digest + (uint64_t)p0 * B, d_size + (uint64_t)p0 * B, d_items + p0,
                     d_root + (uint64_t)p0 * 32, d_nodes ? d_nodes + (uint64_t)p0 * NI * 32 : nullptr};
     if (byte1 > byte0 && (rc = digest_async_biased(c, &cr, byte1, byte1 - byte0))) return rc;
@@ -758,23 +778,27 @@ int mde_extract(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t i
   if ((rc = check_host_records(c, r))) return rc;
   if (!ids || !counts || !part_off || !out_rec) return set_err(c, MDE_E_INVAL, "bad extract arguments");
   const uint64_t P = r->n_partitions, S = P * r->n_buckets;
+  const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
   const uint64_t nvo = r->value_stride ? 0 : (r->n_records + 1);
-  const uint64_t sz[10] = {r->values_bytes, nvo * 8, (S + 1) * 8, P * ids_stride * 4, P * 4,
+  const uint64_t sz[11] = {r->values_bytes, nvo * 8, tagged ? (P + 1) * 8 : (S + 1) * 8, P * ids_stride * 4, P * 4,
                            (P + 1) * 8, rec_cap * 8, out_values ? bytes_cap : 0,
-                           out_value_off ? (rec_cap + 1) * 8 : 0, 4};
-  for (int i = 0; i < 10; i++)
+                           out_value_off ? (rec_cap + 1) * 8 : 0, 4, tagged ? r->n_records * 2 : 0};
+  for (int i = 0; i < 11; i++)
     if ((rc = ensure_buf(c, c->stage[i], sz[i]))) return rc;
   auto dp = [&](int i) { return c->stage[i].p; };
   if (r->values_bytes)
     MDE_HIP(c, hipMemcpyAsync(dp(0), r->values, r->values_bytes, hipMemcpyHostToDevice, c->stream));
   if (nvo) MDE_HIP(c, hipMemcpyAsync(dp(1), r->value_off, nvo * 8, hipMemcpyHostToDevice, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(dp(2), r->seg_rec, (S + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  MDE_HIP(c, hipMemcpyAsync(dp(2), tagged ? r->part_rec : r->seg_rec, sz[2], hipMemcpyHostToDevice, c->stream));
+  if (tagged && sz[10]) MDE_HIP(c, hipMemcpyAsync(dp(10), r->bucket_tag, sz[10], hipMemcpyHostToDevice, c->stream));
   MDE_HIP(c, hipMemcpyAsync(dp(3), ids, sz[3], hipMemcpyHostToDevice, c->stream));
   MDE_HIP(c, hipMemcpyAsync(dp(4), counts, sz[4], hipMemcpyHostToDevice, c->stream));
   mde_records dr = *r;
   dr.values = static_cast<const uint8_t*>(dp(0));
   dr.value_off = nvo ? static_cast<const uint64_t*>(dp(1)) : nullptr;
-  dr.seg_rec = static_cast<const uint64_t*>(dp(2));
+  dr.seg_rec = tagged ? nullptr : static_cast<const uint64_t*>(dp(2));
+  dr.part_rec = tagged ? static_cast<const uint64_t*>(dp(2)) : nullptr;
+  dr.bucket_tag = tagged ? static_cast<const uint16_t*>(dp(10)) : nullptr;
   rc = extract_async(c, &dr, static_cast<const int32_t*>(dp(3)), ids_stride,
                      static_cast<const int32_t*>(dp(4)), static_cast<uint64_t*>(dp(5)),
                      static_cast<uint64_t*>(dp(6)), rec_cap,

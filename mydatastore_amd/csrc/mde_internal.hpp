@@ -121,6 +121,10 @@ struct ExtractLaunch {
   uint64_t bytes_cap;
   int32_t* status;            // MDE_OK or MDE_E_CAPACITY
   uint64_t* scratch;          // [3 * (P + 1)] device scratch
+  // layout B (tag != null): records of partition p are part_rec[p] .. part_rec[p+1], fixed stride
+  const uint16_t* tag;
+  const uint64_t* part_rec;
+  uint32_t stride;
 };
 constexpr uint32_t kExtractMaxBuckets = 1u << 16;
 hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st);

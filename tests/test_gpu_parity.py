@@ -361,6 +361,30 @@ def test_build_streamed_matches_oracle(engine, golden, coracle):
             assert _node_shas(out, P, B) == case["nodes_sha256"]
 
 
+def test_build_streamed_layout_b(engine, golden, coracle):
+    """Host ingest of layout B (write order + tags) through the same ring, chunk sizes that split
+    the arena at every partition."""
+    from tests.datasets import MODES
+    for case in golden("synth_cases.json"):
+        if case["var_len"]:
+            continue
+        n, P, B, V = case["n"], case["P"], case["B"], case["value_len"]
+        gids = np.arange(n, dtype=np.uint64)
+        part, bk = coracle.synth_tags(gids, P, B, MODES[case["part_mode"]], case["keys_per_partition"])
+        order = np.argsort(part, kind="stable")
+        part_rec = np.zeros(P + 1, np.uint64)
+        np.cumsum(np.bincount(part, minlength=P), out=part_rec[1:])
+        values = coracle.synth_values(gids[order], V, case["seed"])
+        for chunk in (1, 4099, 0):
+            out = engine.build_streamed(values, None, P, B, V, chunk_bytes=chunk, part_rec=part_rec,
+                                        bucket_tag=bk[order].astype(np.uint16))
+            assert out["digest"].tolist() == case["digest"], (case["name"], chunk)
+            assert out["size"].tolist() == case["size"], (case["name"], chunk)
+            assert out["items"].tolist() == case["items"], (case["name"], chunk)
+            assert _roots(out, P) == case["root"], (case["name"], chunk)
+            assert _node_shas(out, P, B) == case["nodes_sha256"], (case["name"], chunk)
+
+
 def test_layout_b_matches_fixtures(engine, golden, coracle):
     """Layout B (arrival order within a partition + bucket tags): the engine bins records into
     buckets itself; same record sets as the golden builds, identical outputs."""
@@ -454,3 +478,33 @@ def test_multi_build_group(golden, coracle, devices):
         assert ob["digest"].tolist() == case["digest"], case["name"]
         assert _roots(ob, P) == case["root"], case["name"]
     g.close()
+
+
+def test_extract_layout_b(engine):
+    """Range extract over layout B (write order + tags): the records of the requested buckets
+    (duplicates / out-of-range ids ignored), per partition in arrival order, values included."""
+    rng = np.random.default_rng(77)
+    for V, B in ((8, 30), (64, 64), (1024, 64), (37, 1000), (16, 7)):
+        P = 6
+        counts = rng.integers(0, 700, P)
+        counts[3] = 0
+        part_rec = np.zeros(P + 1, np.uint64)
+        np.cumsum(counts, out=part_rec[1:])
+        n = int(part_rec[-1])
+        tags = rng.integers(0, B, n).astype(np.uint16)
+        values = rng.integers(0, 256, n * V, dtype=np.uint8)
+        cap = 6
+        ids = rng.integers(-2, B + 2, P * cap).astype(np.int32)
+        req = rng.integers(-1, cap + 1, P).astype(np.int32)
+        part_off, rec, vbytes, voff = engine.extract(values, None, P, B, ids, cap, req, value_stride=V,
+                                                     part_rec=part_rec, bucket_tag=tags)
+        want, wpo = [], [0]
+        for p in range(P):
+            sel = {int(b) for b in ids[p * cap:p * cap + max(int(req[p]), 0)] if 0 <= b < B}
+            want += [r for r in range(int(part_rec[p]), int(part_rec[p + 1])) if int(tags[r]) in sel]
+            wpo.append(len(want))
+        assert part_off.tolist() == wpo, (V, B)
+        assert rec.tolist() == want, (V, B)
+        wv = values.reshape(max(n, 1), -1)[want].reshape(-1) if want else np.zeros(0, np.uint8)
+        assert np.array_equal(vbytes, wv), (V, B)
+        assert voff.tolist() == [i * V for i in range(len(want) + 1)], (V, B)
