@@ -130,10 +130,17 @@ def end_to_end(torch, eng, w, B, reps=3):
     `value`, never as it."""
     host = torch.empty(w.values.numel(), dtype=torch.uint8, pin_memory=True)
     host.copy_(w.values)
-    seg = w.seg_rec.cpu().numpy().view(np.uint64)
     P = w.n_partitions
+    if w.bucket_tag is not None:  # layout B: write order + tags
+        pr = w.part_rec.cpu().numpy().view(np.uint64)
+        tg = w.bucket_tag.cpu().numpy().view(np.uint16)
+        build = lambda: eng.build_streamed(host, None, P, B, w.value_len, want_nodes=False, part_rec=pr,
+                                           bucket_tag=tg)
+    else:
+        seg = w.seg_rec.cpu().numpy().view(np.uint64)
+        build = lambda: eng.build_streamed(host, seg, P, B, w.value_len, want_nodes=False)
     res = {}
-    for name, fn in (("streamed_pinned", lambda: eng.build_streamed(host, seg, P, B, w.value_len, want_nodes=False)),):
+    for name, fn in (("streamed_pinned", build),):
         fn()
         t0 = time.perf_counter()
         for _ in range(reps):
@@ -414,7 +421,7 @@ def main():
             result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_baseline_seconds)
         else:
             result["cpu_baseline"] = None
-        if world == 1 and not args.no_e2e and not args.profile and not c5 and args.layout == "a":
+        if world == 1 and not args.no_e2e and not args.profile and not c5:
             result["end_to_end"] = end_to_end(torch, eng, w, B)
         print(json.dumps(result), flush=True)
     if world > 1:
