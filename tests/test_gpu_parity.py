@@ -508,3 +508,58 @@ def test_extract_layout_b(engine):
         wv = values.reshape(max(n, 1), -1)[want].reshape(-1) if want else np.zeros(0, np.uint8)
         assert np.array_equal(vbytes, wv), (V, B)
         assert voff.tolist() == [i * V for i in range(len(want) + 1)], (V, B)
+
+
+def test_abi_error_paths(engine):
+    """Bad arguments come back as MDE_E_* codes with a message -- never a crash or a fault."""
+    import ctypes as C
+    import mydatastore_amd as mde
+    lib, ctx = engine.lib, engine.ctx
+    vals = np.zeros(1024, np.uint8)
+    seg = np.array([0, 4, 2, 8], np.uint64)  # not nondecreasing
+    digest = np.zeros(3, np.uint64)
+    size = np.zeros(3, np.int32)
+    items = np.zeros(1, np.int32)
+    root = np.zeros(32, np.uint8)
+    out = mde.TreeOut(digest.ctypes.data, size.ctypes.data, items.ctypes.data, root.ctypes.data, 0)
+
+    def rc_of(rec):
+        return lib.mde_build(ctx, C.byref(rec), C.byref(out))
+
+    assert lib.mde_build(ctx, None, C.byref(out)) == mde.MDE_E_INVAL
+    assert rc_of(mde.Records(vals.ctypes.data, vals.nbytes, 64, 0, 0, 8, 1, 3, seg.ctypes.data)) == mde.MDE_E_INVAL
+    assert b"nondecreasing" in lib.mde_last_error(ctx)
+    good = np.array([0, 4, 6, 8], np.uint64)
+    assert rc_of(mde.Records(vals.ctypes.data, vals.nbytes, 64, 7, 0, 8, 1, 3, good.ctypes.data)) == mde.MDE_E_INVAL
+    # stride * records beyond the arena
+    assert rc_of(mde.Records(vals.ctypes.data, vals.nbytes, 256, 0, 0, 8, 1, 3, good.ctypes.data)) == mde.MDE_E_INVAL
+    # layout B: a tag out of range, a missing part_rec
+    tags = np.array([0, 1, 5, 2], np.uint16)
+    pr = np.array([0, 4], np.uint64)
+    assert rc_of(mde.Records(vals.ctypes.data, vals.nbytes, 64, 1, 0, 4, 1, 3, 0, tags.ctypes.data,
+                             pr.ctypes.data)) == mde.MDE_E_INVAL
+    assert rc_of(mde.Records(vals.ctypes.data, vals.nbytes, 64, 1, 0, 4, 1, 3, 0, tags.ctypes.data, 0)) == mde.MDE_E_INVAL
+    # capacities
+    ids = np.zeros(4, np.int32)
+    cnt = np.zeros(1, np.int32)
+    d64 = np.zeros(64, np.uint64)
+    n64 = np.zeros(mde.tree_internal_nodes(64) * 32, np.uint8)
+    assert lib.mde_diff(ctx, 1, 64, d64.ctypes.data, n64.ctypes.data, 64, d64.ctypes.data, n64.ctypes.data,
+                        ids.ctypes.data, 4, cnt.ctypes.data) == mde.MDE_E_CAPACITY
+    o = np.zeros(16, np.uint8)
+    ln = np.zeros(1, np.uint32)
+    s64 = np.zeros(64, np.int32)
+    assert lib.mde_encode_epoch_tree_objects(ctx, 1, 64, None, 0, 1, d64.ctypes.data, s64.ctypes.data, None, None,
+                                             o.ctypes.data, 16, ln.ctypes.data) == mde.MDE_E_CAPACITY
+    assert lib.mde_tree_from_digests(ctx, 1, 0, d64.ctypes.data, root.ctypes.data, None) == mde.MDE_E_INVAL
+    v = np.zeros(1, np.uint8)
+    assert lib.mde_verify_epochs(ctx, 1, 0, None, 0, d64.ctypes.data, s64.ctypes.data, n64.ctypes.data, 0, None,
+                                 None, 1, v.ctypes.data, cnt.ctypes.data, ids.ctypes.data, cnt.ctypes.data, None,
+                                 None, 0, None) == mde.MDE_E_INVAL
+    # device groups: a device that does not exist
+    devs = (C.c_int * 2)(0, 99)
+    h = C.c_void_p()
+    assert lib.mde_group_create(devs, 2, C.byref(h)) == mde.MDE_E_INVAL and not h.value
+    # the engine still works after every rejected call
+    good_out = engine.build(np.arange(256, dtype=np.uint8), np.array([0, 2, 4], np.uint64), 1, 2, 64)
+    assert good_out["size"].tolist() == [2, 2]
