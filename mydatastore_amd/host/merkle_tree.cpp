@@ -355,6 +355,74 @@ Error Manager::GetValue(const std::string& key, Value* out) {
   return "";
 }
 
+Error Manager::ScanArena(const std::vector<int>& partitionIds, int64_t lowerEpoch, int64_t upperEpoch,
+                         Bytes* arena, std::vector<uint64_t>* value_off, std::vector<uint64_t>* seg_rec,
+                         std::vector<std::string>* keys) const {
+  // Ingest: the per-bucket range scans of main/merkle_tree.go:90-113 copy each record's value into
+  // one contiguous arena (layout A); seg_rec marks the bucket boundaries.
+  const uint32_t B = (uint32_t)partitionBuckets_;
+  arena->clear();
+  *value_off = {0};
+  *seg_rec = {0};
+  if (keys) keys->clear();
+  for (int p : partitionIds) {
+    for (uint32_t b = 0; b < B; b++) {
+      std::string i1, i2;
+      Error e = BuildEpochIndex(p, b, lowerEpoch, "", &i1);
+      if (!e.empty()) return e;
+      if (!(e = BuildEpochIndex(p, b, upperEpoch, "", &i2)).empty()) return e;
+      for (Iterator it = db_.NewIterator(i1, i2); !it.IsDone(); it.Next()) {
+        const Bytes v = it.Value();
+        arena->insert(arena->end(), v.begin(), v.end());
+        value_off->push_back(arena->size());
+        if (keys) keys->push_back(it.Key());
+      }
+      seg_rec->push_back(value_off->size() - 1);
+    }
+  }
+  if (arena->empty()) arena->push_back(0);  // keep a valid pointer for an all-empty build
+  return "";
+}
+
+Error Manager::StreamBuckets(int PartitionId, const std::vector<int32_t>& Buckets, int64_t LowerEpoch,
+                             int64_t UpperEpoch, std::vector<Value>* out) {
+  out->clear();
+  const uint32_t B = (uint32_t)partitionBuckets_;
+  std::vector<int32_t> ids = Buckets;
+  if (ids.empty())  // main/manager.go:448-452
+    for (uint32_t b = 0; b < B; b++) ids.push_back((int32_t)b);
+  Bytes arena;
+  std::vector<uint64_t> value_off, seg_rec;
+  std::vector<std::string> keys;
+  Error e = ScanArena({PartitionId}, LowerEpoch, UpperEpoch, &arena, &value_off, &seg_rec, &keys);
+  if (!e.empty()) return e;
+  mde_records rec{};
+  rec.values = arena.data();
+  rec.values_bytes = arena.size();
+  rec.value_off = value_off.data();
+  rec.n_records = value_off.size() - 1;
+  rec.n_partitions = 1;
+  rec.n_buckets = B;
+  rec.seg_rec = seg_rec.data();
+  const uint64_t cap = rec.n_records ? rec.n_records : 1;
+  const int32_t count = (int32_t)ids.size();
+  std::vector<uint64_t> part_off(2), out_rec(cap), out_voff(cap + 1);
+  Bytes out_vals(arena.size());
+  int rc = mde_extract(eng_.ctx(), &rec, ids.data(), ids.size(), &count, part_off.data(), out_rec.data(), cap,
+                       out_vals.data(), out_voff.data(), out_vals.size());
+  if (rc != MDE_OK) return eng_.error(rc);
+  for (uint64_t i = 0; i < part_off[1]; i++) {
+    int p;
+    uint64_t b;
+    Value v;
+    if (!(e = ParseEpochIndex(keys[out_rec[i]], &p, &b, &v.Epoch, &v.Key)).empty()) return e;
+    const Bytes ts(out_vals.begin() + out_voff[i], out_vals.begin() + out_voff[i + 1]);
+    if (!(e = DecodeBytesToInt64(ts, &v.UnixTimestamp)).empty()) return e;
+    out->push_back(v);
+  }
+  return "";
+}
+
 Error Manager::RawPartitionMerkleTree(int partitionId, int64_t lowerEpoch, int64_t upperEpoch, MerkleTree* out) {
   std::vector<MerkleTree> trees;
   Error e = RawPartitionMerkleTrees({partitionId}, lowerEpoch, upperEpoch, &trees);
@@ -365,26 +433,11 @@ Error Manager::RawPartitionMerkleTree(int partitionId, int64_t lowerEpoch, int64
 
 Error Manager::RawPartitionMerkleTrees(const std::vector<int>& partitionIds, int64_t lowerEpoch,
                                        int64_t upperEpoch, std::vector<MerkleTree>* out) {
-  // Ingest: the per-bucket range scans of main/merkle_tree.go:90-113 copy each record's value into
-  // one contiguous arena (layout A); seg_rec marks the bucket boundaries.
   const uint32_t B = (uint32_t)partitionBuckets_, P = (uint32_t)partitionIds.size();
   Bytes arena;
-  std::vector<uint64_t> value_off{0}, seg_rec{0};
-  for (int p : partitionIds) {
-    for (uint32_t b = 0; b < B; b++) {
-      std::string i1, i2;
-      Error e = BuildEpochIndex(p, b, lowerEpoch, "", &i1);
-      if (!e.empty()) return e;
-      if (!(e = BuildEpochIndex(p, b, upperEpoch, "", &i2)).empty()) return e;
-      for (Iterator it = db_.NewIterator(i1, i2); !it.IsDone(); it.Next()) {
-        const Bytes v = it.Value();
-        arena.insert(arena.end(), v.begin(), v.end());
-        value_off.push_back(arena.size());
-      }
-      seg_rec.push_back(value_off.size() - 1);
-    }
-  }
-  if (arena.empty()) arena.push_back(0);  // keep a valid pointer for an all-empty build
+  std::vector<uint64_t> value_off, seg_rec;
+  Error se = ScanArena(partitionIds, lowerEpoch, upperEpoch, &arena, &value_off, &seg_rec, nullptr);
+  if (!se.empty()) return se;
   mde_records rec{};
   rec.values = arena.data();
   rec.values_bytes = arena.size();

@@ -202,6 +202,14 @@ class Manager {
   // Tagging through the engine (getKeyBucket main/manager.go:773-778, FindPartitionID).
   Error KeyTags(const std::string& key, uint64_t* bucket, int* partition);
 
+  // StreamBucketsTask (main/manager.go:445-487): every record (key, epoch, timestamp) of the
+  // listed buckets of a partition in [LowerEpoch, UpperEpoch); an empty list means all buckets.
+  // The range scans fill one arena and the device extract (mde_extract) selects and gathers the
+  // records: buckets de-duplicated and in ascending order (VerifyEpoch passes an Int32Set), LSM
+  // order inside a bucket.
+  Error StreamBuckets(int PartitionId, const std::vector<int32_t>& Buckets, int64_t LowerEpoch,
+                      int64_t UpperEpoch, std::vector<Value>* out);
+
   // Manager.VerifyEpoch (main/manager.go:998-1118) without the network: peerObjects are the wire
   // bytes EpochTreeObjectRequest (:729-771) returned for this partition and epoch. Returns nil
   // when the epoch object is (or already was) valid, else the reference's "validCount= ..." error;
@@ -226,6 +234,13 @@ class Manager {
   int PartitionBuckets() const { return partitionBuckets_; }
 
  private:
+  // The per-bucket range scans of main/merkle_tree.go:90-113 for several partitions, copied into
+  // one layout-A arena (values, value_off, seg_rec); keys (optional) receives each record's
+  // epoch-index key.
+  Error ScanArena(const std::vector<int>& partitionIds, int64_t lowerEpoch, int64_t upperEpoch, Bytes* arena,
+                  std::vector<uint64_t>* value_off, std::vector<uint64_t>* seg_rec,
+                  std::vector<std::string>* keys) const;
+
   Engine& eng_;
   int partitionCount_, partitionBuckets_;
   MemStorage db_;

@@ -251,6 +251,39 @@ static void TestVerifyEpoch(Engine& eng) {
   show("b_r2", rs[0]);
 }
 
+// TestStreamBucketsTask (main/manager_test.go:117-211): all buckets of epochs [0,2) stream the N
+// epoch-1 records, [0,3) all 2N; a bucket subset streams exactly that subset's records.
+static void TestStreamBucketsTask(Engine& eng, int writeValuesNum) {
+  Manager manager(eng, 1, 100);
+  for (int i = 0; i < writeValuesNum; i++)
+    CHECK_OK(manager.SetValue({"key" + std::to_string(i), "val" + std::to_string(i), 1, 0}));
+  for (int i = 0; i < writeValuesNum; i++)
+    CHECK_OK(manager.SetValue({"keyz" + std::to_string(i), "valz" + std::to_string(i), 2, 0}));
+  std::vector<Value> items;
+  CHECK_OK(manager.StreamBuckets(0, {}, 0, 2, &items));
+  CHECK((int)items.size() == writeValuesNum, "itemCount is wrong");
+  for (const Value& v : items) CHECK(v.Epoch == 1 && v.Key.rfind("key", 0) == 0, "epoch-1 records");
+  CHECK_OK(manager.StreamBuckets(0, {}, 0, 3, &items));
+  CHECK((int)items.size() == 2 * writeValuesNum, "itemCount is wrong");
+  // a subset (with a duplicate and an out-of-range id): exactly the records of those buckets
+  uint64_t b0 = 0, b1 = 0;
+  int p0;
+  CHECK_OK(manager.KeyTags(items.front().Key, &b0, &p0));
+  CHECK_OK(manager.KeyTags(items.back().Key, &b1, &p0));
+  std::vector<Value> sub;
+  CHECK_OK(manager.StreamBuckets(0, {(int32_t)b1, 99, (int32_t)b0, (int32_t)b1, 1000}, 0, 3, &sub));
+  size_t want = 0;
+  for (const Value& v : items) {
+    uint64_t b;
+    int p;
+    CHECK_OK(manager.KeyTags(v.Key, &b, &p));
+    want += (b == b0 || b == b1 || b == 99) ? 1 : 0;
+  }
+  CHECK(want >= 1, "the subset holds records");
+  CHECK(sub.size() == want, "subset stream");
+  std::printf("STREAM n%d %zu %zu %zu\n", writeValuesNum, items.size(), sub.size(), want);
+}
+
 int main() {
   Engine eng(0);
   if (!eng.ok()) {
@@ -263,6 +296,8 @@ int main() {
   TestIndexStorage();
   TestManagerStorage(eng, 100);
   TestVerifyEpoch(eng);
+  TestStreamBucketsTask(eng, 100);
+  TestStreamBucketsTask(eng, 10);
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);
     return 1;

@@ -30,6 +30,10 @@ def test_cpp_port_matches_golden(golden):
         assert int(lines[("ITEMS", f"n{n}_0_3")]) == fix["trees"]["0_3"]["items"]
         assert lines[("WIRE", f"n{n}_0_3")] == fix["trees"]["0_3"]["wire"]
     assert "PASS" in r.stdout
+    stream = {ln.split()[1]: ln.split()[2:] for ln in r.stdout.splitlines() if ln.startswith("STREAM")}
+    for n in (100, 10):  # TestStreamBucketsTask: 2N records in [0,3); the subset equals its buckets
+        total, sub, want = map(int, stream[f"n{n}"])
+        assert total == 2 * n and sub == want
     got = {ln.split()[1]: ln.split()[2:] for ln in r.stdout.splitlines() if ln.startswith("VERIFY")}
     for name, res in _verify_expected().items():
         diff = ",".join(map(str, res["diff"]))
