@@ -29,6 +29,7 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "Merkle-tree build GiB/s (device-resident KV bytes hashed/s) at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+GATHER_BUCKET = 8  # builds per root-gather collective in fused mode at N > 1
 
 CONFIGS = {
     # name: (n_keys, n_partitions, value_len, n_buckets, part_mode, description)
@@ -62,6 +63,10 @@ def parse():
                          "a per-GPU prediction, reported as such, never the N-GPU value")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each build's tree kernel on the main stream (no overlap with the next build)")
+    ap.add_argument("--pipeline", default="auto", choices=["auto", "fused", "streams", "off"],
+                    help="fused: one launch per build carries the previous build's trees "
+                         "(mde_build_pipelined_async; default for layout a); streams: tree kernel on a "
+                         "second stream (default for layout b); off: digest + tree serially")
     ap.add_argument("--tuning", default="", help="digest kernel 'variant,workgroups_per_cu' (A/B only)")
     return ap.parse_args()
 
@@ -225,7 +230,13 @@ def main():
     # builds. A build's digest kernel runs on the main stream, its tree kernel on `tstream`, so
     # build i's latency-bound tree (11 dependent SHA-256 compressions) overlaps build i+1's HBM
     # streaming instead of serializing behind it. Every build still runs both kernels in full.
-    pipeline = not args.no_pipeline and not c5
+    mode = args.pipeline
+    if args.no_pipeline or c5:
+        mode = "off"
+    elif mode == "auto":
+        mode = "fused" if args.layout == "a" else "streams"
+    fused = mode == "fused"
+    pipeline = mode == "streams"
     engines = [eng]
     tstream = None
     if pipeline:
@@ -257,15 +268,47 @@ def main():
     # Two output sets and two gather slabs: the RCCL root gather of build i runs on a side stream
     # and overlaps build i+1 (the exchange step overlapped with compute); a build's output set is
     # reused only after the gather that read it (two builds earlier) has completed.
-    outs = [(w.out, w.tree_out), w._outs()]
+    # Fused mode at N > 1 buckets the root gathers: one collective per GATHER_BUCKET builds (its
+    # output sets double-buffered: 2 x bucket sets), handed to the side stream once per bucket.
+    bucket = GATHER_BUCKET if (fused and world > 1) else 1
+    outs = [(w.out, w.tree_out)] + [w._outs() for _ in range(2 * bucket - 1)]
     outs_b = [(wb.out, wb.tree_out), wb._outs()] if c5 else None
-    gather = RootGather(P, world, dev, width=64 if c5 else 32) if world > 1 else None
+    gather = RootGather(P, world, dev, width=64 if c5 else 32, batch=bucket) if world > 1 else None
     side = torch.cuda.Stream(dev) if world > 1 else None
     ev_built = [torch.cuda.Event() for _ in range(2)]
     ev_gathered = [torch.cuda.Event() for _ in range(2)]
     n_step = [0]
 
+    def gather_bucket(last):  # RCCL gather of the bucket holding build `last` (its last build)
+        b = last // bucket
+        k = b % 2
+        ev_built[k].record(stream)
+        side.wait_event(ev_built[k])
+        with torch.cuda.stream(side):
+            gather.gather([outs[j % (2 * bucket)][0]["root"] for j in range(b * bucket, last + 1)], k)
+            ev_gathered[k].record(side)
+
+    def step_fused(ev_a=None, ev_b=None):
+        # Launch L digests build L into a scratch slot and builds the trees of build L-1 into
+        # output set (L-1) % (2 x bucket); build L's trees arrive with launch L+1 (or the drain in
+        # join()). N > 1: once launch L completes the last build of a bucket, that bucket's roots
+        # go out in one collective on the side stream; before launch L writes the first build of
+        # bucket b, the main stream waits for the gather of bucket b-2 (same output sets).
+        L = n_step[0]
+        n_step[0] += 1
+        if world > 1 and L >= 1 and (L - 1) % bucket == 0:
+            stream.wait_event(ev_gathered[((L - 1) // bucket) % 2])
+        if ev_a is not None:
+            ev_a.record(stream)
+        eng.build_pipelined_async(w.rec, outs[L % (2 * bucket)][1])
+        if ev_b is not None:
+            ev_b.record(stream)
+        if world > 1 and L >= 1 and L % bucket == 0:
+            gather_bucket(L - 1)
+
     def step(ev_a=None, ev_b=None):
+        if fused:
+            return step_fused(ev_a, ev_b)
         i = n_step[0] % 2
         n_step[0] += 1
         o, to = outs[i]
@@ -313,6 +356,12 @@ def main():
                 ev_gathered[i].record(side)
 
     def join():  # everything issued so far, on the main stream
+        if fused:
+            eng.build_pipeline_drain_async()
+            last = n_step[0] - 1
+            if world > 1 and last >= 0:  # the last bucket (launch L gathers buckets ending at L-1)
+                gather_bucket(last)
+            n_step[0] = 0  # the next run of builds starts a fresh bucket sequence
         if pipeline:
             stream.wait_event(ev_treed[0])
             stream.wait_event(ev_treed[1])
@@ -352,21 +401,42 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    join()  # the timed region runs exactly K digests and K trees (its last trees in its own join)
     n_ev = args.steps
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    # Kernel time for the roofline, from HIP events on the launch stream. Fused mode: one event
+    # pair brackets the K back-to-back build_step_kernel launches (no per-launch events: a timing
+    # event between two launches on ROCm costs a visible gap and slows the next launch's start,
+    # measured 10-55 us per step); the kernel trace shows these launches with no gaps, so the
+    # bracket / K is the average launch duration (the drain's tree launch is outside it).
+    # Other modes: one event pair around each digest launch.
+    bracket = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    if fused:
+        bracket[0].record(stream)
     for i in range(args.steps):
-        step(*evs[i])
+        step(*(() if fused else evs[i]))
+    if fused:
+        bracket[1].record(stream)
+    join()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     eng.set_stream(stream.cuda_stream)
     ms = (t1 - t0) * 1e3 / args.steps
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if world > 1 and fused and not c5 and args.steps > 0:
+        # the last build of the timed run, as gathered: this rank's rows equal its own roots
+        last = args.steps - 1
+        allr = gather.assemble((last // bucket) % 2, last % bucket)
+        parity["gathered_roots_match_after_run"] = bool(np.array_equal(
+            allr[w.partition_ids].reshape(-1), outs[last % (2 * bucket)][0]["root"].cpu().numpy()))
+        parity_ok = parity_ok and parity["gathered_roots_match_after_run"]
+    kern_ms = (bracket[0].elapsed_time(bracket[1]) / args.steps if fused
+               else float(np.mean([a.elapsed_time(b) for a, b in evs])))
     hashed = w.value_bytes * (2 if c5 else 1)
     if world > 1:
         t = torch.tensor([ms, kern_ms], dtype=torch.float64, device=dev)
@@ -405,7 +475,8 @@ def main():
                        "root_gather": ("rccl all_gather_into_tensor of ceil(P/N) x 32 B slabs on a side "
                                        "stream, overlapped with the next build") if world > 1 else None},
             "roofline": {"bound": "hbm",
-                         "kernel": "bucket_digest_kernel" if args.layout == "a" else "tagged_digest_kernel",
+                         "kernel": ("build_step_kernel" if fused else "bucket_digest_kernel")
+                         if args.layout == "a" else "tagged_digest_kernel",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(("c4" if c5 else args.config) + ("" if args.layout == "a" else "_b"),
@@ -414,8 +485,12 @@ def main():
                          "algorithmic_bytes_per_launch": local_bytes},
             "parity": parity,
             "simulated_shard_of_world": shard_world if shard_world != world else None,
-            "pipeline": ("2 contexts alternate builds; each build's tree kernel runs on a second "
-                         "stream, overlapping the next build's digest kernel") if pipeline else None,
+            "pipeline": {"fused": "one build_step_kernel launch per build: this build's digest "
+                                  "workgroups + the previous build's tree workgroups "
+                                  "(mde_build_pipelined_async); the last build's trees in the drain",
+                         "streams": "2 contexts alternate builds; each build's tree kernel runs on a "
+                                    "second stream, overlapping the next build's digest kernel",
+                         "off": None}[mode],
         }
         if world == 1 and not args.no_cpu_baseline and not args.profile:
             result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_baseline_seconds)

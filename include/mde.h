@@ -128,6 +128,18 @@ int mde_build_streamed(mde_ctx* ctx, const mde_records* rec, const mde_tree_out*
  * digest/size/tree kernel. mde_build_async == mde_digest_async + mde_tree_async. */
 int mde_digest_async(mde_ctx* ctx, const mde_records* rec);
 int mde_tree_async(mde_ctx* ctx, const mde_records* rec, const mde_tree_out* out);
+/* Throughput mode for a run of builds (successive epochs, replicas or partition batches of
+ * RawPartitionMerkleTree, main/merkle_tree.go:86-116), software-pipelined on the context stream:
+ * each call enqueues ONE launch that streams rec's arena into a free scratch slot and, in the
+ * same dispatch, builds the trees of the previous pipelined call into that call's outputs. So the
+ * outputs of call i are complete (in stream order) after call i+1 or after
+ * mde_build_pipeline_drain_async; rec's device arrays (seg_rec / part_rec, bucket_tag) and the
+ * outputs of call i must stay valid until then. Results are identical to mde_build_async. Uses
+ * scratch of its own: the other entry points may be interleaved freely. Layout A fuses when the
+ * tree levels fit the fused launch's 32 KiB LDS budget (n_buckets <= 1024 always does); other
+ * shapes run as separate launches on the same stream. */
+int mde_build_pipelined_async(mde_ctx* ctx, const mde_records* rec, const mde_tree_out* out);
+int mde_build_pipeline_drain_async(mde_ctx* ctx);
 
 /* EpochTreeObjectToMerkleTree for n_trees trees of n_buckets leaves each: digests -> nodes.
  * `buckets` are the 8-byte LE bucket hashes exactly as carried on the wire (EpochTreeObject

@@ -33,7 +33,8 @@ EXPORTED_SYMBOLS = (
     "mde_set_stream", "mde_use_own_stream", "mde_set_tuning", "mde_get_stream", "mde_synchronize", "mde_device_info", "mde_tree_depth",
     "mde_tree_internal_nodes", "mde_diff_capacity", "mde_build", "mde_build_async",
     "mde_build_streamed",
-    "mde_digest_async", "mde_tree_async", "mde_tree_from_digests", "mde_tree_from_digests_async",
+    "mde_digest_async", "mde_tree_async", "mde_build_pipelined_async", "mde_build_pipeline_drain_async",
+    "mde_tree_from_digests", "mde_tree_from_digests_async",
     "mde_decode_bucket_hashes", "mde_diff", "mde_diff_async", "mde_diff_digests", "mde_tag_keys_async", "mde_tag_keys",
     "mde_extract", "mde_extract_async", "mde_epoch_tree_object_max_bytes",
     "mde_encode_epoch_tree_objects", "mde_encode_epoch_tree_objects_async",
@@ -106,6 +107,8 @@ def load_library() -> C.CDLL:
         "mde_build_streamed": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), u64]),
         "mde_digest_async": (C.c_int, [vp, C.POINTER(Records)]),
         "mde_tree_async": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
+        "mde_build_pipelined_async": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
+        "mde_build_pipeline_drain_async": (C.c_int, [vp]),
         "mde_tree_from_digests": (C.c_int, [vp, u32, u32, vp, vp, vp]),
         "mde_tree_from_digests_async": (C.c_int, [vp, u32, u32, vp, vp, vp]),
         "mde_decode_bucket_hashes": (C.c_int, [vp, vp, u32, vp]),
@@ -315,6 +318,14 @@ class Engine:
 
     def tree_async(self, rec: Records, out: TreeOut):
         self._check(self.lib.mde_tree_async(self.ctx, C.byref(rec), C.byref(out)))
+
+    def build_pipelined_async(self, rec: Records, out: TreeOut):
+        """One software-pipelined build (mde_build_pipelined_async): this call's digest and the
+        previous call's trees in one launch; `out` is complete after the next call or a drain."""
+        self._check(self.lib.mde_build_pipelined_async(self.ctx, C.byref(rec), C.byref(out)))
+
+    def build_pipeline_drain_async(self):
+        self._check(self.lib.mde_build_pipeline_drain_async(self.ctx))
 
     # -- tree from digests (EpochTreeObjectToMerkleTree) --------------------------------------
     def tree_from_digests(self, digests: np.ndarray, n_buckets: int, want_nodes=True):

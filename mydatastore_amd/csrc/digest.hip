@@ -19,6 +19,8 @@
 // Algorithmic bytes per launch: sum of value lengths.
 #include "mde_device.hpp"
 #include "mde_internal.hpp"
+#include "tree_body.hpp"
+#include <algorithm>
 
 
 namespace mde {
@@ -95,14 +97,15 @@ __device__ __forceinline__ void load_step(u32x4 (&v)[U], const u32x4* src, uint6
 
 // U = 16-byte loads per lane per step (step = U KiB per wave); NT = nontemporal loads;
 // PIPE = issue the next step's loads before reducing the current one (register double buffer).
+// `block` = this workgroup's index among the digest workgroups of the launch.
 template <int U, bool NT, bool PIPE, int PRIO = 0>
-__global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a) {
+__device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t block) {
   constexpr uint64_t kStep = 1024ull * U;
-  // Streaming waves issue little VALU; when a build's tree kernel (back-to-back SHA-256 VALU)
-  // shares the CU, a raised priority keeps the loads flowing and the SHA waves take the slack.
+  // Streaming waves issue little VALU; when tree waves (back-to-back SHA-256 VALU) share the CU,
+  // a raised priority keeps the loads flowing and the SHA waves take the slack.
   if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const int lane = threadIdx.x & 63;
-  const uint32_t wave = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  const uint32_t wave = block * (kThreads / 64) + (threadIdx.x >> 6);
   if (wave >= a.n_waves) return;
   const SegDesc& d = a.seg;
   const uint64_t first = segpos(d, 0) & ~15ull;
@@ -161,20 +164,49 @@ __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a)
   flush(a.sums, s, acc);
 }
 
+template <int U, bool NT, bool PIPE, int PRIO = 0>
+__global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a) {
+  digest_body<U, NT, PIPE, PRIO>(a, blockIdx.x);
+}
+
+// Fused build step (software pipelining of consecutive builds in ONE launch): workgroups
+// [0, tree_blocks) build the trees of the PREVIOUS build from its byte sums (tree_body, LDS
+// levels), the rest stream THIS build's arena into the other scratch slot (digest_body). The
+// latency-bound SHA-256 tree waves co-run with the HBM-bound streaming waves inside one dispatch,
+// so a run of builds on one stream pays neither a second kernel boundary per build nor a
+// cross-stream event wait. A tree workgroup keeps the standalone tree kernel's shape (one live
+// wave per workgroup up to B = 128, the rest exit at once), so the SHA waves spread over many
+// CUs instead of crowding a few; tree workgroups come first so the dispatcher places them before
+// the streaming grid (sized to be fully resident) fills the remaining slots.
+template <int U, bool NT, bool PIPE, int PRIO = 0>
+__global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, TreeLaunch t, uint32_t tree_blocks,
+                                                              uint32_t G, uint32_t lds_words, uint32_t tree_threads) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  if (blockIdx.x < tree_blocks) {
+    tree_body<true>(t, G, lds_words, blockIdx.x, lds, tree_threads);
+    return;
+  }
+  digest_body<U, NT, PIPE, PRIO>(a, blockIdx.x - tree_blocks);
+}
+
 typedef void (*DigestKernel)(DigestLaunch);
+typedef void (*StepKernel)(DigestLaunch, TreeLaunch, uint32_t, uint32_t, uint32_t, uint32_t);
 struct Variant {
   DigestKernel fn;
+  StepKernel step;
   int unroll;
 };
 
-// Kernel variants (tuning knob MDE_DIGEST_VARIANT = index; default 0).
+#define MDE_VARIANT(U, NT, PIPE, PRIO) \
+  { bucket_digest_kernel<U, NT, PIPE, PRIO>, build_step_kernel<U, NT, PIPE, PRIO>, U }
+
+// Kernel variants (tuning knob mde_set_tuning digest_variant = index; default in mde_api.cpp).
 const Variant kVariants[] = {
-    {bucket_digest_kernel<8, true, false>, 8},  {bucket_digest_kernel<8, false, false>, 8},
-    {bucket_digest_kernel<16, true, false>, 16}, {bucket_digest_kernel<4, true, false>, 4},
-    {bucket_digest_kernel<4, true, true>, 4},   {bucket_digest_kernel<8, true, true>, 8},
-    {bucket_digest_kernel<16, false, false>, 16}, {bucket_digest_kernel<4, true, true, 2>, 4},
-    {bucket_digest_kernel<4, true, true, 3>, 4},
+    MDE_VARIANT(8, true, false, 0),  MDE_VARIANT(8, false, false, 0), MDE_VARIANT(16, true, false, 0),
+    MDE_VARIANT(4, true, false, 0),  MDE_VARIANT(4, true, true, 0),   MDE_VARIANT(8, true, true, 0),
+    MDE_VARIANT(16, false, false, 0), MDE_VARIANT(4, true, true, 2),  MDE_VARIANT(4, true, true, 3),
 };
+#undef MDE_VARIANT
 
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
@@ -215,6 +247,29 @@ hipError_t launch_bucket_digest(const DigestLaunch& a, hipStream_t st) {
   // 160 KiB / lds_bytes workgroups fit per CU, and the dispatcher hands the remaining workgroups
   // to whichever CU frees a slot first (load balance around CUs slowed by co-running kernels).
   hipLaunchKernelGGL(variant(a.variant).fn, dim3(blocks), dim3(kThreads), a.lds_bytes, st, a);
+  return hipGetLastError();
+}
+
+bool build_step_fusable(uint32_t B) {
+  TreeGeometry g;
+  return tree_geometry(B, &g) && g.lds_bytes <= kStepTreeLdsMax && g.threads <= kThreads;
+}
+
+hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st) {
+  TreeGeometry g{};
+  uint32_t tree_blocks = 0;
+  if (t && t->P) {
+    if (!build_step_fusable(t->B) || !tree_geometry(t->B, &g)) return hipErrorInvalidValue;
+    tree_blocks = (t->P + g.groups - 1) / g.groups;
+  }
+  const uint32_t digest_blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);
+  if (tree_blocks + digest_blocks == 0) return hipSuccess;
+  const TreeLaunch tl = t ? *t : TreeLaunch{};
+  // LDS: the tree workgroups' level buffers (every workgroup of the dispatch reserves the same
+  // amount; kStepTreeLdsMax keeps the streaming grid fully resident), or the residency cap.
+  const uint32_t lds = std::max<uint32_t>(tree_blocks ? g.lds_bytes : 0u, a.lds_bytes);
+  hipLaunchKernelGGL(variant(a.variant).step, dim3(tree_blocks + digest_blocks), dim3(kThreads), lds, st, a, tl,
+                     tree_blocks, g.G, g.words, g.threads);
   return hipGetLastError();
 }
 

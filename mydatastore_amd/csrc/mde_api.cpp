@@ -53,6 +53,21 @@ struct mde_ctx {
   Buf ring_vals[2], ring_voff[2], ring_seg[2];
   hipStream_t copy_stream = nullptr;
   hipEvent_t ev_loaded[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+  // Software-pipelined builds (mde_build_pipelined_async): two scratch slots of their own, so the
+  // standalone entry points keep using `sums`, and the build whose trees are still owed.
+  struct Slot {
+    unsigned long long* sums = nullptr;
+    uint32_t* counts = nullptr;
+    uint64_t cap = 0;
+    bool dirty = false;
+  };
+  Slot pipe[2];
+  struct Pending {
+    bool active = false;
+    int slot = 0;
+    mde_records rec{};
+    mde_tree_out out{};
+  } pending;
 };
 
 namespace {
@@ -118,6 +133,34 @@ int ensure_sums(mde_ctx* c, uint64_t S) {
     MDE_HIP(c, hipMemsetAsync(c->sums, 0, c->sums_cap * 8, c->stream));
     MDE_HIP(c, hipMemsetAsync(c->counts, 0, c->sums_cap * 4, c->stream));
     c->sums_dirty = false;
+  }
+  return MDE_OK;
+}
+
+int ensure_slot(mde_ctx* c, mde_ctx::Slot& sl, uint64_t S) {
+  if (sl.cap < S || !sl.sums) {
+    if (sl.sums) {
+      MDE_HIP(c, hipStreamSynchronize(c->stream));
+      MDE_HIP(c, hipFree(sl.sums));
+      MDE_HIP(c, hipFree(sl.counts));
+      sl.sums = nullptr;
+      sl.counts = nullptr;
+    }
+    uint64_t cap = S < 1024 ? 1024 : S;
+    if (hipMalloc(&sl.sums, cap * 8) != hipSuccess || hipMalloc(&sl.counts, cap * 4) != hipSuccess) {
+      if (sl.sums) (void)hipFree(sl.sums);
+      sl.sums = nullptr;
+      sl.counts = nullptr;
+      sl.cap = 0;
+      return set_err(c, MDE_E_NOMEM, "pipeline scratch allocation failed");
+    }
+    sl.cap = cap;
+    sl.dirty = true;
+  }
+  if (sl.dirty) {
+    MDE_HIP(c, hipMemsetAsync(sl.sums, 0, sl.cap * 8, c->stream));
+    MDE_HIP(c, hipMemsetAsync(sl.counts, 0, sl.cap * 4, c->stream));
+    sl.dirty = false;
   }
   return MDE_OK;
 }
@@ -201,7 +244,8 @@ int check_host_records(mde_ctx* c, const mde_records* r) {
 
 // span: bytes the records cover (0 = values_bytes); a streamed chunk passes a biased values
 // pointer whose values_bytes includes the bias.
-int tagged_async(mde_ctx* c, const mde_records* r, uint64_t span = 0) {
+int tagged_async(mde_ctx* c, const mde_records* r, uint64_t span = 0, unsigned long long* sums = nullptr,
+                 uint32_t* counts = nullptr) {
   mde::TaggedLaunch t{};
   const uintptr_t v = reinterpret_cast<uintptr_t>(r->values);
   t.base = reinterpret_cast<const uint8_t*>(v & ~uintptr_t(15));
@@ -212,28 +256,33 @@ int tagged_async(mde_ctx* c, const mde_records* r, uint64_t span = 0) {
   t.tag = r->bucket_tag;
   t.P = r->n_partitions;
   t.B = r->n_buckets;
-  t.sums = c->sums;
-  t.counts = c->counts;
+  t.sums = sums ? sums : c->sums;
+  t.counts = counts ? counts : c->counts;
   mde::plan_tagged((span ? span + 16 : r->values_bytes) + t.shift, c->cus, 8, &t.wave_bytes, &t.n_waves);
   MDE_HIP(c, mde::launch_tagged_digest(t, c->stream));
   return MDE_OK;
 }
 
-int digest_async(mde_ctx* c, const mde_records* r) {
+// Digest launch into explicit (zeroed) scratch.
+int digest_into(mde_ctx* c, const mde_records* r, unsigned long long* sums, uint32_t* counts) {
   const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
-  int rc = ensure_sums(c, S);
-  if (rc) return rc;
   if (S == 0 || r->n_records == 0 || r->values_bytes == 0) return MDE_OK;
-  if (r->layout == MDE_LAYOUT_TAGGED) return tagged_async(c, r);
+  if (r->layout == MDE_LAYOUT_TAGGED) return tagged_async(c, r, 0, sums, counts);
   mde::DigestLaunch a{};
   a.seg = seg_desc(r);
-  a.sums = c->sums;
+  a.sums = sums;
   if (!c->digest_blocks_per_cu)
     c->digest_blocks_per_cu = mde::bucket_digest_blocks_per_cu(c->digest_variant, c->digest_cap);
   a.variant = c->digest_variant;
   plan_digest(c, r->values_bytes + a.seg.shift, &a);
   MDE_HIP(c, mde::launch_bucket_digest(a, c->stream));
   return MDE_OK;
+}
+
+int digest_async(mde_ctx* c, const mde_records* r) {
+  int rc = ensure_sums(c, (uint64_t)r->n_partitions * r->n_buckets);
+  if (rc) return rc;
+  return digest_into(c, r, c->sums, c->counts);
 }
 
 // Digest launch for a chunk whose values pointer is biased (mde_build_streamed): positions are
@@ -258,31 +307,107 @@ int digest_async_biased(mde_ctx* c, const mde_records* r, uint64_t end_pos, uint
   return MDE_OK;
 }
 
+// Tree launch of a build whose byte sums (and layout-B counts) sit in `sums` / `counts`.
+int tree_launch_for(mde_ctx* c, const mde_records* r, const mde_tree_out* o, unsigned long long* sums,
+                    uint32_t* counts, mde::TreeLaunch* t) {
+  *t = mde::TreeLaunch{};
+  t->P = r->n_partitions;
+  t->B = r->n_buckets;
+  t->sums_in = sums;
+  t->sums_clear = sums;
+  const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
+  t->seg_rec = tagged ? nullptr : r->seg_rec;
+  t->counts_in = tagged ? counts : nullptr;
+  t->digest_out = o->digest;
+  t->size_out = o->size;
+  t->items_out = o->items;
+  t->root_out = o->root;
+  t->nodes_out = o->nodes;
+  t->n_int = mde::tree_internal(r->n_buckets);
+  if (!t->nodes_out && r->n_buckets > mde::kTreeLdsMaxBuckets) {
+    int rc = ensure_buf(c, c->nodes_scratch, (uint64_t)t->P * t->n_int * 32);
+    if (rc) return rc;
+    t->nodes_out = static_cast<uint8_t*>(c->nodes_scratch.p);
+  }
+  return MDE_OK;
+}
+
 int tree_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
   const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
   int rc = ensure_sums(c, S);
   if (rc) return rc;
-  mde::TreeLaunch t{};
-  t.P = r->n_partitions;
-  t.B = r->n_buckets;
-  t.sums_in = c->sums;
-  t.sums_clear = c->sums;
-  const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
-  t.seg_rec = tagged ? nullptr : r->seg_rec;
-  t.counts_in = tagged ? c->counts : nullptr;
-  t.digest_out = o->digest;
-  t.size_out = o->size;
-  t.items_out = o->items;
-  t.root_out = o->root;
-  t.nodes_out = o->nodes;
-  t.n_int = mde::tree_internal(r->n_buckets);
-  if (!t.nodes_out && r->n_buckets > mde::kTreeLdsMaxBuckets) {
-    rc = ensure_buf(c, c->nodes_scratch, (uint64_t)t.P * t.n_int * 32);
-    if (rc) return rc;
-    t.nodes_out = static_cast<uint8_t*>(c->nodes_scratch.p);
-  }
+  mde::TreeLaunch t;
+  rc = tree_launch_for(c, r, o, c->sums, c->counts, &t);
+  if (rc) return rc;
   MDE_HIP(c, mde::launch_tree(t, c->stream));
+  return MDE_OK;
+}
+
+// The trees still owed by the pipeline, as a standalone launch.
+int pipeline_drain(mde_ctx* c) {
+  if (!c->pending.active) return MDE_OK;
+  mde_ctx::Pending& pd = c->pending;
+  pd.active = false;
+  mde_ctx::Slot& sl = c->pipe[pd.slot];
+  mde::TreeLaunch t;
+  int rc = tree_launch_for(c, &pd.rec, &pd.out, sl.sums, sl.counts, &t);
+  if (rc) return rc;
+  hipError_t e = mde::launch_tree(t, c->stream);
+  if (e != hipSuccess) sl.dirty = true;
+  MDE_HIP(c, e);
+  return MDE_OK;
+}
+
+// One pipelined build: digest `r` into the free slot and, in the same launch, build the trees of
+// the pending build; `r` becomes the pending build. Layout B and B too wide for the fused step's
+// LDS budget run as separate launches on the same stream (same results, no overlap).
+int build_pipelined(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
+  const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
+  mde_ctx::Pending& pd = c->pending;
+  const int slot = pd.active ? 1 - pd.slot : 0;
+  mde_ctx::Slot& sl = c->pipe[slot];
+  int rc = ensure_slot(c, sl, S);
+  if (rc) return rc;
+  const bool fused = r->layout == MDE_LAYOUT_SORTED && mde::build_step_fusable(r->n_buckets) &&
+                     (!pd.active || (pd.rec.layout == MDE_LAYOUT_SORTED && mde::build_step_fusable(pd.rec.n_buckets)));
+  if (!fused) {
+    rc = pipeline_drain(c);
+    if (rc) return rc;
+    // digest into the slot through the standalone kernel, then make it pending
+    rc = digest_into(c, r, sl.sums, sl.counts);
+    if (rc) {
+      sl.dirty = true;
+      return rc;
+    }
+  } else {
+    mde::DigestLaunch a{};
+    if (S && r->n_records && r->values_bytes) {
+      a.seg = seg_desc(r);
+      if (!c->digest_blocks_per_cu)
+        c->digest_blocks_per_cu = mde::bucket_digest_blocks_per_cu(c->digest_variant, c->digest_cap);
+      a.variant = c->digest_variant;
+      plan_digest(c, r->values_bytes + a.seg.shift, &a);
+    }
+    a.sums = sl.sums;
+    mde::TreeLaunch t;
+    if (pd.active) {
+      mde_ctx::Slot& ps = c->pipe[pd.slot];
+      rc = tree_launch_for(c, &pd.rec, &pd.out, ps.sums, ps.counts, &t);
+      if (rc) return rc;
+    }
+    hipError_t e = mde::launch_build_step(a, pd.active ? &t : nullptr, c->stream);
+    if (e != hipSuccess) {
+      sl.dirty = true;
+      if (pd.active) c->pipe[pd.slot].dirty = true;
+      pd.active = false;
+    }
+    MDE_HIP(c, e);
+  }
+  pd.active = true;
+  pd.slot = slot;
+  pd.rec = *r;
+  pd.out = *o;
   return MDE_OK;
 }
 
@@ -391,6 +516,10 @@ void mde_destroy(mde_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->sums) (void)hipFree(c->sums);
     if (c->counts) (void)hipFree(c->counts);
+    for (auto& sl : c->pipe) {
+      if (sl.sums) (void)hipFree(sl.sums);
+      if (sl.counts) (void)hipFree(sl.counts);
+    }
     for (auto& b : c->stage)
       if (b.p) (void)hipFree(b.p);
     if (c->nodes_scratch.p) (void)hipFree(c->nodes_scratch.p);
@@ -482,6 +611,21 @@ int mde_build_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
   rc = digest_async(c, r);
   return rc ? rc : tree_async(c, r, o);
+}
+
+int mde_build_pipelined_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  int rc = check_records(c, r);
+  if (rc) return rc;
+  if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
+  return build_pipelined(c, r, o);
+}
+
+int mde_build_pipeline_drain_async(mde_ctx* c) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  return pipeline_drain(c);
 }
 
 int mde_build(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {

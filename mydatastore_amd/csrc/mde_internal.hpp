@@ -86,6 +86,20 @@ struct TreeLaunch {
 };
 constexpr uint32_t kTreeLdsMaxBuckets = 4096;
 hipError_t launch_tree(const TreeLaunch& a, hipStream_t st);
+struct TreeGeometry {
+  uint32_t G, threads, groups, words, lds_bytes;
+  bool lds;  // levels in LDS (B <= kTreeLdsMaxBuckets)
+};
+// Group width / live threads per workgroup / LDS of the tree builder for B buckets; false when B
+// is too large for LDS levels (the standalone kernel then needs nodes_out).
+bool tree_geometry(uint32_t B, TreeGeometry* g);
+
+// Fused build step (digest.hip): ONE launch digests `a` (this build) and, when t != null, builds
+// the trees of the previous build from its byte sums `t` (another scratch slot). Fusable when the
+// tree workgroups' LDS leaves the streaming grid fully resident.
+constexpr uint32_t kStepTreeLdsMax = 32u * 1024u;
+bool build_step_fusable(uint32_t B);
+hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st);
 
 struct DiffLaunch {
   uint32_t n_pairs;

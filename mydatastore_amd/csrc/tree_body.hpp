@@ -1,0 +1,144 @@
+// tree_body.hpp -- bucket digests -> leaves -> SHA-256 Merkle tree, as a workgroup-level device
+// function shared by tree_kernel (tree.hip) and the fused build-step kernel (digest.hip).
+//
+// Reference semantics:
+//   digest = byte-sum % 999999 (CustomHash, main/merkle_tree.go:19-32); size = record count
+//   (:91,107,111); items = sum of sizes as int32 (MerkleTreeToPartitionEpochObject, :121-134);
+//   leaf bytes = LE64(digest) (MerkleBucket.CalculateHash :64-71, utils/utils.go:67-74);
+//   cbergoon/merkletree v0.2.0 NewTree (:115,156): odd leaf count -> duplicate the last leaf;
+//   node = SHA256(left || right); the last node of an odd level pairs with itself; the node made
+//   from a 2-node level is the root.
+// Output node layout: internal nodes level 1 .. root, 32 bytes each (big-endian digest bytes).
+//
+// Levels live in LDS (ping-pong, <= 96 KiB at B = 4096); larger B reads the previous level back
+// from the global node array (same workgroup, ordered by __syncthreads()).
+#pragma once
+#include "mde_device.hpp"
+#include "mde_internal.hpp"
+
+namespace mde {
+
+__device__ __forceinline__ void load_node(const uint32_t* src, uint32_t h[8]) {
+  const u32x4* s = reinterpret_cast<const u32x4*>(src);
+  const u32x4 a = s[0], b = s[1];
+  h[0] = bswap(a.x); h[1] = bswap(a.y); h[2] = bswap(a.z); h[3] = bswap(a.w);
+  h[4] = bswap(b.x); h[5] = bswap(b.y); h[6] = bswap(b.z); h[7] = bswap(b.w);
+}
+
+__device__ __forceinline__ void store_node(uint32_t* dst, const uint32_t st[8]) {
+  u32x4* d = reinterpret_cast<u32x4*>(dst);
+  d[0] = u32x4{bswap(st[0]), bswap(st[1]), bswap(st[2]), bswap(st[3])};
+  d[1] = u32x4{bswap(st[4]), bswap(st[5]), bswap(st[6]), bswap(st[7])};
+}
+
+// Leaf b of partition p: digest, and (when building from byte sums) its size/digest outputs.
+__device__ __forceinline__ uint64_t tree_leaf(const TreeLaunch& a, uint64_t s, uint32_t& items, uint32_t& sz_out) {
+  uint64_t v;
+  if (a.sums_in) {
+    v = (uint64_t)(a.sums_in[s] % kHashMod);
+    if (a.sums_clear) a.sums_clear[s] = 0ull;
+  } else {
+    v = a.digest_in[s];
+  }
+  if (a.digest_out) a.digest_out[s] = v;
+  if (a.seg_rec || a.counts_in) {
+    uint32_t sz;  // int32 wrap like Go
+    if (a.seg_rec) {
+      sz = (uint32_t)(a.seg_rec[s + 1] - a.seg_rec[s]);
+    } else {
+      sz = a.counts_in[s];
+      a.counts_in[s] = 0u;
+    }
+    if (a.size_out) a.size_out[s] = (int32_t)sz;
+    items += sz;
+    sz_out = sz;
+  }
+  return v;
+}
+
+// One workgroup (`block` = its index among the tree workgroups) builds threads / G trees with its
+// first `threads` threads (a multiple of 64): a "group" of G threads per partition. Waves past
+// `threads` leave at once, before any barrier (s_barrier waits only for waves still running).
+// Every group of a workgroup runs the same level count, so the per-level __syncthreads() is
+// uniform.
+template <bool kLds>
+__device__ __forceinline__ void tree_body(const TreeLaunch& a, uint32_t G, uint32_t lds_words, uint32_t block,
+                                          uint32_t* lds, uint32_t threads) {
+  if (threadIdx.x >= threads) return;
+  const uint32_t groups = threads / G;
+  const uint32_t gi = threadIdx.x / G, tid = threadIdx.x % G;
+  const uint32_t p = block * groups + gi;
+  // Every group runs the level loop of the widest tree (a.B) so that __syncthreads() stays
+  // uniform; a group whose own tree (n_in) is narrower idles once it reaches its root.
+  const int32_t bt = (a.n_in && p < a.P) ? a.n_in[p] : (int32_t)a.B;
+  const bool live = p < a.P && bt > 0 && (uint32_t)bt <= a.B;
+  const uint32_t B = live ? (uint32_t)bt : a.B;
+  const uint32_t n1 = (B + 1) / 2;  // level-1 nodes (leaf count incl. dup / 2)
+  const uint32_t n1_max = (a.B + 1) / 2;
+  const uint64_t s0 = (uint64_t)p * a.B;
+  uint32_t* node_base = (a.nodes_out && live)
+                            ? reinterpret_cast<uint32_t*>(a.nodes_out + (uint64_t)p * a.n_int * 32)
+                            : nullptr;
+  uint32_t* region = lds + (uint64_t)gi * lds_words;
+  uint32_t* counter = region;  // region[0]: items accumulator
+  uint32_t* buf0 = kLds ? region + 4 : node_base;
+  uint32_t* buf1 = kLds ? region + 4 + (uint64_t)n1_max * 8 : nullptr;
+  if (tid == 0) counter[0] = 0;
+  __syncthreads();
+
+  // Leaves + level 1.
+  uint32_t items = 0;
+  if (live) {
+    for (uint32_t j = tid; j < n1; j += G) {
+      const uint32_t bl = 2 * j, br = (2 * j + 1 < B) ? 2 * j + 1 : 2 * j;
+      uint32_t szl = 0, szr = 0;
+      const uint64_t dl = tree_leaf(a, s0 + bl, items, szl);
+      const uint64_t dr = (br != bl) ? tree_leaf(a, s0 + br, items, szr) : dl;
+      if (br == bl) items += szl;  // odd B: the duplicate leaf's size counts again (tree.Leafs walk)
+      uint32_t st[8];
+      sha256_leaf_pair(dl, dr, st);
+      store_node(buf0 + (uint64_t)j * 8, st);
+      if (kLds && node_base) store_node(node_base + (uint64_t)j * 8, st);
+    }
+  }
+  if (items) atomicAdd(counter, items);
+
+  // Upper levels.
+  uint32_t n_max = n1_max;
+  uint32_t n = n1;
+  uint64_t level_off = 0;  // node index of the current level's first node in node_base
+  uint32_t* cur = buf0;
+  uint32_t* nxt = kLds ? buf1 : (node_base ? node_base + (uint64_t)n1 * 8 : nullptr);
+  while (n_max > 1) {
+    __syncthreads();
+    n_max = (n_max + 1) / 2;
+    if (n <= 1) continue;  // this group's tree is complete
+    const uint32_t m = (n + 1) / 2;
+    if (live) {
+      for (uint32_t j = tid; j < m; j += G) {
+        const uint32_t l = 2 * j, r = (2 * j + 1 < n) ? 2 * j + 1 : 2 * j;
+        uint32_t hl[8], hr[8], st[8];
+        load_node(cur + (uint64_t)l * 8, hl);
+        load_node(cur + (uint64_t)r * 8, hr);
+        sha256_node_pair(hl, hr, st);
+        store_node(nxt + (uint64_t)j * 8, st);
+        if (kLds && node_base) store_node(node_base + (level_off + n + j) * 8, st);
+      }
+    }
+    level_off += n;
+    n = m;
+    if (kLds) {
+      uint32_t* t = cur; cur = nxt; nxt = t;
+    } else if (node_base) {
+      cur = nxt;
+      nxt = node_base + (level_off + n) * 8;
+    }
+  }
+  __syncthreads();
+  if (live) {
+    if (tid < 8) reinterpret_cast<uint32_t*>(a.root_out + (uint64_t)p * 32)[tid] = cur[tid];
+    if (tid == 0 && a.items_out) a.items_out[p] = (int32_t)counter[0];
+  }
+}
+
+}  // namespace mde

@@ -38,23 +38,34 @@ def shard_gids(n_keys: int, n_partitions: int, part_mode: str, keys_per_partitio
 
 class RootGather:
     """Fixed-size slab all-gather of per-partition 32-byte roots, double-buffered so a caller can
-    keep the gather of build i in flight while build i+1 computes."""
+    keep the gather of build i in flight while build i+1 computes. `batch` > 1 buckets the roots
+    of that many builds into one collective (slab [batch][ceil(P/world)][width] per rank): on a
+    node each collective costs the same few tens of microseconds whatever its size (32 KiB per
+    build at C4), and each cross-stream hand-off to the collective's stream costs ~10 us, so a
+    run of builds gathers once per bucket."""
 
-    def __init__(self, n_partitions: int, world: int, device, nbuf: int = 2, width: int = 32):
+    def __init__(self, n_partitions: int, world: int, device, nbuf: int = 2, width: int = 32,
+                 batch: int = 1):
         """width: bytes per partition (32 = one root; 64 = the roots of two replicas)."""
         import torch
-        self.P, self.world, self.width = n_partitions, world, width
+        self.P, self.world, self.width, self.batch = n_partitions, world, width, batch
         self.slab = -(-n_partitions // world)
-        self.send = [torch.zeros(self.slab * width, dtype=torch.uint8, device=device) for _ in range(nbuf)]
-        self.recv = [torch.zeros(world * self.slab * width, dtype=torch.uint8, device=device)
-                     for _ in range(nbuf)]
+        per_rank = batch * self.slab * width
+        self.send = [torch.zeros(per_rank, dtype=torch.uint8, device=device) for _ in range(nbuf)]
+        self.recv = [torch.zeros(world * per_rank, dtype=torch.uint8, device=device) for _ in range(nbuf)]
 
     def gather(self, roots, buf: int = 0):
-        """roots: this rank's [n_local * width] uint8 tensor. Enqueued on the current stream."""
+        """roots: this rank's [n_local * width] uint8 tensor, or a list of up to `batch` of them
+        (one per build). Enqueued on the current stream."""
         import torch
         import torch.distributed as dist
-        n = roots.numel()
-        self.send[buf][:n].copy_(roots, non_blocking=True)
+        if not isinstance(roots, (list, tuple)):
+            roots = [roots]
+        if len(roots) > self.batch:
+            raise ValueError(f"{len(roots)} builds exceed the gather bucket of {self.batch}")
+        stride = self.slab * self.width
+        for j, r in enumerate(roots):
+            self.send[buf][j * stride:j * stride + r.numel()].copy_(r.reshape(-1), non_blocking=True)
         if dist.get_backend() == "gloo":  # CPU tests / single-GPU rehearsal: stage through host
             send = self.send[buf].cpu()
             parts = [t.cpu() for t in self.recv[buf].view(self.world, -1).unbind(0)]
@@ -64,10 +75,10 @@ class RootGather:
             dist.all_gather_into_tensor(self.recv[buf], self.send[buf])
         return self.recv[buf]
 
-    def assemble(self, buf: int = 0) -> np.ndarray:
-        """All roots in global partition order: [P, width] uint8 (slot i of rank r = partition
-        r + i * world)."""
-        g = self.recv[buf].view(self.world, self.slab, self.width).cpu().numpy()
+    def assemble(self, buf: int = 0, build: int = 0) -> np.ndarray:
+        """All roots of the bucket's `build`-th build in global partition order: [P, width] uint8
+        (slot i of rank r = partition r + i * world)."""
+        g = self.recv[buf].view(self.world, self.batch, self.slab, self.width)[:, build].cpu().numpy()
         out = np.zeros((self.P, self.width), np.uint8)
         for r in range(self.world):
             pids = local_partitions(self.P, r, self.world)

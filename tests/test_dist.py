@@ -25,7 +25,7 @@ def _oracle_roots(co, gids, n_parts_global, rank, world, mode):
     return out["root"]
 
 
-def _worker(rank, world, port, mode, q):
+def _worker(rank, world, port, mode, q, batch=1):
     import torch
     import torch.distributed as dist
     import sys
@@ -39,9 +39,13 @@ def _worker(rank, world, port, mode, q):
         kpp = -(-N_KEYS // P)
         gids = shard_gids(N_KEYS, P, mode, kpp, rank, world)
         roots = _oracle_roots(co, gids, P, rank, world, mode)
-        g = RootGather(P, world, torch.device("cpu"))
-        g.gather(torch.from_numpy(roots.copy()), 0)
-        allr = g.assemble(0)
+        g = RootGather(P, world, torch.device("cpu"), batch=batch)
+        if batch == 1:
+            g.gather(torch.from_numpy(roots.copy()), 0)
+            allr = g.assemble(0)
+        else:  # a bucket of builds: build j's roots are the real roots with every byte + j
+            g.gather([torch.from_numpy((roots + j).astype(np.uint8)) for j in range(batch)], 1)
+            allr = np.stack([g.assemble(1, j) for j in range(batch)])
         if rank == 0:
             q.put(allr)
     finally:
@@ -56,12 +60,12 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("world,mode", [(2, "mod"), (2, "block"), (3, "mod")])
-def test_sharded_gather_matches_single_process(world, mode, coracle):
+@pytest.mark.parametrize("world,mode,batch", [(2, "mod", 1), (2, "block", 1), (3, "mod", 1), (2, "mod", 3)])
+def test_sharded_gather_matches_single_process(world, mode, batch, coracle):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q, batch)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
@@ -69,7 +73,11 @@ def test_sharded_gather_matches_single_process(world, mode, coracle):
         p.join(timeout=60)
         assert p.exitcode == 0
     full = _oracle_roots(coracle, np.arange(N_KEYS, dtype=np.uint64), P, 0, 1, mode).reshape(P, 32)
-    assert np.array_equal(got, full)
+    if batch == 1:
+        assert np.array_equal(got, full)
+    else:
+        for j in range(batch):
+            assert np.array_equal(got[j], (full + j).astype(np.uint8)), j
 
 
 def test_shard_partitions_cover_everything():

@@ -10,9 +10,9 @@ export TMPDIR=/tmp
 out=gpurun_out/prof_${tag}_${label}
 mkdir -p $out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- \
-  python3 bench.py --profile --config $cfg --steps 10 --warmup 2 --no-pipeline $extra > $out/bench_trace.json 2> $out/trace.err || { tail -20 $out/trace.err; exit 1; }
+  python3 bench.py --profile --config $cfg --steps 30 --warmup 2 $extra > $out/bench_trace.json 2> $out/trace.err || { tail -20 $out/trace.err; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc_fetch -o run -- \
-  python3 bench.py --profile --config $cfg --steps 3 --warmup 1 --no-pipeline $extra > $out/bench_fetch.json 2> $out/fetch.err || { tail -20 $out/fetch.err; exit 1; }
+  python3 bench.py --profile --config $cfg --steps 3 --warmup 1 $extra > $out/bench_fetch.json 2> $out/fetch.err || { tail -20 $out/fetch.err; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc_write -o run -- \
-  python3 bench.py --profile --config $cfg --steps 3 --warmup 1 --no-pipeline $extra > $out/bench_write.json 2> $out/write.err || { tail -20 $out/write.err; exit 1; }
+  python3 bench.py --profile --config $cfg --steps 3 --warmup 1 $extra > $out/bench_write.json 2> $out/write.err || { tail -20 $out/write.err; exit 1; }
 find $out -name "*.csv" | head -20

@@ -1,0 +1,163 @@
+// readceil.hip -- HBM read-ceiling probe for the digest kernel's roofline (not product code).
+//
+// Streams a 10.24 GB buffer (the C4 arena size) with the same per-lane work as
+// bucket_digest_kernel's fast path (16-B loads, one v_sad_u8 per dword, one atomic per wave) but
+// none of its bucket bookkeeping, under several access shapes, to measure what a read-only stream
+// achieves on this chip. The digest kernel's roofline.frac is quoted against the 8 TB/s spec; this
+// gives the measured ceiling beside it.
+//
+//   hipcc -O3 --offload-arch=gfx950 tools/readceil.hip -o tools/readceil && tools/readceil
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <algorithm>
+#include <vector>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));   \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+// Contiguous range per wave (the digest kernel's shape). U 16-B loads per lane per step.
+template <int U, bool NT, bool PIPE>
+__global__ __launch_bounds__(256) void read_contig(const u32x4* __restrict__ buf, uint64_t n16,
+                                                   uint64_t per_wave16, unsigned long long* out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t beg = wave * per_wave16, end = std::min(beg + per_wave16, n16);
+  uint32_t acc = 0;
+  constexpr uint64_t kStep = 64ull * U;
+  u32x4 cur[U];
+  if (PIPE && beg < end) {
+#pragma unroll
+    for (int u = 0; u < U; u++) cur[u] = NT ? __builtin_nontemporal_load(buf + beg + u * 64 + lane) : buf[beg + u * 64 + lane];
+  }
+  for (uint64_t p = beg; p + kStep <= end; p += kStep) {
+    u32x4 v[U];
+    if (PIPE) {
+      u32x4 nx[U];
+      if (p + 2 * kStep <= end) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          nx[u] = NT ? __builtin_nontemporal_load(buf + p + kStep + u * 64 + lane) : buf[p + kStep + u * 64 + lane];
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) { v[u] = cur[u]; cur[u] = nx[u]; }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = NT ? __builtin_nontemporal_load(buf + p + u * 64 + lane) : buf[p + u * 64 + lane];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
+      acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
+      acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
+      acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
+    }
+  }
+  unsigned long long s = acc;
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) atomicAdd(out, s);
+}
+
+// Grid-stride: consecutive waves read consecutive KiB (all waves sweep the buffer together).
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void read_stride(const u32x4* __restrict__ buf, uint64_t n16,
+                                                   unsigned long long* out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  uint32_t acc = 0;
+  for (uint64_t p = wave * 64 * U; p + 64 * U <= n16; p += nw * 64 * U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = NT ? __builtin_nontemporal_load(buf + p + u * 64 + lane) : buf[p + u * 64 + lane];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
+      acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
+      acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
+      acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
+    }
+  }
+  unsigned long long s = acc;
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) atomicAdd(out, s);
+}
+
+__global__ void fill(uint32_t* p, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = (uint32_t)(i * 2654435761u);
+}
+
+int main(int argc, char** argv) {
+  const uint64_t bytes = argc > 1 ? strtoull(argv[1], 0, 10) : 10240000000ull;
+  const uint64_t n16 = bytes / 16;
+  u32x4* buf;
+  unsigned long long* out;
+  CK(hipMalloc(&buf, bytes));
+  CK(hipMalloc(&out, 8));
+  hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, (uint32_t*)buf, bytes / 4);
+  CK(hipDeviceSynchronize());
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+
+  auto time_it = [&](auto launch) {
+    for (int i = 0; i < 2; i++) launch();
+    std::vector<float> ms;
+    for (int r = 0; r < 10; r++) {
+      CK(hipEventRecord(a, 0));
+      launch();
+      CK(hipEventRecord(b, 0));
+      CK(hipEventSynchronize(b));
+      float t;
+      CK(hipEventElapsedTime(&t, a, b));
+      ms.push_back(t);
+    }
+    std::sort(ms.begin(), ms.end());
+    return ms[ms.size() / 2];
+  };
+  auto report = [&](const char* name, int wg_per_cu, float ms) {
+    printf("{\"shape\": \"%s\", \"wg_per_cu\": %d, \"bytes\": %llu, \"ms\": %.4f, \"GBps\": %.1f}\n", name,
+           wg_per_cu, (unsigned long long)bytes, ms, bytes / (ms * 1e-3) / 1e9);
+    fflush(stdout);
+  };
+
+  for (int wpc : {1, 2, 3, 4, 8}) {
+    const uint64_t waves = (uint64_t)cus * wpc * 4;
+    uint64_t per = (n16 + waves - 1) / waves;
+    per = (per + 255) / 256 * 256;
+    const uint32_t blocks = (uint32_t)((n16 + per * 4 - 1) / (per * 4));
+    report("contig U4 nt pipe", wpc, time_it([&] {
+             hipLaunchKernelGGL((read_contig<4, true, true>), dim3(blocks), dim3(256), 0, 0, buf, n16, per, out);
+           }));
+    report("contig U8 nt", wpc, time_it([&] {
+             hipLaunchKernelGGL((read_contig<8, true, false>), dim3(blocks), dim3(256), 0, 0, buf, n16, per, out);
+           }));
+    report("contig U8 default", wpc, time_it([&] {
+             hipLaunchKernelGGL((read_contig<8, false, false>), dim3(blocks), dim3(256), 0, 0, buf, n16, per, out);
+           }));
+    report("contig U16 nt", wpc, time_it([&] {
+             hipLaunchKernelGGL((read_contig<16, true, false>), dim3(blocks), dim3(256), 0, 0, buf, n16, per, out);
+           }));
+    report("stride U4 nt", wpc, time_it([&] {
+             hipLaunchKernelGGL((read_stride<4, true>), dim3(cus * wpc), dim3(256), 0, 0, buf, n16, out);
+           }));
+    report("stride U8 default", wpc, time_it([&] {
+             hipLaunchKernelGGL((read_stride<8, false>), dim3(cus * wpc), dim3(256), 0, 0, buf, n16, out);
+           }));
+  }
+  CK(hipFree(buf));
+  CK(hipFree(out));
+  return 0;
+}
