@@ -84,6 +84,33 @@ def bench_sweep(eng, worlds=(1, 8), reps=3):
     return res
 
 
+def bench_ab(eng, variants, worlds=(1, 8), reps=5, cap=2):
+    """Interleaved A/B of digest variants at one workgroups-per-CU cap (same data, same clocks)."""
+    from mydatastore_amd.workload import make_workload
+    res = []
+    for world in worlds:
+        w = make_workload(eng, n_partitions=1024, n_buckets=64, value_len=1024, part_mode="mod",
+                          n_keys=10_000_000, rank=0, world=world)
+        ref = None
+        times = {v: [] for v in variants}
+        for _ in range(reps):
+            for v in variants:
+                eng.set_tuning(v, cap)
+                times[v].append(timeit(w.digest_async, reps=10, warm=2))
+                o = w.build()
+                if ref is None:
+                    ref = o["root"].cpu()
+                assert bool((o["root"].cpu() == ref).all()), f"variant {v} roots differ"
+        eng.set_tuning(-1, -1)
+        for v, t in times.items():
+            med = float(np.median(t))
+            res.append({"world": world, "variant": v, "cap": cap, "digest_us": round(med, 2),
+                        "GBps": round(w.value_bytes / med / 1e3, 1)})
+            print(json.dumps(res[-1]), flush=True)
+        del w
+    return res
+
+
 def main():
     import torch
     import mydatastore_amd as mde
@@ -98,6 +125,8 @@ def main():
     if "sweep" in what:
         out["sweep"] = bench_sweep(eng)
     for w in what:
+        if w.startswith("ab:"):
+            out["ab"] = bench_ab(eng, [int(x) for x in w.split(":")[1].split(",")])
         if w.startswith("digest:"):
             out["digest"] = bench_digest(eng, [int(x) for x in w.split(":")[1].split(",")])
     Path("gpurun_out").mkdir(exist_ok=True)
