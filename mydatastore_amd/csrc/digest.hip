@@ -180,17 +180,17 @@ __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a)
 // the streaming grid (sized to be fully resident) fills the remaining slots.
 template <int U, bool NT, bool PIPE, int PRIO = 0>
 __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, TreeLaunch t, uint32_t tree_blocks,
-                                                              uint32_t G, uint32_t lds_words, uint32_t tree_threads) {
+                                                              uint32_t Q) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   if (blockIdx.x < tree_blocks) {
-    tree_body<true>(t, G, lds_words, blockIdx.x, lds, tree_threads);
+    tree_body_packed(t, Q, blockIdx.x, lds);
     return;
   }
   digest_body<U, NT, PIPE, PRIO>(a, blockIdx.x - tree_blocks);
 }
 
 typedef void (*DigestKernel)(DigestLaunch);
-typedef void (*StepKernel)(DigestLaunch, TreeLaunch, uint32_t, uint32_t, uint32_t, uint32_t);
+typedef void (*StepKernel)(DigestLaunch, TreeLaunch, uint32_t, uint32_t);
 struct Variant {
   DigestKernel fn;
   StepKernel step;
@@ -250,26 +250,31 @@ hipError_t launch_bucket_digest(const DigestLaunch& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-bool build_step_fusable(uint32_t B) {
-  TreeGeometry g;
-  return tree_geometry(B, &g) && g.lds_bytes <= kStepTreeLdsMax && g.threads <= kThreads;
+// Partitions per tree wave in the fused step: up to 16, as many as the LDS budget holds.
+uint32_t step_tree_q(uint32_t B) {
+  const uint32_t n1 = (B + 1) / 2;
+  const uint32_t per = (n1 + (n1 + 1) / 2) * 8u * 4u;  // bytes of level buffers per partition
+  const uint32_t q = (kStepTreeLdsMax - 64u) / per;
+  return q > 16u ? 16u : q;
 }
 
+bool build_step_fusable(uint32_t B) { return B >= 1 && step_tree_q(B) >= 1; }
+
 hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st) {
-  TreeGeometry g{};
-  uint32_t tree_blocks = 0;
+  uint32_t tree_blocks = 0, Q = 0, lds = a.lds_bytes;
   if (t && t->P) {
-    if (!build_step_fusable(t->B) || !tree_geometry(t->B, &g)) return hipErrorInvalidValue;
-    tree_blocks = (t->P + g.groups - 1) / g.groups;
+    if (!build_step_fusable(t->B) || !t->sums_in) return hipErrorInvalidValue;
+    Q = step_tree_q(t->B);
+    tree_blocks = (t->P + Q - 1) / Q;
+    // every workgroup of the dispatch reserves the tree waves' LDS; kStepTreeLdsMax keeps the
+    // streaming grid fully resident
+    lds = std::max<uint32_t>(lds, packed_tree_lds_words(t->B, Q) * 4u);
   }
   const uint32_t digest_blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);
   if (tree_blocks + digest_blocks == 0) return hipSuccess;
   const TreeLaunch tl = t ? *t : TreeLaunch{};
-  // LDS: the tree workgroups' level buffers (every workgroup of the dispatch reserves the same
-  // amount; kStepTreeLdsMax keeps the streaming grid fully resident), or the residency cap.
-  const uint32_t lds = std::max<uint32_t>(tree_blocks ? g.lds_bytes : 0u, a.lds_bytes);
   hipLaunchKernelGGL(variant(a.variant).step, dim3(tree_blocks + digest_blocks), dim3(kThreads), lds, st, a, tl,
-                     tree_blocks, g.G, g.words, g.threads);
+                     tree_blocks, Q);
   return hipGetLastError();
 }
 

@@ -95,9 +95,10 @@ struct TreeGeometry {
 bool tree_geometry(uint32_t B, TreeGeometry* g);
 
 // Fused build step (digest.hip): ONE launch digests `a` (this build) and, when t != null, builds
-// the trees of the previous build from its byte sums `t` (another scratch slot). Fusable when the
-// tree workgroups' LDS leaves the streaming grid fully resident.
-constexpr uint32_t kStepTreeLdsMax = 32u * 1024u;
+// the trees of the previous build from its byte sums `t` (another scratch slot), Q partitions per
+// tree wave (tree_body_packed). Fusable when one partition's level buffers fit the LDS budget
+// that keeps the streaming grid fully resident (B <= 1024 always does).
+constexpr uint32_t kStepTreeLdsMax = 24u * 1024u + 64u;
 bool build_step_fusable(uint32_t B);
 hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st);
 

@@ -141,4 +141,79 @@ __device__ __forceinline__ void tree_body(const TreeLaunch& a, uint32_t G, uint3
   }
 }
 
+// Throughput shape for the fused build step: ONE wave builds the trees of Q consecutive
+// partitions (same B, byte-sum input), level by level, with the level's Q x n nodes spread over
+// the 64 lanes. tree_body's shape (64/G partitions per wave, G = level-1 width) leaves most lanes
+// idle above level 1 -- 11 compression rounds per 2 partitions at B = 64 -- where this one takes
+// 26 rounds per 16 partitions: 3.4x fewer wave-instructions for the same trees, at a longer
+// critical path (26 vs 11 rounds) that the co-running HBM stream hides. Waves past the first
+// leave at once. LDS: [Q] item counters, then two level buffers of Q x n1 and Q x ceil(n1/2)
+// nodes (packed_tree_lds_words).
+__host__ __device__ inline uint32_t packed_tree_lds_words(uint32_t B, uint32_t Q) {
+  const uint32_t n1 = (B + 1) / 2;
+  return 16u + Q * (n1 + (n1 + 1) / 2) * 8u;
+}
+
+__device__ __forceinline__ void tree_body_packed(const TreeLaunch& a, uint32_t Q, uint32_t block, uint32_t* lds) {
+  if (threadIdx.x >= 64) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t B = a.B;
+  const uint32_t p0 = block * Q;
+  if (p0 >= a.P) return;
+  const uint32_t nq = min(Q, a.P - p0);
+  const uint32_t n1 = (B + 1) / 2;
+  uint32_t* cnt = lds;
+  uint32_t* cur = lds + 16;
+  uint32_t* nxt = cur + (uint64_t)Q * n1 * 8;
+  for (uint32_t i = lane; i < Q; i += 64) cnt[i] = 0;
+  __syncthreads();
+
+  // Leaves + level 1: item i = (partition q, node j).
+  for (uint32_t i = lane; i < nq * n1; i += 64) {
+    const uint32_t q = i / n1, j = i - q * n1;
+    const uint64_t s0 = (uint64_t)(p0 + q) * B;
+    const uint32_t bl = 2 * j, br = (2 * j + 1 < B) ? 2 * j + 1 : 2 * j;
+    uint32_t items = 0, szl = 0, szr = 0;
+    const uint64_t dl = tree_leaf(a, s0 + bl, items, szl);
+    const uint64_t dr = (br != bl) ? tree_leaf(a, s0 + br, items, szr) : dl;
+    if (br == bl) items += szl;  // odd B: the duplicate leaf's size counts again (tree.Leafs walk)
+    if (items) atomicAdd(cnt + q, items);
+    uint32_t st[8];
+    sha256_leaf_pair(dl, dr, st);
+    store_node(cur + ((uint64_t)q * n1 + j) * 8, st);
+    if (a.nodes_out)
+      store_node(reinterpret_cast<uint32_t*>(a.nodes_out + ((uint64_t)(p0 + q) * a.n_int + j) * 32), st);
+  }
+  __syncthreads();
+
+  // Upper levels.
+  uint32_t n = n1;
+  uint64_t level_off = 0;
+  while (n > 1) {
+    const uint32_t m = (n + 1) / 2;
+    for (uint32_t i = lane; i < nq * m; i += 64) {
+      const uint32_t q = i / m, j = i - q * m;
+      const uint32_t l = 2 * j, r = (2 * j + 1 < n) ? 2 * j + 1 : 2 * j;
+      uint32_t hl[8], hr[8], st[8];
+      load_node(cur + ((uint64_t)q * n + l) * 8, hl);
+      load_node(cur + ((uint64_t)q * n + r) * 8, hr);
+      sha256_node_pair(hl, hr, st);
+      store_node(nxt + ((uint64_t)q * m + j) * 8, st);
+      if (a.nodes_out)
+        store_node(reinterpret_cast<uint32_t*>(a.nodes_out + ((uint64_t)(p0 + q) * a.n_int + level_off + n + j) * 32),
+                   st);
+    }
+    level_off += n;
+    n = m;
+    uint32_t* t = cur; cur = nxt; nxt = t;
+    __syncthreads();
+  }
+  for (uint32_t i = lane; i < nq * 8; i += 64) {
+    const uint32_t q = i / 8, w = i % 8;
+    reinterpret_cast<uint32_t*>(a.root_out + (uint64_t)(p0 + q) * 32)[w] = cur[(uint64_t)q * 8 + w];
+  }
+  if (a.items_out)
+    for (uint32_t i = lane; i < nq; i += 64) a.items_out[p0 + i] = (int32_t)cnt[i];
+}
+
 }  // namespace mde
