@@ -28,6 +28,8 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr uint64_t kMaxStepBytes = 16ull * 1024ull;  // largest wave step over all variants
+constexpr uint32_t kStealHeads = 16;                 // ticket counters of the tail pool
+constexpr uint32_t kStageSteps = 3;                  // steps between chunk-acquisition stages
 
 // Largest s in [lo, S) with segpos(s) <= x (lo if none). 64-ary search: one vector load and one
 // ballot per round, log64(S) rounds. Must be called by all 64 lanes.
@@ -164,10 +166,208 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
   flush(a.sums, s, acc);
 }
 
-template <int U, bool NT, bool PIPE, int PRIO = 0>
-__global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a) {
-  digest_body<U, NT, PIPE, PRIO>(a, blockIdx.x);
+
+// Tail stealing (fixed-length values). Wave w owns [first + w*wave_bytes, +wave_bytes) as in
+// digest_body, but streams only its head (the first head_bytes); the tails of all waves, cut into
+// tail_chunks pieces of chunk_bytes, form a pool the waves drain through one atomic ticket
+// counter once their heads are done. Why: under a static split wave end times spread by ~5 %
+// (whole XCDs stream consistently slower; measured per wave with s_memrealtime), and the launch
+// lasts as long as the slowest wave.
+// A chunk switch must not stall the wave's memory pipeline, so the next chunk is acquired while
+// the current one streams: one stage per step -- ticket atomic, then the rounds of a 64-ary
+// search of the chunk's first bucket (seg_rec is L2-resident), then that bucket's bounds -- and
+// the first step of the next chunk is prefetched across the switch like any other step.
+template <int U, bool NT, int PRIO = 0>
+__device__ __forceinline__ void digest_body_steal(const DigestLaunch& a, uint32_t block) {
+  constexpr uint64_t kStep = 1024ull * U;
+  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = block * (kThreads / 64) + (threadIdx.x >> 6);
+  if (wave >= a.n_waves) return;
+  const SegDesc& d = a.seg;
+  // Ticket heads: kStealHeads counters + an exhausted-heads mask per parity. One returning atomic
+  // word saturates near 90 dequeues/us (MI355X_MICROARCH.md "dequeue"), far below what 2,048
+  // waves draw, so head h serves the tickets t = h + kStealHeads * k; a wave starts at head
+  // wave % kStealHeads, and moves on (skipping heads the mask marks empty) when its head runs dry.
+  unsigned long long* heads = a.steal + a.steal_parity * (kStealHeads + 1);
+  unsigned long long* mask = heads + kStealHeads;
+  if (wave == 0 && lane <= kStealHeads)  // the next launch's heads and mask
+    a.steal[(a.steal_parity ^ 1u) * (kStealHeads + 1) + lane] = 0ull;
+  const uint64_t first = segpos(d, 0) & ~15ull;
+  const uint64_t last = segpos(d, d.S);
+  const uint64_t tickets = (uint64_t)a.n_waves * a.tail_chunks;
+  const u32x4* lane_base = reinterpret_cast<const u32x4*>(d.base) + lane;
+  const uint64_t stride = d.stride;
+  const uint64_t nrec = d.n_records;
+
+  // Acquisition state of the next chunk (wave-uniform): 0 = ticket not requested, 1 = ticket
+  // in flight, 2 = search round in flight, 3 = bounds in flight, 4 = ready, 5 = pool empty,
+  // -1 = head mask in flight (the current head ran dry): every non-final state is below 4.
+  int nst = 0;
+  unsigned long long tk = 0, mk = 0, dry = 0;
+  uint32_t h = wave % kStealHeads;
+  uint64_t nb = 0, ne = 0, nsb = 0, nse = 0, sval = 0;
+  uint32_t lo = 0, hi = 0, stp = 0, ns = 0;
+  auto pos_of = [&](uint64_t r) {  // segpos from a loaded seg_rec value
+    const uint64_t p = d.shift + (r < nrec ? r : nrec) * stride;
+    return p < d.end ? p : d.end;
+  };
+  auto issue_round = [&]() {
+    stp = (hi - lo + 63u) / 64u;
+    const uint32_t idx = lo + (uint32_t)lane * stp;
+    sval = idx < hi ? d.seg_rec[idx] : 0ull;
+  };
+  auto advance = [&]() {  // one acquisition stage
+    if (nst == 0) {
+      if (lane == 0) tk = atomicAdd(heads + h, 1ull);
+      nst = 1;
+    } else if (nst == -1) {
+      // heads this wave found dry itself, plus those others marked before its atomicOr (the
+      // atomic's return value: a plain load could hit a stale line in this XCD's L2)
+      const unsigned long long m = __shfl(mk, 0) | dry;
+      if (m == (1ull << kStealHeads) - 1ull) {
+        nst = 5;
+        return;
+      }
+      while ((m >> h) & 1ull) h = (h + 1u) % kStealHeads;
+      nst = 0;
+    } else if (nst == 1) {
+      const unsigned long long t = (unsigned long long)h + kStealHeads * __shfl(tk, 0);
+      if (t >= tickets) {  // head h is dry: mark it; the returned old mask says which are left
+        dry |= 1ull << h;
+        if (lane == 0) mk = atomicOr(mask, 1ull << h);
+        nst = -1;
+        return;
+      }
+      const uint32_t owner = (uint32_t)(t % a.n_waves), piece = (uint32_t)(t / a.n_waves);
+      const uint64_t ob = first + (uint64_t)owner * a.wave_bytes;
+      const uint64_t oe = min(ob + a.wave_bytes, last);
+      nb = ob + a.head_bytes + (uint64_t)piece * a.chunk_bytes;
+      if (ob >= last || nb >= oe) {  // an empty piece: take another ticket
+        nst = 0;
+        return;
+      }
+      ne = min(nb + a.chunk_bytes, oe);
+      lo = 0;
+      hi = d.S;
+      issue_round();
+      nst = 2;
+    } else if (nst == 2) {
+      const uint32_t idx = lo + (uint32_t)lane * stp;
+      const bool pred = idx < hi && pos_of(sval) <= nb;
+      const uint32_t c = (uint32_t)__popcll(__ballot(pred));
+      bool done = c == 0;
+      if (!done) {
+        lo = lo + (c - 1u) * stp;
+        hi = min(lo + stp, hi);
+        done = hi - lo <= 1u;
+      }
+      if (done) {
+        ns = lo;
+        sval = lane < 2 ? d.seg_rec[ns + (uint32_t)lane] : 0ull;
+        nst = 3;
+      } else {
+        issue_round();
+      }
+    } else if (nst == 3) {
+      nsb = pos_of(__shfl(sval, 0));
+      nse = pos_of(__shfl(sval, 1));
+      nst = 4;
+    }
+  };
+
+  // First segment: this wave's head, or (a wave with an empty range) a stolen chunk.
+  uint64_t cb, ce, sb, se;
+  uint32_t s;
+  const uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
+  if (beg < last) {
+    cb = beg;
+    ce = min(beg + a.head_bytes, min(beg + a.wave_bytes, last));
+    s = seg_search(d, 0u, cb, lane);
+    sb = segpos(d, s);
+    se = segpos(d, s + 1);
+  } else {
+    while (nst < 4) advance();
+    if (nst == 5) return;
+    cb = nb; ce = ne; s = ns; sb = nsb; se = nse;
+    nst = 0;
+  }
+  uint32_t acc = 0;
+  u32x4 cur[U];
+  load_step<U, NT>(cur, lane_base + (cb >> 4), cb, ce, lane, cb + kStep <= ce);
+  uint64_t p = cb;
+  uint32_t tick = 0;
+  for (;;) {
+    // one acquisition stage every kStageSteps steps: an atomic's or a search load's latency
+    // (1-3 us under a full stream) is then covered by the steps streamed meanwhile instead of
+    // stalling the wave's in-order load queue
+    if (nst < 4 && ++tick % kStageSteps == 0) advance();
+    // prefetch the next step: in this segment, or the first step of the next chunk
+    const uint64_t pn = p + kStep;
+    const bool last_step = pn >= ce;
+    u32x4 nxt[U];
+    if (!last_step) {
+      load_step<U, NT>(nxt, lane_base + (pn >> 4), pn, ce, lane, pn + kStep <= ce);
+    } else if (nst == 4) {
+      load_step<U, NT>(nxt, lane_base + (nb >> 4), nb, ne, lane, nb + kStep <= ne);
+    }
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) { v[u] = cur[u]; cur[u] = nxt[u]; }
+    const bool full = !last_step || pn == ce;
+    if (full && sb <= p && pn <= se) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
+      }
+    } else {
+      const uint64_t q = min(pn, ce);
+      for (;;) {
+        const uint64_t lo_b = max(sb, p), hi_b = min(se, q);
+        if (lo_b < hi_b) {
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const int64_t x = (int64_t)(p + (uint64_t)u * 1024u + (uint64_t)lane * 16u);
+            acc = masked_sum16(v[u], (int64_t)lo_b - x, (int64_t)hi_b - x, acc);
+          }
+        }
+        if (se >= q) break;
+        flush(a.sums, s, acc);
+        acc = 0;
+        s = seg_next(d, s, se, lane);
+        sb = segpos(d, s);
+        se = segpos(d, s + 1);
+      }
+    }
+    if (!last_step) {
+      p = pn;
+      continue;
+    }
+    // segment done: switch to the next chunk
+    flush(a.sums, s, acc);
+    acc = 0;
+    const bool prefetched = nst == 4;
+    while (nst < 4) advance();  // not ready yet (short segment): finish synchronously
+    if (nst == 5) return;
+    cb = nb; ce = ne; s = ns; sb = nsb; se = nse;
+    p = cb;
+    nst = 0;
+    if (!prefetched) load_step<U, NT>(cur, lane_base + (cb >> 4), cb, ce, lane, cb + kStep <= ce);
+  }
 }
+
+template <int U, bool NT, bool PIPE, int PRIO = 0, bool STEAL = false>
+__global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a) {
+  if (STEAL)
+    digest_body_steal<U, NT, PRIO>(a, blockIdx.x);
+  else
+    digest_body<U, NT, PIPE, PRIO>(a, blockIdx.x);
+}
+
+
 
 // Fused build step (software pipelining of consecutive builds in ONE launch): workgroups
 // [0, tree_blocks) build the trees of the PREVIOUS build from its byte sums (tree_body, LDS
@@ -178,7 +378,7 @@ __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a)
 // wave per workgroup up to B = 128, the rest exit at once), so the SHA waves spread over many
 // CUs instead of crowding a few; tree workgroups come first so the dispatcher places them before
 // the streaming grid (sized to be fully resident) fills the remaining slots.
-template <int U, bool NT, bool PIPE, int PRIO = 0>
+template <int U, bool NT, bool PIPE, int PRIO = 0, bool STEAL = false>
 __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, TreeLaunch t, uint32_t tree_blocks,
                                                               uint32_t Q) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -186,7 +386,10 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
     tree_body_packed(t, Q, blockIdx.x, lds);
     return;
   }
-  digest_body<U, NT, PIPE, PRIO>(a, blockIdx.x - tree_blocks);
+  if (STEAL)
+    digest_body_steal<U, NT, PRIO>(a, blockIdx.x - tree_blocks);
+  else
+    digest_body<U, NT, PIPE, PRIO>(a, blockIdx.x - tree_blocks);
 }
 
 typedef void (*DigestKernel)(DigestLaunch);
@@ -195,16 +398,20 @@ struct Variant {
   DigestKernel fn;
   StepKernel step;
   int unroll;
+  bool steal;
 };
 
-#define MDE_VARIANT(U, NT, PIPE, PRIO) \
-  { bucket_digest_kernel<U, NT, PIPE, PRIO>, build_step_kernel<U, NT, PIPE, PRIO>, U }
+#define MDE_VARIANT(U, NT, PIPE, PRIO, STEAL) \
+  { bucket_digest_kernel<U, NT, PIPE, PRIO, STEAL>, build_step_kernel<U, NT, PIPE, PRIO, STEAL>, U, STEAL }
 
 // Kernel variants (tuning knob mde_set_tuning digest_variant = index; default in mde_api.cpp).
 const Variant kVariants[] = {
-    MDE_VARIANT(8, true, false, 0),  MDE_VARIANT(8, false, false, 0), MDE_VARIANT(16, true, false, 0),
-    MDE_VARIANT(4, true, false, 0),  MDE_VARIANT(4, true, true, 0),   MDE_VARIANT(8, true, true, 0),
-    MDE_VARIANT(16, false, false, 0), MDE_VARIANT(4, true, true, 2),  MDE_VARIANT(4, true, true, 3),
+    MDE_VARIANT(8, true, false, 0, false),  MDE_VARIANT(8, false, false, 0, false),
+    MDE_VARIANT(16, true, false, 0, false), MDE_VARIANT(4, true, false, 0, false),
+    MDE_VARIANT(4, true, true, 0, false),   MDE_VARIANT(8, true, true, 0, false),
+    MDE_VARIANT(16, false, false, 0, false), MDE_VARIANT(4, true, true, 2, false),
+    MDE_VARIANT(4, true, true, 3, false),   MDE_VARIANT(4, true, true, 2, true),
+    MDE_VARIANT(8, true, true, 2, true),
 };
 #undef MDE_VARIANT
 
@@ -215,6 +422,22 @@ const Variant& variant(int v) { return kVariants[(v >= 0 && v < kNumVariants) ? 
 }  // namespace
 
 int bucket_digest_variants() { return kNumVariants; }
+
+bool bucket_digest_steals(int v) { return variant(v).steal; }
+
+void plan_steal(uint64_t wave_bytes, uint64_t* head_bytes, uint64_t* chunk_bytes, uint32_t* tail_chunks) {
+  // Tail = about 1/6 of each wave range in up to 16 pieces of >= 16 KiB (the max step), at most
+  // 1/4 of the range. The pool absorbs a ~5 % spread of head finish times; pieces are small
+  // enough (~15 us per wave at C4) that the last ones do not leave a tail of their own.
+  uint64_t c = wave_bytes / 96 / kMaxStepBytes * kMaxStepBytes;
+  if (c < 4 * kMaxStepBytes) c = 4 * kMaxStepBytes;
+  uint32_t n = 16;
+  while (n > 1 && (uint64_t)n * c * 4 > wave_bytes) n /= 2;
+  if ((uint64_t)n * c * 4 > wave_bytes) n = 0;  // range too short to split
+  *chunk_bytes = c;
+  *tail_chunks = n;
+  *head_bytes = wave_bytes - (uint64_t)n * c;
+}
 
 int bucket_digest_blocks_per_cu(int v, int cap) {
   int blocks = 0;

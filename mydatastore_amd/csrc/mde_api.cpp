@@ -23,6 +23,7 @@
 
 // Digest-kernel tuning defaults (tools/digest_sweep.sh, profiles/r01_digest_sweep.json).
 constexpr int kDefaultDigestVariant = 7;  // U=4 nontemporal, register-prefetched, s_setprio 2
+constexpr int kStaticDigestVariant = 7;   // used when a stealing variant cannot steal
 constexpr int kDefaultDigestCap = 2;      // 2 workgroups (8 waves) per CU
 constexpr int kDefaultDigestOversub = 1;  // grid = resident slots x oversub
 
@@ -62,6 +63,10 @@ struct mde_ctx {
     bool dirty = false;
   };
   Slot pipe[2];
+  // Tail-stealing ticket heads of the digest kernel (two parities, zeroed at allocation; each
+  // stealing launch uses one parity and zeroes the other for the next launch).
+  unsigned long long* steal = nullptr;
+  uint32_t steal_parity = 0;
   struct Pending {
     bool active = false;
     int slot = 0;
@@ -207,10 +212,29 @@ mde::SegDesc seg_desc(const mde_records* r) {
   return d;
 }
 
-void plan_digest(mde_ctx* c, uint64_t bytes, mde::DigestLaunch* a) {
+int plan_digest(mde_ctx* c, uint64_t bytes, mde::DigestLaunch* a) {
   mde::plan_bucket_digest(bytes, c->cus, c->digest_blocks_per_cu, c->digest_oversub, &a->wave_bytes,
                           &a->n_waves);
   a->lds_bytes = c->digest_oversub > 1 ? (uint32_t)((160u * 1024u) / (uint32_t)c->digest_blocks_per_cu) & ~255u : 0u;
+  // Tail stealing needs fixed-length values and a split range; otherwise the static sibling.
+  if (mde::bucket_digest_steals(a->variant)) {
+    mde::plan_steal(a->wave_bytes, &a->head_bytes, &a->chunk_bytes, &a->tail_chunks);
+    if (!a->seg.stride || !a->tail_chunks) {
+      a->variant = kStaticDigestVariant;
+    } else {
+      if (!c->steal) {
+        if (hipMalloc(&c->steal, mde::kStealScratchBytes) != hipSuccess) {
+          c->steal = nullptr;
+          return set_err(c, MDE_E_NOMEM, "steal counter allocation failed");
+        }
+        MDE_HIP(c, hipMemsetAsync(c->steal, 0, mde::kStealScratchBytes, c->stream));
+      }
+      a->steal = c->steal;
+      a->steal_parity = c->steal_parity;
+      c->steal_parity ^= 1u;
+    }
+  }
+  return MDE_OK;
 }
 
 // Full validation of host-resident inputs (mde_build): the device API trusts its inputs but the
@@ -274,7 +298,8 @@ int digest_into(mde_ctx* c, const mde_records* r, unsigned long long* sums, uint
   if (!c->digest_blocks_per_cu)
     c->digest_blocks_per_cu = mde::bucket_digest_blocks_per_cu(c->digest_variant, c->digest_cap);
   a.variant = c->digest_variant;
-  plan_digest(c, r->values_bytes + a.seg.shift, &a);
+  int rc = plan_digest(c, r->values_bytes + a.seg.shift, &a);
+  if (rc) return rc;
   MDE_HIP(c, mde::launch_bucket_digest(a, c->stream));
   return MDE_OK;
 }
@@ -302,7 +327,8 @@ int digest_async_biased(mde_ctx* c, const mde_records* r, uint64_t end_pos, uint
     c->digest_blocks_per_cu = mde::bucket_digest_blocks_per_cu(c->digest_variant, c->digest_cap);
   a.variant = c->digest_variant;
   // plan over the bytes this chunk actually covers (span is known on the host)
-  plan_digest(c, span + 16, &a);
+  rc = plan_digest(c, span + 16, &a);
+  if (rc) return rc;
   MDE_HIP(c, mde::launch_bucket_digest(a, c->stream));
   return MDE_OK;
 }
@@ -387,7 +413,8 @@ int build_pipelined(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
       if (!c->digest_blocks_per_cu)
         c->digest_blocks_per_cu = mde::bucket_digest_blocks_per_cu(c->digest_variant, c->digest_cap);
       a.variant = c->digest_variant;
-      plan_digest(c, r->values_bytes + a.seg.shift, &a);
+      rc = plan_digest(c, r->values_bytes + a.seg.shift, &a);
+      if (rc) return rc;
     }
     a.sums = sl.sums;
     mde::TreeLaunch t;
@@ -516,6 +543,7 @@ void mde_destroy(mde_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->sums) (void)hipFree(c->sums);
     if (c->counts) (void)hipFree(c->counts);
+    if (c->steal) (void)hipFree(c->steal);
     for (auto& sl : c->pipe) {
       if (sl.sums) (void)hipFree(sl.sums);
       if (sl.counts) (void)hipFree(sl.counts);

@@ -38,6 +38,15 @@ struct DigestLaunch {
   uint32_t n_waves;
   int variant;                // kernel variant (unroll / load policy), see digest.hip
   uint32_t lds_bytes;         // residency cap for oversubscribed grids (0 = none)
+  // Tail stealing (variants with bucket_digest_steals; fixed-length values only): two parities of
+  // ticket heads + exhausted-heads mask (kStealScratchBytes) -- a launch uses parity
+  // steal_parity and zeroes the other for the next launch of the same context (launches of one
+  // context are stream-ordered).
+  unsigned long long* steal;
+  uint32_t steal_parity;
+  uint64_t head_bytes;        // bytes of each wave range its owner streams
+  uint64_t chunk_bytes;       // tail piece size (multiple of the 16 KiB max step)
+  uint32_t tail_chunks;       // tail pieces per wave
 };
 hipError_t launch_bucket_digest(const DigestLaunch& a, hipStream_t st);
 // Waves and wave range for an arena of `bytes` on a device with `cus` CUs.
@@ -45,6 +54,10 @@ void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, int oversub,
                         uint32_t* n_waves);
 int bucket_digest_blocks_per_cu(int variant, int cap);
 int bucket_digest_variants();
+bool bucket_digest_steals(int variant);
+constexpr uint64_t kStealScratchBytes = 512;
+// Head / tail split of each wave range for tail stealing (tail_chunks = 0: no split).
+void plan_steal(uint64_t wave_bytes, uint64_t* head_bytes, uint64_t* chunk_bytes, uint32_t* tail_chunks);
 
 struct TaggedLaunch {
   const uint8_t* base;        // values rounded down to 16 B

@@ -124,3 +124,118 @@ def test_pipelined_full_size_equals_standalone(engine):
     for o, _ in sets:
         for k in ("digest", "size", "items", "root", "nodes"):
             assert torch.equal(o[k], ref[k]), k
+
+
+def _variant_count(engine):
+    import mydatastore_amd as mde
+    n = 0
+    while True:
+        try:
+            engine.set_tuning(n, -1)
+        except mde.MdeError:
+            break
+        n += 1
+    engine.set_tuning(-1, -1)
+    return n
+
+
+def test_every_digest_variant_matches_golden(engine, golden, coracle):
+    """Every digest-kernel variant (static ranges, tail stealing; U = 4..16; both cache policies)
+    through both the standalone and the fused path gives the golden outputs."""
+    import torch
+    dev = torch.device("cuda:0")
+    engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    nv = _variant_count(engine)
+    assert nv >= 10
+    cases = golden("synth_cases.json")
+    try:
+        for v in range(nv):
+            engine.set_tuning(v, -1)
+            built = []
+            for c in cases:
+                rec, o, to, keep = _device_case(c, coracle, "a", dev)
+                engine.build_async(rec, to)
+                built.append((c, o, keep))
+                rec2, o2, to2, keep2 = _device_case(c, coracle, "a", dev)
+                engine.build_pipelined_async(rec2, to2)
+                built.append((c, o2, keep2))
+            engine.build_pipeline_drain_async()
+            engine.synchronize()
+            for c, o, _ in built:
+                _check(c, o, (c["name"], v))
+    finally:
+        engine.set_tuning(-1, -1)
+
+
+def test_every_digest_variant_full_size(engine):
+    """C4 at N=1 and the N=8 shard: every variant's roots equal the default build's (stealing
+    variants hand tail chunks between waves; any lost or doubled chunk changes the roots)."""
+    import torch
+    from mydatastore_amd.workload import make_workload
+    nv = _variant_count(engine)
+    for world in (8, 1):
+        w = make_workload(engine, n_partitions=1024, n_buckets=64, value_len=1024, part_mode="mod",
+                          n_keys=10_000_000, rank=0, world=world)
+        ref = w.build()
+        try:
+            for v in range(nv):
+                engine.set_tuning(v, -1)
+                for _ in range(2):  # twice: the stealing counters alternate between launches
+                    o = w.build()
+                    for k in ("digest", "root"):
+                        assert torch.equal(o[k], ref[k]), (world, v, k)
+        finally:
+            engine.set_tuning(-1, -1)
+        del w
+
+
+def test_stealing_skewed_arena_matches_torch_sums(engine):
+    """Tail stealing on a 300 MB arena with skew: 13-byte records (never 16-byte aligned), the
+    arena start 5 bytes past an allocation, 37 partitions x 100 buckets with empty buckets and
+    partitions and a few buckets of tens of MB. Digests of every variant equal per-bucket byte
+    sums computed by torch (cumsum over per-record sums) mod 999999."""
+    import torch
+    import mydatastore_amd as mde
+    dev = torch.device("cuda:0")
+    engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    P, B, V = 37, 100, 13
+    counts = torch.randint(0, 12_000, (P * B,), generator=g)
+    counts[torch.randint(0, P * B, (900,), generator=g)] = 0          # empty buckets
+    counts[5 * B:6 * B] = 0                                            # an empty partition
+    counts[torch.tensor([17, 1234, 3001])] = torch.tensor([4_000_000, 2_500_000, 3_000_000])
+    seg = torch.zeros(P * B + 1, dtype=torch.int64)
+    seg[1:] = torch.cumsum(counts, 0)
+    n = int(seg[-1])
+    buf = torch.randint(0, 256, (n * V + 32,), dtype=torch.uint8, device=dev)
+    vals = buf[5:5 + n * V]
+    rs = vals.view(n, V).to(torch.int64).sum(1)
+    cs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    cs[1:] = torch.cumsum(rs, 0)
+    dseg = seg.to(dev)
+    want = ((cs[dseg[1:]] - cs[dseg[:-1]]) % 999999).cpu()
+    rec = mde.Records(vals.data_ptr(), n * V, V, mde.LAYOUT_SORTED, 0, n, P, B, dseg.data_ptr())
+    nv = _variant_count(engine)
+    roots = {}
+    try:
+        for v in range(nv):
+            engine.set_tuning(v, -1)
+            for rep in range(2):
+                o = {"digest": torch.zeros(P * B, dtype=torch.int64, device=dev),
+                     "size": torch.zeros(P * B, dtype=torch.int32, device=dev),
+                     "items": torch.zeros(P, dtype=torch.int32, device=dev),
+                     "root": torch.zeros(P * 32, dtype=torch.uint8, device=dev)}
+                to = mde.TreeOut(o["digest"].data_ptr(), o["size"].data_ptr(), o["items"].data_ptr(),
+                                 o["root"].data_ptr(), 0)
+                if rep == 0:
+                    engine.build_async(rec, to)
+                else:
+                    engine.build_pipelined_async(rec, to)
+                    engine.build_pipeline_drain_async()
+                engine.synchronize()
+                assert torch.equal(o["digest"].cpu(), want), (v, rep)
+                assert torch.equal(o["size"].cpu().to(torch.int64), counts), (v, rep)
+                roots.setdefault("r", o["root"].cpu())
+                assert torch.equal(o["root"].cpu(), roots["r"]), (v, rep)
+    finally:
+        engine.set_tuning(-1, -1)
