@@ -194,7 +194,9 @@ int mde_extract(mde_ctx* ctx, const mde_records* rec, const int32_t* ids, uint64
  * MerkleTreeToPartitionEpochObject's object (main/merkle_tree.go:118-138, main/manager.go:1045):
  * leaves follow tree.Leafs (an odd B repeats the last bucket), zero scalars omitted, sizes packed.
  * Object i is written at out + i*out_stride (out_stride >= mde_epoch_tree_object_max_bytes(B)),
- * its length in out_len[i]. partition/valid/items may be NULL (0 / false / the tree.Leafs sum). */
+ * its length in out_len[i]. partition/valid/items may be NULL (0 / false / the tree.Leafs sum).
+ * n_buckets = 0 encodes objects without buckets (scalars only; digest/size may then be NULL), as
+ * proto.Marshal does for an RpcEpochTreeObject built field by field (main/manager_test.go:245). */
 uint64_t mde_epoch_tree_object_max_bytes(uint32_t n_buckets);
 int mde_encode_epoch_tree_objects_async(mde_ctx* ctx, uint32_t n, uint32_t n_buckets,
                                         const int32_t* partition, int64_t lower_epoch,

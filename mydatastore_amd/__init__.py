@@ -417,12 +417,13 @@ class Engine:
 
     # -- EpochTreeObject wire bytes -----------------------------------------------------------
     def encode_objects(self, n_buckets, digest, size, partition=None, lower=0, upper=0, valid=None,
-                       items=None):
-        """proto.Marshal(EpochTreeObject) for each of the n trees: list of bytes objects."""
+                       items=None, n_objects=None):
+        """proto.Marshal(EpochTreeObject) for each of the n trees: list of bytes objects
+        (n_buckets = 0: objects without buckets; pass n_objects)."""
         B = n_buckets
         digest = np.ascontiguousarray(digest, dtype=np.uint64)
         size = np.ascontiguousarray(size, dtype=np.int32)
-        n = digest.size // B
+        n = n_objects if n_objects is not None else digest.size // B
         stride = int(self.lib.mde_epoch_tree_object_max_bytes(B))
         out = np.zeros(n * stride, np.uint8)
         ln = np.zeros(n, np.uint32)

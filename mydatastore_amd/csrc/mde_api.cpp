@@ -1002,7 +1002,7 @@ int mde_extract(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t i
   return MDE_OK;
 }
 
-uint64_t mde_epoch_tree_object_max_bytes(uint32_t B) { return B ? mde::wire_max_bytes(B) : 0; }
+uint64_t mde_epoch_tree_object_max_bytes(uint32_t B) { return mde::wire_max_bytes(B); }
 
 int mde_encode_epoch_tree_objects_async(mde_ctx* c, uint32_t n, uint32_t B, const int32_t* partition,
                                         int64_t lower, int64_t upper, const uint64_t* digest,
@@ -1010,7 +1010,7 @@ int mde_encode_epoch_tree_objects_async(mde_ctx* c, uint32_t n, uint32_t B, cons
                                         uint8_t* out, uint64_t out_stride, uint32_t* out_len) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
-  if (!B || !digest || !size || !out || !out_len) return set_err(c, MDE_E_INVAL, "bad encode arguments");
+  if ((B && (!digest || !size)) || !out || !out_len) return set_err(c, MDE_E_INVAL, "bad encode arguments");
   if (out_stride < mde::wire_max_bytes(B)) return set_err(c, MDE_E_CAPACITY, "out_stride too small");
   mde::WireEncodeLaunch a{n, B, partition, lower, upper, digest, size, valid, items, out, out_stride, out_len};
   MDE_HIP(c, mde::launch_wire_encode(a, c->stream));
@@ -1023,7 +1023,7 @@ int mde_encode_epoch_tree_objects(mde_ctx* c, uint32_t n, uint32_t B, const int3
                                   uint64_t out_stride, uint32_t* out_len) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
-  if (!B || !digest || !size || !out || !out_len) return set_err(c, MDE_E_INVAL, "bad encode arguments");
+  if ((B && (!digest || !size)) || !out || !out_len) return set_err(c, MDE_E_INVAL, "bad encode arguments");
   if (out_stride < mde::wire_max_bytes(B)) return set_err(c, MDE_E_CAPACITY, "out_stride too small");
   const uint64_t N = n;
   const uint64_t sz[7] = {N * 4, N * B * 8, N * B * 4, N, N * 4, N * out_stride, N * 4};

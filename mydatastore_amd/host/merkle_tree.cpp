@@ -146,10 +146,9 @@ Error DifferentMerkleTreeBuckets(Engine& eng, const MerkleTree& t1, const Merkle
 }
 
 Error MarshalEpochTreeObject(Engine& eng, const EpochTreeObject& obj, Bytes* out) {
-  const uint32_t L = (uint32_t)obj.Buckets.size();
-  if (L == 0) return "cannot marshal an object without buckets";  // no tree has zero leaves
-  std::vector<uint64_t> digest(L);
-  std::vector<int32_t> size(L, 0);
+  const uint32_t L = (uint32_t)obj.Buckets.size();  // 0: an object without buckets (scalars only)
+  std::vector<uint64_t> digest(L + 1);
+  std::vector<int32_t> size(L + 1, 0);
   for (uint32_t i = 0; i < L; i++) {
     int64_t v;
     Error e = DecodeBytesToInt64(obj.Buckets[i], &v);
@@ -283,13 +282,27 @@ Error BuildEpochTreeObjectIndex(int partition, int64_t epoch, std::string* out) 
 }
 
 // ---------------------------------------------------------------- storage slice
-Iterator::Iterator(const std::map<std::string, Bytes>* m, const std::string& start, const std::string& limit)
-    : m_(m), it_(m->lower_bound(start)), limit_(limit) {}
+Iterator::Iterator(const std::map<std::string, Bytes>* m, const std::string& start, const std::string& limit,
+                   bool reverse)
+    : m_(m), limit_(limit), reverse_(reverse) {
+  if (!reverse) {
+    it_ = m->lower_bound(start);
+  } else {  // badger reverse Seek(Limit): the largest key <= Limit
+    it_ = m->upper_bound(limit);
+    if (it_ == m->begin()) valid_ = false;
+    else --it_;
+  }
+}
 
-bool Iterator::IsDone() const { return it_ == m_->end() || it_->first.compare(limit_) >= 0; }
+bool Iterator::IsDone() const { return !valid_ || it_ == m_->end() || it_->first.compare(limit_) >= 0; }
 
 bool Iterator::Next() {
-  ++it_;
+  if (!reverse_) {
+    ++it_;
+  } else if (valid_) {
+    if (it_ == m_->begin()) valid_ = false;
+    else --it_;
+  }
   return !IsDone();
 }
 
@@ -301,6 +314,29 @@ bool MemStorage::Get(const std::string& k, Bytes* v) const {
 }
 
 // ---------------------------------------------------------------- Manager slice
+Error Manager::GetEpochTreeLastValid(int32_t partitionId, EpochTreeObject* out) {
+  std::string index1, index2;
+  Error e = BuildEpochTreeObjectIndex(partitionId, 0, &index1);
+  if (!e.empty()) return "BuildEpochTreeObjectIndex: " + e;
+  e = BuildEpochTreeObjectIndex(partitionId, CurrentEpoch, &index2);
+  if (!e.empty()) return "BuildEpochTreeObjectIndex: " + e;
+  for (Iterator it = db_.NewIterator(index1, index2, true); !it.IsDone(); it.Next()) {
+    EpochTreeObject obj;
+    e = UnmarshalEpochTreeObject(eng_, it.Value(), &obj);
+    if (!e.empty()) return "RpcEpochTreeObject Unmarshal: " + e;
+    if (obj.Valid) {
+      *out = std::move(obj);
+      return "";
+    }
+  }
+  EpochTreeObject none;
+  none.Partition = partitionId;
+  none.LowerEpoch = -1;
+  none.UpperEpoch = -1;
+  *out = std::move(none);
+  return "";
+}
+
 Error Manager::KeyTags(const std::string& key, uint64_t* bucket, int* partition) {
   const uint64_t off[2] = {0, key.size()};
   uint32_t b = 0, p = 0;

@@ -12,6 +12,7 @@
 //   EpochTreeObjectToMerkleTree       main/merkle_tree.go:140-157  -> mde_tree_from_digests
 //   DifferentMerkleTreeBuckets        main/merkle_tree.go:159-216  -> mde_diff
 //   Manager.VerifyEpoch               main/manager.go:998-1118     -> mde_verify_epochs
+//   Manager.GetEpochTreeLastValid     main/manager.go:838-867      -> mde_decode_epoch_tree_objects
 //   CustomHash / MerkleBucket         main/merkle_tree.go:21-84
 //   merkletree.MerkleTree / Node      cbergoon/merkletree v0.2.0 (Root, Leafs, MerkleRoot, Left,
 //                                     Right, Hash, C)
@@ -153,9 +154,15 @@ Error BuildKeyIndex(const std::string& key, std::string* out);
 Error BuildEpochTreeObjectIndex(int partition, int64_t epoch, std::string* out);
 
 // ---------------------------------------------------------------- storage.Storage slice
+// storage/badger_storage.go:79-130. Forward: Seek(Start), then ascending keys until one is
+// >= Limit. Reverse (reverse = true): Seek(Limit) -- the largest key <= Limit -- then descending
+// keys; IsDone still tests only key >= Limit, so a reverse scan is NOT bounded below by Start
+// (it walks on into smaller keys, e.g. other partitions' objects) and a key equal to Limit ends
+// it at once. Reproduced as the reference behaves.
 class Iterator {
  public:
-  Iterator(const std::map<std::string, Bytes>* m, const std::string& start, const std::string& limit);
+  Iterator(const std::map<std::string, Bytes>* m, const std::string& start, const std::string& limit,
+           bool reverse = false);
   bool IsDone() const;
   bool Next();
   const std::string& Key() const { return it_->first; }
@@ -165,14 +172,16 @@ class Iterator {
   const std::map<std::string, Bytes>* m_;
   std::map<std::string, Bytes>::const_iterator it_;
   std::string limit_;
+  bool reverse_ = false;
+  bool valid_ = true;
 };
 
 class MemStorage {  // ordered KV with Badger iterator semantics (storage/badger_storage.go:79-130)
  public:
   void Put(const std::string& k, const Bytes& v) { kv_[k] = v; }
   bool Get(const std::string& k, Bytes* v) const;
-  Iterator NewIterator(const std::string& start, const std::string& limit) const {
-    return Iterator(&kv_, start, limit);
+  Iterator NewIterator(const std::string& start, const std::string& limit, bool reverse = false) const {
+    return Iterator(&kv_, start, limit, reverse);
   }
   size_t size() const { return kv_.size(); }
 
@@ -229,6 +238,13 @@ class Manager {
   Error VerifyEpochs(const std::vector<int>& partitionIds, int64_t Epoch,
                      const std::vector<std::vector<Bytes>>& peerObjects, int replicaCount,
                      std::vector<VerifyResult>* out, std::vector<Error>* errs);
+
+  // Manager.GetEpochTreeLastValid (main/manager.go:838-867): the newest stored EpochTreeObject
+  // with Valid set, scanning epochtree_{p}_ keys downward from CurrentEpoch (reverse iterator,
+  // with its unbounded-below quirk); none found -> {Partition: p, LowerEpoch: -1, UpperEpoch: -1}.
+  // The stored objects are decoded by the engine's wire decoder.
+  Error GetEpochTreeLastValid(int32_t partitionId, EpochTreeObject* out);
+  int64_t CurrentEpoch = 0;
 
   MemStorage& db() { return db_; }
   int PartitionBuckets() const { return partitionBuckets_; }

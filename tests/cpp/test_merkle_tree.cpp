@@ -4,6 +4,7 @@
 //   TestIndexManager    main/indexs_test.go:9-41
 //   TestIndexStorage    storage/index_test.go:9-40
 //   TestManagerStorage  main/manager_test.go:30-115 (range-iteration counts)
+//   TestGetEpochTreeLastValidObjectTask  main/manager_test.go:213-301
 // Prints "ROOT <name> <hex>" lines (checked against tests/golden by tests/test_cpp_port.py) and
 // exits non-zero on the first failed assertion.
 #include <cstdio>
@@ -284,6 +285,39 @@ static void TestStreamBucketsTask(Engine& eng, int writeValuesNum) {
   std::printf("STREAM n%d %zu %zu %zu\n", writeValuesNum, items.size(), sub.size(), want);
 }
 
+// TestGetEpochTreeLastValidObjectTask (main/manager_test.go:213-301): no stored object -> the
+// LowerEpoch -1 object; objects at epochs 1 (valid), 2 (valid), 3 (not valid) -> epoch 2. Plus the
+// reverse iterator's unbounded-below quirk: partition 2, with no objects of its own, finds
+// partition 1's newest valid object ("epochtree_1_..." < "epochtree_2_...").
+static void TestGetEpochTreeLastValid(Engine& eng) {
+  Manager manager(eng, 200, 100);
+  manager.CurrentEpoch = 100;
+  const int writePartition = 1;
+  EpochTreeObject got;
+  CHECK_OK(manager.GetEpochTreeLastValid(writePartition, &got));
+  CHECK(got.LowerEpoch == -1 && got.UpperEpoch == -1 && !got.Valid && got.Partition == writePartition,
+        "no stored object: LowerEpoch -1");
+  const struct { int64_t epoch; bool valid; } objs[] = {{1, true}, {2, true}, {3, false}};
+  for (const auto& o : objs) {
+    EpochTreeObject obj;
+    obj.Partition = writePartition;
+    obj.LowerEpoch = o.epoch;
+    obj.Valid = o.valid;
+    Bytes data;
+    std::string index;
+    CHECK_OK(MarshalEpochTreeObject(eng, obj, &data));
+    CHECK_OK(BuildEpochTreeObjectIndex(writePartition, obj.LowerEpoch, &index));
+    manager.db().Put(index, data);
+  }
+  CHECK_OK(manager.GetEpochTreeLastValid(writePartition, &got));
+  CHECK(got.LowerEpoch == 2 && got.Valid, "the correct object was returned");
+  CHECK_OK(manager.GetEpochTreeLastValid(2, &got));
+  CHECK(got.LowerEpoch == 2 && got.Partition == 1, "reverse scan walks below its Start bound");
+  manager.CurrentEpoch = 3;  // Seek(Limit) lands on epochtree_1_0000000003 == Limit: done at once
+  CHECK_OK(manager.GetEpochTreeLastValid(writePartition, &got));
+  CHECK(got.LowerEpoch == -1, "a key equal to Limit ends the reverse scan");
+}
+
 int main() {
   Engine eng(0);
   if (!eng.ok()) {
@@ -296,6 +330,7 @@ int main() {
   TestIndexStorage();
   TestManagerStorage(eng, 100);
   TestVerifyEpoch(eng);
+  TestGetEpochTreeLastValid(eng);
   TestStreamBucketsTask(eng, 100);
   TestStreamBucketsTask(eng, 10);
   if (failures) {

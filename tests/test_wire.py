@@ -58,6 +58,17 @@ def test_encode_matches_protobuf(engine, golden, coracle):
             want = wire_pb.marshal([-1, 2**31 - 1][t], -(2**40), 2**62, dg[t * B:(t + 1) * B].tolist(),
                                    sz[t * B:(t + 1) * B].tolist(), False, int(items[t]))
             assert got[t] == want, B
+    # objects without buckets (built field by field, main/manager_test.go:245-287)
+    parts = np.array([0, 1, -3], np.int32)
+    valid = np.array([1, 0, 1], np.uint8)
+    items = np.array([0, 5, -1], np.int32)
+    got = engine.encode_objects(0, np.zeros(0, np.uint64), np.zeros(0, np.int32), parts, 2, 0, valid,
+                                items, n_objects=3)
+    for t in range(3):
+        want = wire_pb.marshal(int(parts[t]), 2, 0, [], [], bool(valid[t]), int(items[t]))
+        assert got[t] == want, t
+        m = wire_pb.unmarshal(got[t])
+        assert len(m.buckets) == 0 and m.valid == bool(valid[t])
 
 
 @pytest.mark.gpu
