@@ -135,9 +135,9 @@ int mde_tree_async(mde_ctx* ctx, const mde_records* rec, const mde_tree_out* out
  * outputs of call i are complete (in stream order) after call i+1 or after
  * mde_build_pipeline_drain_async; rec's device arrays (seg_rec / part_rec, bucket_tag) and the
  * outputs of call i must stay valid until then. Results are identical to mde_build_async. Uses
- * scratch of its own: the other entry points may be interleaved freely. Layout A fuses when the
- * tree levels fit the fused launch's 32 KiB LDS budget (n_buckets <= 1024 always does); other
- * shapes run as separate launches on the same stream. */
+ * scratch of its own: the other entry points may be interleaved freely. Both layouts fuse when
+ * the previous build's tree levels fit the fused launch's 24 KiB LDS budget (n_buckets <= 1024
+ * always does); wider trees run as a separate tree launch on the same stream. */
 int mde_build_pipelined_async(mde_ctx* ctx, const mde_records* rec, const mde_tree_out* out);
 int mde_build_pipeline_drain_async(mde_ctx* ctx);
 

@@ -474,20 +474,20 @@ hipError_t launch_bucket_digest(const DigestLaunch& a, hipStream_t st) {
 }
 
 // Partitions per tree wave in the fused step: up to 16, as many as the LDS budget holds.
-uint32_t step_tree_q(uint32_t B) {
+uint32_t build_step_tree_q(uint32_t B) {
   const uint32_t n1 = (B + 1) / 2;
   const uint32_t per = (n1 + (n1 + 1) / 2) * 8u * 4u;  // bytes of level buffers per partition
   const uint32_t q = (kStepTreeLdsMax - 64u) / per;
   return q > 16u ? 16u : q;
 }
 
-bool build_step_fusable(uint32_t B) { return B >= 1 && step_tree_q(B) >= 1; }
+bool build_step_fusable(uint32_t B) { return B >= 1 && build_step_tree_q(B) >= 1; }
 
 hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st) {
   uint32_t tree_blocks = 0, Q = 0, lds = a.lds_bytes;
   if (t && t->P) {
     if (!build_step_fusable(t->B) || !t->sums_in) return hipErrorInvalidValue;
-    Q = step_tree_q(t->B);
+    Q = build_step_tree_q(t->B);
     tree_blocks = (t->P + Q - 1) / Q;
     // every workgroup of the dispatch reserves the tree waves' LDS; kStepTreeLdsMax keeps the
     // streaming grid fully resident

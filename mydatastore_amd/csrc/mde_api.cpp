@@ -268,9 +268,10 @@ int check_host_records(mde_ctx* c, const mde_records* r) {
 
 // span: bytes the records cover (0 = values_bytes); a streamed chunk passes a biased values
 // pointer whose values_bytes includes the bias.
-int tagged_async(mde_ctx* c, const mde_records* r, uint64_t span = 0, unsigned long long* sums = nullptr,
-                 uint32_t* counts = nullptr) {
-  mde::TaggedLaunch t{};
+void plan_tagged_launch(mde_ctx* c, const mde_records* r, uint64_t span, unsigned long long* sums,
+                        uint32_t* counts, mde::TaggedLaunch* out) {
+  mde::TaggedLaunch& t = *out;
+  t = mde::TaggedLaunch{};
   const uintptr_t v = reinterpret_cast<uintptr_t>(r->values);
   t.base = reinterpret_cast<const uint8_t*>(v & ~uintptr_t(15));
   t.shift = v & 15u;
@@ -280,9 +281,15 @@ int tagged_async(mde_ctx* c, const mde_records* r, uint64_t span = 0, unsigned l
   t.tag = r->bucket_tag;
   t.P = r->n_partitions;
   t.B = r->n_buckets;
-  t.sums = sums ? sums : c->sums;
-  t.counts = counts ? counts : c->counts;
+  t.sums = sums;
+  t.counts = counts;
   mde::plan_tagged((span ? span + 16 : r->values_bytes) + t.shift, c->cus, 8, &t.wave_bytes, &t.n_waves);
+}
+
+int tagged_async(mde_ctx* c, const mde_records* r, uint64_t span = 0, unsigned long long* sums = nullptr,
+                 uint32_t* counts = nullptr) {
+  mde::TaggedLaunch t;
+  plan_tagged_launch(c, r, span, sums ? sums : c->sums, counts ? counts : c->counts, &t);
   MDE_HIP(c, mde::launch_tagged_digest(t, c->stream));
   return MDE_OK;
 }
@@ -395,8 +402,9 @@ int build_pipelined(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   mde_ctx::Slot& sl = c->pipe[slot];
   int rc = ensure_slot(c, sl, S);
   if (rc) return rc;
-  const bool fused = r->layout == MDE_LAYOUT_SORTED && mde::build_step_fusable(r->n_buckets) &&
-                     (!pd.active || (pd.rec.layout == MDE_LAYOUT_SORTED && mde::build_step_fusable(pd.rec.n_buckets)));
+  // The digest role follows this build's layout (bucket_digest / tagged binning); the tree role
+  // only needs the pending build's B to fit the packed trees' LDS budget.
+  const bool fused = !pd.active || mde::build_step_fusable(pd.rec.n_buckets);
   if (!fused) {
     rc = pipeline_drain(c);
     if (rc) return rc;
@@ -406,6 +414,23 @@ int build_pipelined(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
       sl.dirty = true;
       return rc;
     }
+  } else if (r->layout == MDE_LAYOUT_TAGGED) {
+    mde::TaggedLaunch a;
+    plan_tagged_launch(c, r, 0, sl.sums, sl.counts, &a);
+    if (!(S && r->n_records && r->values_bytes)) a.n_waves = 0;
+    mde::TreeLaunch t;
+    if (pd.active) {
+      mde_ctx::Slot& ps = c->pipe[pd.slot];
+      rc = tree_launch_for(c, &pd.rec, &pd.out, ps.sums, ps.counts, &t);
+      if (rc) return rc;
+    }
+    hipError_t e = mde::launch_tagged_step(a, pd.active ? &t : nullptr, c->stream);
+    if (e != hipSuccess) {
+      sl.dirty = true;
+      if (pd.active) c->pipe[pd.slot].dirty = true;
+      pd.active = false;
+    }
+    MDE_HIP(c, e);
   } else {
     mde::DigestLaunch a{};
     if (S && r->n_records && r->values_bytes) {

@@ -78,6 +78,9 @@ struct TaggedLaunch {
 constexpr uint32_t kTaggedLdsMaxBuckets = 4096;
 void plan_tagged(uint64_t bytes, int cus, int waves_per_cu, uint64_t* wave_bytes, uint32_t* n_waves);
 hipError_t launch_tagged_digest(TaggedLaunch& a, hipStream_t st);
+struct TreeLaunch;
+// Fused build step for layout B (tagged.hip): this build's binning + the previous build's trees.
+hipError_t launch_tagged_step(TaggedLaunch& a, const TreeLaunch* t, hipStream_t st);
 
 struct TreeLaunch {
   uint32_t P, B;
@@ -113,6 +116,7 @@ bool tree_geometry(uint32_t B, TreeGeometry* g);
 // that keeps the streaming grid fully resident (B <= 1024 always does).
 constexpr uint32_t kStepTreeLdsMax = 24u * 1024u + 64u;
 bool build_step_fusable(uint32_t B);
+uint32_t build_step_tree_q(uint32_t B);  // partitions per packed tree wave
 hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st);
 
 struct DiffLaunch {

@@ -22,6 +22,9 @@
 // Fixed-length values only (0 < value_stride <= 2^30).
 #include "mde_device.hpp"
 #include "mde_internal.hpp"
+#include "tree_body.hpp"
+
+#include <algorithm>
 
 namespace mde {
 namespace {
@@ -94,8 +97,8 @@ __device__ __forceinline__ void load_step(u32x4 (&v)[kU], const u32x4* lane_base
   }
 }
 
-__global__ __launch_bounds__(kThreads) void tagged_digest_kernel(TaggedLaunch a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+// `block` = this workgroup's index among the digest workgroups of the launch.
+__device__ __forceinline__ void tagged_body(const TaggedLaunch& a, uint32_t block, uint32_t* smem) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t L = a.lrep;
   WaveBins w{nullptr, nullptr};
@@ -105,7 +108,7 @@ __global__ __launch_bounds__(kThreads) void tagged_digest_kernel(TaggedLaunch a)
     w.cnt = w.sum + (uint64_t)a.B * L;
     for (uint64_t j = lane; j < words; j += 64) w.sum[j] = 0;
   }
-  const uint32_t wave = blockIdx.x * (kThreads / 64) + wid;
+  const uint32_t wave = block * (kThreads / 64) + wid;
   if (wave >= a.n_waves) return;
   const uint64_t V = a.stride;
   const uint64_t r_lo = a.part_rec[0], r_hi = a.part_rec[a.P];
@@ -237,6 +240,38 @@ __global__ __launch_bounds__(kThreads) void tagged_digest_kernel(TaggedLaunch a)
   flush_bins(a, w, q, lane);
 }
 
+__global__ __launch_bounds__(kThreads) void tagged_digest_kernel(TaggedLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  tagged_body(a, blockIdx.x, smem);
+}
+
+// Fused build step for layout B (see build_step_kernel in digest.hip): the binning workgroups
+// come first, then tree_blocks workgroups build the previous build's trees (tree_body_packed,
+// first wave only). Both roles share one LDS reservation, the bins of two waves (33 KiB at
+// B = 64), so four binning workgroups fill a CU's LDS: tree workgroups placed first would each
+// hold back a binning workgroup until the tree is done (measured: 1.584 vs 1.551 ms at C4 with
+// the trees last); placed last they start in LDS left over and in the first slots that free up.
+__global__ __launch_bounds__(kThreads) void tagged_step_kernel(TaggedLaunch a, TreeLaunch t, uint32_t tree_blocks,
+                                                               uint32_t Q) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t digest_blocks = gridDim.x - tree_blocks;
+  if (blockIdx.x >= digest_blocks) {
+    tree_body_packed(t, Q, blockIdx.x - digest_blocks, smem);
+    return;
+  }
+  tagged_body(a, blockIdx.x, smem);
+}
+
+size_t prepare_tagged(TaggedLaunch& a) {  // launcher-set fields; returns the bins' LDS bytes
+  a.use_lds = a.B <= kTaggedLdsMaxBuckets ? 1 : 0;
+  // bins of one workgroup <= 64 KiB: (kThreads/64) * B * (L + 1) * 4 bytes
+  uint32_t L = 64;
+  while (L > 1 && (uint64_t)a.B * (L + 1) * (kThreads / 64) * 4 > 65536) L >>= 1;
+  a.lrep = L;
+  a.inv_stride_f = 1.0f / (float)a.stride;
+  return a.use_lds ? (size_t)(kThreads / 64) * ((size_t)a.B * L + a.B) * 4 : 0;
+}
+
 }  // namespace
 
 void plan_tagged(uint64_t bytes, int cus, int waves_per_cu, uint64_t* wave_bytes, uint32_t* n_waves) {
@@ -251,15 +286,26 @@ void plan_tagged(uint64_t bytes, int cus, int waves_per_cu, uint64_t* wave_bytes
 
 hipError_t launch_tagged_digest(TaggedLaunch& a, hipStream_t st) {
   if (a.n_waves == 0) return hipSuccess;
-  a.use_lds = a.B <= kTaggedLdsMaxBuckets ? 1 : 0;
-  // bins of one workgroup <= 64 KiB: (kThreads/64) * B * (L + 1) * 4 bytes
-  uint32_t L = 64;
-  while (L > 1 && (uint64_t)a.B * (L + 1) * (kThreads / 64) * 4 > 65536) L >>= 1;
-  a.lrep = L;
-  a.inv_stride_f = 1.0f / (float)a.stride;
-  const size_t lds = a.use_lds ? (size_t)(kThreads / 64) * ((size_t)a.B * L + a.B) * 4 : 0;
+  const size_t lds = prepare_tagged(a);
   const uint32_t blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);
   hipLaunchKernelGGL(tagged_digest_kernel, dim3(blocks), dim3(kThreads), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_tagged_step(TaggedLaunch& a, const TreeLaunch* t, hipStream_t st) {
+  const size_t bins = a.n_waves ? prepare_tagged(a) : 0;
+  uint32_t tree_blocks = 0, Q = 0;
+  size_t lds = bins;
+  if (t && t->P) {
+    if (!build_step_fusable(t->B) || !t->sums_in) return hipErrorInvalidValue;
+    Q = build_step_tree_q(t->B);
+    tree_blocks = (t->P + Q - 1) / Q;
+    lds = std::max<size_t>(lds, (size_t)packed_tree_lds_words(t->B, Q) * 4u);
+  }
+  const uint32_t blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);
+  if (tree_blocks + blocks == 0) return hipSuccess;
+  const TreeLaunch tl = t ? *t : TreeLaunch{};
+  hipLaunchKernelGGL(tagged_step_kernel, dim3(tree_blocks + blocks), dim3(kThreads), lds, st, a, tl, tree_blocks, Q);
   return hipGetLastError();
 }
 

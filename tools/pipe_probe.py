@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of build pipelining modes in ONE process (probe, not product code): ms per build for
 digest-only, fused (mde_build_pipelined_async) and two-stream pipelining, interleaved 3 times.
-    python tools/pipe_probe.py [world] [steps]
+    python tools/pipe_probe.py [world] [steps] [layout a|b]
 """
 import json
 import sys
@@ -10,14 +10,14 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 
-def main(world=1, steps=20):
+def main(world=1, steps=20, layout="a"):
     import torch
     import mydatastore_amd as mde
     from mydatastore_amd.workload import make_workload
     dev = torch.device("cuda", 0)
     e1, e2 = mde.Engine(0), mde.Engine(0)
     w = make_workload(e1, n_partitions=1024, n_buckets=64, value_len=1024, part_mode="mod",
-                      n_keys=10_000_000, rank=0, world=world)
+                      n_keys=10_000_000, rank=0, world=world, layout=layout)
     main_s = torch.cuda.current_stream(dev)
     tree_s = torch.cuda.Stream(dev)
     outs = [w.tree_out, w._outs()[1]]
@@ -97,9 +97,10 @@ def main(world=1, steps=20):
                               ("fused+side/4", lambda i: fused_side(i, 4), lambda: (e1.set_stream(main_s.cuda_stream), e1.build_pipeline_drain_async(), main_s.wait_stream(side))),
                               ("streams", streams, streams_join), ("serial", serial, None)):
             ms = timed(fn, fin)
-            print(json.dumps({"world": world, "mode": name, "rep": rep, "ms_per_build": round(ms, 4),
+            print(json.dumps({"world": world, "layout": layout, "mode": name, "rep": rep, "ms_per_build": round(ms, 4),
                               "GBps": round(w.value_bytes / ms / 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":
-    main(*(int(x) for x in sys.argv[1:]))
+    a = sys.argv[1:]
+    main(*(int(x) for x in a[:2]), *a[2:3])
