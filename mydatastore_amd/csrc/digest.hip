@@ -28,6 +28,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr uint64_t kMaxStepBytes = 16ull * 1024ull;  // largest wave step over all variants
+constexpr uint64_t kMaxWaveBytes = 256ull << 20;    // largest contiguous range per wave
 constexpr uint32_t kStealHeads = 16;                 // ticket counters of the tail pool
 constexpr uint32_t kStageSteps = 3;                  // steps between chunk-acquisition stages
 
@@ -458,7 +459,11 @@ void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, int oversub,
   uint64_t wb = (bytes + target_waves - 1) / target_waves;
   wb = (wb + kMaxStepBytes - 1) / kMaxStepBytes * kMaxStepBytes;
   if (wb < 2 * kMaxStepBytes) wb = 2 * kMaxStepBytes;
-  if (wb > (8ull << 20)) wb = 8ull << 20;  // keeps every u32 lane accumulator exact
+  // A lane reads wave_bytes / 64 bytes of its range, so its u32 accumulator holds at most
+  // 255 * wave_bytes / 64 (< 2^30 at the cap): exact. The cap sits far above every resident
+  // grid's range (64 GiB over 2,048 waves = 32 MiB), so big arenas keep one range per resident
+  // wave instead of queueing extra rounds of waves (C3 with an 8 MiB cap: 3.8 rounds, a tail).
+  if (wb > kMaxWaveBytes) wb = kMaxWaveBytes;
   *wave_bytes = wb;
   *n_waves = (uint32_t)((bytes + 16 + wb - 1) / wb);
 }

@@ -241,6 +241,48 @@ def test_many_tiny_buckets(engine, coracle):
         assert np.array_equal(out[k], exp[k]), k
 
 
+def test_long_wave_ranges_stay_exact():
+    """Arenas large enough that each streaming wave owns tens of MiB (here 20 GiB of 0xff over
+    the 1,024 waves of a 1-workgroup-per-CU grid, 20 MiB per wave, C3 gives 32 MiB): the u32 lane
+    accumulators stay exact and bucket boundaries at arbitrary records inside long ranges are
+    honoured, in the standalone build and in the fused pipelined step."""
+    import torch
+    import mydatastore_amd as mde
+    dev = torch.device("cuda:0")
+    eng = mde.Engine(0)
+    try:
+        eng.set_tuning(digest_blocks_per_cu=1)
+        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        V = 16
+        n = (20 << 30) // V + 3
+        vals = torch.full((n * V,), 255, dtype=torch.uint8, device=dev)
+        P, B = 2, 2
+        seg = np.array([0, 1_234_567, 700_000_001, 700_000_002, n], np.uint64)
+        dseg = torch.from_numpy(seg.view(np.int64)).to(dev)
+        rec = mde.Records(vals.data_ptr(), n * V, V, mde.LAYOUT_SORTED, 0, n, P, B, dseg.data_ptr())
+        cnt = np.diff(seg)
+        exp = [int(c) * V * 255 % O.HASH_MOD for c in cnt]
+        sets = []
+        for _ in range(3):
+            o = {"digest": torch.full((P * B,), -1, dtype=torch.int64, device=dev),
+                 "size": torch.zeros(P * B, dtype=torch.int32, device=dev),
+                 "items": torch.zeros(P, dtype=torch.int32, device=dev),
+                 "root": torch.zeros(P * 32, dtype=torch.uint8, device=dev),
+                 "nodes": torch.zeros(P * O.n_internal_nodes(B) * 32, dtype=torch.uint8, device=dev)}
+            sets.append((o, mde.TreeOut(*(o[k].data_ptr() for k in ("digest", "size", "items", "root", "nodes")))))
+        eng.build_async(rec, sets[0][1])
+        eng.build_pipelined_async(rec, sets[1][1])
+        eng.build_pipelined_async(rec, sets[2][1])
+        eng.build_pipeline_drain_async()
+        eng.synchronize()
+        for i, (o, _) in enumerate(sets):
+            assert o["digest"].cpu().numpy().view(np.uint64).tolist() == exp, i
+            assert o["size"].cpu().numpy().tolist() == [int(c) for c in cnt], i
+        del vals
+    finally:
+        eng.close()
+
+
 def test_full_size_properties(engine):
     """BASELINE config 2 shape (256 partitions x 100k keys x 256 B, B = 64) generated on device:
     per-partition mod-sum linearity, sizes, roots == tree(digests), exact recomputation of
