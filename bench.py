@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 logic on one GPU: ranks share cuda:0, gloo gather (not a measurement)")
+    ap.add_argument("--rccl-selftest", action="store_true",
+                    help="run the distributed path (nccl process group + root gather) even at one rank")
     ap.add_argument("--layout", default="a", choices=["a", "b"],
                     help="a: records sorted by (partition, bucket); b: grouped by partition in arrival "
                          "order with per-record bucket tags (binned on device)")
@@ -199,11 +201,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    # --rccl-selftest: the N>1 code path (process group, sharding, bucketed RCCL root gather on the
+    # side stream) with however many ranks were launched, one of them is enough (not a measurement)
+    use_dist = world > 1 or args.rccl_selftest
     if args.rehearse:
         local_rank = local_rank % torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if args.rehearse:
             dist.init_process_group("gloo")
@@ -270,11 +275,11 @@ def main():
     # reused only after the gather that read it (two builds earlier) has completed.
     # Fused mode at N > 1 buckets the root gathers: one collective per GATHER_BUCKET builds (its
     # output sets double-buffered: 2 x bucket sets), handed to the side stream once per bucket.
-    bucket = GATHER_BUCKET if (fused and world > 1) else 1
+    bucket = GATHER_BUCKET if (fused and use_dist) else 1
     outs = [(w.out, w.tree_out)] + [w._outs() for _ in range(2 * bucket - 1)]
     outs_b = [(wb.out, wb.tree_out), wb._outs()] if c5 else None
-    gather = RootGather(P, world, dev, width=64 if c5 else 32, batch=bucket) if world > 1 else None
-    side = torch.cuda.Stream(dev) if world > 1 else None
+    gather = RootGather(P, world, dev, width=64 if c5 else 32, batch=bucket) if use_dist else None
+    side = torch.cuda.Stream(dev) if use_dist else None
     ev_built = [torch.cuda.Event() for _ in range(2)]
     ev_gathered = [torch.cuda.Event() for _ in range(2)]
     n_step = [0]
@@ -296,14 +301,14 @@ def main():
         # bucket b, the main stream waits for the gather of bucket b-2 (same output sets).
         L = n_step[0]
         n_step[0] += 1
-        if world > 1 and L >= 1 and (L - 1) % bucket == 0:
+        if use_dist and L >= 1 and (L - 1) % bucket == 0:
             stream.wait_event(ev_gathered[((L - 1) // bucket) % 2])
         if ev_a is not None:
             ev_a.record(stream)
         eng.build_pipelined_async(w.rec, outs[L % (2 * bucket)][1])
         if ev_b is not None:
             ev_b.record(stream)
-        if world > 1 and L >= 1 and L % bucket == 0:
+        if use_dist and L >= 1 and L % bucket == 0:
             gather_bucket(L - 1)
 
     def step(ev_a=None, ev_b=None):
@@ -312,7 +317,7 @@ def main():
         i = n_step[0] % 2
         n_step[0] += 1
         o, to = outs[i]
-        if world > 1 and not pipeline:
+        if use_dist and not pipeline:
             stream.wait_event(ev_gathered[i])
         if pipeline:
             e = engines[i]
@@ -325,7 +330,7 @@ def main():
                 ev_b.record(stream)
             ev_digested[i].record(stream)
             tstream.wait_event(ev_digested[i])
-            if world > 1:
+            if use_dist:
                 tstream.wait_event(ev_gathered[i])  # output set i no longer read by its gather
             e.set_stream(tstream.cuda_stream)
             e.tree_async(w.rec, to)
@@ -347,8 +352,8 @@ def main():
             eng.diff_async(Pl, B, o["digest"], o["nodes"], B, ob["digest"], ob["nodes"], diff_ids, cap, diff_cnt)
             eng.extract_async(wb.rec, diff_ids, cap, diff_cnt, part_off, out_rec, rec_cap, out_vals,
                               out_voff, bytes_cap, status)
-            roots = torch.cat([o["root"], ob["root"]]) if world > 1 else None
-        if world > 1:
+            roots = torch.cat([o["root"], ob["root"]]) if use_dist else None
+        if use_dist:
             ev_built[i].record(build_stream)
             side.wait_event(ev_built[i])
             with torch.cuda.stream(side):
@@ -359,7 +364,7 @@ def main():
         if fused:
             eng.build_pipeline_drain_async()
             last = n_step[0] - 1
-            if world > 1 and last >= 0:  # the last bucket (launch L gathers buckets ending at L-1)
+            if use_dist and last >= 0:  # the last bucket (launch L gathers buckets ending at L-1)
                 gather_bucket(last)
             n_step[0] = 0  # the next run of builds starts a fresh bucket sequence
         if pipeline:
@@ -376,7 +381,7 @@ def main():
     root_ref, _ = eng.tree_from_digests(w.out["digest"].cpu().numpy().view(np.uint64), B)
     parity = {"tree_of_device_digests_equals_device_roots":
               bool(np.array_equal(root_ref, w.out["root"].cpu().numpy()))}
-    if world > 1 and not c5:  # the gathered slab of this rank holds exactly its own roots
+    if use_dist and not c5:  # the gathered slab of this rank holds exactly its own roots
         allr = gather.assemble(0)
         parity["gathered_roots_match"] = bool(np.array_equal(allr[w.partition_ids].reshape(-1),
                                                              w.out["root"].cpu().numpy()))
@@ -404,7 +409,7 @@ def main():
     join()  # the timed region runs exactly K digests and K trees (its last trees in its own join)
     n_ev = args.steps
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -423,12 +428,12 @@ def main():
         bracket[1].record(stream)
     join()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     t1 = time.perf_counter()
     eng.set_stream(stream.cuda_stream)
     ms = (t1 - t0) * 1e3 / args.steps
-    if world > 1 and fused and not c5 and args.steps > 0:
+    if use_dist and fused and not c5 and args.steps > 0:
         # the last build of the timed run, as gathered: this rank's rows equal its own roots
         last = args.steps - 1
         allr = gather.assemble((last // bucket) % 2, last % bucket)
@@ -438,7 +443,7 @@ def main():
     kern_ms = (bracket[0].elapsed_time(bracket[1]) / args.steps if fused
                else float(np.mean([a.elapsed_time(b) for a, b in evs])))
     hashed = w.value_bytes * (2 if c5 else 1)
-    if world > 1:
+    if use_dist:
         t = torch.tensor([ms, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms = float(t[0])
@@ -473,10 +478,10 @@ def main():
                        "n_buckets": B, "bytes_hashed_per_step": total_bytes,
                        "partitions_per_gpu": Pl, "parallelism": f"partition-shard x{world}",
                        "root_gather": ("rccl all_gather_into_tensor of ceil(P/N) x 32 B slabs on a side "
-                                       "stream, overlapped with the next build") if world > 1 else None},
+                                       "stream, overlapped with the next build") if use_dist else None},
             "roofline": {"bound": "hbm",
                          "kernel": ("build_step_kernel" if fused else "bucket_digest_kernel")
-                         if args.layout == "a" else "tagged_digest_kernel",
+                         if args.layout == "a" else ("tagged_step_kernel" if fused else "tagged_digest_kernel"),
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(("c4" if c5 else args.config) + ("" if args.layout == "a" else "_b"),
@@ -499,7 +504,7 @@ def main():
         if world == 1 and not args.no_e2e and not args.profile and not c5:
             result["end_to_end"] = end_to_end(torch, eng, w, B)
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
     eng.close()
