@@ -236,7 +236,7 @@ def main():
     # build i's latency-bound tree (11 dependent SHA-256 compressions) overlaps build i+1's HBM
     # streaming instead of serializing behind it. Every build still runs both kernels in full.
     mode = args.pipeline
-    if args.no_pipeline or c5:
+    if args.no_pipeline or (c5 and mode == "streams"):
         mode = "off"
     elif mode == "auto":
         mode = "fused" if args.layout == "a" else "streams"
@@ -275,7 +275,7 @@ def main():
     # reused only after the gather that read it (two builds earlier) has completed.
     # Fused mode at N > 1 buckets the root gathers: one collective per GATHER_BUCKET builds (its
     # output sets double-buffered: 2 x bucket sets), handed to the side stream once per bucket.
-    bucket = GATHER_BUCKET if (fused and use_dist) else 1
+    bucket = GATHER_BUCKET if (fused and use_dist and not c5) else 1
     outs = [(w.out, w.tree_out)] + [w._outs() for _ in range(2 * bucket - 1)]
     outs_b = [(wb.out, wb.tree_out), wb._outs()] if c5 else None
     gather = RootGather(P, world, dev, width=64 if c5 else 32, batch=bucket) if use_dist else None
@@ -311,7 +311,37 @@ def main():
         if use_dist and L >= 1 and L % bucket == 0:
             gather_bucket(L - 1)
 
+    def c5_compare(j):  # diff + extract (+ N>1 root gather) of step j; its trees precede in stream order
+        k = j % 2
+        o, ob = outs[k][0], outs_b[k][0]
+        eng.diff_async(Pl, B, o["digest"], o["nodes"], B, ob["digest"], ob["nodes"], diff_ids, cap, diff_cnt)
+        eng.extract_async(wb.rec, diff_ids, cap, diff_cnt, part_off, out_rec, rec_cap, out_vals,
+                          out_voff, bytes_cap, status)
+        if use_dist:
+            roots = torch.cat([o["root"], ob["root"]])
+            ev_built[k].record(stream)
+            side.wait_event(ev_built[k])
+            with torch.cuda.stream(side):
+                gather.gather(roots, k)
+                ev_gathered[k].record(side)
+
+    def step_c5_fused(ev_a=None, ev_b=None):
+        # Launch 2L digests replica A of step L and builds replica B's trees of step L-1; step
+        # L-1's diff + extract follow it; launch 2L+1 digests replica B and builds A's trees of
+        # step L. Output sets alternate per step (the compare of L-1 reads set (L-1) % 2 while
+        # step L writes set L % 2); at N > 1 a set is rewritten only after its gather completed.
+        L = n_step[0]
+        n_step[0] += 1
+        if use_dist:
+            stream.wait_event(ev_gathered[L % 2])
+        eng.build_pipelined_async(w.rec, outs[L % 2][1])
+        if L >= 1:
+            c5_compare(L - 1)
+        eng.build_pipelined_async(wb.rec, outs_b[L % 2][1])
+
     def step(ev_a=None, ev_b=None):
+        if fused and c5:
+            return step_c5_fused(ev_a, ev_b)
         if fused:
             return step_fused(ev_a, ev_b)
         i = n_step[0] % 2
@@ -364,7 +394,9 @@ def main():
         if fused:
             eng.build_pipeline_drain_async()
             last = n_step[0] - 1
-            if use_dist and last >= 0:  # the last bucket (launch L gathers buckets ending at L-1)
+            if c5 and last >= 0:
+                c5_compare(last)
+            elif use_dist and last >= 0:  # the last bucket (launch L gathers buckets ending at L-1)
                 gather_bucket(last)
             n_step[0] = 0  # the next run of builds starts a fresh bucket sequence
         if pipeline:
@@ -440,7 +472,9 @@ def main():
         parity["gathered_roots_match_after_run"] = bool(np.array_equal(
             allr[w.partition_ids].reshape(-1), outs[last % (2 * bucket)][0]["root"].cpu().numpy()))
         parity_ok = parity_ok and parity["gathered_roots_match_after_run"]
-    kern_ms = (bracket[0].elapsed_time(bracket[1]) / args.steps if fused
+    # C5 fused: two build_step_kernel launches + the compare kernels per step inside the bracket;
+    # the per-launch figure is bracket / 2K (the compare kernels counted against it, conservative)
+    kern_ms = (bracket[0].elapsed_time(bracket[1]) / args.steps / (2 if c5 else 1) if fused
                else float(np.mean([a.elapsed_time(b) for a, b in evs])))
     hashed = w.value_bytes * (2 if c5 else 1)
     if use_dist:
@@ -492,7 +526,9 @@ def main():
             "simulated_shard_of_world": shard_world if shard_world != world else None,
             "pipeline": {"fused": "one build_step_kernel launch per build: this build's digest "
                                   "workgroups + the previous build's tree workgroups "
-                                  "(mde_build_pipelined_async); the last build's trees in the drain",
+                                  "(mde_build_pipelined_async); the last build's trees in the drain"
+                                  + ("; C5: replicas A and B alternate on one context, each step's "
+                                     "diff + extract after the launch that completes its trees" if c5 else ""),
                          "streams": "2 contexts alternate builds; each build's tree kernel runs on a "
                                     "second stream, overlapping the next build's digest kernel",
                          "off": None}[mode],
