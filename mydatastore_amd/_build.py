@@ -6,6 +6,7 @@ Outputs (git-ignored, but shipped to the GPU box with the snapshot):
   mydatastore_amd/libmde.so         C ABI (include/mde.h) + gfx950 kernels
   mydatastore_amd/libmde_host.so    C++ mirror of main/merkle_tree.go over the C ABI
   tests/cpp/build/test_merkle_tree  C++ port of the reference's Merkle tests
+  tests/cpp/build/cabi_bench        plain-C driver of the C ABI (C4 build, no PyTorch)
   oracle/build/liboracle.so         CPU restatement (test infrastructure only)
 """
 from __future__ import annotations
@@ -29,6 +30,7 @@ LIB = PKG / "libmde.so"
 HOST_LIB = PKG / "libmde_host.so"
 ORACLE_LIB = ROOT / "oracle" / "build" / "liboracle.so"
 CPP_TEST = ROOT / "tests" / "cpp" / "build" / "test_merkle_tree"
+C_BENCH = ROOT / "tests" / "cpp" / "build" / "cabi_bench"
 
 
 def _stale(target: Path, deps) -> bool:
@@ -73,6 +75,12 @@ def build_host(verbose: bool = True) -> Path:
         _run(["g++", "-O2", "-std=c++17", "-Wall", f"-I{ROOT / 'include'}", f"-I{hdir}", test_src,
               "-o", CPP_TEST, f"-L{PKG}", "-lmde_host", "-lmde",
               f"-Wl,-rpath,{PKG}", "-Wl,-rpath,$ORIGIN/../../../mydatastore_amd"], verbose)
+    c_src = ROOT / "tests" / "cpp" / "cabi_bench.c"
+    if c_src.exists() and _stale(C_BENCH, [c_src, ROOT / "include" / "mde.h", LIB]):
+        C_BENCH.parent.mkdir(parents=True, exist_ok=True)
+        _run(["gcc", "-O2", "-std=c11", "-D_POSIX_C_SOURCE=199309L", "-Wall", f"-I{ROOT / 'include'}",
+              c_src, "-o", C_BENCH, f"-L{PKG}", "-lmde", f"-Wl,-rpath,{PKG}",
+              "-Wl,-rpath,$ORIGIN/../../../mydatastore_amd"], verbose)
     return HOST_LIB
 
 
