@@ -457,8 +457,17 @@ void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, int oversub,
                                 (uint64_t)(blocks_per_cu > 0 ? blocks_per_cu : 4) * (kThreads / 64) *
                                 (uint64_t)(oversub > 0 ? oversub : 1);
   uint64_t wb = (bytes + target_waves - 1) / target_waves;
-  wb = (wb + kMaxStepBytes - 1) / kMaxStepBytes * kMaxStepBytes;
-  if (wb < 2 * kMaxStepBytes) wb = 2 * kMaxStepBytes;
+  if (wb > kMaxStepBytes) {
+    wb = (wb + kMaxStepBytes - 1) / kMaxStepBytes * kMaxStepBytes;
+    if (wb < 2 * kMaxStepBytes) wb = 2 * kMaxStepBytes;
+  } else {
+    // Small arenas (under 32 MiB at 2,048 waves): short ranges (16-byte multiples, >= 256 B) over
+    // the whole grid. Each bucket boundary a wave crosses is one dependent seg_rec load (~1-2 us),
+    // so one wave walking all 64 buckets of an 8 KB one-partition build took ~60 us; spread over
+    // 32 waves it takes two or three such loads per wave.
+    wb = (wb + 15) / 16 * 16;
+    if (wb < 256) wb = 256;
+  }
   // A lane reads wave_bytes / 64 bytes of its range, so its u32 accumulator holds at most
   // 255 * wave_bytes / 64 (< 2^30 at the cap): exact. The cap sits far above every resident
   // grid's range (64 GiB over 2,048 waves = 32 MiB), so big arenas keep one range per resident

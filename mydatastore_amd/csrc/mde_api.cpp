@@ -48,6 +48,9 @@ struct mde_ctx {
   struct Buf { void* p = nullptr; uint64_t cap = 0; };
   Buf stage[16];
   Buf nodes_scratch;
+  // Small host-API calls (mde_build): inputs and outputs each travel as ONE copy between a
+  // pinned host region (pin_*) and a device region (packed_*).
+  Buf packed_in, packed_out, pin_in, pin_out;
   Buf extract_scratch;
   Buf verify_scratch;
   // Host-ingest ring (mde_build_streamed): two slots of values / value_off / seg_rec.
@@ -113,6 +116,39 @@ int ensure_buf(mde_ctx* c, mde_ctx::Buf& b, uint64_t bytes) {
   b.cap = cap;
   return MDE_OK;
 }
+
+int ensure_pinned(mde_ctx* c, mde_ctx::Buf& b, uint64_t bytes) {
+  if (b.cap >= bytes && b.p) return MDE_OK;
+  if (b.p) {
+    MDE_HIP(c, hipStreamSynchronize(c->stream));
+    MDE_HIP(c, hipHostFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  uint64_t cap = bytes < 4096 ? 4096 : bytes;
+  if (hipHostMalloc(&b.p, cap, hipHostMallocDefault) != hipSuccess) {
+    b.p = nullptr;
+    return set_err(c, MDE_E_NOMEM, "pinned host allocation of %llu bytes failed", (unsigned long long)cap);
+  }
+  b.cap = cap;
+  return MDE_OK;
+}
+
+// 256-byte aligned pieces of one staging region.
+struct Pack {
+  uint64_t total = 0;
+  uint64_t add(uint64_t bytes) {
+    const uint64_t o = total;
+    total += (bytes + 255) & ~255ull;
+    return o;
+  }
+};
+
+// Calls whose inputs and outputs each fit this go through the packed path: a pageable
+// hipMemcpy costs ~10-20 us of fixed overhead per call, so the six to eight separate copies of
+// a one-partition build cost more than the build itself; one pinned copy each way plus host
+// memcpys does not. Larger calls keep the direct copies (the runtime pipelines those).
+constexpr uint64_t kPackedCallMax = 8ull << 20;
 
 int ensure_sums(mde_ctx* c, uint64_t S) {
   if (c->sums_cap < S || !c->sums) {
@@ -576,6 +612,10 @@ void mde_destroy(mde_ctx* c) {
     for (auto& b : c->stage)
       if (b.p) (void)hipFree(b.p);
     if (c->nodes_scratch.p) (void)hipFree(c->nodes_scratch.p);
+    if (c->packed_in.p) (void)hipFree(c->packed_in.p);
+    if (c->packed_out.p) (void)hipFree(c->packed_out.p);
+    if (c->pin_in.p) (void)hipHostFree(c->pin_in.p);
+    if (c->pin_out.p) (void)hipHostFree(c->pin_out.p);
     if (c->extract_scratch.p) (void)hipFree(c->extract_scratch.p);
     if (c->verify_scratch.p) (void)hipFree(c->verify_scratch.p);
     for (int i = 0; i < 2; i++) {
@@ -693,6 +733,41 @@ int mde_build(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   const uint64_t nvo = r->value_stride ? 0 : (r->n_records + 1);
   const uint64_t sizes[10] = {r->values_bytes, nvo * 8, tagged ? (P + 1) * 8 : (S + 1) * 8, S * 8, S * 4, P * 4,
                               P * 32, o->nodes ? P * NI * 32 : 0, tagged ? r->n_records * 2 : 0, 0};
+  Pack pin, pout;
+  const uint64_t in_off[4] = {pin.add(sizes[0]), pin.add(sizes[1]), pin.add(sizes[2]), pin.add(sizes[8])};
+  const uint64_t out_off[5] = {pout.add(sizes[3]), pout.add(sizes[4]), pout.add(sizes[5]), pout.add(sizes[6]),
+                               pout.add(sizes[7])};
+  if (pin.total <= kPackedCallMax && pout.total <= kPackedCallMax) {
+    if ((rc = ensure_buf(c, c->packed_in, pin.total)) || (rc = ensure_buf(c, c->packed_out, pout.total)) ||
+        (rc = ensure_pinned(c, c->pin_in, pin.total)) || (rc = ensure_pinned(c, c->pin_out, pout.total)))
+      return rc;
+    uint8_t* hi = static_cast<uint8_t*>(c->pin_in.p);
+    uint8_t* di = static_cast<uint8_t*>(c->packed_in.p);
+    uint8_t* ho = static_cast<uint8_t*>(c->pin_out.p);
+    uint8_t* dd = static_cast<uint8_t*>(c->packed_out.p);
+    const void* src[4] = {r->values, r->value_off, tagged ? r->part_rec : r->seg_rec, r->bucket_tag};
+    const uint64_t len[4] = {sizes[0], sizes[1], sizes[2], sizes[8]};
+    for (int i = 0; i < 4; i++)
+      if (len[i]) std::memcpy(hi + in_off[i], src[i], len[i]);
+    MDE_HIP(c, hipMemcpyAsync(di, hi, pin.total, hipMemcpyHostToDevice, c->stream));
+    mde_records dr = *r;
+    dr.values = di + in_off[0];
+    dr.value_off = nvo ? reinterpret_cast<const uint64_t*>(di + in_off[1]) : nullptr;
+    dr.seg_rec = tagged ? nullptr : reinterpret_cast<const uint64_t*>(di + in_off[2]);
+    dr.part_rec = tagged ? reinterpret_cast<const uint64_t*>(di + in_off[2]) : nullptr;
+    dr.bucket_tag = tagged ? reinterpret_cast<const uint16_t*>(di + in_off[3]) : nullptr;
+    mde_tree_out dout{reinterpret_cast<uint64_t*>(dd + out_off[0]), reinterpret_cast<int32_t*>(dd + out_off[1]),
+                      reinterpret_cast<int32_t*>(dd + out_off[2]), dd + out_off[3],
+                      o->nodes ? dd + out_off[4] : nullptr};
+    if ((rc = digest_async(c, &dr))) return rc;
+    if ((rc = tree_async(c, &dr, &dout))) return rc;
+    MDE_HIP(c, hipMemcpyAsync(ho, dd, pout.total, hipMemcpyDeviceToHost, c->stream));
+    MDE_HIP(c, hipStreamSynchronize(c->stream));
+    void* dst[5] = {o->digest, o->size, o->items, o->root, o->nodes};
+    for (int i = 0; i < 5; i++)
+      if (dst[i] && sizes[3 + i]) std::memcpy(dst[i], ho + out_off[i], sizes[3 + i]);
+    return MDE_OK;
+  }
   for (int i = 0; i < 9; i++)
     if ((rc = ensure_buf(c, c->stage[i], sizes[i]))) return rc;
   auto dp = [&](int i) { return c->stage[i].p; };
