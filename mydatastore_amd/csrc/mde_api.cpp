@@ -150,6 +150,81 @@ struct Pack {
 // memcpys does not. Larger calls keep the direct copies (the runtime pipelines those).
 constexpr uint64_t kPackedCallMax = 8ull << 20;
 
+// Staging of one synchronous host-API call: declare the inputs (host source, device bytes) and
+// outputs (host destination, bytes), then upload() -> launch on dev_in/dev_out -> download().
+// Packed calls use the context's packed_* / pin_* regions; larger ones one stage[] buffer per
+// piece (inputs first, then outputs) with direct copies. A NULL host pointer skips its copy.
+class HostIo {
+ public:
+  explicit HostIo(mde_ctx* c) : c_(c) {}
+  int in(const void* src, uint64_t copy_bytes, uint64_t dev_bytes) {
+    pieces_[n_] = {const_cast<void*>(src), copy_bytes, dev_bytes, pin_.add(dev_bytes), true};
+    return n_++;
+  }
+  int out(void* dst, uint64_t bytes) {
+    pieces_[n_] = {dst, bytes, bytes, pout_.add(bytes), false};
+    return n_++;
+  }
+  void* dev(int i) const { return dev_[i]; }
+  int upload() {
+    packed_ = pin_.total <= kPackedCallMax && pout_.total <= kPackedCallMax;
+    int rc;
+    if (packed_) {
+      if ((rc = ensure_buf(c_, c_->packed_in, pin_.total)) || (rc = ensure_buf(c_, c_->packed_out, pout_.total)) ||
+          (rc = ensure_pinned(c_, c_->pin_in, pin_.total)) || (rc = ensure_pinned(c_, c_->pin_out, pout_.total)))
+        return rc;
+      uint8_t* hi = static_cast<uint8_t*>(c_->pin_in.p);
+      for (int i = 0; i < n_; i++) {
+        const Piece& q = pieces_[i];
+        dev_[i] = static_cast<uint8_t*>(q.input ? c_->packed_in.p : c_->packed_out.p) + q.off;
+        if (q.input && q.host && q.copy) std::memcpy(hi + q.off, q.host, q.copy);
+      }
+      MDE_HIP(c_, hipMemcpyAsync(c_->packed_in.p, hi, pin_.total, hipMemcpyHostToDevice, c_->stream));
+      return MDE_OK;
+    }
+    for (int i = 0; i < n_; i++) {
+      const Piece& q = pieces_[i];
+      if ((rc = ensure_buf(c_, c_->stage[i], q.dev))) return rc;
+      dev_[i] = c_->stage[i].p;
+      if (q.input && q.host && q.copy)
+        MDE_HIP(c_, hipMemcpyAsync(dev_[i], q.host, q.copy, hipMemcpyHostToDevice, c_->stream));
+    }
+    return MDE_OK;
+  }
+  int download() {
+    if (packed_) {
+      uint8_t* ho = static_cast<uint8_t*>(c_->pin_out.p);
+      MDE_HIP(c_, hipMemcpyAsync(ho, c_->packed_out.p, pout_.total, hipMemcpyDeviceToHost, c_->stream));
+      MDE_HIP(c_, hipStreamSynchronize(c_->stream));
+      for (int i = 0; i < n_; i++) {
+        const Piece& q = pieces_[i];
+        if (!q.input && q.host && q.copy) std::memcpy(q.host, ho + q.off, q.copy);
+      }
+      return MDE_OK;
+    }
+    for (int i = 0; i < n_; i++) {
+      const Piece& q = pieces_[i];
+      if (!q.input && q.host && q.copy)
+        MDE_HIP(c_, hipMemcpyAsync(q.host, dev_[i], q.copy, hipMemcpyDeviceToHost, c_->stream));
+    }
+    MDE_HIP(c_, hipStreamSynchronize(c_->stream));
+    return MDE_OK;
+  }
+
+ private:
+  struct Piece {
+    void* host;
+    uint64_t copy, dev, off;
+    bool input;
+  };
+  mde_ctx* c_;
+  Piece pieces_[16];
+  void* dev_[16] = {};
+  int n_ = 0;
+  Pack pin_, pout_;
+  bool packed_ = false;
+};
+
 int ensure_sums(mde_ctx* c, uint64_t S) {
   if (c->sums_cap < S || !c->sums) {
     if (c->sums) {
@@ -731,71 +806,27 @@ int mde_build(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   const uint64_t P = r->n_partitions, S = P * r->n_buckets, NI = mde::tree_internal(r->n_buckets);
   const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
   const uint64_t nvo = r->value_stride ? 0 : (r->n_records + 1);
-  const uint64_t sizes[10] = {r->values_bytes, nvo * 8, tagged ? (P + 1) * 8 : (S + 1) * 8, S * 8, S * 4, P * 4,
-                              P * 32, o->nodes ? P * NI * 32 : 0, tagged ? r->n_records * 2 : 0, 0};
-  Pack pin, pout;
-  const uint64_t in_off[4] = {pin.add(sizes[0]), pin.add(sizes[1]), pin.add(sizes[2]), pin.add(sizes[8])};
-  const uint64_t out_off[5] = {pout.add(sizes[3]), pout.add(sizes[4]), pout.add(sizes[5]), pout.add(sizes[6]),
-                               pout.add(sizes[7])};
-  if (pin.total <= kPackedCallMax && pout.total <= kPackedCallMax) {
-    if ((rc = ensure_buf(c, c->packed_in, pin.total)) || (rc = ensure_buf(c, c->packed_out, pout.total)) ||
-        (rc = ensure_pinned(c, c->pin_in, pin.total)) || (rc = ensure_pinned(c, c->pin_out, pout.total)))
-      return rc;
-    uint8_t* hi = static_cast<uint8_t*>(c->pin_in.p);
-    uint8_t* di = static_cast<uint8_t*>(c->packed_in.p);
-    uint8_t* ho = static_cast<uint8_t*>(c->pin_out.p);
-    uint8_t* dd = static_cast<uint8_t*>(c->packed_out.p);
-    const void* src[4] = {r->values, r->value_off, tagged ? r->part_rec : r->seg_rec, r->bucket_tag};
-    const uint64_t len[4] = {sizes[0], sizes[1], sizes[2], sizes[8]};
-    for (int i = 0; i < 4; i++)
-      if (len[i]) std::memcpy(hi + in_off[i], src[i], len[i]);
-    MDE_HIP(c, hipMemcpyAsync(di, hi, pin.total, hipMemcpyHostToDevice, c->stream));
-    mde_records dr = *r;
-    dr.values = di + in_off[0];
-    dr.value_off = nvo ? reinterpret_cast<const uint64_t*>(di + in_off[1]) : nullptr;
-    dr.seg_rec = tagged ? nullptr : reinterpret_cast<const uint64_t*>(di + in_off[2]);
-    dr.part_rec = tagged ? reinterpret_cast<const uint64_t*>(di + in_off[2]) : nullptr;
-    dr.bucket_tag = tagged ? reinterpret_cast<const uint16_t*>(di + in_off[3]) : nullptr;
-    mde_tree_out dout{reinterpret_cast<uint64_t*>(dd + out_off[0]), reinterpret_cast<int32_t*>(dd + out_off[1]),
-                      reinterpret_cast<int32_t*>(dd + out_off[2]), dd + out_off[3],
-                      o->nodes ? dd + out_off[4] : nullptr};
-    if ((rc = digest_async(c, &dr))) return rc;
-    if ((rc = tree_async(c, &dr, &dout))) return rc;
-    MDE_HIP(c, hipMemcpyAsync(ho, dd, pout.total, hipMemcpyDeviceToHost, c->stream));
-    MDE_HIP(c, hipStreamSynchronize(c->stream));
-    void* dst[5] = {o->digest, o->size, o->items, o->root, o->nodes};
-    for (int i = 0; i < 5; i++)
-      if (dst[i] && sizes[3 + i]) std::memcpy(dst[i], ho + out_off[i], sizes[3 + i]);
-    return MDE_OK;
-  }
-  for (int i = 0; i < 9; i++)
-    if ((rc = ensure_buf(c, c->stage[i], sizes[i]))) return rc;
-  auto dp = [&](int i) { return c->stage[i].p; };
-  if (r->values_bytes)
-    MDE_HIP(c, hipMemcpyAsync(dp(0), r->values, r->values_bytes, hipMemcpyHostToDevice, c->stream));
-  if (nvo)
-    MDE_HIP(c, hipMemcpyAsync(dp(1), r->value_off, nvo * 8, hipMemcpyHostToDevice, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(dp(2), tagged ? r->part_rec : r->seg_rec, sizes[2], hipMemcpyHostToDevice, c->stream));
-  if (tagged && r->n_records)
-    MDE_HIP(c, hipMemcpyAsync(dp(8), r->bucket_tag, sizes[8], hipMemcpyHostToDevice, c->stream));
+  const uint64_t nseg = (tagged ? P + 1 : S + 1) * 8, ntag = tagged ? r->n_records * 2 : 0;
+  HostIo io(c);
+  const int i_val = io.in(r->values, r->values_bytes, r->values_bytes);
+  const int i_voff = io.in(r->value_off, nvo * 8, nvo * 8);
+  const int i_seg = io.in(tagged ? r->part_rec : r->seg_rec, nseg, nseg);
+  const int i_tag = io.in(r->bucket_tag, ntag, ntag);
+  const int o_dig = io.out(o->digest, S * 8), o_size = io.out(o->size, S * 4), o_items = io.out(o->items, P * 4);
+  const int o_root = io.out(o->root, P * 32), o_nodes = io.out(o->nodes, o->nodes ? P * NI * 32 : 0);
+  if ((rc = io.upload())) return rc;
   mde_records dr = *r;
-  dr.values = static_cast<const uint8_t*>(dp(0));
-  dr.value_off = nvo ? static_cast<const uint64_t*>(dp(1)) : nullptr;
-  dr.seg_rec = tagged ? nullptr : static_cast<const uint64_t*>(dp(2));
-  dr.part_rec = tagged ? static_cast<const uint64_t*>(dp(2)) : nullptr;
-  dr.bucket_tag = tagged ? static_cast<const uint16_t*>(dp(8)) : nullptr;
-  mde_tree_out dout{static_cast<uint64_t*>(dp(3)), static_cast<int32_t*>(dp(4)),
-                    static_cast<int32_t*>(dp(5)), static_cast<uint8_t*>(dp(6)),
-                    o->nodes ? static_cast<uint8_t*>(dp(7)) : nullptr};
+  dr.values = static_cast<const uint8_t*>(io.dev(i_val));
+  dr.value_off = nvo ? static_cast<const uint64_t*>(io.dev(i_voff)) : nullptr;
+  dr.seg_rec = tagged ? nullptr : static_cast<const uint64_t*>(io.dev(i_seg));
+  dr.part_rec = tagged ? static_cast<const uint64_t*>(io.dev(i_seg)) : nullptr;
+  dr.bucket_tag = tagged ? static_cast<const uint16_t*>(io.dev(i_tag)) : nullptr;
+  mde_tree_out dout{static_cast<uint64_t*>(io.dev(o_dig)), static_cast<int32_t*>(io.dev(o_size)),
+                    static_cast<int32_t*>(io.dev(o_items)), static_cast<uint8_t*>(io.dev(o_root)),
+                    o->nodes ? static_cast<uint8_t*>(io.dev(o_nodes)) : nullptr};
   if ((rc = digest_async(c, &dr))) return rc;
   if ((rc = tree_async(c, &dr, &dout))) return rc;
-  if (o->digest) MDE_HIP(c, hipMemcpyAsync(o->digest, dout.digest, S * 8, hipMemcpyDeviceToHost, c->stream));
-  if (o->size) MDE_HIP(c, hipMemcpyAsync(o->size, dout.size, S * 4, hipMemcpyDeviceToHost, c->stream));
-  if (o->items) MDE_HIP(c, hipMemcpyAsync(o->items, dout.items, P * 4, hipMemcpyDeviceToHost, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(o->root, dout.root, P * 32, hipMemcpyDeviceToHost, c->stream));
-  if (o->nodes) MDE_HIP(c, hipMemcpyAsync(o->nodes, dout.nodes, P * NI * 32, hipMemcpyDeviceToHost, c->stream));
-  MDE_HIP(c, hipStreamSynchronize(c->stream));
-  return MDE_OK;
+  return io.download();
 }
 
 int mde_build_streamed(mde_ctx* c, const mde_records* r, const mde_tree_out* o, uint64_t chunk_bytes) {
@@ -965,29 +996,24 @@ int mde_diff(mde_ctx* c, uint32_t n_pairs, uint32_t Ba, const uint64_t* da, cons
   if (out_stride < mde_diff_capacity(Ba, Bb))
     return set_err(c, MDE_E_CAPACITY, "out_stride too small");
   const uint64_t T = n_pairs, NA = mde::tree_internal(Ba), NB = mde::tree_internal(Bb);
-  const uint64_t sz[6] = {T * Ba * 8, T * NA * 32, T * Bb * 8, T * NB * 32, T * out_stride * 4, T * 4};
-  int rc;
-  for (int i = 0; i < 6; i++)
-    if ((rc = ensure_buf(c, c->stage[i], sz[i]))) return rc;
-  MDE_HIP(c, hipMemcpyAsync(c->stage[0].p, da, sz[0], hipMemcpyHostToDevice, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(c->stage[1].p, na, sz[1], hipMemcpyHostToDevice, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(c->stage[2].p, db, sz[2], hipMemcpyHostToDevice, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(c->stage[3].p, nb, sz[3], hipMemcpyHostToDevice, c->stream));
+  HostIo io(c);
+  const int i_da = io.in(da, T * Ba * 8, T * Ba * 8), i_na = io.in(na, T * NA * 32, T * NA * 32);
+  const int i_db = io.in(db, T * Bb * 8, T * Bb * 8), i_nb = io.in(nb, T * NB * 32, T * NB * 32);
+  const int o_ids = io.out(out_ids, T * out_stride * 4), o_cnt = io.out(out_count, T * 4);
+  int rc = io.upload();
+  if (rc) return rc;
   mde::DiffLaunch a{n_pairs,
                     Ba,
                     Bb,
-                    static_cast<const uint64_t*>(c->stage[0].p),
-                    static_cast<const uint8_t*>(c->stage[1].p),
-                    static_cast<const uint64_t*>(c->stage[2].p),
-                    static_cast<const uint8_t*>(c->stage[3].p),
-                    static_cast<int32_t*>(c->stage[4].p),
+                    static_cast<const uint64_t*>(io.dev(i_da)),
+                    static_cast<const uint8_t*>(io.dev(i_na)),
+                    static_cast<const uint64_t*>(io.dev(i_db)),
+                    static_cast<const uint8_t*>(io.dev(i_nb)),
+                    static_cast<int32_t*>(io.dev(o_ids)),
                     out_stride,
-                    static_cast<int32_t*>(c->stage[5].p)};
+                    static_cast<int32_t*>(io.dev(o_cnt))};
   MDE_HIP(c, mde::launch_diff(a, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(out_ids, c->stage[4].p, sz[4], hipMemcpyDeviceToHost, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(out_count, c->stage[5].p, sz[5], hipMemcpyDeviceToHost, c->stream));
-  MDE_HIP(c, hipStreamSynchronize(c->stream));
-  return MDE_OK;
+  return io.download();
 }
 
 int mde_diff_digests(mde_ctx* c, uint32_t n_pairs, uint32_t Ba, const uint64_t* da, uint32_t Bb,
@@ -1315,39 +1341,32 @@ int mde_verify_epochs(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partiti
   const uint64_t nbytes = T ? peer_off[T] - peer_off[0] : 0;
   if (nbytes && !peer_bytes) return set_err(c, MDE_E_INVAL, "peer_bytes is NULL");
   const uint64_t ostride = object_out ? object_stride : 0;
-  const uint64_t sz[14] = {N * 4, N * B * 8, N * B * 4, N * NI * 32, nbytes + 1, (T + 1) * 8,
-                           N, N * 4, N * B * 4, N * 4, T * 4, N * ostride, N * 4, 0};
-  int rc;
-  for (int i = 0; i < 13; i++)
-    if ((rc = ensure_buf(c, c->stage[i], sz[i]))) return rc;
-  auto dp = [&](int i) { return c->stage[i].p; };
   std::vector<uint64_t> rel(T + 1, 0);
   for (uint64_t i = 0; i <= T && T; i++) rel[i] = peer_off[i] - peer_off[0];
-  if (partition) MDE_HIP(c, hipMemcpyAsync(dp(0), partition, sz[0], hipMemcpyHostToDevice, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(dp(1), digest, sz[1], hipMemcpyHostToDevice, c->stream));
-  if (size) MDE_HIP(c, hipMemcpyAsync(dp(2), size, sz[2], hipMemcpyHostToDevice, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(dp(3), nodes, sz[3], hipMemcpyHostToDevice, c->stream));
-  if (nbytes) MDE_HIP(c, hipMemcpyAsync(dp(4), peer_bytes + peer_off[0], nbytes, hipMemcpyHostToDevice, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(dp(5), rel.data(), (T + 1) * 8, hipMemcpyHostToDevice, c->stream));
-  rc = verify_async(c, P, B, partition ? static_cast<const int32_t*>(dp(0)) : nullptr, epoch,
-                    static_cast<const uint64_t*>(dp(1)), size ? static_cast<const int32_t*>(dp(2)) : nullptr,
-                    static_cast<const uint8_t*>(dp(3)), R, static_cast<const uint8_t*>(dp(4)),
-                    static_cast<const uint64_t*>(dp(5)), replica_count, static_cast<uint8_t*>(dp(6)),
-                    static_cast<int32_t*>(dp(7)), static_cast<int32_t*>(dp(8)), static_cast<int32_t*>(dp(9)),
-                    static_cast<int32_t*>(dp(10)), object_out ? static_cast<uint8_t*>(dp(11)) : nullptr,
-                    ostride, object_out ? static_cast<uint32_t*>(dp(12)) : nullptr);
+  HostIo io(c);
+  const int i_part = io.in(partition, partition ? N * 4 : 0, N * 4);
+  const int i_dig = io.in(digest, N * B * 8, N * B * 8);
+  const int i_size = io.in(size, size ? N * B * 4 : 0, N * B * 4);
+  const int i_nodes = io.in(nodes, N * NI * 32, N * NI * 32);
+  const int i_peer = io.in(nbytes ? peer_bytes + peer_off[0] : nullptr, nbytes, nbytes + 1);
+  const int i_rel = io.in(rel.data(), (T + 1) * 8, (T + 1) * 8);
+  const int o_valid = io.out(valid, N), o_vc = io.out(valid_count, N * 4), o_ids = io.out(diff_ids, N * B * 4);
+  const int o_dc = io.out(diff_count, N * 4), o_ps = io.out(T ? peer_status : nullptr, T * 4);
+  const int o_obj = io.out(object_out, N * ostride), o_olen = io.out(object_out ? object_len : nullptr, N * 4);
+  int rc = io.upload();
   if (rc) return rc;
-  MDE_HIP(c, hipMemcpyAsync(valid, dp(6), sz[6], hipMemcpyDeviceToHost, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(valid_count, dp(7), sz[7], hipMemcpyDeviceToHost, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(diff_ids, dp(8), sz[8], hipMemcpyDeviceToHost, c->stream));
-  MDE_HIP(c, hipMemcpyAsync(diff_count, dp(9), sz[9], hipMemcpyDeviceToHost, c->stream));
-  if (peer_status && T) MDE_HIP(c, hipMemcpyAsync(peer_status, dp(10), sz[10], hipMemcpyDeviceToHost, c->stream));
-  if (object_out) {
-    MDE_HIP(c, hipMemcpyAsync(object_out, dp(11), sz[11], hipMemcpyDeviceToHost, c->stream));
-    MDE_HIP(c, hipMemcpyAsync(object_len, dp(12), sz[12], hipMemcpyDeviceToHost, c->stream));
-  }
-  MDE_HIP(c, hipStreamSynchronize(c->stream));
-  return MDE_OK;
+  rc = verify_async(c, P, B, partition ? static_cast<const int32_t*>(io.dev(i_part)) : nullptr, epoch,
+                    static_cast<const uint64_t*>(io.dev(i_dig)),
+                    size ? static_cast<const int32_t*>(io.dev(i_size)) : nullptr,
+                    static_cast<const uint8_t*>(io.dev(i_nodes)), R, static_cast<const uint8_t*>(io.dev(i_peer)),
+                    static_cast<const uint64_t*>(io.dev(i_rel)), replica_count,
+                    static_cast<uint8_t*>(io.dev(o_valid)), static_cast<int32_t*>(io.dev(o_vc)),
+                    static_cast<int32_t*>(io.dev(o_ids)), static_cast<int32_t*>(io.dev(o_dc)),
+                    static_cast<int32_t*>(io.dev(o_ps)),
+                    object_out ? static_cast<uint8_t*>(io.dev(o_obj)) : nullptr, ostride,
+                    object_out ? static_cast<uint32_t*>(io.dev(o_olen)) : nullptr);
+  if (rc) return rc;
+  return io.download();
 }
 
 int mde_tag_keys_async(mde_ctx* c, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
