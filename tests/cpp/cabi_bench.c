@@ -188,6 +188,51 @@ int main(int argc, char** argv) {
   free(root);
   free(root2);
   free(seg);
+
+  /* Call latency of the synchronous host-buffer entry point at the production shape: ONE
+   * partition per call (VerifyEpoch -> RawPartitionMerkleTree, main/manager.go:1036), values =
+   * 8-byte LE timestamps (main/manager.go:816), B = n_buckets; host arena -> H2D -> digest ->
+   * tree -> D2H of digests, sizes, items, root. Median of 200 calls per record count. */
+  for (int k = 0; k < 3; k++) {
+    const uint64_t nr = k == 0 ? 1000u : k == 1 ? 10000u : 100000u;
+    uint8_t* hv = xmalloc(nr * 8);
+    for (uint64_t i = 0; i < nr * 8; i++) hv[i] = (uint8_t)(i * 131u + 7u);
+    uint64_t* hs = xmalloc(((uint64_t)B + 1) * 8);
+    for (uint32_t b = 0; b <= B; b++) hs[b] = nr * b / B;
+    uint64_t* hd = xmalloc((uint64_t)B * 8);
+    int32_t *hz = xmalloc((uint64_t)B * 4), hi = 0;
+    uint8_t hr[32];
+    mde_records r1;
+    memset(&r1, 0, sizeof r1);
+    r1.values = hv;
+    r1.values_bytes = nr * 8;
+    r1.value_stride = 8;
+    r1.layout = MDE_LAYOUT_SORTED;
+    r1.n_records = nr;
+    r1.n_partitions = 1;
+    r1.n_buckets = B;
+    r1.seg_rec = hs;
+    mde_tree_out o1 = {hd, hz, &hi, hr, NULL};
+    double lat[200];
+    for (int i = 0; i < 210; i++) {
+      const double a = now_s();
+      CHECK(mde_build(ctx, &r1, &o1));
+      if (i >= 10) lat[i - 10] = now_s() - a;
+    }
+    for (int i = 1; i < 200; i++)  /* insertion sort: 200 samples */
+      for (int j = i; j > 0 && lat[j] < lat[j - 1]; j--) {
+        const double t = lat[j];
+        lat[j] = lat[j - 1];
+        lat[j - 1] = t;
+      }
+    printf("{\"latency\": \"mde_build (host buffers, synchronous), 1 partition\", \"records\": %" PRIu64
+           ", \"value_len\": 8, \"n_buckets\": %u, \"median_us\": %.1f, \"p10_us\": %.1f, \"p90_us\": %.1f}\n",
+           nr, B, lat[100] * 1e6, lat[20] * 1e6, lat[180] * 1e6);
+    free(hv);
+    free(hs);
+    free(hd);
+    free(hz);
+  }
   mde_destroy(ctx);
   return ok_tree && ok_sum && ok_run ? 0 : 3;
 }

@@ -89,6 +89,8 @@ def test_cabi_bench_parity():
     r = subprocess.run([str(C_BENCH), "1000000", "256", "256", "64", "4", "1"], capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    d = json.loads(r.stdout.strip().splitlines()[-1])
+    lines = [json.loads(ln) for ln in r.stdout.strip().splitlines()]
+    d = lines[0]
     assert all(d["parity"].values()), d
     assert d["device"].startswith("gfx950")
+    assert [x["records"] for x in lines[1:]] == [1000, 10000, 100000]
