@@ -67,8 +67,8 @@ def parse():
                     help="run each build's tree kernel on the main stream (no overlap with the next build)")
     ap.add_argument("--pipeline", default="auto", choices=["auto", "fused", "streams", "off"],
                     help="fused: one launch per build carries the previous build's trees "
-                         "(mde_build_pipelined_async; default for layout a); streams: tree kernel on a "
-                         "second stream (default for layout b); off: digest + tree serially")
+                         "(mde_build_pipelined_async; the default, except layout b at N=1); streams: "
+                         "tree kernel on a second stream; off: digest + tree serially")
     ap.add_argument("--tuning", default="", help="digest kernel 'variant,workgroups_per_cu' (A/B only)")
     return ap.parse_args()
 
@@ -239,7 +239,10 @@ def main():
     if args.no_pipeline or (c5 and mode == "streams"):
         mode = "off"
     elif mode == "auto":
-        mode = "fused" if args.layout == "a" else "streams"
+        # layout B on a whole C4 arena: the tree kernel on a second stream costs 0.4 % over bare
+        # binning, the fused step 1.5 %; on an N=8 shard fused costs 1 %, two streams 6 %
+        # (profiles/r01f_pipeline_modes_layout_b.jsonl)
+        mode = "fused" if (args.layout == "a" or shard_world > 1) else "streams"
     fused = mode == "fused"
     pipeline = mode == "streams"
     engines = [eng]

@@ -99,6 +99,9 @@ __device__ __forceinline__ void load_step(u32x4 (&v)[kU], const u32x4* lane_base
 
 // `block` = this workgroup's index among the digest workgroups of the launch.
 __device__ __forceinline__ void tagged_body(const TaggedLaunch& a, uint32_t block, uint32_t* smem) {
+  // As in the layout-A digest: co-running SHA-256 tree waves (fused step, or a tree kernel on a
+  // second stream) take the issue slots the binning waves leave, not the other way round.
+  __builtin_amdgcn_s_setprio(2);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t L = a.lrep;
   WaveBins w{nullptr, nullptr};
