@@ -157,3 +157,46 @@ def test_verify_epochs_device_api_after_build(engine):
     want = _oracle_verify(B, dg, sz, peers, 2, 9, np.zeros(P, np.int32))
     assert [x["valid"] for x in want] == ref["valid"]
     assert [x["diff"] for x in want] == ref["diff"]
+
+
+@pytest.mark.gpu
+def test_verify_epochs_large_call_equals_small_calls(engine):
+    """A host call too large for the packed staging (nodes alone 10 MB > 8 MiB: direct copies)
+    returns exactly what the same partitions give in small packed calls (oracle-checked above)."""
+    rng = np.random.default_rng(77)
+    P, B, E, replica = 5000, 64, 3, 2
+    digests = rng.integers(0, 999999, size=P * B, dtype=np.uint64)
+    sizes = rng.integers(0, 5000, size=P * B).astype(np.int32)
+    _, nodes = engine.tree_from_digests(digests, B)
+    assert nodes.nbytes > 8 << 20
+    peers = [_peer_objects(rng, B, digests[p * B:(p + 1) * B], sizes[p * B:(p + 1) * B], p, E)
+             for p in range(P)]
+    big = engine.verify_epochs(B, digests, sizes, nodes, peers, replica, E)
+    NI = nodes.size // P
+    for lo in range(0, P, 1000):
+        hi = lo + 1000
+        small = engine.verify_epochs(B, digests[lo * B:hi * B], sizes[lo * B:hi * B], nodes[lo * NI:hi * NI],
+                                     peers[lo:hi], replica, E)
+        for k in big:
+            assert big[k][lo:hi] == small[k], (k, lo)
+
+
+@pytest.mark.gpu
+def test_diff_large_call_equals_small_calls(engine):
+    """mde_diff over 20,000 pairs (direct copies) == the same pairs in packed calls of 1,000."""
+    rng = np.random.default_rng(78)
+    T, B = 20000, 64
+    da = rng.integers(0, 999999, T * B).astype(np.uint64)
+    db = da.copy()
+    flip = rng.random(T * B) < 0.02
+    db[flip] = (db[flip] + 1) % 999999
+    _, na = engine.tree_from_digests(da, B)
+    _, nb = engine.tree_from_digests(db, B)
+    assert na.nbytes > 8 << 20
+    big = engine.diff(B, da, na, B, db, nb, n_pairs=T)
+    NI = na.size // T
+    for lo in range(0, T, 1000):
+        hi = lo + 1000
+        small = engine.diff(B, da[lo * B:hi * B], na[lo * NI:hi * NI], B, db[lo * B:hi * B], nb[lo * NI:hi * NI],
+                            n_pairs=1000)
+        assert big[lo:hi] == small, lo
