@@ -23,7 +23,7 @@ def rows(path):
 
 
 def short(name):
-    for k in ("build_step_kernel", "bucket_digest_kernel", "tagged_digest_kernel", "tree_kernel", "diff_kernel",
+    for k in ("build_step_kernel", "bucket_digest_kernel", "tagged_step_kernel", "tagged_digest_kernel", "tree_kernel", "diff_kernel",
               "synth_values_kernel", "synth_tags_kernel", "tag_keys_kernel", "verify_kernel",
               "encode_kernel", "decode_kernel", "extract"):
         if k in name:
