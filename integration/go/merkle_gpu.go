@@ -1,0 +1,167 @@
+// merkle_gpu.go -- cgo shim: drop-in for the hot path of main/merkle_tree.go (MyDataStore).
+//
+// Copy into the reference's main/ package and delete RawPartitionMerkleTree and
+// DifferentMerkleTreeBuckets from merkle_tree.go (INTEGRATION.md section 2). It binds only what
+// include/mde.h declares (tests/test_integration.py checks every C.* name against the header).
+// Not compiled in this repository: the image has no Go toolchain (DESIGN.md section 1).
+package main
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../mi355x/include
+#cgo LDFLAGS: -L${SRCDIR}/../mi355x/mydatastore_amd -lmde -Wl,-rpath,${SRCDIR}/../mi355x/mydatastore_amd
+#include <stdlib.h>
+#include "mde.h"
+*/
+import "C"
+
+import (
+	"bytes"
+	"sync"
+	"unsafe"
+
+	"github.com/cbergoon/merkletree"
+	"github.com/pkg/errors"
+)
+
+var (
+	mdeOnce sync.Once
+	mdeCtx  *C.mde_ctx
+	mdeErr  error
+)
+
+func mdeEngine() (*C.mde_ctx, error) {
+	mdeOnce.Do(func() {
+		var ctx *C.mde_ctx
+		if rc := C.mde_create(0, &ctx); rc != C.MDE_OK {
+			mdeErr = errors.Errorf("mde_create: %s", C.GoString(C.mde_strerror(rc)))
+			return
+		}
+		mdeCtx = ctx
+	})
+	return mdeCtx, mdeErr
+}
+
+func cU64(v []uint64) unsafe.Pointer { return C.CBytes(unsafe.Slice((*byte)(unsafe.Pointer(&v[0])), len(v)*8)) }
+
+// RawPartitionMerkleTree -- drop-in for main/merkle_tree.go:86-116. The per-bucket range scans are
+// unchanged; the values go into one arena that the MI355X engine reduces (bucket digests + SHA-256
+// tree on device).
+func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, upperEpoch int64) (*merkletree.MerkleTree, error) {
+	ctx, err := mdeEngine()
+	if err != nil {
+		return nil, err
+	}
+	B := manager.config.Manager.PartitionBuckets
+	values := make([]byte, 0, 1<<16)
+	valueOff := []uint64{0}
+	segRec := []uint64{0}
+	for i := 0; i < B; i++ {
+		index1, err := BuildEpochIndex(partitionId, uint64(i), lowerEpoch, "")
+		if err != nil {
+			return nil, err
+		}
+		index2, err := BuildEpochIndex(partitionId, uint64(i), upperEpoch, "")
+		if err != nil {
+			return nil, err
+		}
+		it := manager.db.NewIterator([]byte(index1), []byte(index2), false)
+		for !it.IsDone() {
+			values = append(values, it.Value()...)
+			valueOff = append(valueOff, uint64(len(values)))
+			it.Next()
+		}
+		it.Release()
+		segRec = append(segRec, uint64(len(valueOff)-1))
+	}
+	if len(values) == 0 {
+		values = append(values, 0)
+	}
+	cValues, cOff, cSeg := C.CBytes(values), cU64(valueOff), cU64(segRec)
+	defer C.free(cValues)
+	defer C.free(cOff)
+	defer C.free(cSeg)
+	cDigest := C.malloc(C.size_t(8 * B))
+	cSize := C.malloc(C.size_t(4 * B))
+	cItems := C.malloc(4)
+	cRoot := C.malloc(32)
+	defer C.free(cDigest)
+	defer C.free(cSize)
+	defer C.free(cItems)
+	defer C.free(cRoot)
+	rec := C.mde_records{
+		values: (*C.uint8_t)(cValues), values_bytes: C.uint64_t(len(values)),
+		value_off: (*C.uint64_t)(cOff), n_records: C.uint64_t(len(valueOff) - 1),
+		n_partitions: 1, n_buckets: C.uint32_t(B), seg_rec: (*C.uint64_t)(cSeg),
+	}
+	out := C.mde_tree_out{digest: (*C.uint64_t)(cDigest), size: (*C.int32_t)(cSize),
+		items: (*C.int32_t)(cItems), root: (*C.uint8_t)(cRoot)}
+	if rc := C.mde_build(ctx, &rec, &out); rc != C.MDE_OK {
+		return nil, errors.Errorf("mde_build: %s", C.GoString(C.mde_last_error(ctx)))
+	}
+	digest := unsafe.Slice((*uint64)(cDigest), B)
+	size := unsafe.Slice((*int32)(cSize), B)
+	// Rebuild the reference's tree type from the device digests so every caller keeps its types;
+	// merkletree.NewTree costs B-1 host SHA-256s, and the device root cross-checks it.
+	bucketList := make([]merkletree.Content, B)
+	for i := 0; i < B; i++ {
+		bucketList[i] = &MerkleBucket{bucketId: int32(i), hasher: &CustomHash{value: int64(digest[i])}, size: size[i]}
+	}
+	tree, err := merkletree.NewTree(bucketList)
+	if err != nil {
+		return nil, err
+	}
+	if !bytes.Equal(tree.MerkleRoot(), C.GoBytes(cRoot, 32)) {
+		return nil, errors.New("device root differs from merkletree root")
+	}
+	return tree, nil
+}
+
+// DifferentMerkleTreeBuckets -- drop-in for main/merkle_tree.go:159-161 (DFS order, duplicates).
+func DifferentMerkleTreeBuckets(tree1 *merkletree.MerkleTree, tree2 *merkletree.MerkleTree) ([]int32, error) {
+	ctx, err := mdeEngine()
+	if err != nil {
+		return nil, err
+	}
+	digests := func(t *merkletree.MerkleTree) ([]uint64, error) {
+		n := len(t.Leafs)
+		if n > 1 && t.Leafs[n-1].C == t.Leafs[n-2].C { // merkletree's duplicate of the last leaf
+			n--
+		}
+		d := make([]uint64, n)
+		for i := 0; i < n; i++ {
+			b, ok := t.Leafs[i].C.(*MerkleBucket)
+			if !ok {
+				return nil, errors.New("failed to decode MerkleBucket")
+			}
+			d[i] = uint64(b.hasher.Hash())
+		}
+		return d, nil
+	}
+	d1, err := digests(tree1)
+	if err != nil {
+		return nil, err
+	}
+	d2, err := digests(tree2)
+	if err != nil {
+		return nil, err
+	}
+	capIds := C.mde_diff_capacity(C.uint32_t(len(d1)), C.uint32_t(len(d2)))
+	cA, cB := cU64(d1), cU64(d2)
+	defer C.free(cA)
+	defer C.free(cB)
+	cIds := C.malloc(C.size_t(4 * capIds))
+	cCount := C.malloc(4)
+	defer C.free(cIds)
+	defer C.free(cCount)
+	if rc := C.mde_diff_digests(ctx, 1, C.uint32_t(len(d1)), (*C.uint64_t)(cA), C.uint32_t(len(d2)),
+		(*C.uint64_t)(cB), (*C.int32_t)(cIds), capIds, (*C.int32_t)(cCount)); rc != C.MDE_OK {
+		return nil, errors.Errorf("mde_diff: %s", C.GoString(C.mde_last_error(ctx)))
+	}
+	n := *(*int32)(cCount)
+	if n == C.MDE_E_TREE {
+		return nil, errors.New("bucketIds dont match (or a merkletree.Node is nil)")
+	}
+	out := make([]int32, n)
+	copy(out, unsafe.Slice((*int32)(cIds), n))
+	return out, nil
+}
