@@ -204,6 +204,8 @@ def main():
     # --rccl-selftest: the N>1 code path (process group, sharding, bucketed RCCL root gather on the
     # side stream) with however many ranks were launched, one of them is enough (not a measurement)
     use_dist = world > 1 or args.rccl_selftest
+    if args.rccl_selftest and args.simulate_world:
+        raise SystemExit("--rccl-selftest gathers the launched ranks' partitions; drop --simulate-world")
     if args.rehearse:
         local_rank = local_rank % torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
