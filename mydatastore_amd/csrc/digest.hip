@@ -99,9 +99,11 @@ __device__ __forceinline__ void load_step(u32x4 (&v)[U], const u32x4* src, uint6
 }
 
 // U = 16-byte loads per lane per step (step = U KiB per wave); NT = nontemporal loads;
-// PIPE = issue the next step's loads before reducing the current one (register double buffer).
+// PIPE = issue the next step's loads before reducing the current one (register double buffer);
+// PIPE = 2 also issues the first step's loads before the bucket search, so the wave's first HBM
+// round trip overlaps the search's dependent seg_rec loads.
 // `block` = this workgroup's index among the digest workgroups of the launch.
-template <int U, bool NT, bool PIPE, int PRIO = 0>
+template <int U, bool NT, int PIPE, int PRIO = 0>
 __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t block) {
   constexpr uint64_t kStep = 1024ull * U;
   // Streaming waves issue little VALU; when tree waves (back-to-back SHA-256 VALU) share the CU,
@@ -117,13 +119,13 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
   if (beg >= last) return;
   const uint64_t end = min(beg + a.wave_bytes, last);
 
+  const u32x4* lane_base = reinterpret_cast<const u32x4*>(d.base) + lane;
+  u32x4 cur[U];
+  if (PIPE == 2) load_step<U, NT>(cur, lane_base + (beg >> 4), beg, end, lane, beg + kStep <= end);
   uint32_t s = seg_search(d, 0u, beg, lane);
   uint64_t sb = segpos(d, s), se = segpos(d, s + 1);
   uint32_t acc = 0;
-  const u32x4* lane_base = reinterpret_cast<const u32x4*>(d.base) + lane;
-
-  u32x4 cur[U];
-  if (PIPE) load_step<U, NT>(cur, lane_base + (beg >> 4), beg, end, lane, beg + kStep <= end);
+  if (PIPE == 1) load_step<U, NT>(cur, lane_base + (beg >> 4), beg, end, lane, beg + kStep <= end);
   for (uint64_t p = beg; p < end; p += kStep) {
     u32x4 v[U];
     const bool full = p + kStep <= end;
@@ -360,7 +362,7 @@ __device__ __forceinline__ void digest_body_steal(const DigestLaunch& a, uint32_
   }
 }
 
-template <int U, bool NT, bool PIPE, int PRIO = 0, bool STEAL = false>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool STEAL = false>
 __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a) {
   if (STEAL)
     digest_body_steal<U, NT, PRIO>(a, blockIdx.x);
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a)
 // wave per workgroup up to B = 128, the rest exit at once), so the SHA waves spread over many
 // CUs instead of crowding a few; tree workgroups come first so the dispatcher places them before
 // the streaming grid (sized to be fully resident) fills the remaining slots.
-template <int U, bool NT, bool PIPE, int PRIO = 0, bool STEAL = false>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool STEAL = false>
 __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, TreeLaunch t, uint32_t tree_blocks,
                                                               uint32_t Q) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -412,7 +414,7 @@ const Variant kVariants[] = {
     MDE_VARIANT(4, true, true, 0, false),   MDE_VARIANT(8, true, true, 0, false),
     MDE_VARIANT(16, false, false, 0, false), MDE_VARIANT(4, true, true, 2, false),
     MDE_VARIANT(4, true, true, 3, false),   MDE_VARIANT(4, true, true, 2, true),
-    MDE_VARIANT(8, true, true, 2, true),
+    MDE_VARIANT(8, true, true, 2, true),    MDE_VARIANT(4, true, 2, 2, false),
 };
 #undef MDE_VARIANT
 

@@ -22,8 +22,9 @@
 #include "mde_internal.hpp"
 
 // Digest-kernel tuning defaults (tools/digest_sweep.sh, profiles/r01_digest_sweep.json).
-constexpr int kDefaultDigestVariant = 7;  // U=4 nontemporal, register-prefetched, s_setprio 2
-constexpr int kStaticDigestVariant = 7;   // used when a stealing variant cannot steal
+constexpr int kDefaultDigestVariant = 11;  // U=4 nontemporal, register-prefetched (first step before
+                                           // the bucket search), s_setprio 2
+constexpr int kStaticDigestVariant = 11;  // used when a stealing variant cannot steal
 constexpr int kDefaultDigestCap = 2;      // 2 workgroups (8 waves) per CU
 constexpr int kDefaultDigestOversub = 1;  // grid = resident slots x oversub
 
