@@ -3,6 +3,7 @@
 
     python tools/microbench.py tree            # tree kernel vs partitions / buckets
     python tools/microbench.py digest          # digest kernel vs arena size (C4 shards)
+    python tools/microbench.py verify          # mde_verify_epochs vs partitions (2 peers each)
 """
 import json
 import sys
@@ -111,6 +112,53 @@ def bench_ab(eng, variants, worlds=(1, 8), reps=5, cap=2):
     return res
 
 
+def bench_verify(eng, P=1024, B=64, R=2):
+    """VerifyEpoch decision step (mde_verify_epochs) for P partitions x R peer objects: peer 0
+    agrees, peer 1 differs in one bucket. Device-resident call timed with HIP events; the
+    synchronous host call (copies included) with the wall clock."""
+    import time
+    import torch
+    from mydatastore_amd.workload import make_workload
+    dev = torch.device("cuda:0")
+    w = make_workload(eng, n_partitions=P, n_buckets=B, value_len=64, part_mode="mod", n_keys=P * 2000)
+    out = w.build()
+    dg = out["digest"].cpu().numpy().view(np.uint64)
+    sz = out["size"].cpu().numpy()
+    same = eng.encode_objects(B, dg, sz, partition=np.arange(P, dtype=np.int32), lower=5, upper=6)
+    d2 = dg.copy()
+    d2[::B] = (d2[::B] + 1) % 999999
+    diff = eng.encode_objects(B, d2, sz, partition=np.arange(P, dtype=np.int32), lower=5, upper=6)
+    peers = [[same[p], diff[p]][:R] for p in range(P)]
+    flat = [o for row in peers for o in row]
+    off = np.zeros(len(flat) + 1, np.int64)
+    off[1:] = np.cumsum([len(o) for o in flat])
+    blob = torch.from_numpy(np.frombuffer(b"".join(flat), dtype=np.uint8).copy()).to(dev)
+    doff = torch.from_numpy(off).to(dev)
+    stride = int(eng.lib.mde_epoch_tree_object_max_bytes(B))
+    o = {"valid": torch.zeros(P, dtype=torch.uint8, device=dev), "vc": torch.zeros(P, dtype=torch.int32, device=dev),
+         "ids": torch.zeros(P * B, dtype=torch.int32, device=dev), "dc": torch.zeros(P, dtype=torch.int32, device=dev),
+         "st": torch.zeros(P * R, dtype=torch.int32, device=dev),
+         "obj": torch.zeros(P * stride, dtype=torch.uint8, device=dev), "olen": torch.zeros(P, dtype=torch.int32, device=dev)}
+
+    def dev_call():
+        eng.verify_epochs_async(P, B, None, 5, out["digest"], out["size"], out["nodes"], R, blob, doff, 2,
+                                o["valid"], o["vc"], o["ids"], o["dc"], o["st"], o["obj"], stride, o["olen"])
+
+    us_dev = timeit(dev_call, reps=20, warm=3)
+    assert int(o["vc"].sum()) == P and int(o["dc"].sum()) == P  # one agreeing peer, one differing bucket
+    nodes = out["nodes"].cpu().numpy()
+    eng.verify_epochs(B, dg, sz, nodes, peers, 2, 5)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        eng.verify_epochs(B, dg, sz, nodes, peers, 2, 5)
+    us_host = (time.perf_counter() - t0) / 5 * 1e6
+    r = {"partitions": P, "buckets": B, "peers": R, "peer_bytes": int(off[-1]),
+         "device_us_per_call": round(us_dev, 1), "device_partitions_per_s": round(P / us_dev * 1e6),
+         "host_api_us_per_call_incl_copies_and_python": round(us_host, 1)}
+    print(json.dumps(r), flush=True)
+    return r
+
+
 def main():
     import torch
     import mydatastore_amd as mde
@@ -124,6 +172,8 @@ def main():
         out["digest"] = bench_digest(eng)
     if "sweep" in what:
         out["sweep"] = bench_sweep(eng)
+    if "verify" in what:
+        out["verify"] = [bench_verify(eng, P=p) for p in (1, 64, 1024, 8192)]
     for w in what:
         if w.startswith("ab:"):
             out["ab"] = bench_ab(eng, [int(x) for x in w.split(":")[1].split(",")])
