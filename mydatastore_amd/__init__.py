@@ -75,8 +75,9 @@ def load_library() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not LIB_PATH.exists():
-        raise ImportError(f"{LIB_PATH} not built: run `python -m mydatastore_amd._build`")
+    path = Path(os.environ.get("MDE_LIBRARY", LIB_PATH))  # override: A/B of two builds
+    if not path.exists():
+        raise ImportError(f"{path} not built: run `python -m mydatastore_amd._build`")
     # One HIP runtime per process. torch ships its own libamdhip64 (SONAME libamdhip64.so.7, the
     # same SONAME as /opt/rocm's) but its libc10_hip asks for the unversioned file name, so if
     # libmde.so loaded /opt/rocm's runtime first, torch would load a second one and fail to find
@@ -85,7 +86,7 @@ def load_library() -> C.CDLL:
         import torch  # noqa: F401
     except ImportError:  # standalone use: libmde.so binds /opt/rocm's runtime
         pass
-    lib = C.CDLL(str(LIB_PATH))
+    lib = C.CDLL(str(path))
     u32, u64, i32, vp = C.c_uint32, C.c_uint64, C.c_int32, C.c_void_p
     sig = {
         "mde_abi_version": (C.c_int, []),
