@@ -395,6 +395,45 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
     digest_body<U, NT, PIPE, PRIO>(a, blockIdx.x - tree_blocks);
 }
 
+// One-launch build of a small arena (the synchronous one-partition calls of VerifyEpoch). Digest
+// phase bucket-parallel: thread i sums bucket i's bytes with 16-byte loads (a wave walking the
+// bucket boundaries of a small arena in order pays one dependent seg_rec load per bucket, which is
+// what bounds the streaming kernel there); then, after a device-scope fence and a barrier, the same
+// workgroup builds the <= 256/G partitions' trees with tree_body. It saves the second launch of
+// the digest + tree pair.
+__global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLaunch t, uint32_t G, uint32_t words) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const u32x4* base = reinterpret_cast<const u32x4*>(d.base);
+  unsigned long long* sums = const_cast<unsigned long long*>(t.sums_in);  // zero on entry
+  // K threads per bucket (K = 256 / S rounded down to a power of two, >= 1), each taking every
+  // K-th 16-byte vector of the bucket, four loads in flight
+  uint32_t K = 1;
+  while (K * 2 * d.S <= (uint32_t)kThreads) K *= 2;
+  const uint32_t j = threadIdx.x % K;
+  for (uint32_t s = threadIdx.x / K; s < d.S; s += kThreads / K) {
+    const uint64_t lo = segpos(d, s), hi = segpos(d, s + 1);
+    const int64_t l = (int64_t)lo, h = (int64_t)hi;
+    uint32_t acc = 0;
+    uint64_t x = (lo & ~15ull) + 16ull * j;
+    for (; x + 48ull * K < hi; x += 64ull * K) {
+      const u32x4 v0 = __builtin_nontemporal_load(base + (x >> 4));
+      const u32x4 v1 = __builtin_nontemporal_load(base + ((x + 16ull * K) >> 4));
+      const u32x4 v2 = __builtin_nontemporal_load(base + ((x + 32ull * K) >> 4));
+      const u32x4 v3 = __builtin_nontemporal_load(base + ((x + 48ull * K) >> 4));
+      acc = masked_sum16(v0, l - (int64_t)x, h - (int64_t)x, acc);
+      acc = masked_sum16(v1, l - (int64_t)(x + 16ull * K), h - (int64_t)(x + 16ull * K), acc);
+      acc = masked_sum16(v2, l - (int64_t)(x + 32ull * K), h - (int64_t)(x + 32ull * K), acc);
+      acc = masked_sum16(v3, l - (int64_t)(x + 48ull * K), h - (int64_t)(x + 48ull * K), acc);
+    }
+    for (; x < hi; x += 16ull * K)
+      acc = masked_sum16(__builtin_nontemporal_load(base + (x >> 4)), l - (int64_t)x, h - (int64_t)x, acc);
+    if (acc) atomicAdd(sums + s, (unsigned long long)acc);
+  }
+  __threadfence();  // the sums are visible before any wave reads them
+  __syncthreads();
+  tree_body<true>(t, G, words, 0, lds, kThreads);
+}
+
 typedef void (*DigestKernel)(DigestLaunch);
 typedef void (*StepKernel)(DigestLaunch, TreeLaunch, uint32_t, uint32_t);
 struct Variant {
@@ -425,6 +464,20 @@ const Variant& variant(int v) { return kVariants[(v >= 0 && v < kNumVariants) ? 
 }  // namespace
 
 int bucket_digest_variants() { return kNumVariants; }
+
+bool small_build_fits(uint64_t bytes, uint32_t P, uint32_t B) {
+  TreeGeometry g;
+  if (!tree_geometry(B, &g) || g.G > (uint32_t)kThreads) return false;
+  return bytes <= kSmallBuildMaxBytes && P >= 1 && P <= (uint32_t)kThreads / g.G;
+}
+
+hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t st) {
+  TreeGeometry g;
+  tree_geometry(t.B, &g);
+  const size_t lds = (size_t)g.words * 4u * ((uint32_t)kThreads / g.G);
+  hipLaunchKernelGGL(small_build_kernel, dim3(1), dim3(kThreads), lds, st, d, t, g.G, g.words);
+  return hipGetLastError();
+}
 
 bool bucket_digest_steals(int v) { return variant(v).steal; }
 

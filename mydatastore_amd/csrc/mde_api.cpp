@@ -489,6 +489,23 @@ int tree_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   return MDE_OK;
 }
 
+// digest + tree of one build on the context stream: one launch for a small layout-A arena
+// (latency of the one-partition calls), else the digest kernel then the tree kernel.
+int build_async_impl(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
+  const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
+  if (r->layout == MDE_LAYOUT_SORTED && S && r->n_records && r->values_bytes &&
+      mde::small_build_fits(r->values_bytes + 16, r->n_partitions, r->n_buckets)) {
+    int rc = ensure_sums(c, S);
+    if (rc) return rc;
+    mde::TreeLaunch t;
+    if ((rc = tree_launch_for(c, r, o, c->sums, c->counts, &t))) return rc;
+    MDE_HIP(c, mde::launch_small_build(seg_desc(r), t, c->stream));
+    return MDE_OK;
+  }
+  int rc = digest_async(c, r);
+  return rc ? rc : tree_async(c, r, o);
+}
+
 // The trees still owed by the pipeline, as a standalone launch.
 int pipeline_drain(mde_ctx* c) {
   if (!c->pending.active) return MDE_OK;
@@ -778,8 +795,7 @@ int mde_build_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   int rc = check_records(c, r);
   if (rc) return rc;
   if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
-  rc = digest_async(c, r);
-  return rc ? rc : tree_async(c, r, o);
+  return build_async_impl(c, r, o);
 }
 
 int mde_build_pipelined_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
@@ -825,8 +841,7 @@ int mde_build(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   mde_tree_out dout{static_cast<uint64_t*>(io.dev(o_dig)), static_cast<int32_t*>(io.dev(o_size)),
                     static_cast<int32_t*>(io.dev(o_items)), static_cast<uint8_t*>(io.dev(o_root)),
                     o->nodes ? static_cast<uint8_t*>(io.dev(o_nodes)) : nullptr};
-  if ((rc = digest_async(c, &dr))) return rc;
-  if ((rc = tree_async(c, &dr, &dout))) return rc;
+  if ((rc = build_async_impl(c, &dr, &dout))) return rc;
   return io.download();
 }
 

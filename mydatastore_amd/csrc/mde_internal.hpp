@@ -118,6 +118,11 @@ constexpr uint32_t kStepTreeLdsMax = 24u * 1024u + 64u;
 bool build_step_fusable(uint32_t B);
 uint32_t build_step_tree_q(uint32_t B);  // partitions per packed tree wave
 hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st);
+// One-launch build of a small layout-A arena (digest.hip small_build_kernel); t.sums_in is the
+// (zeroed) scratch the digest phase writes and the tree phase reads and clears.
+constexpr uint64_t kSmallBuildMaxBytes = 96u * 1024u;
+bool small_build_fits(uint64_t bytes, uint32_t P, uint32_t B);
+hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t st);
 
 struct DiffLaunch {
   uint32_t n_pairs;
