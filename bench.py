@@ -4,13 +4,16 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3|c1]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-A step = one RawPartitionMerkleTree build of every partition this rank holds (bucket digest
-kernel + digest/tree kernel), plus -- for N > 1 -- the RCCL all-gather of the per-partition roots
-(the one exchange step of the path). --config c5 (BASELINE config 5): build replicas A and B,
+A step = one RawPartitionMerkleTree build of every partition this rank holds: the byte sums of
+every bucket and the SHA-256 tree of every partition. By default (--pipeline fused) each step is
+one build_step_kernel launch that streams this build's arena and builds the previous build's
+trees; the timed region drains the pipeline on both sides, so it holds exactly K digests and K
+tree passes. For N > 1 a step also carries the RCCL all-gather of the per-partition roots (the one
+exchange step of the path), bucketed 8 builds per collective on a side stream. --config c5 (BASELINE config 5): build replicas A and B,
 device DFS-order diff of every partition, out-of-sync range extract of B's differing buckets;
 value counts the bytes of both builds. Default workload = BASELINE config 4: 10M keys x 1 KiB values
 over 1024 partitions, partition p on GPU p % N (total work fixed: strong scaling). The output is
-one JSON line on rank 0 with `roofline` (digest kernel, HIP events on the launch stream) and
+one JSON line on rank 0 with `roofline` (the dominant kernel, HIP events on the launch stream) and
 `cpu_baseline` (the C restatement on the host cores, rank 0 at N = 1 only).
 """
 from __future__ import annotations
