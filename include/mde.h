@@ -106,6 +106,10 @@ int mde_device_info(mde_ctx* ctx, int* cu_count, char* arch_name, int arch_cap);
  * oversubscription (-1 = the built-in defaults). Results are identical for every setting; only
  * speed changes. */
 int mde_set_tuning(mde_ctx* ctx, int digest_variant, int digest_blocks_per_cu, int digest_oversub);
+/* Launch shape of mde_verify_epochs[_async]: 0 (default) = one fused launch whenever
+ * n_peers <= 64 and mde_verify_peer_capacity(n_buckets) <= 1024, else the five-launch chain;
+ * 1 = always the chain. Results are identical; only latency changes. */
+int mde_set_verify_mode(mde_ctx* ctx, int mode);
 
 /* Tree geometry (merkletree v0.2.0 shape: dup last leaf if odd, self-pair odd levels). */
 uint32_t mde_tree_depth(uint32_t n_buckets);          /* internal levels, root included */

@@ -30,7 +30,7 @@ LAYOUT_TAGGED = 1  # layout B: grouped by partition, per-record bucket tags
 # Every symbol include/mde.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
     "mde_abi_version", "mde_strerror", "mde_create", "mde_destroy", "mde_last_error",
-    "mde_set_stream", "mde_use_own_stream", "mde_set_tuning", "mde_get_stream", "mde_synchronize", "mde_device_info", "mde_tree_depth",
+    "mde_set_stream", "mde_use_own_stream", "mde_set_tuning", "mde_set_verify_mode", "mde_get_stream", "mde_synchronize", "mde_device_info", "mde_tree_depth",
     "mde_tree_internal_nodes", "mde_diff_capacity", "mde_build", "mde_build_async",
     "mde_build_streamed",
     "mde_digest_async", "mde_tree_async", "mde_build_pipelined_async", "mde_build_pipeline_drain_async",
@@ -97,6 +97,7 @@ def load_library() -> C.CDLL:
         "mde_set_stream": (C.c_int, [vp, vp]),
         "mde_use_own_stream": (C.c_int, [vp]),
         "mde_set_tuning": (C.c_int, [vp, C.c_int, C.c_int, C.c_int]),
+        "mde_set_verify_mode": (C.c_int, [vp, C.c_int]),
         "mde_get_stream": (vp, [vp]),
         "mde_synchronize": (C.c_int, [vp]),
         "mde_device_info": (C.c_int, [vp, C.POINTER(C.c_int), C.c_char_p, C.c_int]),
@@ -221,6 +222,10 @@ class Engine:
 
     def set_tuning(self, digest_variant: int = -1, digest_blocks_per_cu: int = -1, digest_oversub: int = -1):
         self._check(self.lib.mde_set_tuning(self.ctx, digest_variant, digest_blocks_per_cu, digest_oversub))
+
+    def set_verify_mode(self, mode: int):
+        """0 = fused one-launch verify when it fits (default), 1 = the five-launch chain."""
+        self._check(self.lib.mde_set_verify_mode(self.ctx, mode))
 
     def use_own_stream(self):
         self._check(self.lib.mde_use_own_stream(self.ctx))

@@ -54,6 +54,7 @@ struct mde_ctx {
   Buf packed_in, packed_out, pin_in, pin_out;
   Buf extract_scratch;
   Buf verify_scratch;
+  bool verify_chain = false;  // mde_set_verify_mode(1): the five-launch chain even when fusable
   // Host-ingest ring (mde_build_streamed): two slots of values / value_off / seg_rec.
   Buf ring_vals[2], ring_voff[2], ring_seg[2];
   hipStream_t copy_stream = nullptr;
@@ -737,6 +738,14 @@ int mde_set_tuning(mde_ctx* c, int digest_variant, int digest_blocks_per_cu, int
   return MDE_OK;
 }
 
+int mde_set_verify_mode(mde_ctx* c, int mode) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (mode < 0 || mode > 1) return set_err(c, MDE_E_INVAL, "verify mode %d out of range", mode);
+  c->verify_chain = mode == 1;
+  return MDE_OK;
+}
+
 int mde_use_own_stream(mde_ctx* c) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
@@ -1297,6 +1306,25 @@ int verify_async(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, i
   uint8_t* pnodes = static_cast<uint8_t*>(at(4));
   int32_t* pids = static_cast<int32_t*>(at(6));
   int32_t* pst = peer_status ? peer_status : static_cast<int32_t*>(at(7));
+  if (mde::verify_fused_fits(R, cap) && !c->verify_chain) {
+    // one launch: decode (LDS-staged) -> trees of other-shape peers -> diffs -> fold -> encode
+    mde::VerifyFusedLaunch f{};
+    f.dec = mde::WireDecodeLaunch{(uint32_t)T, peer_bytes, peer_off, cap, nullptr, nullptr, nullptr, pd,
+                                  static_cast<int32_t*>(at(1)), pvalid, nullptr, nbk};
+    f.tree.B = cap;
+    f.tree.digest_in = pd;
+    f.tree.root_out = static_cast<uint8_t*>(at(5));
+    f.tree.nodes_out = pnodes;
+    f.tree.n_int = NI;
+    f.diff = mde::DiffLaunch{(uint32_t)T, B, cap, digest, nodes, pd, pnodes, pids, idcap, pst, R, nbk};
+    f.fold = mde::VerifyLaunch{P, R, B, pst, pids, idcap, pvalid, replica_count, valid, valid_count, diff_ids,
+                               diff_count};
+    if (object_out)
+      f.enc = mde::WireEncodeLaunch{P, B, partition, epoch, epoch + 1, digest, size, valid, nullptr,
+                                    object_out, object_stride, object_len};
+    MDE_HIP(c, mde::launch_verify_fused(f, c->stream));
+    return MDE_OK;
+  }
   if (T) {
     // EpochTreeObjectToMerkleTree: decode (>cap buckets can only diff with an error: deeper tree)
     mde::WireDecodeLaunch d{(uint32_t)T, peer_bytes, peer_off, cap, nullptr, nullptr, nullptr, pd,

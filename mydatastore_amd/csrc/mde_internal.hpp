@@ -212,6 +212,24 @@ struct VerifyLaunch {
 constexpr uint32_t kVerifyMaxBuckets = 1u << 16;
 hipError_t launch_verify(const VerifyLaunch& a, hipStream_t st);
 
+// The whole decision step in ONE launch, one workgroup per partition (verify.hip): decode the R
+// peer objects (staged through LDS), rebuild only the peer trees whose shape differs from the
+// local tree, diff (leaf-only for same-shape peers, diff_body.hpp), fold, encode. Used when
+// R <= kVerifyFusedMaxPeers and the peer capacity is <= kVerifyFusedMaxCap; the five-launch chain
+// otherwise. The member launches carry the scratch pointers of the chain (tree.n_in is set
+// in-kernel per partition).
+constexpr uint32_t kVerifyFusedMaxPeers = 64;
+constexpr uint32_t kVerifyFusedMaxCap = 1024;
+struct VerifyFusedLaunch {
+  WireDecodeLaunch dec;  // n = P*R
+  TreeLaunch tree;       // P = R per partition, B = cap; digest_in/nodes_out/root_out at partition 0
+  DiffLaunch diff;       // n_pairs = P*R, a_div = R
+  VerifyLaunch fold;
+  WireEncodeLaunch enc;  // enc.n = 0: no object
+};
+bool verify_fused_fits(uint32_t R, uint32_t cap);
+hipError_t launch_verify_fused(const VerifyFusedLaunch& a, hipStream_t st);
+
 hipError_t launch_tag_keys(const uint8_t* keys, const uint64_t* key_off, uint64_t n, uint32_t B,
                            uint32_t P, uint32_t* bucket, uint32_t* partition, hipStream_t st);
 hipError_t launch_synth_tags(const uint64_t* gids, uint64_t n, uint32_t P, uint32_t B, int mode,

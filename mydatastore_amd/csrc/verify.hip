@@ -7,22 +7,44 @@
 // epoch object is valid iff validCount >= ReplicaCount or validDiff; otherwise the node requests
 // diffSet.List() from its peers (PoliteStreamRequest).
 //
-// One 256-thread workgroup per partition: the diff ids of its R peers are OR-ed into an LDS
-// bitmap of B bits (the Int32Set), then compacted in ascending order with a block prefix sum over
-// the bitmap words. Go's map iteration order is unspecified; ascending is the canonical order.
-#include "mde_device.hpp"
-#include "mde_internal.hpp"
+// Fold (verify_body): one 256-thread workgroup per partition; the diff ids of its R peers are
+// OR-ed into an LDS bitmap of B bits (the Int32Set), then compacted in ascending order with a
+// block prefix sum over the bitmap words. Go's map iteration order is unspecified; ascending is
+// the canonical order.
+//
+// Two launch shapes:
+//   * verify_kernel: the fold alone, after the decode / tree / diff kernels of the chain
+//     (mde_api.cpp verify_async) -- any R and B;
+//   * verify_fused_kernel: the whole step in one launch per call. A one-partition VerifyEpoch
+//     spent ~93 us in the chain on the device, 52 us of it in the decoder's lane-0 byte walk over
+//     global memory (one dependent load per varint byte) and 28 us rebuilding the peer trees (11
+//     dependent SHA-256 compressions). Here each wave stages one peer object into LDS with wide
+//     loads and parses it there with all 64 lanes (wire_body.hpp), and a peer tree is rebuilt
+//     only when its shape differs from the local tree's: same-shape peers diff on the leaf
+//     digests alone (diff_body<true>).
+#include "diff_body.hpp"
+#include "tree_body.hpp"
+#include "wire_body.hpp"
 
 namespace mde {
 namespace {
 
 constexpr int kThreads = 256;
 constexpr uint32_t kWords = kVerifyMaxBuckets / 32;
+constexpr uint32_t kFusedWords = kVerifyFusedMaxCap / 32;
+constexpr uint32_t kStageMaxBytes = 16u * 1024u;  // per wave
 
-__global__ __launch_bounds__(kThreads) void verify_kernel(VerifyLaunch a) {
-  __shared__ uint32_t bits[kWords];
-  __shared__ uint32_t wave_tot[kThreads / 64];
-  const uint32_t p = blockIdx.x, t = threadIdx.x;
+// Phase timestamps of a one-workgroup fused launch (build with -DMDE_VERIFY_PROF; diagnostics only).
+#ifdef MDE_VERIFY_PROF
+#define MDE_PROF_MARK(k) \
+  if (gridDim.x == 1 && threadIdx.x == 0) prof_t[k] = wall_clock64()
+#else
+#define MDE_PROF_MARK(k)
+#endif
+
+// Partition p's fold by all 256 threads (uniform: contains barriers). bits: >= ceil(B/32) words.
+__device__ __forceinline__ void verify_body(const VerifyLaunch& a, uint32_t p, uint32_t* bits, uint32_t* wave_tot) {
+  const uint32_t t = threadIdx.x;
   const uint32_t W = (a.B + 31) / 32;
   for (uint32_t w = t; w < W; w += kThreads) bits[w] = 0;
   __syncthreads();
@@ -79,12 +101,131 @@ __global__ __launch_bounds__(kThreads) void verify_kernel(VerifyLaunch a) {
   }
 }
 
+__global__ __launch_bounds__(kThreads) void verify_kernel(VerifyLaunch a) {
+  __shared__ uint32_t bits[kWords];
+  __shared__ uint32_t wave_tot[kThreads / 64];
+  verify_body(a, blockIdx.x, bits, wave_tot);
+}
+
+__global__ __launch_bounds__(kThreads) void verify_fused_kernel(VerifyFusedLaunch f, uint32_t G, uint32_t words,
+                                                                uint32_t stage_bytes) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];  // object stages, then tree levels
+  __shared__ uint32_t bits[kFusedWords];
+  __shared__ uint32_t wave_tot[kThreads / 64];
+  __shared__ DiffLds ds;
+  __shared__ int32_t tree_n[kVerifyFusedMaxPeers];
+  __shared__ uint32_t need_tree;
+  const uint32_t p = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t R = f.fold.R, B = f.fold.B, cap = f.dec.cap;
+  const uint64_t i0 = (uint64_t)p * R;
+#ifdef MDE_VERIFY_PROF
+  uint64_t prof_t[8] = {};
+#endif
+  MDE_PROF_MARK(0);
+
+  // 1. EpochTreeObjectToMerkleTree, decode half: wave w takes peers w, w + 4, ...
+  uint8_t* stage = reinterpret_cast<uint8_t*>(dyn) + (uint64_t)wid * stage_bytes;
+  for (uint32_t r0 = 0; r0 < R; r0 += kThreads / 64) {
+    const uint32_t r = r0 + wid;
+    const uint8_t* obj = nullptr;
+    const uint8_t* staged = nullptr;
+    uint64_t n = 0;
+    if (r < R) {
+      const uint64_t o0 = f.dec.off[i0 + r];
+      n = f.dec.off[i0 + r + 1] - o0;
+      obj = f.dec.bytes + o0;
+      if (n + 4 <= stage_bytes) staged = stage_object(obj, n, stage, lane);
+    }
+    __syncthreads();
+    MDE_PROF_MARK(1);
+    if (r < R) {
+      // two call sites, so the staged one reads LDS (ds_read) rather than through flat loads
+      if (staged)
+        decode_object(f.dec, (uint32_t)(i0 + r), staged, n, lane);
+      else
+        decode_object(f.dec, (uint32_t)(i0 + r), obj, n, lane);
+    }
+    __syncthreads();
+  }
+  MDE_PROF_MARK(2);
+
+  // 2. Rebuild only the peer trees whose shape (leaf count incl. the odd duplicate) differs from
+  // the local tree's; same-shape peers are diffed on their leaves.
+  const uint32_t leaves = B + (B & 1u);
+  if (threadIdx.x == 0) need_tree = 0;
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < R; r += kThreads) {
+    const int32_t nb = f.dec.n_buckets[i0 + r];
+    const bool other = nb > 0 && (uint32_t)nb + ((uint32_t)nb & 1u) != leaves;
+    tree_n[r] = other ? nb : 0;
+    if (other) need_tree = 1;
+  }
+  __syncthreads();
+  if (need_tree) {
+    TreeLaunch t = f.tree;
+    t.P = R;
+    t.digest_in += i0 * cap;
+    t.nodes_out += i0 * t.n_int * 32;
+    t.root_out += i0 * 32;
+    t.n_in = tree_n;
+    const uint32_t groups = kThreads / G;
+    for (uint32_t blk = 0; blk * groups < R; blk++) tree_body<true>(t, G, words, blk, dyn, kThreads);
+  }
+
+  MDE_PROF_MARK(3);
+  // 3. DifferentMerkleTreeBuckets(myTree, otherTree) per peer.
+  for (uint32_t r = 0; r < R; r++) {
+    if (tree_n[r] == 0)
+      diff_body<true>(f.diff, (uint32_t)(i0 + r), ds);
+    else
+      diff_body<false>(f.diff, (uint32_t)(i0 + r), ds);
+  }
+  __syncthreads();
+
+  MDE_PROF_MARK(4);
+  // 4. validCount / validDiff / diffSet.
+  verify_body(f.fold, p, bits, wave_tot);
+  MDE_PROF_MARK(5);
+
+  // 5. The object VerifyEpoch persists.
+  if (f.enc.n) {
+    __syncthreads();
+    if (wid == 0) encode_object(f.enc, p, lane);
+  }
+  MDE_PROF_MARK(6);
+#ifdef MDE_VERIFY_PROF
+  if (gridDim.x == 1 && threadIdx.x == 0)
+    printf("verify_prof stage %lu decode %lu shape %lu diff %lu fold %lu encode %lu (x10ns)\n", prof_t[1] - prof_t[0],
+           prof_t[2] - prof_t[1], prof_t[3] - prof_t[2], prof_t[4] - prof_t[3], prof_t[5] - prof_t[4],
+           prof_t[6] - prof_t[5]);
+#endif
+}
+
 }  // namespace
 
 hipError_t launch_verify(const VerifyLaunch& a, hipStream_t st) {
   if (a.P == 0) return hipSuccess;
   if (a.B == 0 || a.B > kVerifyMaxBuckets) return hipErrorInvalidValue;
   hipLaunchKernelGGL(verify_kernel, dim3(a.P), dim3(kThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+bool verify_fused_fits(uint32_t R, uint32_t cap) {
+  return R <= kVerifyFusedMaxPeers && cap >= 1 && cap <= kVerifyFusedMaxCap;
+}
+
+hipError_t launch_verify_fused(const VerifyFusedLaunch& a, hipStream_t st) {
+  const uint32_t P = a.fold.P, cap = a.dec.cap;
+  if (P == 0) return hipSuccess;
+  if (!verify_fused_fits(a.fold.R, cap) || a.fold.B == 0 || a.fold.B > cap) return hipErrorInvalidValue;
+  TreeGeometry g;
+  tree_geometry(cap, &g);
+  const uint32_t tree_bytes = g.words * 4u * ((uint32_t)kThreads / g.G);
+  uint64_t stage = (wire_max_bytes(cap) + 4 + 15) / 16 * 16;
+  if (stage > kStageMaxBytes) stage = kStageMaxBytes;
+  const uint64_t stage_all = stage * (kThreads / 64);
+  const size_t lds = tree_bytes > stage_all ? tree_bytes : stage_all;
+  hipLaunchKernelGGL(verify_fused_kernel, dim3(P), dim3(kThreads), lds, st, a, g.G, g.words, (uint32_t)stage);
   return hipGetLastError();
 }
 

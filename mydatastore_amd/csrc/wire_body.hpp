@@ -1,0 +1,269 @@
+// wire_body.hpp -- EpochTreeObject protobuf encode/decode of ONE object, as device functions
+// shared by the standalone wire kernels (wire.hip) and the fused verify kernel (verify.hip).
+//
+// Reference: VerifyEpoch persists and serves proto.Marshal(MerkleTreeToPartitionEpochObject(...))
+// (main/manager.go:1041-1056, rpc/server.go:170-187) and peers decode it back into a tree
+// (EpochTreeObjectToMerkleTree, main/merkle_tree.go:140-157). Message (datap/data.proto:60-68):
+//   1 int32 partition | 2 int64 lower_epoch | 3 int64 upper_epoch | 4 repeated bytes buckets
+//   5 repeated int32 buckets_size (packed) | 6 bool valid | 7 int32 items
+// proto3 encoding as protobuf-go emits it: fields in number order, zero scalars omitted, each
+// bucket a length-delimited 8-byte LE64 digest, sizes one packed run of varints, negative int32
+// sign-extended to a 10-byte varint. Leaves follow tree.Leafs: an odd B repeats the last bucket.
+#pragma once
+#include "mde_device.hpp"
+#include "mde_internal.hpp"
+
+namespace mde {
+
+__device__ __forceinline__ uint32_t varint_len(uint64_t v) {
+  uint32_t n = 1;
+  while (v >= 0x80) { v >>= 7; n++; }
+  return n;
+}
+
+__device__ __forceinline__ uint32_t put_varint(uint8_t* p, uint64_t v) {
+  uint32_t n = 0;
+  while (v >= 0x80) { p[n++] = (uint8_t)(v | 0x80); v >>= 7; }
+  p[n++] = (uint8_t)v;
+  return n;
+}
+
+__device__ __forceinline__ uint64_t sx32(int32_t v) { return (uint64_t)(int64_t)v; }
+
+// Object i by one wave (lane = 0..63); no barriers, so a fused kernel may call it from one wave.
+__device__ __forceinline__ void encode_object(const WireEncodeLaunch& a, uint32_t i, uint32_t lane) {
+  const uint32_t B = a.B, L = B + (B & 1u);
+  const uint64_t* dg = a.digest + (uint64_t)i * B;
+  const int32_t* sz = a.size + (uint64_t)i * B;
+  uint8_t* out = a.out + (uint64_t)i * a.out_stride;
+  const int32_t part = a.partition ? a.partition[i] : 0;
+  const bool valid = a.valid && a.valid[i];
+  // items: given, or the tree.Leafs sum (duplicate leaf counted again), int32 wrap
+  int32_t items;
+  if (a.items) {
+    items = a.items[i];
+  } else {
+    uint32_t acc = 0;
+    for (uint32_t j = lane; j < L; j += 64) acc += (uint32_t)sz[min(j, B - 1)];
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    items = (int32_t)acc;
+  }
+  // header (lane 0) -- identical length computation in every lane
+  uint32_t hdr = 0;
+  if (part) hdr += 1 + varint_len(sx32(part));
+  if (a.lower) hdr += 1 + varint_len((uint64_t)a.lower);
+  if (a.upper) hdr += 1 + varint_len((uint64_t)a.upper);
+  if (lane == 0) {
+    uint32_t q = 0;
+    if (part) { out[q++] = 0x08; q += put_varint(out + q, sx32(part)); }
+    if (a.lower) { out[q++] = 0x10; q += put_varint(out + q, (uint64_t)a.lower); }
+    if (a.upper) { out[q++] = 0x18; q += put_varint(out + q, (uint64_t)a.upper); }
+  }
+  // buckets: L entries of [0x22, 0x08, LE64]
+  for (uint32_t j = lane; j < L; j += 64) {
+    uint8_t* e = out + hdr + (uint64_t)j * 10;
+    const uint64_t d = dg[min(j, B - 1)];
+    e[0] = 0x22;
+    e[1] = 0x08;
+#pragma unroll
+    for (int k = 0; k < 8; k++) e[2 + k] = (uint8_t)(d >> (8 * k));
+  }
+  uint32_t q = hdr + L * 10;
+  // buckets_size: packed varints
+  uint32_t plen = 0;
+  for (uint32_t j = lane; j < L; j += 64) plen += varint_len(sx32(sz[min(j, B - 1)]));
+  for (int o = 32; o > 0; o >>= 1) plen += __shfl_xor(plen, o);
+  if (L) {
+    if (lane == 0) {
+      out[q] = 0x2a;
+      put_varint(out + q + 1, plen);
+    }
+    q += 1 + varint_len(plen);
+    uint32_t base = q;
+    for (uint32_t j0 = 0; j0 < L; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      const uint32_t len = j < L ? varint_len(sx32(sz[min(j, B - 1)])) : 0;
+      uint32_t incl = len;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = __shfl_up(incl, o);
+        if ((int)lane >= o) incl += x;
+      }
+      if (j < L) put_varint(out + base + incl - len, sx32(sz[min(j, B - 1)]));
+      base += __shfl(incl, 63);
+    }
+    q += plen;
+  }
+  if (lane == 0) {
+    if (valid) { out[q] = 0x30; out[q + 1] = 0x01; }
+    uint32_t t = q + (valid ? 2 : 0);
+    if (items) { out[t++] = 0x38; t += put_varint(out + t, sx32(items)); }
+    a.out_len[i] = t;
+  }
+}
+
+// Copy the n bytes at src into LDS at dst + (src & 3) with 4-byte loads (8 per lane in flight)
+// for the aligned interior and byte loads for the <= 3 + 3 edge bytes; nothing outside
+// [src, src + n) is read. One wave; returns the staged copy of src.
+__device__ __forceinline__ const uint8_t* stage_object(const uint8_t* src, uint64_t n, uint8_t* dst, uint32_t lane) {
+  const uint64_t s = reinterpret_cast<uint64_t>(src), e = s + n, base = s & ~3ull;
+  const uint64_t wa = (s + 3) & ~3ull, wb = e & ~3ull;
+  if (wa < wb) {
+    const uint32_t nw = (uint32_t)((wb - wa) >> 2);
+    const uint32_t* gw = reinterpret_cast<const uint32_t*>(wa);
+    uint32_t* lw = reinterpret_cast<uint32_t*>(dst + (wa - base));
+    for (uint32_t k0 = 0; k0 < nw; k0 += 8 * 64) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const uint32_t k = k0 + u * 64 + lane;
+        v[u] = k < nw ? gw[k] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const uint32_t k = k0 + u * 64 + lane;
+        if (k < nw) lw[k] = v[u];
+      }
+    }
+    if (lane < wa - s) dst[s - base + lane] = src[lane];
+    if (lane < e - wb) dst[wb - base + lane] = reinterpret_cast<const uint8_t*>(wb)[lane];
+  } else {
+    for (uint32_t k = lane; k < n; k += 64) dst[s - base + k] = src[k];
+  }
+  return dst + (s - base);
+}
+
+// Decoder cursor. Every lane of the wave holds the same cursor and reads the same bytes (LDS
+// broadcast when the object is staged there), so control flow stays wave-uniform and the lanes
+// are free for the two runs that dominate an object: the bucket entries and the packed sizes.
+struct Cursor {
+  const uint8_t* p;
+  uint64_t n, pos;
+  bool ok;
+  __device__ __forceinline__ uint64_t varint() {
+    uint64_t v = 0;
+    for (int s = 0; s < 64; s += 7) {
+      if (pos >= n) { ok = false; return 0; }
+      const uint8_t b = p[pos++];
+      v |= (uint64_t)(b & 0x7f) << s;
+      if (!(b & 0x80)) return v;
+    }
+    ok = false;
+    return 0;
+  }
+  // Advance by len bytes; fails (without wrapping) past the end.
+  __device__ __forceinline__ void skip(uint64_t len) {
+    if (len > n - pos) { ok = false; return; }
+    pos += len;
+  }
+};
+
+// Object i by ALL 64 lanes of one wave (lane = 0..63), parsing the n bytes at p (the object in
+// a.bytes, or a copy staged in LDS). Same results as a one-field-at-a-time walk:
+//   * a run of canonical bucket entries [0x22 0x08 LE64] is checked and extracted 64 entries at a
+//     time (ballot: the run ends at the first lane whose entry is not canonical; that entry then
+//     goes through the generic path), entry number cap + 1 fails with MDE_E_CAPACITY;
+//   * a packed sizes run is split at its varint terminators 64 bytes at a time (ballot; element
+//     index = terminators before it); a varint longer than 10 bytes or crossing the run's end is
+//     a decode error, as it is for the serial walk.
+__device__ __forceinline__ void decode_object(const WireDecodeLaunch& a, uint32_t i, const uint8_t* p, uint64_t n,
+                                              uint32_t lane) {
+  Cursor c{p, n, 0, true};
+  int32_t part = 0, items = 0;
+  int64_t lower = 0, upper = 0;
+  uint8_t valid = 0;
+  uint32_t nb = 0, ns = 0;
+  int32_t err = 0;
+  const uint32_t cap = a.cap;
+  uint64_t* dg = a.digest + (uint64_t)i * cap;
+  int32_t* sz = a.size + (uint64_t)i * cap;
+  while (c.ok && c.pos < c.n && !err) {
+    if (c.p[c.pos] == 0x22 && c.n - c.pos >= 10 && c.p[c.pos + 1] == 0x08) {
+      const uint64_t q = c.pos + 10ull * lane;
+      const bool good = q + 10 <= c.n && c.p[q] == 0x22 && c.p[q + 1] == 0x08;
+      const uint64_t bad = ~__ballot(good);
+      const uint32_t run = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;  // >= 1
+      const uint32_t room = nb < cap ? cap - nb : 0u;
+      const uint32_t take = run < room ? run : room;
+      if (lane < take) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int k = 7; k >= 0; k--) v = (v << 8) | c.p[q + 2 + k];
+        dg[nb + lane] = v;
+      }
+      nb += take;
+      c.pos += 10ull * take;
+      if (take < run) { err = -5; break; }  // entry cap + 1
+      continue;
+    }
+    const uint64_t key = c.varint();
+    if (!c.ok) break;
+    const uint32_t field = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
+    if (field == 1 && wt == 0) { part = (int32_t)c.varint(); continue; }
+    if (field == 2 && wt == 0) { lower = (int64_t)c.varint(); continue; }
+    if (field == 3 && wt == 0) { upper = (int64_t)c.varint(); continue; }
+    if (field == 6 && wt == 0) { valid = c.varint() != 0; continue; }
+    if (field == 7 && wt == 0) { items = (int32_t)c.varint(); continue; }
+    if (field == 4 && wt == 2) {  // a non-canonical entry (e.g. a length other than 8)
+      const uint64_t len = c.varint();
+      if (!c.ok || len > c.n - c.pos) { c.ok = false; break; }
+      if (len != 8) { err = -6; break; }  // DecodeBytesToInt64 (utils/utils.go:80-82)
+      if (nb >= cap) { err = -5; break; }
+      uint64_t v = 0;
+      for (int k = 7; k >= 0; k--) v = (v << 8) | c.p[c.pos + k];
+      if (lane == 0) dg[nb] = v;
+      nb++;
+      c.pos += len;
+      continue;
+    }
+    if (field == 5 && wt == 2) {  // packed
+      const uint64_t len = c.varint();
+      if (!c.ok || len > c.n - c.pos) { c.ok = false; break; }
+      const uint64_t end = c.pos + len;
+      while (c.pos < end) {
+        const uint64_t q = c.pos + lane;
+        const uint8_t b = q < end ? c.p[q] : (uint8_t)0x80;
+        const bool term = !(b & 0x80);
+        const uint64_t T = __ballot(term);
+        if (!T) { c.ok = false; break; }  // > 64 bytes, or crosses the run's end
+        const uint64_t below = T & ((1ull << lane) - 1ull);
+        const uint32_t start = below ? 64u - (uint32_t)__builtin_clzll(below) : 0u;
+        const bool too_long = term && lane - start >= 10u;
+        if (__ballot(too_long)) { c.ok = false; break; }
+        if (term) {
+          uint64_t v = 0;
+          for (uint32_t k = start; k <= lane; k++) v |= (uint64_t)(c.p[c.pos + k] & 0x7f) << (7 * (k - start));
+          const uint32_t idx = ns + (uint32_t)__popcll(below);
+          if (idx < cap) sz[idx] = (int32_t)v;
+        }
+        ns += (uint32_t)__popcll(T);
+        c.pos += 64u - (uint32_t)__builtin_clzll(T);
+      }
+      continue;
+    }
+    if (field == 5 && wt == 0) {  // unpacked element (parsers must accept both)
+      const int32_t v = (int32_t)c.varint();
+      if (lane == 0 && ns < cap) sz[ns] = v;
+      ns++;
+      continue;
+    }
+    // unknown field: skip by wire type
+    if (wt == 0) { c.varint(); continue; }
+    if (wt == 1) { c.skip(8); continue; }
+    if (wt == 5) { c.skip(4); continue; }
+    if (wt == 2) { const uint64_t len = c.varint(); if (c.ok) c.skip(len); continue; }
+    c.ok = false;
+  }
+  if (!c.ok && !err) err = -6;
+  // sizes default to 0 when BucketsSize is shorter (main/merkle_tree.go:147-152)
+  for (uint32_t j = ns + lane; j < nb && j < cap; j += 64) sz[j] = 0;
+  if (lane == 0) {
+    if (a.partition) a.partition[i] = part;
+    if (a.lower) a.lower[i] = lower;
+    if (a.upper) a.upper[i] = upper;
+    if (a.valid) a.valid[i] = valid;
+    if (a.items) a.items[i] = items;
+    a.n_buckets[i] = err ? err : (int32_t)nb;
+  }
+}
+
+}  // namespace mde

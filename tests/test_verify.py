@@ -91,8 +91,11 @@ def test_oracle_verify_testmerkletreeraw_relations(golden):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B", [64, 30, 7, 1, 1000])
-def test_verify_epochs_matches_oracle(engine, B):
+@pytest.mark.parametrize("mode", [0, 1], ids=["fused", "chain"])
+@pytest.mark.parametrize("B", [64, 30, 7, 1, 1000, 2000])
+def test_verify_epochs_matches_oracle(engine, B, mode):
+    """Both launch shapes (one fused launch; the decode/tree/diff/fold/encode chain) against the
+    oracle. B = 2000 exceeds the fused kernel's peer capacity and runs the chain in both modes."""
     rng = np.random.default_rng(1000 + B)
     P, E, replica = 16, 41, 2
     digests = rng.integers(0, 999999, size=P * B, dtype=np.uint64)
@@ -101,7 +104,11 @@ def test_verify_epochs_matches_oracle(engine, B):
     _, nodes = engine.tree_from_digests(digests, B)
     peers = [_peer_objects(rng, B, digests[p * B:(p + 1) * B], sizes[p * B:(p + 1) * B], int(parts[p]), E)
              for p in range(P)]
-    got = engine.verify_epochs(B, digests, sizes, nodes, peers, replica, E, partition=parts)
+    engine.set_verify_mode(mode)
+    try:
+        got = engine.verify_epochs(B, digests, sizes, nodes, peers, replica, E, partition=parts)
+    finally:
+        engine.set_verify_mode(0)
     want = _oracle_verify(B, digests, sizes, peers, replica, E, parts)
     for p in range(P):
         w = want[p]
@@ -110,6 +117,34 @@ def test_verify_epochs_matches_oracle(engine, B):
         assert got["diff"][p] == w["diff"], (B, p)
         assert got["peer_status"][p] == [STATUS.get(x, x) for x in w["status"]], (B, p)
         assert got["objects"][p] == w["object"], (B, p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [1, 5, 9, 64, 65])
+def test_verify_epochs_peer_counts(engine, R):
+    """Peer counts around the fused kernel's wave loop (4 objects staged per pass) and its limit
+    (64 peers; 65 runs the chain): one partition, every peer case of _peer_objects cycled, fused
+    vs chain vs oracle."""
+    rng = np.random.default_rng(300 + R)
+    B, E, replica = 64, 12, 3
+    digests = rng.integers(0, 999999, size=B, dtype=np.uint64)
+    sizes = rng.integers(0, 5000, size=B).astype(np.int32)
+    _, nodes = engine.tree_from_digests(digests, B)
+    pool = [o for k in range(8) for o in _peer_objects(rng, B, digests, sizes, k, E)]
+    peers = [[pool[(r * 5) % len(pool)] for r in range(R)]]
+    res = []
+    for mode in (0, 1):
+        engine.set_verify_mode(mode)
+        try:
+            res.append(engine.verify_epochs(B, digests, sizes, nodes, peers, replica, E))
+        finally:
+            engine.set_verify_mode(0)
+    assert res[0] == res[1]
+    w = _oracle_verify(B, digests, sizes, peers, replica, E, np.zeros(1, np.int32))[0]
+    assert res[0]["valid"][0] == w["valid"] and res[0]["valid_count"][0] == w["valid_count"]
+    assert res[0]["diff"][0] == w["diff"]
+    assert res[0]["peer_status"][0] == [STATUS.get(x, x) for x in w["status"]]
+    assert res[0]["objects"][0] == w["object"]
 
 
 @pytest.mark.gpu

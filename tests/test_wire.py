@@ -115,3 +115,58 @@ def test_wire_roundtrip_rebuilds_same_tree(engine, golden, coracle):
     d = np.array([x for o in dec for x in o["digest"]], np.uint64)
     roots, _ = engine.tree_from_digests(d, B)
     assert [roots[32 * p:32 * p + 32].tobytes().hex() for p in range(P)] == case["root"]
+
+
+def _varint(v):
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+@pytest.mark.gpu
+def test_decode_wave_runs_and_hostile_lengths(engine):
+    """The wave-parallel decoder's run boundaries (bucket runs and packed-size windows of 64,
+    capacity inside a run, a non-canonical entry splitting a run, 10-byte negative sizes, objects
+    above the 8 KiB LDS stage) and hostile lengths that must fail, not wrap (a length field near
+    2^64 once moved the cursor backwards: an endless parse)."""
+    import mydatastore_amd as mde
+    rng = np.random.default_rng(64)
+    cls = wire_pb.epoch_tree_object_class()
+    objs, exp = [], []
+    for B in (63, 64, 65, 127, 128, 129, 700, 1000):
+        d = rng.integers(0, 999999, B).tolist()
+        s = rng.integers(-2**31, 2**31, B).tolist()  # 5- and 10-byte varints
+        b = wire_pb.marshal(3, 4, 5, d, s, True, None)
+        objs.append(b)
+        exp.append(wire_pb.unmarshal(b))
+    assert len(objs[-1]) > 8 << 10  # parsed from global memory, not the LDS stage
+    got = engine.decode_objects(objs, cap=1024)
+    for g, e in zip(got, exp):
+        assert g["digest"] == [int.from_bytes(x, "little") for x in e.buckets]
+        assert g["size"] == list(e.buckets_size)
+        assert g["valid"] == e.valid and g["partition"] == e.partition
+    # capacity reached inside a run (entry cap + 1 fails), for several window offsets
+    for B, cap in ((65, 64), (129, 100), (700, 640), (64, 64)):
+        r = engine.decode_objects([objs[(63, 64, 65, 127, 128, 129, 700, 1000).index(B)]], cap=cap)[0]
+        assert (r == mde.MDE_E_CAPACITY) if B > cap else isinstance(r, dict)
+    # a run split by a non-canonical entry: overlong key varint 0xA2 0x00 (= field 4, wire type 2)
+    ent = [int(x) for x in rng.integers(0, 999999, 6)]
+    body = b"".join(b"\x22\x08" + v.to_bytes(8, "little") for v in ent[:3])
+    body += b"\xa2\x00\x08" + ent[3].to_bytes(8, "little")
+    body += b"".join(b"\x22\x08" + v.to_bytes(8, "little") for v in ent[4:])
+    pk = b"".join(_varint(x) for x in (1, 300, 2**32 - 1))
+    split = body + b"\x2a" + _varint(len(pk)) + pk
+    g = engine.decode_objects([split], cap=16)[0]
+    assert g["digest"] == ent and g["size"] == [1, 300, -1, 0, 0, 0]
+    assert [int.from_bytes(x, "little") for x in cls.FromString(split).buckets] == ent
+    # failures: 11-byte size varint, a varint crossing the packed run's end, wrapping lengths
+    eleven = b"\x2a\x0b" + b"\xff" * 10 + b"\x01"
+    cross = b"\x2a\x02\x01\x80\x01"
+    wrap_unknown = b"\x08\x01\x0a" + _varint(2**64 - 12)  # field 1, wire type 2: skipped
+    wrap_bucket = b"\x22" + _varint(2**64 - 1)
+    wrap_packed = b"\x2a" + _varint(2**64 - 11) + b"\x01"
+    res = engine.decode_objects([eleven, cross, wrap_unknown, wrap_bucket, wrap_packed], cap=16)
+    assert res == [mde.MDE_E_DECODE] * 5

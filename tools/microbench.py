@@ -112,7 +112,7 @@ def bench_ab(eng, variants, worlds=(1, 8), reps=5, cap=2):
     return res
 
 
-def bench_verify(eng, P=1024, B=64, R=2):
+def bench_verify(eng, P=1024, B=64, R=2, mode=0):
     """VerifyEpoch decision step (mde_verify_epochs) for P partitions x R peer objects: peer 0
     agrees, peer 1 differs in one bucket. Device-resident call timed with HIP events; the
     synchronous host call (copies included) with the wall clock."""
@@ -144,6 +144,7 @@ def bench_verify(eng, P=1024, B=64, R=2):
         eng.verify_epochs_async(P, B, None, 5, out["digest"], out["size"], out["nodes"], R, blob, doff, 2,
                                 o["valid"], o["vc"], o["ids"], o["dc"], o["st"], o["obj"], stride, o["olen"])
 
+    eng.set_verify_mode(mode)
     us_dev = timeit(dev_call, reps=20, warm=3)
     assert int(o["vc"].sum()) == P and int(o["dc"].sum()) == P  # one agreeing peer, one differing bucket
     nodes = out["nodes"].cpu().numpy()
@@ -152,7 +153,8 @@ def bench_verify(eng, P=1024, B=64, R=2):
     for _ in range(5):
         eng.verify_epochs(B, dg, sz, nodes, peers, 2, 5)
     us_host = (time.perf_counter() - t0) / 5 * 1e6
-    r = {"partitions": P, "buckets": B, "peers": R, "peer_bytes": int(off[-1]),
+    eng.set_verify_mode(0)
+    r = {"mode": ["fused", "chain"][mode], "partitions": P, "buckets": B, "peers": R, "peer_bytes": int(off[-1]),
          "device_us_per_call": round(us_dev, 1), "device_partitions_per_s": round(P / us_dev * 1e6),
          "host_api_us_per_call_incl_copies_and_python": round(us_host, 1)}
     print(json.dumps(r), flush=True)
@@ -173,7 +175,7 @@ def main():
     if "sweep" in what:
         out["sweep"] = bench_sweep(eng)
     if "verify" in what:
-        out["verify"] = [bench_verify(eng, P=p) for p in (1, 64, 1024, 8192)]
+        out["verify"] = [bench_verify(eng, P=p, mode=m) for p in (1, 64, 1024, 8192) for m in (0, 1)]
     for w in what:
         if w.startswith("ab:"):
             out["ab"] = bench_ab(eng, [int(x) for x in w.split(":")[1].split(",")])
