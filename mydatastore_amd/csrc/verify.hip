@@ -115,6 +115,7 @@ __global__ __launch_bounds__(kThreads) void verify_fused_kernel(VerifyFusedLaunc
   __shared__ DiffLds ds;
   __shared__ int32_t tree_n[kVerifyFusedMaxPeers];
   __shared__ uint32_t need_tree;
+  __shared__ uint32_t gstack[kThreads / 64][kWireGroupDepth];
   const uint32_t p = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t R = f.fold.R, B = f.fold.B, cap = f.dec.cap;
   const uint64_t i0 = (uint64_t)p * R;
@@ -141,9 +142,9 @@ __global__ __launch_bounds__(kThreads) void verify_fused_kernel(VerifyFusedLaunc
     if (r < R) {
       // two call sites, so the staged one reads LDS (ds_read) rather than through flat loads
       if (staged)
-        decode_object(f.dec, (uint32_t)(i0 + r), staged, n, lane);
+        decode_object(f.dec, (uint32_t)(i0 + r), staged, n, lane, gstack[wid]);
       else
-        decode_object(f.dec, (uint32_t)(i0 + r), obj, n, lane);
+        decode_object(f.dec, (uint32_t)(i0 + r), obj, n, lane, gstack[wid]);
     }
     __syncthreads();
   }

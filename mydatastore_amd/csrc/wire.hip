@@ -19,15 +19,16 @@ constexpr uint32_t kDecodeStageBytes = 8u * 1024u;
 
 __global__ __launch_bounds__(64) void decode_kernel(WireDecodeLaunch a) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[kDecodeStageBytes];
+  __shared__ uint32_t gstack[kWireGroupDepth];
   const uint32_t i = blockIdx.x, lane = threadIdx.x;
   const uint8_t* obj = a.bytes + a.off[i];
   const uint64_t n = a.off[i + 1] - a.off[i];
   if (n + 4 <= kDecodeStageBytes) {
     const uint8_t* staged = stage_object(obj, n, stage, lane);
     __syncthreads();
-    decode_object(a, i, staged, n, lane);
+    decode_object(a, i, staged, n, lane, gstack);
   } else {
-    decode_object(a, i, obj, n, lane);
+    decode_object(a, i, obj, n, lane, gstack);
   }
 }
 

@@ -139,16 +139,19 @@ struct Cursor {
   const uint8_t* p;
   uint64_t n, pos;
   bool ok;
+  // protowire.ConsumeVarint: at most 10 bytes, the 10th 0 or 1 (else errCodeOverflow).
   __device__ __forceinline__ uint64_t varint() {
     uint64_t v = 0;
-    for (int s = 0; s < 64; s += 7) {
+    for (int s = 0; s < 63; s += 7) {
       if (pos >= n) { ok = false; return 0; }
       const uint8_t b = p[pos++];
       v |= (uint64_t)(b & 0x7f) << s;
       if (!(b & 0x80)) return v;
     }
-    ok = false;
-    return 0;
+    if (pos >= n) { ok = false; return 0; }
+    const uint8_t b = p[pos++];
+    if (b > 1) { ok = false; return 0; }
+    return v | ((uint64_t)b << 63);
   }
   // Advance by len bytes; fails (without wrapping) past the end.
   __device__ __forceinline__ void skip(uint64_t len) {
@@ -157,16 +160,52 @@ struct Cursor {
   }
 };
 
+// protowire.consumeFieldValueD for an unknown group (start tag `num` already read): nested
+// fields are skipped by wire type until the end tag of the same number; inner tags need a number
+// in [1, MaxInt32]. The open groups' numbers live in gstack (wave-uniform LDS, kWireGroupDepth
+// words): groups nested deeper than that fail, where protobuf-go allows 10,000 levels.
+constexpr uint32_t kWireGroupDepth = 64;
+__device__ __forceinline__ void skip_group(Cursor& c, uint64_t num, uint32_t* gstack) {
+  uint32_t depth = 1;
+  gstack[0] = (uint32_t)num;
+  while (c.ok) {
+    const uint64_t key = c.varint();
+    if (!c.ok) return;
+    const uint64_t n2 = key >> 3;
+    const uint32_t w = (uint32_t)(key & 7);
+    if (n2 < 1 || n2 > 0x7FFFFFFFull) { c.ok = false; return; }
+    if (w == 4) {
+      if ((uint32_t)n2 != gstack[depth - 1]) { c.ok = false; return; }
+      if (--depth == 0) return;
+      continue;
+    }
+    if (w == 3) {
+      if (depth == kWireGroupDepth) { c.ok = false; return; }
+      gstack[depth++] = (uint32_t)n2;
+      continue;
+    }
+    if (w == 0) { c.varint(); continue; }
+    if (w == 1) { c.skip(8); continue; }
+    if (w == 5) { c.skip(4); continue; }
+    if (w == 2) { const uint64_t len = c.varint(); if (c.ok) c.skip(len); continue; }
+    c.ok = false;  // reserved wire types 6, 7
+  }
+}
+
 // Object i by ALL 64 lanes of one wave (lane = 0..63), parsing the n bytes at p (the object in
 // a.bytes, or a copy staged in LDS). Same results as a one-field-at-a-time walk:
 //   * a run of canonical bucket entries [0x22 0x08 LE64] is checked and extracted 64 entries at a
 //     time (ballot: the run ends at the first lane whose entry is not canonical; that entry then
-//     goes through the generic path), entry number cap + 1 fails with MDE_E_CAPACITY;
+//     goes through the generic path); entries past cap are counted, not stored, and the object
+//     then fails with MDE_E_CAPACITY unless it has a decode error;
 //   * a packed sizes run is split at its varint terminators 64 bytes at a time (ballot; element
-//     index = terminators before it); a varint longer than 10 bytes or crossing the run's end is
-//     a decode error, as it is for the serial walk.
+//     index = terminators before it); a varint longer than 10 bytes, with a 10th byte above 1, or
+//     crossing the run's end is a decode error, as it is for the serial walk.
+// Errors follow protobuf-go v1.30's proto.Unmarshal (main/go.mod:15; the restatement is
+// oracle/wire_pb.py unmarshal): varint overflow, field numbers outside [1, 2^29-1], truncation,
+// stray end groups, reserved wire types. Unknown fields are skipped, groups included.
 __device__ __forceinline__ void decode_object(const WireDecodeLaunch& a, uint32_t i, const uint8_t* p, uint64_t n,
-                                              uint32_t lane) {
+                                              uint32_t lane, uint32_t* gstack) {
   Cursor c{p, n, 0, true};
   int32_t part = 0, items = 0;
   int64_t lower = 0, upper = 0;
@@ -182,21 +221,19 @@ __device__ __forceinline__ void decode_object(const WireDecodeLaunch& a, uint32_
       const bool good = q + 10 <= c.n && c.p[q] == 0x22 && c.p[q + 1] == 0x08;
       const uint64_t bad = ~__ballot(good);
       const uint32_t run = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;  // >= 1
-      const uint32_t room = nb < cap ? cap - nb : 0u;
-      const uint32_t take = run < room ? run : room;
-      if (lane < take) {
+      if (lane < run && nb + lane < cap) {
         uint64_t v = 0;
 #pragma unroll
         for (int k = 7; k >= 0; k--) v = (v << 8) | c.p[q + 2 + k];
         dg[nb + lane] = v;
       }
-      nb += take;
-      c.pos += 10ull * take;
-      if (take < run) { err = -5; break; }  // entry cap + 1
+      nb += run;
+      c.pos += 10ull * run;
       continue;
     }
     const uint64_t key = c.varint();
     if (!c.ok) break;
+    if ((key >> 3) < 1 || (key >> 3) > 0x1FFFFFFFull) { c.ok = false; break; }  // MaxValidNumber
     const uint32_t field = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
     if (field == 1 && wt == 0) { part = (int32_t)c.varint(); continue; }
     if (field == 2 && wt == 0) { lower = (int64_t)c.varint(); continue; }
@@ -207,10 +244,11 @@ __device__ __forceinline__ void decode_object(const WireDecodeLaunch& a, uint32_
       const uint64_t len = c.varint();
       if (!c.ok || len > c.n - c.pos) { c.ok = false; break; }
       if (len != 8) { err = -6; break; }  // DecodeBytesToInt64 (utils/utils.go:80-82)
-      if (nb >= cap) { err = -5; break; }
-      uint64_t v = 0;
-      for (int k = 7; k >= 0; k--) v = (v << 8) | c.p[c.pos + k];
-      if (lane == 0) dg[nb] = v;
+      if (nb < cap) {
+        uint64_t v = 0;
+        for (int k = 7; k >= 0; k--) v = (v << 8) | c.p[c.pos + k];
+        if (lane == 0) dg[nb] = v;
+      }
       nb++;
       c.pos += len;
       continue;
@@ -227,7 +265,7 @@ __device__ __forceinline__ void decode_object(const WireDecodeLaunch& a, uint32_
         if (!T) { c.ok = false; break; }  // > 64 bytes, or crosses the run's end
         const uint64_t below = T & ((1ull << lane) - 1ull);
         const uint32_t start = below ? 64u - (uint32_t)__builtin_clzll(below) : 0u;
-        const bool too_long = term && lane - start >= 10u;
+        const bool too_long = term && (lane - start >= 10u || (lane - start == 9u && b > 1));
         if (__ballot(too_long)) { c.ok = false; break; }
         if (term) {
           uint64_t v = 0;
@@ -251,9 +289,13 @@ __device__ __forceinline__ void decode_object(const WireDecodeLaunch& a, uint32_
     if (wt == 1) { c.skip(8); continue; }
     if (wt == 5) { c.skip(4); continue; }
     if (wt == 2) { const uint64_t len = c.varint(); if (c.ok) c.skip(len); continue; }
-    c.ok = false;
+    if (wt == 3) { skip_group(c, key >> 3, gstack); continue; }
+    c.ok = false;  // a stray end group, reserved wire types 6, 7
   }
   if (!c.ok && !err) err = -6;
+  // More buckets than fit: reported only for an object Go would unmarshal (a later wire error
+  // makes the whole object a decode error), after the scan that checked the rest of it.
+  if (!err && nb > cap) err = -5;
   // sizes default to 0 when BucketsSize is shorter (main/merkle_tree.go:147-152)
   for (uint32_t j = ns + lane; j < nb && j < cap; j += 64) sz[j] = 0;
   if (lane == 0) {

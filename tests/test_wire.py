@@ -170,3 +170,105 @@ def test_decode_wave_runs_and_hostile_lengths(engine):
     wrap_packed = b"\x2a" + _varint(2**64 - 11) + b"\x01"
     res = engine.decode_objects([eleven, cross, wrap_unknown, wrap_bucket, wrap_packed], cap=16)
     assert res == [mde.MDE_E_DECODE] * 5
+
+
+GO_RULE_CASES = {  # object bytes -> True when protobuf-go v1.30 proto.Unmarshal accepts them
+    "field0": (b"\x00\x05", False),
+    "varint_10th_byte_2": (b"\x08" + b"\xff" * 9 + b"\x02", False),  # upb accepts; Go overflows
+    "varint_10th_byte_1": (b"\x08" + b"\xff" * 9 + b"\x01", True),
+    "packed_10th_byte_2": (b"\x2a\x0a" + b"\xff" * 9 + b"\x02", False),
+    "unknown_group": (b"\x4b\x08\x01\x53\x54\x4c\x08\x05", True),  # 9{1:1 10{}} then partition=5
+    "group_end_mismatch": (b"\x4b\x54", False),
+    "stray_end_group": (b"\x4c", False),
+    "wire_type_6": (b"\x4e", False),
+    "wire_type_7": (b"\x4f", False),
+    "top_field_2pow29": (b"\x80\x80\x80\x80\x10\x01", False),
+    "top_field_max": (b"\xf8\xff\xff\xff\x0f\x01", True),
+    "group_inner_field_2pow29": (b"\x4b\x80\x80\x80\x80\x10\x01\x4c", True),  # ConsumeTag: <= MaxInt32
+    "group_inner_field_2pow31": (b"\x4b\x80\x80\x80\x80\x80\x02\x01\x4c", False),
+    "known_field_other_wire_type": (b"\x0d\x01\x02\x03\x04\x22\x08" + bytes(8), True),
+    "bool_2": (b"\x30\x02", True),
+    "overlong_key": (b"\x88\x00\x05", True),
+}
+
+
+def test_oracle_unmarshal_go_rules():
+    """oracle/wire_pb.unmarshal (the protobuf-go restatement) on the wire-format edge cases, and
+    agreement with the upb runtime on well-formed objects."""
+    for name, (b, ok) in GO_RULE_CASES.items():
+        try:
+            wire_pb.unmarshal(b)
+            got = True
+        except wire_pb.WireError:
+            got = False
+        assert got == ok, name
+    assert wire_pb.unmarshal(GO_RULE_CASES["unknown_group"][0]).partition == 5
+    assert wire_pb.unmarshal(GO_RULE_CASES["bool_2"][0]).valid
+    rng = np.random.default_rng(9)
+    for B in (0, 1, 2, 7, 64, 129):
+        d = rng.integers(0, 999999, B).tolist()
+        s = rng.integers(-2**31, 2**31, B).tolist()
+        b = wire_pb.marshal(int(rng.integers(-5, 5)), 3, 4, d, s, bool(B % 2))
+        a, u = wire_pb.unmarshal(b), wire_pb.unmarshal_upb(b)
+        for k in ("partition", "lower_epoch", "upper_epoch", "valid", "items"):
+            assert getattr(a, k) == getattr(u, k)
+        assert list(a.buckets) == list(u.buckets) and list(a.buckets_size) == list(u.buckets_size)
+
+
+def _expect_decode(obj, cap):
+    import mydatastore_amd as mde
+    try:
+        m = wire_pb.unmarshal(obj)
+    except wire_pb.WireError:
+        return mde.MDE_E_DECODE
+    if any(len(x) != 8 for x in m.buckets):
+        return mde.MDE_E_DECODE  # EpochTreeObjectToMerkleTree -> DecodeBytesToInt64
+    nb = len(m.buckets)
+    if nb > cap:
+        return mde.MDE_E_CAPACITY
+    return {"partition": m.partition, "lower": m.lower_epoch, "upper": m.upper_epoch, "valid": m.valid,
+            "items": m.items, "digest": [int.from_bytes(x, "little") for x in m.buckets],
+            "size": (list(m.buckets_size) + [0] * nb)[:nb]}
+
+
+def _mutate(rng, b):
+    b = bytearray(b)
+    for _ in range(int(rng.integers(1, 4))):
+        op = int(rng.integers(0, 6))
+        at = int(rng.integers(0, len(b) + 1))
+        if op == 0 and b:      # overwrite a byte
+            b[min(at, len(b) - 1)] = int(rng.integers(0, 256))
+        elif op == 1:          # insert random bytes
+            b[at:at] = bytes(rng.integers(0, 256, int(rng.integers(1, 4))).tolist())
+        elif op == 2 and b:    # delete a range
+            del b[at:at + int(rng.integers(1, 12))]
+        elif op == 3:          # truncate
+            del b[at:]
+        elif op == 4:          # splice one of the wire-rule cases
+            b[at:at] = list(GO_RULE_CASES.values())[int(rng.integers(0, len(GO_RULE_CASES)))][0]
+        else:                  # set / clear a continuation bit
+            if b:
+                b[min(at, len(b) - 1)] ^= 0x80
+    return bytes(b)
+
+
+@pytest.mark.gpu
+def test_decode_follows_go_unmarshal(engine):
+    """Device decoder vs the protobuf-go restatement: the wire-rule cases, then 3,000 seeded
+    mutations (byte overwrites, insertions, deletions, truncations, continuation-bit flips,
+    spliced edge cases) of valid objects -- same error class or the same decoded fields."""
+    rng = np.random.default_rng(2024)
+    cap = 64
+    objs = [b for b, _ in GO_RULE_CASES.values()]
+    base = []
+    for B in (1, 3, 30, 64, 70):
+        d = rng.integers(0, 999999, B).tolist()
+        s = rng.integers(-2**31, 2**31, B).tolist() if B % 2 else rng.integers(0, 300, B).tolist()
+        base.append(wire_pb.marshal(int(rng.integers(-9, 9)), 6, 7, d, s, bool(B % 2)))
+    objs += base
+    objs += [_mutate(rng, base[int(rng.integers(0, len(base)))]) for _ in range(3000)]
+    got = engine.decode_objects(objs, cap=cap)
+    bad = [(i, g, _expect_decode(o, cap)) for i, (g, o) in enumerate(zip(got, objs)) if g != _expect_decode(o, cap)]
+    assert not bad, bad[:5]
+    n_err = sum(1 for g in got if not isinstance(g, dict))
+    assert 300 < n_err < 2900  # the mutations exercise both outcomes
