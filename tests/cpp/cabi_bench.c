@@ -173,7 +173,7 @@ int main(int argc, char** argv) {
 
   /* the last timed build's roots equal the standalone build's */
   CHECK(mde_memcpy_d2h(ctx, root2, outs[(steps - 1) & 1].root, (uint64_t)P * 32));
-  const int ok_run = memcmp(root, root2, (size_t)P * 32) == 0;
+  int ok_run = memcmp(root, root2, (size_t)P * 32) == 0;
   const double ms = dt * 1e3 / steps;
   printf("{\"metric\": \"Merkle-tree build GiB/s (device-resident KV bytes hashed/s)\", \"host\": \"C via "
          "include/mde.h (no PyTorch)\", \"value\": %.3f, \"unit\": \"GiB/s\", \"ms_per_step\": %.5f, "
@@ -232,6 +232,91 @@ int main(int argc, char** argv) {
     free(hs);
     free(hd);
     free(hz);
+  }
+
+  /* One whole VerifyEpoch's device work for one partition, from C: RawPartitionMerkleTree
+   * (mde_build with the nodes output, 1,000 records) then the decision step (mde_verify_epochs)
+   * against two peer objects -- one agreeing, one with a single differing bucket -- persisting the
+   * object (main/manager.go:1036-1118). Median of 200 of each call. */
+  {
+    const uint64_t nr = 1000;
+    const uint64_t NI = mde_tree_internal_nodes(B);
+    uint8_t* hv = xmalloc(nr * 8);
+    for (uint64_t i = 0; i < nr * 8; i++) hv[i] = (uint8_t)(i * 131u + 7u);
+    uint64_t* hs = xmalloc(((uint64_t)B + 1) * 8);
+    for (uint32_t b = 0; b <= B; b++) hs[b] = nr * b / B;
+    uint64_t* hd = xmalloc((uint64_t)B * 8);
+    uint64_t* hd2 = xmalloc((uint64_t)B * 8);
+    int32_t *hz = xmalloc((uint64_t)B * 4), hi = 0;
+    uint8_t hr[32];
+    uint8_t* hn = xmalloc(NI * 32);
+    mde_records r1;
+    memset(&r1, 0, sizeof r1);
+    r1.values = hv;
+    r1.values_bytes = nr * 8;
+    r1.value_stride = 8;
+    r1.layout = MDE_LAYOUT_SORTED;
+    r1.n_records = nr;
+    r1.n_partitions = 1;
+    r1.n_buckets = B;
+    r1.seg_rec = hs;
+    mde_tree_out o1 = {hd, hz, &hi, hr, hn};
+    CHECK(mde_build(ctx, &r1, &o1));
+    /* peer objects: this tree's object, and one with bucket 0 perturbed */
+    const uint64_t stride = mde_epoch_tree_object_max_bytes(B);
+    uint8_t* peers = xmalloc(2 * stride);
+    uint32_t plen[2];
+    memcpy(hd2, hd, (size_t)B * 8);
+    hd2[0] = (hd2[0] + 1) % 999999u;
+    const int32_t part = 7;
+    CHECK(mde_encode_epoch_tree_objects(ctx, 1, B, &part, 5, 6, hd, hz, NULL, NULL, peers, stride, plen));
+    CHECK(mde_encode_epoch_tree_objects(ctx, 1, B, &part, 5, 6, hd2, hz, NULL, NULL, peers + plen[0], stride,
+                                        plen + 1));
+    const uint64_t poff[3] = {0, plen[0], (uint64_t)plen[0] + plen[1]};
+    uint8_t valid = 0;
+    int32_t vc = 0, dc = 0, st[2];
+    int32_t* ids = xmalloc((uint64_t)B * 4);
+    uint8_t* obj = xmalloc(stride);
+    uint32_t olen = 0;
+    double lb[200], lv[200];
+    for (int i = 0; i < 210; i++) {
+      const double a = now_s();
+      CHECK(mde_build(ctx, &r1, &o1));
+      const double m = now_s();
+      CHECK(mde_verify_epochs(ctx, 1, B, &part, 5, hd, hz, hn, 2, peers, poff, 2, &valid, &vc, ids, &dc, st, obj,
+                              stride, &olen));
+      if (i >= 10) {
+        lb[i - 10] = m - a;
+        lv[i - 10] = now_s() - m;
+      }
+    }
+    const int ok_verify = vc == 1 && dc == 1 && ids[0] == 0 && st[0] == 0 && st[1] == 1 && !valid && olen > 0;
+    for (int i = 1; i < 200; i++)
+      for (int j = i; j > 0 && lb[j] < lb[j - 1]; j--) {
+        const double t = lb[j];
+        lb[j] = lb[j - 1];
+        lb[j - 1] = t;
+      }
+    for (int i = 1; i < 200; i++)
+      for (int j = i; j > 0 && lv[j] < lv[j - 1]; j--) {
+        const double t = lv[j];
+        lv[j] = lv[j - 1];
+        lv[j - 1] = t;
+      }
+    printf("{\"latency\": \"VerifyEpoch device work, 1 partition: mde_build (nodes out) + mde_verify_epochs (2 peers)\", "
+           "\"records\": %" PRIu64 ", \"n_buckets\": %u, \"build_median_us\": %.1f, \"verify_median_us\": %.1f, "
+           "\"verify_p10_us\": %.1f, \"verify_p90_us\": %.1f, \"verify_ok\": %s}\n",
+           nr, B, lb[100] * 1e6, lv[100] * 1e6, lv[20] * 1e6, lv[180] * 1e6, ok_verify ? "true" : "false");
+    free(hv);
+    free(hs);
+    free(hd);
+    free(hd2);
+    free(hz);
+    free(hn);
+    free(peers);
+    free(ids);
+    free(obj);
+    if (!ok_verify) ok_run = 0;
   }
   mde_destroy(ctx);
   return ok_tree && ok_sum && ok_run ? 0 : 3;
