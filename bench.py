@@ -460,17 +460,29 @@ def main():
     # bracket / K is the average launch duration (the drain's tree launch is outside it).
     # Other modes: one event pair around each digest launch.
     bracket = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    ev_joined = torch.cuda.Event(enable_timing=True)
     if fused:
         bracket[0].record(stream)
     for i in range(args.steps):
         step(*(() if fused else evs[i]))
+    t_enq = time.perf_counter()
     if fused:
         bracket[1].record(stream)
     join()
+    ev_joined.record(stream)
+    t_join = time.perf_counter()
     torch.cuda.synchronize(dev)
+    t_sync = time.perf_counter()
     if use_dist:
         dist.barrier()
     t1 = time.perf_counter()
+    # where the wall time of the timed region went (host clock; the drain on the device clock)
+    host_timing = {"enqueue_ms": round((t_enq - t0) * 1e3, 3), "join_ms": round((t_join - t_enq) * 1e3, 3),
+                   "sync_wait_ms": round((t_sync - t_join) * 1e3, 3), "barrier_ms": round((t1 - t_sync) * 1e3, 3),
+                   "wall_ms": round((t1 - t0) * 1e3, 3)}
+    if fused:
+        host_timing["bracket_ms"] = round(bracket[0].elapsed_time(bracket[1]), 3)
+        host_timing["drain_ms"] = round(bracket[1].elapsed_time(ev_joined), 3)
     eng.set_stream(stream.cuda_stream)
     ms = (t1 - t0) * 1e3 / args.steps
     if use_dist and fused and not c5 and args.steps > 0:
@@ -531,6 +543,7 @@ def main():
                          "kernel_ms": round(kern_ms, 5),
                          "algorithmic_bytes_per_launch": local_bytes},
             "parity": parity,
+            "host_timing": host_timing,
             "simulated_shard_of_world": shard_world if shard_world != world else None,
             "pipeline": {"fused": "one build_step_kernel launch per build: this build's digest "
                                   "workgroups + the previous build's tree workgroups "

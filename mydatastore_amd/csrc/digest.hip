@@ -385,14 +385,24 @@ template <int U, bool NT, int PIPE, int PRIO = 0, bool STEAL = false>
 __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, TreeLaunch t, uint32_t tree_blocks,
                                                               uint32_t Q) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+#ifdef MDE_STEP_TREES_LAST
+  const uint32_t digest_blocks = gridDim.x - tree_blocks;
+  if (blockIdx.x >= digest_blocks) {
+    tree_body_packed(t, Q, blockIdx.x - digest_blocks, lds);
+    return;
+  }
+  const uint32_t db = blockIdx.x;
+#else
   if (blockIdx.x < tree_blocks) {
     tree_body_packed(t, Q, blockIdx.x, lds);
     return;
   }
+  const uint32_t db = blockIdx.x - tree_blocks;
+#endif
   if (STEAL)
-    digest_body_steal<U, NT, PRIO>(a, blockIdx.x - tree_blocks);
+    digest_body_steal<U, NT, PRIO>(a, db);
   else
-    digest_body<U, NT, PIPE, PRIO>(a, blockIdx.x - tree_blocks);
+    digest_body<U, NT, PIPE, PRIO>(a, db);
 }
 
 // One-launch build of a small arena (the synchronous one-partition calls of VerifyEpoch). Digest
@@ -547,7 +557,10 @@ uint32_t build_step_tree_q(uint32_t B) {
   const uint32_t n1 = (B + 1) / 2;
   const uint32_t per = (n1 + (n1 + 1) / 2) * 8u * 4u;  // bytes of level buffers per partition
   const uint32_t q = (kStepTreeLdsMax - 64u) / per;
-  return q > 16u ? 16u : q;
+#ifndef MDE_STEP_TREE_QMAX
+#define MDE_STEP_TREE_QMAX 16u
+#endif
+  return q > MDE_STEP_TREE_QMAX ? MDE_STEP_TREE_QMAX : q;
 }
 
 bool build_step_fusable(uint32_t B) { return B >= 1 && build_step_tree_q(B) >= 1; }
