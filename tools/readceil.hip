@@ -92,6 +92,33 @@ __global__ __launch_bounds__(256) void read_stride(const u32x4* __restrict__ buf
   if (lane == 0) atomicAdd(out, s);
 }
 
+// Contiguous range per WORKGROUP: its W waves interleave at U KiB granularity (wave w takes steps
+// w, w+W, ...), so the workgroup sweeps one region front to back with W*U KiB in flight -- W times
+// fewer concurrent streams than read_contig at the same wave count.
+template <int U, int W>
+__global__ __launch_bounds__(64 * W) void read_wgcontig(const u32x4* __restrict__ buf, uint64_t n16,
+                                                       uint64_t per_wg16, unsigned long long* out) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t beg = (uint64_t)blockIdx.x * per_wg16, end = std::min(beg + per_wg16, n16);
+  uint32_t acc = 0;
+  constexpr uint64_t kStep = 64ull * U;
+  for (uint64_t p = beg + wid * kStep; p + kStep <= end; p += W * kStep) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(buf + p + u * 64 + lane);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
+      acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
+      acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
+      acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
+    }
+  }
+  unsigned long long s = acc;
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) atomicAdd(out, s);
+}
+
 __global__ void fill(uint32_t* p, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     p[i] = (uint32_t)(i * 2654435761u);
@@ -156,6 +183,23 @@ int main(int argc, char** argv) {
     report("stride U8 default", wpc, time_it([&] {
              hipLaunchKernelGGL((read_stride<8, false>), dim3(cus * wpc), dim3(256), 0, 0, buf, n16, out);
            }));
+    {  // one stream per 4-wave / 8-wave workgroup (wpc = 4-wave workgroups per CU, as above)
+      const uint64_t per4 = ((n16 + (uint64_t)cus * wpc - 1) / ((uint64_t)cus * wpc) + 255) / 256 * 256;
+      const uint32_t b4 = (uint32_t)((n16 + per4 - 1) / per4);
+      report("wgcontig W4 U4 nt", wpc, time_it([&] {
+               hipLaunchKernelGGL((read_wgcontig<4, 4>), dim3(b4), dim3(256), 0, 0, buf, n16, per4, out);
+             }));
+      report("wgcontig W4 U8 nt", wpc, time_it([&] {
+               hipLaunchKernelGGL((read_wgcontig<8, 4>), dim3(b4), dim3(256), 0, 0, buf, n16, per4, out);
+             }));
+      if (wpc % 2 == 0) {
+        const uint64_t per8 = ((n16 + (uint64_t)cus * wpc / 2 - 1) / ((uint64_t)cus * wpc / 2) + 255) / 256 * 256;
+        const uint32_t b8 = (uint32_t)((n16 + per8 - 1) / per8);
+        report("wgcontig W8 U4 nt", wpc, time_it([&] {
+                 hipLaunchKernelGGL((read_wgcontig<4, 8>), dim3(b8), dim3(512), 0, 0, buf, n16, per8, out);
+               }));
+      }
+    }
   }
   CK(hipFree(buf));
   CK(hipFree(out));
