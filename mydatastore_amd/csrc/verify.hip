@@ -32,7 +32,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr uint32_t kWords = kVerifyMaxBuckets / 32;
 constexpr uint32_t kFusedWords = kVerifyFusedMaxCap / 32;
-constexpr uint32_t kStageMaxBytes = 16u * 1024u;  // per wave
+constexpr uint32_t kStageMaxBytes = 24u * 1024u;  // per wave: a whole object up to B = 1024 (20.5 KB)
 
 // Phase timestamps of a one-workgroup fused launch (build with -DMDE_VERIFY_PROF; diagnostics only).
 #ifdef MDE_VERIFY_PROF

@@ -176,6 +176,7 @@ def main():
         out["sweep"] = bench_sweep(eng)
     if "verify" in what:
         out["verify"] = [bench_verify(eng, P=p, mode=m) for p in (1, 64, 1024, 8192) for m in (0, 1)]
+        out["verify"] += [bench_verify(eng, P=p, B=1000, mode=m) for p in (1, 64) for m in (0, 1)]
     for w in what:
         if w.startswith("ab:"):
             out["ab"] = bench_ab(eng, [int(x) for x in w.split(":")[1].split(",")])
