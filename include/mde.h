@@ -279,6 +279,11 @@ const char* mde_group_last_error(const mde_group* group);
 /* RawPartitionMerkleTree for P partitions over the group (host pointers, synchronous); same
  * contract as mde_build. */
 int mde_multi_build(mde_group* group, const mde_records* rec, const mde_tree_out* out);
+/* Host ingest over the group: each device's contiguous partition block goes through
+ * mde_build_streamed on that device (its own two-slot ring, chunk_bytes as there), concurrently --
+ * one PCIe link per device. Same contract and results as mde_multi_build. */
+int mde_multi_build_streamed(mde_group* group, const mde_records* rec, const mde_tree_out* out,
+                             uint64_t chunk_bytes);
 
 /* Write-time tagging of raw keys (device): bucket = BE64(SHA256(key)[:8]) % n_buckets
  * (main/manager.go:773-778), partition = XXH64(key, 0) % n_partitions (hashring.go:108-110).

@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = (
     "mde_decode_epoch_tree_objects", "mde_decode_epoch_tree_objects_async", "mde_synth_tags_async", "mde_synth_values_async", "mde_dev_alloc", "mde_dev_free",
     "mde_memcpy_h2d", "mde_memcpy_d2h", "mde_verify_peer_capacity", "mde_verify_epochs",
     "mde_verify_epochs_async", "mde_group_create", "mde_group_destroy", "mde_group_size",
-    "mde_group_ctx", "mde_group_last_error", "mde_multi_build",
+    "mde_group_ctx", "mde_group_last_error", "mde_multi_build", "mde_multi_build_streamed",
 )
 
 
@@ -137,6 +137,7 @@ def load_library() -> C.CDLL:
         "mde_group_ctx": (vp, [vp, u32]),
         "mde_group_last_error": (C.c_char_p, [vp]),
         "mde_multi_build": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
+        "mde_multi_build_streamed": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), C.c_uint64]),
         "mde_synth_tags_async": (C.c_int, [vp, vp, u64, u32, u32, C.c_int, u64, vp, vp]),
         "mde_synth_values_async": (C.c_int, [vp, vp, vp, u64, u32, u64]),
         "mde_dev_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
@@ -570,9 +571,9 @@ class Group:
         return int(self.lib.mde_group_size(self.g))
 
     def build(self, values, n_partitions, n_buckets, value_stride=0, value_off=None, seg_rec=None,
-              part_rec=None, bucket_tag=None, want_nodes=True):
-        """mde_multi_build from host arrays (layout A with seg_rec, or layout B with part_rec +
-        bucket_tag); same outputs as Engine.build."""
+              part_rec=None, bucket_tag=None, want_nodes=True, streamed=False, chunk_bytes=0):
+        """mde_multi_build (or mde_multi_build_streamed) from host arrays (layout A with seg_rec,
+        or layout B with part_rec + bucket_tag); same outputs as Engine.build."""
         P, B = n_partitions, n_buckets
         values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)
         if value_off is not None:
@@ -593,7 +594,10 @@ class Group:
             "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
         }
         to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
-        rc = self.lib.mde_multi_build(self.g, C.byref(rec), C.byref(to))
+        if streamed:
+            rc = self.lib.mde_multi_build_streamed(self.g, C.byref(rec), C.byref(to), chunk_bytes)
+        else:
+            rc = self.lib.mde_multi_build(self.g, C.byref(rec), C.byref(to))
         if rc != MDE_OK:
             raise MdeError(rc, (self.lib.mde_group_last_error(self.g) or b"").decode())
         return out

@@ -1545,7 +1545,10 @@ mde_ctx* mde_group_ctx(mde_group* g, uint32_t i) { return g && i < g->ctx.size()
 
 const char* mde_group_last_error(const mde_group* g) { return g ? g->err.c_str() : "null group"; }
 
-int mde_multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o) {
+namespace {
+// mde_multi_build / mde_multi_build_streamed: split P partitions into G contiguous blocks and
+// build each on its own device, one host thread per device (streamed: chunk_bytes ring per device).
+int multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o, bool streamed, uint64_t chunk_bytes) {
   if (!g || g->ctx.empty()) return MDE_E_INVAL;
   g->err.clear();
   mde_ctx* c0 = g->ctx[0];
@@ -1608,7 +1611,11 @@ int mde_multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o) {
   // one host thread per device: each shard's H2D, build and D2H run concurrently
   std::vector<std::thread> th;
   for (uint32_t i = 0; i < G; i++)
-    if (sh[i].live) th.emplace_back([&, i] { sh[i].rc = mde_build(g->ctx[i], &sh[i].rec, &sh[i].out); });
+    if (sh[i].live)
+      th.emplace_back([&, i] {
+        sh[i].rc = streamed ? mde_build_streamed(g->ctx[i], &sh[i].rec, &sh[i].out, chunk_bytes)
+                            : mde_build(g->ctx[i], &sh[i].rec, &sh[i].out);
+      });
   for (auto& t : th) t.join();
   for (uint32_t i = 0; i < G; i++)
     if (sh[i].rc != MDE_OK) {
@@ -1616,4 +1623,13 @@ int mde_multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o) {
       return sh[i].rc;
     }
   return MDE_OK;
+}
+}  // namespace
+
+int mde_multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o) {
+  return multi_build(g, r, o, false, 0);
+}
+
+int mde_multi_build_streamed(mde_group* g, const mde_records* r, const mde_tree_out* o, uint64_t chunk_bytes) {
+  return multi_build(g, r, o, true, chunk_bytes);
 }
