@@ -1,7 +1,8 @@
 // merkle_gpu.go -- cgo shim: drop-in for the hot path of main/merkle_tree.go (MyDataStore).
 //
 // Copy into the reference's main/ package and delete RawPartitionMerkleTree and
-// DifferentMerkleTreeBuckets from merkle_tree.go (INTEGRATION.md section 2). It binds only what
+// DifferentMerkleTreeBuckets from merkle_tree.go (INTEGRATION.md section 2); VerifyEpoch may then
+// replace its peer loop (main/manager.go:1072-1104) with verifyEpochDecision. It binds only what
 // include/mde.h declares (tests/test_integration.py checks every C.* name against the header).
 // Not compiled in this repository: the image has no Go toolchain (DESIGN.md section 1).
 package main
@@ -21,6 +22,9 @@ import (
 
 	"github.com/cbergoon/merkletree"
 	"github.com/pkg/errors"
+	"google.golang.org/protobuf/proto"
+
+	"github.com/andrew-delph/my-key-store/rpc"
 )
 
 var (
@@ -164,4 +168,89 @@ func DifferentMerkleTreeBuckets(tree1 *merkletree.MerkleTree, tree2 *merkletree.
 	out := make([]int32, n)
 	copy(out, unsafe.Slice((*int32)(cIds), n))
 	return out, nil
+}
+
+// verifyEpochDecision -- the decision step of Manager.VerifyEpoch (main/manager.go:1072-1104) in
+// one mde_verify_epochs call: every peer object is decoded, rebuilt and diffed against myTree on
+// the device; failed peers are skipped (the reference logs and continues); validCount, validDiff
+// and diffSet fold as the reference does. Returns valid (validCount >= replicaCount || validDiff),
+// validCount, diffSet (ascending) and the EpochTreeObject to persist (Valid set) as wire bytes.
+// VerifyEpoch keeps its own flow: on valid it stores data, otherwise it calls
+// PoliteStreamRequest(partitionId, epoch, epoch+1, diffSet).
+func verifyEpochDecision(myTree *merkletree.MerkleTree, partitionId int, epoch int64,
+	epochTreeObjects []*rpc.RpcEpochTreeObject, replicaCount int) (bool, int, []int32, []byte, error) {
+	ctx, err := mdeEngine()
+	if err != nil {
+		return false, 0, nil, nil, err
+	}
+	// the local tree as bucket digests + sizes (tree.Leafs without merkletree's odd duplicate)
+	n := len(myTree.Leafs)
+	if n > 1 && myTree.Leafs[n-1].C == myTree.Leafs[n-2].C {
+		n--
+	}
+	B := n
+	digest := make([]uint64, B)
+	size := make([]int32, B)
+	for i := 0; i < B; i++ {
+		b, ok := myTree.Leafs[i].C.(*MerkleBucket)
+		if !ok {
+			return false, 0, nil, nil, errors.New("failed to decode MerkleBucket")
+		}
+		digest[i] = uint64(b.hasher.Hash())
+		size[i] = b.size
+	}
+	cDigest := cU64(digest)
+	defer C.free(cDigest)
+	cSize := C.CBytes(unsafe.Slice((*byte)(unsafe.Pointer(&size[0])), B*4))
+	defer C.free(cSize)
+	nodeBytes := C.size_t(C.mde_tree_internal_nodes(C.uint32_t(B)) * 32)
+	cNodes := C.malloc(nodeBytes)
+	cRoot := C.malloc(32)
+	defer C.free(cNodes)
+	defer C.free(cRoot)
+	if rc := C.mde_tree_from_digests(ctx, 1, C.uint32_t(B), (*C.uint64_t)(cDigest), (*C.uint8_t)(cRoot),
+		(*C.uint8_t)(cNodes)); rc != C.MDE_OK {
+		return false, 0, nil, nil, errors.Errorf("mde_tree_from_digests: %s", C.GoString(C.mde_last_error(ctx)))
+	}
+	// peer objects back to wire bytes (gRPC already unmarshalled them); a nil object is absent
+	R := len(epochTreeObjects)
+	var blob []byte
+	off := make([]uint64, R+1)
+	for r, obj := range epochTreeObjects {
+		if obj != nil {
+			b, err := proto.Marshal(obj)
+			if err != nil {
+				return false, 0, nil, nil, err
+			}
+			blob = append(blob, b...)
+		}
+		off[r+1] = uint64(len(blob))
+	}
+	blob = append(blob, 0) // never a zero-length allocation
+	cBlob := C.CBytes(blob)
+	cOff := cU64(off)
+	defer C.free(cBlob)
+	defer C.free(cOff)
+	stride := C.mde_epoch_tree_object_max_bytes(C.uint32_t(B))
+	cObj := C.malloc(C.size_t(stride))
+	cIds := C.malloc(C.size_t(4 * B))
+	cStatus := C.malloc(C.size_t(4 * (R + 1)))
+	cOut := C.malloc(16) // valid (u8), validCount, diffCount, objectLen
+	defer C.free(cObj)
+	defer C.free(cIds)
+	defer C.free(cStatus)
+	defer C.free(cOut)
+	part := C.int32_t(partitionId)
+	outs := unsafe.Slice((*int32)(cOut), 4)
+	if rc := C.mde_verify_epochs(ctx, 1, C.uint32_t(B), &part, C.int64_t(epoch), (*C.uint64_t)(cDigest),
+		(*C.int32_t)(cSize), (*C.uint8_t)(cNodes), C.uint32_t(R), (*C.uint8_t)(cBlob), (*C.uint64_t)(cOff),
+		C.uint32_t(replicaCount), (*C.uint8_t)(unsafe.Pointer(&outs[0])), (*C.int32_t)(unsafe.Pointer(&outs[1])),
+		(*C.int32_t)(cIds), (*C.int32_t)(unsafe.Pointer(&outs[2])), (*C.int32_t)(cStatus), (*C.uint8_t)(cObj),
+		stride, (*C.uint32_t)(unsafe.Pointer(&outs[3]))); rc != C.MDE_OK {
+		return false, 0, nil, nil, errors.Errorf("mde_verify_epochs: %s", C.GoString(C.mde_last_error(ctx)))
+	}
+	valid := *(*uint8)(unsafe.Pointer(&outs[0])) != 0
+	diffSet := make([]int32, outs[2])
+	copy(diffSet, unsafe.Slice((*int32)(cIds), outs[2]))
+	return valid, int(outs[1]), diffSet, C.GoBytes(cObj, C.int(outs[3])), nil
 }
