@@ -235,3 +235,53 @@ def test_diff_large_call_equals_small_calls(engine):
         small = engine.diff(B, da[lo * B:hi * B], na[lo * NI:hi * NI], B, db[lo * B:hi * B], nb[lo * NI:hi * NI],
                             n_pairs=1000)
         assert big[lo:hi] == small, lo
+
+
+@pytest.mark.gpu
+def test_verify_epochs_fuzz_fused_chain_oracle(engine):
+    """Seeded fuzz of the whole decision step: 120 partitions with random B (1..70), each with
+    1-6 peer objects drawn from perturbed copies, other bucket counts (shallower, same depth,
+    deeper), odd-B duplicates, absent peers and byte-mutated objects. Fused launch == chain ==
+    oracle on every output (valid, validCount, diffSet, peer statuses, persisted object)."""
+    from tests.test_wire import _mutate
+    rng = np.random.default_rng(4242)
+    for trial in range(120):
+        B = int(rng.integers(1, 71))
+        E, replica = int(rng.integers(0, 50)), int(rng.integers(1, 4))
+        digests = rng.integers(0, 999999, size=B, dtype=np.uint64)
+        sizes = rng.integers(0, 3000, size=B).astype(np.int32)
+        _, nodes = engine.tree_from_digests(digests, B)
+        d, s = [int(x) for x in digests], [int(x) for x in sizes]
+        peers = []
+        for _ in range(int(rng.integers(1, 7))):
+            kind = int(rng.integers(0, 6))
+            if kind == 0:
+                peers.append(None)
+                continue
+            dd, ss = list(d), list(s)
+            if kind in (1, 5):  # perturb some buckets
+                for b in rng.choice(B, size=int(rng.integers(1, B + 1)), replace=False):
+                    dd[b] = (dd[b] + 1 + int(rng.integers(0, 999997))) % 999999
+            elif kind == 2:     # another bucket count
+                nb = max(1, int(rng.integers(1, 2 * B + 2)))
+                dd = [int(x) for x in rng.integers(0, 999999, nb)] if nb > B else dd[:nb]
+                ss = [int(x) for x in rng.integers(0, 3000, len(dd))]
+            obj = wire_pb.marshal(trial, E, E + 1, dd, ss, valid=bool(rng.integers(0, 2)))
+            if kind == 5:
+                obj = _mutate(rng, obj)
+            peers.append(obj)
+        res = []
+        for mode in (0, 1):
+            engine.set_verify_mode(mode)
+            try:
+                res.append(engine.verify_epochs(B, digests, sizes, nodes, [peers], replica, E,
+                                                partition=np.array([trial], np.int32)))
+            finally:
+                engine.set_verify_mode(0)
+        assert res[0] == res[1], trial
+        w = _oracle_verify(B, digests, sizes, [peers], replica, E, np.array([trial], np.int32))[0]
+        g = res[0]
+        assert g["valid"][0] == w["valid"] and g["valid_count"][0] == w["valid_count"], trial
+        assert g["diff"][0] == w["diff"], trial
+        assert g["peer_status"][0] == [STATUS.get(x, x) for x in w["status"]], trial
+        assert g["objects"][0] == w["object"], trial
