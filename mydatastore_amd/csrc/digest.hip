@@ -394,7 +394,9 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
   const uint32_t db = blockIdx.x;
 #else
   if (blockIdx.x < tree_blocks) {
+#ifndef MDE_STEP_SKIP_TREES  // probe only: the dispatch shape without the tree work
     tree_body_packed(t, Q, blockIdx.x, lds);
+#endif
     return;
   }
   const uint32_t db = blockIdx.x - tree_blocks;
