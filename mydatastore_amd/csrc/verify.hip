@@ -175,11 +175,43 @@ __global__ __launch_bounds__(kThreads) void verify_fused_kernel(VerifyFusedLaunc
 
   MDE_PROF_MARK(3);
   // 3. DifferentMerkleTreeBuckets(myTree, otherTree) per peer.
+  // 3a. Same-shape peers of a tree with <= 64 root-to-leaf paths (B <= 64): one wave per peer,
+  // lane v walks path v, and the wave's ballot gives the DFS output order directly (diff_body's
+  // leaf-only rule, without its block-wide prefix sums and barriers).
+  if (threadIdx.x == 0) make_diff_shape(B, ds.sa);
+  __syncthreads();
+  const uint32_t D = ds.sa.L - 1;
+  const bool wave_diff = D <= 6;
+  if (wave_diff) {
+    for (uint32_t r = wid; r < R; r += kThreads / 64) {
+      if (tree_n[r] != 0) continue;
+      const uint64_t i = i0 + r;
+      const int32_t bt = f.dec.n_buckets[i];
+      if (bt <= 0 || (uint32_t)bt > cap) {
+        if (lane == 0) f.diff.out_count[i] = bt == -5 ? -4 : -6;
+        continue;
+      }
+      uint32_t ia = 0;
+      for (uint32_t d = 0; d < D; d++) {
+        const uint32_t la = D - d, ca = 2 * ia + ((lane >> (D - 1 - d)) & 1u);
+        ia = ca < ds.sa.sizes[la - 1] ? ca : 2 * ia;
+      }
+      const uint32_t ida = min(ia, B - 1), idb = min(ia, (uint32_t)bt - 1);
+      const bool emit = lane < (1u << D) && f.diff.da[(uint64_t)p * B + ida] != f.diff.db[i * cap + idb];
+      const uint64_t bal = __ballot(emit);
+      const bool bad = __ballot(emit && ida != idb) != 0;  // "bucketIds dont match"
+      if (emit) f.diff.out_ids[i * f.diff.out_stride + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)ida;
+      if (lane == 0) f.diff.out_count[i] = bad ? -4 : (int32_t)__popcll(bal);
+    }
+  }
+  __syncthreads();
+  // 3b. The rest: other-shape peers (node hashes), and same-shape peers of deeper trees.
   for (uint32_t r = 0; r < R; r++) {
-    if (tree_n[r] == 0)
-      diff_body<true>(f.diff, (uint32_t)(i0 + r), ds);
-    else
+    if (tree_n[r] == 0) {
+      if (!wave_diff) diff_body<true>(f.diff, (uint32_t)(i0 + r), ds);
+    } else {
       diff_body<false>(f.diff, (uint32_t)(i0 + r), ds);
+    }
   }
   __syncthreads();
 
