@@ -5,12 +5,16 @@ stride 1..2048 B incl. odd and power-of-two strides, or variable 0..600 B), aren
 and the entry point (host mde_build, device mde_build_async, pipelined, layout B for fixed
 strides). Every output is compared bit for bit: digests, sizes, items, roots, all internal nodes.
 """
+import os
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = 160
+# MDE_FUZZ_SEED / MDE_FUZZ_CASES override the seed and case count for longer one-off runs
+N_CASES = int(os.environ.get("MDE_FUZZ_CASES", "160"))
+SEED = int(os.environ.get("MDE_FUZZ_SEED", "20261016"))
 MAX_BYTES = 96 << 20  # per case; the C oracle checks it on one host thread
 
 
@@ -73,7 +77,7 @@ def test_random_builds_match_oracle(engine, coracle):
     import mydatastore_amd as mde
     dev = torch.device("cuda:0")
     engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    rng = np.random.default_rng(20261016)
+    rng = np.random.default_rng(SEED)
     pending = []
     for i in range(N_CASES):
         P, B, counts, var, stride = _case(rng)
