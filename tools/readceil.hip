@@ -12,6 +12,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <algorithm>
+#include <string>
 #include <vector>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -154,6 +155,44 @@ int main(int argc, char** argv) {
     std::sort(ms.begin(), ms.end());
     return ms[ms.size() / 2];
   };
+  if (argc > 2 && std::string(argv[2]) == "cumask") {
+    // Streaming on a subset of the CUs (hipExtStreamCreateWithCUMask): is HBM still saturated
+    // when a few CUs are set aside? off CUs masked, either the last ones or one per 32.
+    for (int spread = 0; spread < 2; spread++)
+      for (int off : {0, 8, 16, 32}) {
+        std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+        int on = 0;
+        for (int c = 0; c < cus; c++) {
+          const bool masked = spread ? (off && (c % (cus / off)) == (cus / off) - 1) : c >= cus - off;
+          if (!masked) { mask[c / 32] |= 1u << (c % 32); on++; }
+        }
+        hipStream_t st;
+        CK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+        for (int wpc : {2, 3}) {
+          const uint64_t waves = (uint64_t)on * wpc * 4;
+          uint64_t per = (n16 + waves - 1) / waves;
+          per = (per + 255) / 256 * 256;
+          const uint32_t blocks = (uint32_t)((n16 + per * 4 - 1) / (per * 4));
+          std::vector<float> ms;
+          for (int r = 0; r < 12; r++) {
+            CK(hipEventRecord(a, st));
+            hipLaunchKernelGGL((read_contig<4, true, true>), dim3(blocks), dim3(256), 0, st, buf, n16, per, out);
+            CK(hipEventRecord(b, st));
+            CK(hipEventSynchronize(b));
+            float t;
+            CK(hipEventElapsedTime(&t, a, b));
+            if (r >= 2) ms.push_back(t);
+          }
+          std::sort(ms.begin(), ms.end());
+          const float m = ms[ms.size() / 2];
+          printf("{\"shape\": \"contig U4 nt pipe, CU mask\", \"cus_on\": %d, \"spread\": %d, \"wg_per_cu\": %d, "
+                 "\"ms\": %.4f, \"GBps\": %.1f}\n", on, spread, wpc, m, bytes / (m * 1e-3) / 1e9);
+          fflush(stdout);
+        }
+        CK(hipStreamDestroy(st));
+      }
+    return 0;
+  }
   auto report = [&](const char* name, int wg_per_cu, float ms) {
     printf("{\"shape\": \"%s\", \"wg_per_cu\": %d, \"bytes\": %llu, \"ms\": %.4f, \"GBps\": %.1f}\n", name,
            wg_per_cu, (unsigned long long)bytes, ms, bytes / (ms * 1e-3) / 1e9);
