@@ -107,6 +107,7 @@ __global__ __launch_bounds__(kThreads) void verify_kernel(VerifyLaunch a) {
   verify_body(a, blockIdx.x, bits, wave_tot);
 }
 
+template <bool kDeep>
 __global__ __launch_bounds__(kThreads) void verify_fused_kernel(VerifyFusedLaunch f, uint32_t G, uint32_t words,
                                                                 uint32_t stage_bytes) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];  // object stages, then tree levels
@@ -175,14 +176,22 @@ __global__ __launch_bounds__(kThreads) void verify_fused_kernel(VerifyFusedLaunc
 
   MDE_PROF_MARK(3);
   // 3. DifferentMerkleTreeBuckets(myTree, otherTree) per peer.
-  // 3a. Same-shape peers of a tree with <= 64 root-to-leaf paths (B <= 64): one wave per peer,
-  // lane v walks path v, and the wave's ballot gives the DFS output order directly (diff_body's
-  // leaf-only rule, without its block-wide prefix sums and barriers).
+  // 3a. Same-shape peers: one wave per peer, lane v of step k walks path 64k + v, and the wave's
+  // ballots give the DFS output order directly (diff_body's leaf-only rule, without its
+  // block-wide prefix sums and barriers). kDeep (B > 64): 512 paths per register batch, every
+  // digest load of a batch issued before its first id store (on gfx9 one vmcnt counter covers
+  // loads and stores, so a load behind stores waits for them). The B <= 64 instantiation keeps the
+  // one-step form, and with it the register count and occupancy of the common case.
   if (threadIdx.x == 0) make_diff_shape(B, ds.sa);
   __syncthreads();
   const uint32_t D = ds.sa.L - 1;
-  const bool wave_diff = D <= 6;
+  const bool wave_diff = kDeep ? D <= 10 : D <= 6;
   if (wave_diff) {
+    constexpr uint32_t kPathBatch = kDeep ? 8 : 1;
+    const uint32_t n_paths = 1u << D;
+    uint32_t lvl[10];  // lvl[d]: size of the level a path's step d descends into (from LDS once)
+#pragma unroll
+    for (uint32_t d = 0; d < 10; d++) lvl[d] = d < D ? ds.sa.sizes[D - 1 - d] : 0u;
     for (uint32_t r = wid; r < R; r += kThreads / 64) {
       if (tree_n[r] != 0) continue;
       const uint64_t i = i0 + r;
@@ -191,17 +200,45 @@ __global__ __launch_bounds__(kThreads) void verify_fused_kernel(VerifyFusedLaunc
         if (lane == 0) f.diff.out_count[i] = bt == -5 ? -4 : -6;
         continue;
       }
-      uint32_t ia = 0;
-      for (uint32_t d = 0; d < D; d++) {
-        const uint32_t la = D - d, ca = 2 * ia + ((lane >> (D - 1 - d)) & 1u);
-        ia = ca < ds.sa.sizes[la - 1] ? ca : 2 * ia;
+      const uint64_t* da = f.diff.da + (uint64_t)p * B;
+      const uint64_t* db = f.diff.db + i * cap;
+      int32_t* out = f.diff.out_ids + i * f.diff.out_stride;
+      uint32_t base = 0;
+      bool bad = false;
+      for (uint32_t c0 = 0; c0 < n_paths; c0 += 64 * kPathBatch) {
+        uint32_t leaf[kPathBatch];
+        uint64_t xa[kPathBatch], xb[kPathBatch];
+        // wave-uniform exits: the last batch of a tree runs only the steps it has
+#pragma unroll
+        for (uint32_t k = 0; k < kPathBatch; k++) {
+          if (c0 + k * 64 >= n_paths) break;
+          const uint32_t v = c0 + k * 64 + lane;
+          uint32_t ia = 0;
+#pragma unroll
+          for (uint32_t d = 0; d < 10; d++) {
+            if (d >= D) break;
+            const uint32_t ca = 2 * ia + ((v >> (D - 1 - d)) & 1u);
+            ia = ca < lvl[d] ? ca : 2 * ia;
+          }
+          leaf[k] = ia;
+          const bool in = v < n_paths;
+          xa[k] = in ? da[min(ia, B - 1)] : 0ull;
+          xb[k] = in ? db[min(ia, (uint32_t)bt - 1)] : 0ull;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kPathBatch; k++) {
+          if (c0 + k * 64 >= n_paths) break;
+          const uint32_t v = c0 + k * 64 + lane;
+          const uint32_t ida = min(leaf[k], B - 1), idb = min(leaf[k], (uint32_t)bt - 1);
+          const bool emit = v < n_paths && xa[k] != xb[k];
+          const uint64_t bal = __ballot(emit);
+          bad |= __ballot(emit && ida != idb) != 0;  // "bucketIds dont match"
+          const uint32_t at = base + __popcll(bal & ((1ull << lane) - 1ull));
+          if (emit && at < f.diff.out_stride) out[at] = (int32_t)ida;
+          base += __popcll(bal);
+        }
       }
-      const uint32_t ida = min(ia, B - 1), idb = min(ia, (uint32_t)bt - 1);
-      const bool emit = lane < (1u << D) && f.diff.da[(uint64_t)p * B + ida] != f.diff.db[i * cap + idb];
-      const uint64_t bal = __ballot(emit);
-      const bool bad = __ballot(emit && ida != idb) != 0;  // "bucketIds dont match"
-      if (emit) f.diff.out_ids[i * f.diff.out_stride + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)ida;
-      if (lane == 0) f.diff.out_count[i] = bad ? -4 : (int32_t)__popcll(bal);
+      if (lane == 0) f.diff.out_count[i] = bad ? -4 : base > f.diff.out_stride ? -5 : (int32_t)base;
     }
   }
   __syncthreads();
@@ -258,7 +295,11 @@ hipError_t launch_verify_fused(const VerifyFusedLaunch& a, hipStream_t st) {
   if (stage > kStageMaxBytes) stage = kStageMaxBytes;
   const uint64_t stage_all = stage * (kThreads / 64);
   const size_t lds = tree_bytes > stage_all ? tree_bytes : stage_all;
-  hipLaunchKernelGGL(verify_fused_kernel, dim3(P), dim3(kThreads), lds, st, a, g.G, g.words, (uint32_t)stage);
+  if (a.fold.B > 64)
+    hipLaunchKernelGGL(verify_fused_kernel<true>, dim3(P), dim3(kThreads), lds, st, a, g.G, g.words, (uint32_t)stage);
+  else
+    hipLaunchKernelGGL(verify_fused_kernel<false>, dim3(P), dim3(kThreads), lds, st, a, g.G, g.words,
+                       (uint32_t)stage);
   return hipGetLastError();
 }
 
