@@ -116,6 +116,7 @@ __global__ __launch_bounds__(kThreads) void verify_fused_kernel(VerifyFusedLaunc
   __shared__ DiffLds ds;
   __shared__ int32_t tree_n[kVerifyFusedMaxPeers];
   __shared__ uint32_t need_tree;
+  __shared__ uint32_t enc_red[16];
   __shared__ uint32_t gstack[kThreads / 64][kWireGroupDepth];
   const uint32_t p = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t R = f.fold.R, B = f.fold.B, cap = f.dec.cap;
@@ -260,7 +261,11 @@ __global__ __launch_bounds__(kThreads) void verify_fused_kernel(VerifyFusedLaunc
   // 5. The object VerifyEpoch persists.
   if (f.enc.n) {
     __syncthreads();
-    if (wid == 0) encode_object(f.enc, p, lane);
+    if (kDeep) {
+      encode_object_block(f.enc, p, threadIdx.x, kThreads, enc_red);  // B > 64: all four waves
+    } else if (wid == 0) {
+      encode_object(f.enc, p, lane);
+    }
   }
   MDE_PROF_MARK(6);
 #ifdef MDE_VERIFY_PROF

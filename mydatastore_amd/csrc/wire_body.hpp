@@ -101,6 +101,100 @@ __device__ __forceinline__ void encode_object(const WireEncodeLaunch& a, uint32_
   }
 }
 
+// Object i by a whole workgroup of nt threads (a multiple of 64, nt / 64 <= 8 waves; thread t):
+// the same bytes as encode_object, with the per-entry work spread over every wave. The one-wave
+// form is instruction-latency bound at large B (a dependent chain of shuffles, varint loops and
+// ten byte stores per 64 entries: ~13 us at B = 1,000). Uniform: contains barriers. red: >= 16
+// words of LDS.
+__device__ __forceinline__ void encode_object_block(const WireEncodeLaunch& a, uint32_t i, uint32_t t,
+                                                    uint32_t nt, uint32_t* red) {
+  const uint32_t B = a.B, L = B + (B & 1u);
+  const uint32_t lane = t & 63, wid = t >> 6, nw = nt >> 6;
+  const uint64_t* dg = a.digest + (uint64_t)i * B;
+  const int32_t* sz = a.size + (uint64_t)i * B;
+  uint8_t* out = a.out + (uint64_t)i * a.out_stride;
+  const int32_t part = a.partition ? a.partition[i] : 0;
+  const bool valid = a.valid && a.valid[i];
+  // items (tree.Leafs sum, int32 wrap) and the packed length of buckets_size
+  uint32_t acc = 0, plen = 0;
+  for (uint32_t j = t; j < L; j += nt) {
+    const int32_t v = sz[min(j, B - 1)];
+    acc += (uint32_t)v;
+    plen += varint_len(sx32(v));
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    acc += __shfl_xor(acc, o);
+    plen += __shfl_xor(plen, o);
+  }
+  if (lane == 0) {
+    red[wid] = acc;
+    red[8 + wid] = plen;
+  }
+  __syncthreads();
+  acc = 0;
+  plen = 0;
+  for (uint32_t w = 0; w < nw; w++) {
+    acc += red[w];
+    plen += red[8 + w];
+  }
+  __syncthreads();  // red is reused by the size scan below
+  const int32_t items = a.items ? a.items[i] : (int32_t)acc;
+  uint32_t hdr = 0;
+  if (part) hdr += 1 + varint_len(sx32(part));
+  if (a.lower) hdr += 1 + varint_len((uint64_t)a.lower);
+  if (a.upper) hdr += 1 + varint_len((uint64_t)a.upper);
+  if (t == 0) {
+    uint32_t q = 0;
+    if (part) { out[q++] = 0x08; q += put_varint(out + q, sx32(part)); }
+    if (a.lower) { out[q++] = 0x10; q += put_varint(out + q, (uint64_t)a.lower); }
+    if (a.upper) { out[q++] = 0x18; q += put_varint(out + q, (uint64_t)a.upper); }
+  }
+  for (uint32_t j = t; j < L; j += nt) {
+    uint8_t* e = out + hdr + (uint64_t)j * 10;
+    const uint64_t d = dg[min(j, B - 1)];
+    e[0] = 0x22;
+    e[1] = 0x08;
+#pragma unroll
+    for (int k = 0; k < 8; k++) e[2 + k] = (uint8_t)(d >> (8 * k));
+  }
+  uint32_t q = hdr + L * 10;
+  if (L) {
+    if (t == 0) {
+      out[q] = 0x2a;
+      put_varint(out + q + 1, plen);
+    }
+    q += 1 + varint_len(plen);
+    uint32_t base = q;
+    for (uint32_t j0 = 0; j0 < L; j0 += nt) {  // block-wide prefix sum of the varint lengths
+      const uint32_t j = j0 + t;
+      const int32_t v = j < L ? sz[min(j, B - 1)] : 0;
+      const uint32_t len = j < L ? varint_len(sx32(v)) : 0;
+      uint32_t incl = len;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = __shfl_up(incl, o);
+        if ((int)lane >= o) incl += x;
+      }
+      if (lane == 63) red[wid] = incl;
+      __syncthreads();
+      uint32_t before = 0, tot = 0;
+      for (uint32_t w = 0; w < nw; w++) {
+        before += w < wid ? red[w] : 0u;
+        tot += red[w];
+      }
+      if (j < L) put_varint(out + base + before + incl - len, sx32(v));
+      base += tot;
+      __syncthreads();
+    }
+    q += plen;
+  }
+  if (t == 0) {
+    if (valid) { out[q] = 0x30; out[q + 1] = 0x01; }
+    uint32_t e = q + (valid ? 2 : 0);
+    if (items) { out[e++] = 0x38; e += put_varint(out + e, sx32(items)); }
+    a.out_len[i] = e;
+  }
+}
+
 // Copy the n bytes at src into LDS at dst + (src & 3) with 4-byte loads (8 per lane in flight)
 // for the aligned interior and byte loads for the <= 3 + 3 edge bytes; nothing outside
 // [src, src + n) is read. One wave; returns the staged copy of src.
