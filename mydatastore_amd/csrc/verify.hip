@@ -143,10 +143,11 @@ __global__ __launch_bounds__(kThreads) void verify_fused_kernel(VerifyFusedLaunc
     MDE_PROF_MARK(1);
     if (r < R) {
       // two call sites, so the staged one reads LDS (ds_read) rather than through flat loads
+      // kDeep (B > 64): 256 canonical bucket entries per step instead of 64
       if (staged)
-        decode_object(f.dec, (uint32_t)(i0 + r), staged, n, lane, gstack[wid]);
+        decode_object<kDeep ? 4 : 1>(f.dec, (uint32_t)(i0 + r), staged, n, lane, gstack[wid]);
       else
-        decode_object(f.dec, (uint32_t)(i0 + r), obj, n, lane, gstack[wid]);
+        decode_object<kDeep ? 4 : 1>(f.dec, (uint32_t)(i0 + r), obj, n, lane, gstack[wid]);
     }
     __syncthreads();
   }

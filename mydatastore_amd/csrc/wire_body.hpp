@@ -288,16 +288,17 @@ __device__ __forceinline__ void skip_group(Cursor& c, uint64_t num, uint32_t* gs
 
 // Object i by ALL 64 lanes of one wave (lane = 0..63), parsing the n bytes at p (the object in
 // a.bytes, or a copy staged in LDS). Same results as a one-field-at-a-time walk:
-//   * a run of canonical bucket entries [0x22 0x08 LE64] is checked and extracted 64 entries at a
-//     time (ballot: the run ends at the first lane whose entry is not canonical; that entry then
-//     goes through the generic path); entries past cap are counted, not stored, and the object
-//     then fails with MDE_E_CAPACITY unless it has a decode error;
+//   * a run of canonical bucket entries [0x22 0x08 LE64] is checked and extracted 64 x kWin
+//     entries at a time (kWin per lane; ballots: the run ends at the first entry that is not
+//     canonical, which then goes through the generic path); entries past cap are counted, not
+//     stored, and the object then fails with MDE_E_CAPACITY unless it has a decode error;
 //   * a packed sizes run is split at its varint terminators 64 bytes at a time (ballot; element
 //     index = terminators before it); a varint longer than 10 bytes, with a 10th byte above 1, or
 //     crossing the run's end is a decode error, as it is for the serial walk.
 // Errors follow protobuf-go v1.30's proto.Unmarshal (main/go.mod:15; the restatement is
 // oracle/wire_pb.py unmarshal): varint overflow, field numbers outside [1, 2^29-1], truncation,
 // stray end groups, reserved wire types. Unknown fields are skipped, groups included.
+template <uint32_t kWin = 1>
 __device__ __forceinline__ void decode_object(const WireDecodeLaunch& a, uint32_t i, const uint8_t* p, uint64_t n,
                                               uint32_t lane, uint32_t* gstack) {
   Cursor c{p, n, 0, true};
@@ -311,15 +312,32 @@ __device__ __forceinline__ void decode_object(const WireDecodeLaunch& a, uint32_
   int32_t* sz = a.size + (uint64_t)i * cap;
   while (c.ok && c.pos < c.n && !err) {
     if (c.p[c.pos] == 0x22 && c.n - c.pos >= 10 && c.p[c.pos + 1] == 0x08) {
-      const uint64_t q = c.pos + 10ull * lane;
-      const bool good = q + 10 <= c.n && c.p[q] == 0x22 && c.p[q + 1] == 0x08;
-      const uint64_t bad = ~__ballot(good);
-      const uint32_t run = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;  // >= 1
-      if (lane < run && nb + lane < cap) {
-        uint64_t v = 0;
+      bool good[kWin];
 #pragma unroll
-        for (int k = 7; k >= 0; k--) v = (v << 8) | c.p[q + 2 + k];
-        dg[nb + lane] = v;
+      for (uint32_t u = 0; u < kWin; u++) {
+        const uint64_t q = c.pos + 10ull * (u * 64 + lane);
+        good[u] = q + 10 <= c.n && c.p[q] == 0x22 && c.p[q + 1] == 0x08;
+      }
+      uint32_t run = 0;  // >= 1: the first entry is canonical
+#pragma unroll
+      for (uint32_t u = 0; u < kWin; u++) {
+        const uint64_t bad = ~__ballot(good[u]);
+        if (bad) {
+          run = u * 64 + (uint32_t)__builtin_ctzll(bad);
+          break;
+        }
+        run = (u + 1) * 64;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kWin; u++) {
+        const uint32_t e = u * 64 + lane;
+        if (e < run && nb + e < cap) {
+          const uint64_t q = c.pos + 10ull * e;
+          uint64_t v = 0;
+#pragma unroll
+          for (int k = 7; k >= 0; k--) v = (v << 8) | c.p[q + 2 + k];
+          dg[nb + e] = v;
+        }
       }
       nb += run;
       c.pos += 10ull * run;
