@@ -36,7 +36,9 @@ def main(seeds=4, n_dec=20000, n_ver=300):
                               "mismatches": len(bad), "first": [objs[i].hex() for i in bad[:3]]}), flush=True)
         mism = 0
         for trial in range(n_ver):
-            B = int(rng.integers(1, 130))
+            # B > 64 takes the fused kernel's kDeep instantiation (batched diff, block encode,
+            # 256-entry decode window); up to the fused capacity of 1,024
+            B = int(rng.integers(1, 130)) if trial % 4 else int(rng.integers(130, 1025))
             E, replica = int(rng.integers(0, 50)), int(rng.integers(1, 4))
             digests = rng.integers(0, 999999, size=B, dtype=np.uint64)
             sizes = rng.integers(0, 3000, size=B).astype(np.int32)
