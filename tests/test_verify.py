@@ -92,7 +92,7 @@ def test_oracle_verify_testmerkletreeraw_relations(golden):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [0, 1], ids=["fused", "chain"])
-@pytest.mark.parametrize("B", [64, 30, 7, 1, 1000, 2000])
+@pytest.mark.parametrize("B", [64, 30, 7, 1, 65, 129, 513, 1000, 1024, 2000])
 def test_verify_epochs_matches_oracle(engine, B, mode):
     """Both launch shapes (one fused launch; the decode/tree/diff/fold/encode chain) against the
     oracle. B = 2000 exceeds the fused kernel's peer capacity and runs the chain in both modes."""
