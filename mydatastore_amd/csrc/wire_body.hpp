@@ -369,6 +369,48 @@ __device__ __forceinline__ void decode_object(const WireDecodeLaunch& a, uint32_
       const uint64_t len = c.varint();
       if (!c.ok || len > c.n - c.pos) { c.ok = false; break; }
       const uint64_t end = c.pos + len;
+      if (kWin > 1) {  // 64 x kWin bytes per step; byte e = 64u + lane of the window
+        while (c.pos < end) {
+          uint8_t bv[kWin];
+          uint64_t T[kWin];
+          uint32_t last = 0, any = 0;
+#pragma unroll
+          for (uint32_t u = 0; u < kWin; u++) {
+            const uint64_t q = c.pos + u * 64 + lane;
+            bv[u] = q < end ? c.p[q] : (uint8_t)0x80;
+            T[u] = __ballot(!(bv[u] & 0x80));
+            if (T[u]) {
+              last = u * 64 + 63 - (uint32_t)__builtin_clzll(T[u]);
+              any = 1;
+            }
+          }
+          if (!any) { c.ok = false; break; }  // > 64 x kWin bytes, or crosses the run's end
+          bool too_long = false;
+          uint32_t prev_end = 0, cnt = 0;  // (last terminator before word u) + 1; terminators before it
+#pragma unroll
+          for (uint32_t u = 0; u < kWin; u++) {
+            const uint32_t e = u * 64 + lane;
+            const bool term = !(bv[u] & 0x80);
+            const uint64_t below = T[u] & ((1ull << lane) - 1ull);
+            const uint32_t start = below ? u * 64 + 64u - (uint32_t)__builtin_clzll(below) : prev_end;
+            too_long |= term && (e - start >= 10u || (e - start == 9u && bv[u] > 1));
+            if (term && !too_long) {
+              uint64_t v = 0;
+              for (uint32_t k = start; k <= e; k++) v |= (uint64_t)(c.p[c.pos + k] & 0x7f) << (7 * (k - start));
+              const uint32_t idx = ns + cnt + (uint32_t)__popcll(below);
+              if (idx < cap) sz[idx] = (int32_t)v;
+            }
+            if (T[u]) prev_end = u * 64 + 64u - (uint32_t)__builtin_clzll(T[u]);
+            cnt += (uint32_t)__popcll(T[u]);
+          }
+          // an object with an over-long varint fails whole; the sizes written before it are
+          // scratch that no caller reads for a failed object
+          if (__ballot(too_long)) { c.ok = false; break; }
+          ns += cnt;
+          c.pos += last + 1;
+        }
+        continue;
+      }
       while (c.pos < end) {
         const uint64_t q = c.pos + lane;
         const uint8_t b = q < end ? c.p[q] : (uint8_t)0x80;
