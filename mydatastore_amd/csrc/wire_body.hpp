@@ -195,9 +195,10 @@ __device__ __forceinline__ void encode_object_block(const WireEncodeLaunch& a, u
   }
 }
 
-// Copy the n bytes at src into LDS at dst + (src & 3) with 4-byte loads (8 per lane in flight)
+// Copy the n bytes at src into LDS at dst + (src & 3) with 4-byte loads (kBatch per lane in flight)
 // for the aligned interior and byte loads for the <= 3 + 3 edge bytes; nothing outside
 // [src, src + n) is read. One wave; returns the staged copy of src.
+template <uint32_t kBatch = 8>
 __device__ __forceinline__ const uint8_t* stage_object(const uint8_t* src, uint64_t n, uint8_t* dst, uint32_t lane) {
   const uint64_t s = reinterpret_cast<uint64_t>(src), e = s + n, base = s & ~3ull;
   const uint64_t wa = (s + 3) & ~3ull, wb = e & ~3ull;
@@ -205,15 +206,15 @@ __device__ __forceinline__ const uint8_t* stage_object(const uint8_t* src, uint6
     const uint32_t nw = (uint32_t)((wb - wa) >> 2);
     const uint32_t* gw = reinterpret_cast<const uint32_t*>(wa);
     uint32_t* lw = reinterpret_cast<uint32_t*>(dst + (wa - base));
-    for (uint32_t k0 = 0; k0 < nw; k0 += 8 * 64) {
-      uint32_t v[8];
+    for (uint32_t k0 = 0; k0 < nw; k0 += kBatch * 64) {
+      uint32_t v[kBatch];
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (uint32_t u = 0; u < kBatch; u++) {
         const uint32_t k = k0 + u * 64 + lane;
         v[u] = k < nw ? gw[k] : 0u;
       }
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (uint32_t u = 0; u < kBatch; u++) {
         const uint32_t k = k0 + u * 64 + lane;
         if (k < nw) lw[k] = v[u];
       }
