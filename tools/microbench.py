@@ -4,6 +4,7 @@
     python tools/microbench.py tree            # tree kernel vs partitions / buckets
     python tools/microbench.py digest          # digest kernel vs arena size (C4 shards)
     python tools/microbench.py verify          # mde_verify_epochs vs partitions (2 peers each)
+    python tools/microbench.py decode          # mde_decode_epoch_tree_objects_async, B = 64 / 1000
 """
 import json
 import sys
@@ -161,6 +162,40 @@ def bench_verify(eng, P=1024, B=64, R=2, mode=0):
     return r
 
 
+def bench_decode(eng, n_obj=1, B=1000, cap=1024):
+    """Device decode of n_obj EpochTreeObjects of B buckets (mde_decode_epoch_tree_objects_async,
+    device-resident inputs and outputs), timed with HIP events."""
+    import ctypes as C
+    import torch
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(7)
+    dg = rng.integers(0, 999999, n_obj * B, dtype=np.uint64)
+    sz = rng.integers(0, 300, n_obj * B).astype(np.int32)
+    objs = eng.encode_objects(B, dg, sz, partition=np.arange(n_obj, dtype=np.int32), lower=5, upper=6)
+    off = np.zeros(n_obj + 1, np.int64)
+    off[1:] = np.cumsum([len(o) for o in objs])
+    blob = torch.from_numpy(np.frombuffer(b"".join(objs), dtype=np.uint8).copy()).to(dev)
+    doff = torch.from_numpy(off).to(dev)
+    o = [torch.zeros(n_obj, dtype=torch.int32, device=dev), torch.zeros(n_obj, dtype=torch.int64, device=dev),
+         torch.zeros(n_obj, dtype=torch.int64, device=dev), torch.zeros(n_obj * cap, dtype=torch.int64, device=dev),
+         torch.zeros(n_obj * cap, dtype=torch.int32, device=dev), torch.zeros(n_obj, dtype=torch.uint8, device=dev),
+         torch.zeros(n_obj, dtype=torch.int32, device=dev), torch.zeros(n_obj, dtype=torch.int32, device=dev)]
+    vp = lambda t: C.c_void_p(t.data_ptr())
+
+    def call():
+        rc = eng.lib.mde_decode_epoch_tree_objects_async(eng.ctx, n_obj, vp(blob), vp(doff), cap, *(vp(t) for t in o))
+        assert rc == 0, rc
+
+    us = timeit(call, reps=50, warm=5)
+    torch.cuda.synchronize()
+    assert (o[7].cpu().numpy() == B).all()
+    got = o[3].cpu().numpy().view(np.uint64).reshape(n_obj, cap)[:, :B]
+    assert (got == dg.reshape(n_obj, B)).all()
+    r = {"decode": True, "objects": n_obj, "buckets": B, "cap": cap, "bytes": int(off[-1]), "device_us_per_call": round(us, 2)}
+    print(json.dumps(r), flush=True)
+    return r
+
+
 def main():
     import torch
     import mydatastore_amd as mde
@@ -177,6 +212,8 @@ def main():
     if "verify" in what:
         out["verify"] = [bench_verify(eng, P=p, mode=m) for p in (1, 64, 1024, 8192) for m in (0, 1)]
         out["verify"] += [bench_verify(eng, P=p, B=1000, mode=m) for p in (1, 64) for m in (0, 1)]
+    if "decode" in what:
+        out["decode"] = [bench_decode(eng, n, B, cap) for n in (1, 1024) for B, cap in ((64, 64), (1000, 1024))]
     for w in what:
         if w.startswith("ab:"):
             out["ab"] = bench_ab(eng, [int(x) for x in w.split(":")[1].split(",")])
