@@ -24,8 +24,10 @@
  *  - Plain pointers and sizes only. `*_async` entry points take DEVICE pointers and enqueue on the
  *    context's stream (mde_set_stream); the others take HOST pointers and are synchronous.
  *  - Return 0 (MDE_OK) or a negative MDE_E_* code; never abort or throw across the ABI. The Go
- *    shim maps codes to errors.Errorf. mde_last_error(ctx) gives the message for the calling
- *    context (one context per calling thread, or share one: every entry point locks the context).
+ *    shim maps codes to errors.Errorf. Every entry point locks its context, so one context may be
+ *    shared by many threads. The message of the last failed call on a context: mde_last_error_copy
+ *    (copied under the context lock -- use it when the context is shared), or mde_last_error (a
+ *    pointer into the context, valid until the next call on it: single-threaded use only).
  *  - Host input buffers are read only during the call and never retained (cgo pointer rules).
  *    Outputs are caller-allocated.
  */
@@ -94,6 +96,11 @@ const char* mde_strerror(int code);
 int mde_create(int device, mde_ctx** out);
 void mde_destroy(mde_ctx* ctx);
 const char* mde_last_error(mde_ctx* ctx);
+/* Copy the last error message of ctx into buf (at most cap-1 bytes + NUL) under the context
+ * lock; returns the message's full length. Safe while other threads use the context. To pair a
+ * failed call with its own message on a shared context, the caller serialises call + copy (the
+ * Go shim holds a mutex across both: calls on one context are serialised by its lock anyway). */
+uint64_t mde_last_error_copy(mde_ctx* ctx, char* buf, uint64_t cap);
 /* Launch stream for *_async calls and internal copies. A new context uses its own stream (a
  * blocking stream: ordered after work on the null stream). NULL selects the null stream, which
  * is torch's default stream. */
@@ -276,6 +283,8 @@ void mde_group_destroy(mde_group* group);
 uint32_t mde_group_size(const mde_group* group);
 mde_ctx* mde_group_ctx(mde_group* group, uint32_t i);
 const char* mde_group_last_error(const mde_group* group);
+/* mde_last_error_copy for a group (its multi-build calls are serialised by a group lock). */
+uint64_t mde_group_last_error_copy(mde_group* group, char* buf, uint64_t cap);
 /* RawPartitionMerkleTree for P partitions over the group (host pointers, synchronous); same
  * contract as mde_build. */
 int mde_multi_build(mde_group* group, const mde_records* rec, const mde_tree_out* out);

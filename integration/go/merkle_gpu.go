@@ -31,7 +31,24 @@ var (
 	mdeOnce sync.Once
 	mdeCtx  *C.mde_ctx
 	mdeErr  error
+	// VerifyEpoch runs on a pool of worker goroutines (main/manager.go:166-170,491) that share
+	// mdeCtx. mdeMu pairs each call with its own error message; it costs no concurrency, since
+	// the context lock serialises calls on one context anyway.
+	mdeMu sync.Mutex
 )
+
+// mdeCall runs one engine call and, when it fails, returns ITS message (copied under the context
+// lock by mde_last_error_copy while mdeMu is still held).
+func mdeCall(ctx *C.mde_ctx, name string, call func() C.int) error {
+	mdeMu.Lock()
+	defer mdeMu.Unlock()
+	if rc := call(); rc != C.MDE_OK {
+		var buf [512]C.char
+		C.mde_last_error_copy(ctx, &buf[0], C.uint64_t(len(buf)))
+		return errors.Errorf("%s: %s", name, C.GoString(&buf[0]))
+	}
+	return nil
+}
 
 func mdeEngine() (*C.mde_ctx, error) {
 	mdeOnce.Do(func() {
@@ -99,8 +116,8 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 	}
 	out := C.mde_tree_out{digest: (*C.uint64_t)(cDigest), size: (*C.int32_t)(cSize),
 		items: (*C.int32_t)(cItems), root: (*C.uint8_t)(cRoot)}
-	if rc := C.mde_build(ctx, &rec, &out); rc != C.MDE_OK {
-		return nil, errors.Errorf("mde_build: %s", C.GoString(C.mde_last_error(ctx)))
+	if err := mdeCall(ctx, "mde_build", func() C.int { return C.mde_build(ctx, &rec, &out) }); err != nil {
+		return nil, err
 	}
 	digest := unsafe.Slice((*uint64)(cDigest), B)
 	size := unsafe.Slice((*int32)(cSize), B)
@@ -157,9 +174,11 @@ func DifferentMerkleTreeBuckets(tree1 *merkletree.MerkleTree, tree2 *merkletree.
 	cCount := C.malloc(4)
 	defer C.free(cIds)
 	defer C.free(cCount)
-	if rc := C.mde_diff_digests(ctx, 1, C.uint32_t(len(d1)), (*C.uint64_t)(cA), C.uint32_t(len(d2)),
-		(*C.uint64_t)(cB), (*C.int32_t)(cIds), capIds, (*C.int32_t)(cCount)); rc != C.MDE_OK {
-		return nil, errors.Errorf("mde_diff: %s", C.GoString(C.mde_last_error(ctx)))
+	if err := mdeCall(ctx, "mde_diff", func() C.int {
+		return C.mde_diff_digests(ctx, 1, C.uint32_t(len(d1)), (*C.uint64_t)(cA), C.uint32_t(len(d2)),
+			(*C.uint64_t)(cB), (*C.int32_t)(cIds), capIds, (*C.int32_t)(cCount))
+	}); err != nil {
+		return nil, err
 	}
 	n := *(*int32)(cCount)
 	if n == C.MDE_E_TREE {
@@ -208,9 +227,11 @@ func verifyEpochDecision(myTree *merkletree.MerkleTree, partitionId int, epoch i
 	cRoot := C.malloc(32)
 	defer C.free(cNodes)
 	defer C.free(cRoot)
-	if rc := C.mde_tree_from_digests(ctx, 1, C.uint32_t(B), (*C.uint64_t)(cDigest), (*C.uint8_t)(cRoot),
-		(*C.uint8_t)(cNodes)); rc != C.MDE_OK {
-		return false, 0, nil, nil, errors.Errorf("mde_tree_from_digests: %s", C.GoString(C.mde_last_error(ctx)))
+	if err := mdeCall(ctx, "mde_tree_from_digests", func() C.int {
+		return C.mde_tree_from_digests(ctx, 1, C.uint32_t(B), (*C.uint64_t)(cDigest), (*C.uint8_t)(cRoot),
+			(*C.uint8_t)(cNodes))
+	}); err != nil {
+		return false, 0, nil, nil, err
 	}
 	// peer objects back to wire bytes (gRPC already unmarshalled them); a nil object is absent
 	R := len(epochTreeObjects)
@@ -242,12 +263,14 @@ func verifyEpochDecision(myTree *merkletree.MerkleTree, partitionId int, epoch i
 	defer C.free(cOut)
 	part := C.int32_t(partitionId)
 	outs := unsafe.Slice((*int32)(cOut), 4)
-	if rc := C.mde_verify_epochs(ctx, 1, C.uint32_t(B), &part, C.int64_t(epoch), (*C.uint64_t)(cDigest),
-		(*C.int32_t)(cSize), (*C.uint8_t)(cNodes), C.uint32_t(R), (*C.uint8_t)(cBlob), (*C.uint64_t)(cOff),
-		C.uint32_t(replicaCount), (*C.uint8_t)(unsafe.Pointer(&outs[0])), (*C.int32_t)(unsafe.Pointer(&outs[1])),
-		(*C.int32_t)(cIds), (*C.int32_t)(unsafe.Pointer(&outs[2])), (*C.int32_t)(cStatus), (*C.uint8_t)(cObj),
-		stride, (*C.uint32_t)(unsafe.Pointer(&outs[3]))); rc != C.MDE_OK {
-		return false, 0, nil, nil, errors.Errorf("mde_verify_epochs: %s", C.GoString(C.mde_last_error(ctx)))
+	if err := mdeCall(ctx, "mde_verify_epochs", func() C.int {
+		return C.mde_verify_epochs(ctx, 1, C.uint32_t(B), &part, C.int64_t(epoch), (*C.uint64_t)(cDigest),
+			(*C.int32_t)(cSize), (*C.uint8_t)(cNodes), C.uint32_t(R), (*C.uint8_t)(cBlob), (*C.uint64_t)(cOff),
+			C.uint32_t(replicaCount), (*C.uint8_t)(unsafe.Pointer(&outs[0])), (*C.int32_t)(unsafe.Pointer(&outs[1])),
+			(*C.int32_t)(cIds), (*C.int32_t)(unsafe.Pointer(&outs[2])), (*C.int32_t)(cStatus), (*C.uint8_t)(cObj),
+			stride, (*C.uint32_t)(unsafe.Pointer(&outs[3])))
+	}); err != nil {
+		return false, 0, nil, nil, err
 	}
 	valid := *(*uint8)(unsafe.Pointer(&outs[0])) != 0
 	diffSet := make([]int32, outs[2])

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import threading
 from pathlib import Path
 
 import numpy as np
@@ -30,6 +31,7 @@ LAYOUT_TAGGED = 1  # layout B: grouped by partition, per-record bucket tags
 # Every symbol include/mde.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
     "mde_abi_version", "mde_strerror", "mde_create", "mde_destroy", "mde_last_error",
+    "mde_last_error_copy", "mde_group_last_error_copy",
     "mde_set_stream", "mde_use_own_stream", "mde_set_tuning", "mde_set_verify_mode", "mde_get_stream", "mde_synchronize", "mde_device_info", "mde_tree_depth",
     "mde_tree_internal_nodes", "mde_diff_capacity", "mde_build", "mde_build_async",
     "mde_build_streamed",
@@ -94,6 +96,7 @@ def load_library() -> C.CDLL:
         "mde_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
         "mde_destroy": (None, [vp]),
         "mde_last_error": (C.c_char_p, [vp]),
+        "mde_last_error_copy": (C.c_uint64, [vp, C.c_char_p, C.c_uint64]),
         "mde_set_stream": (C.c_int, [vp, vp]),
         "mde_use_own_stream": (C.c_int, [vp]),
         "mde_set_tuning": (C.c_int, [vp, C.c_int, C.c_int, C.c_int]),
@@ -136,6 +139,7 @@ def load_library() -> C.CDLL:
         "mde_group_size": (u32, [vp]),
         "mde_group_ctx": (vp, [vp, u32]),
         "mde_group_last_error": (C.c_char_p, [vp]),
+        "mde_group_last_error_copy": (C.c_uint64, [vp, C.c_char_p, C.c_uint64]),
         "mde_multi_build": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
         "mde_multi_build_streamed": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), C.c_uint64]),
         "mde_synth_tags_async": (C.c_int, [vp, vp, u64, u32, u32, C.c_int, u64, vp, vp]),
@@ -191,6 +195,7 @@ class Engine:
     methods take device tensors and enqueue on the context stream (see :meth:`set_stream`)."""
 
     def __init__(self, device: int = 0):
+        self._mu = threading.Lock()
         self.lib = load_library()
         h = C.c_void_p()
         rc = self.lib.mde_create(device, C.byref(h))
@@ -211,33 +216,40 @@ class Engine:
         except Exception:
             pass
 
-    def _check(self, rc: int):
-        if rc != MDE_OK:
-            msg = self.lib.mde_last_error(self.ctx)
-            raise MdeError(rc, (msg or b"").decode() or self.lib.mde_strerror(rc).decode())
+    def _call(self, name: str, *args):
+        """Call entry point `name` on this context and raise MdeError with ITS message: the call
+        and the message copy are one critical section, so threads sharing the Engine cannot
+        swap messages (the context lock serialises the calls anyway)."""
+        with self._mu:
+            rc = getattr(self.lib, name)(self.ctx, *args)
+            if rc == MDE_OK:
+                return
+            buf = C.create_string_buffer(512)
+            self.lib.mde_last_error_copy(self.ctx, buf, len(buf))
+        raise MdeError(rc, buf.value.decode(errors="replace") or self.lib.mde_strerror(rc).decode())
 
     # -- context ------------------------------------------------------------------------------
     def set_stream(self, stream_handle: int):
         """Launch on a HIP stream handle (0 = the null stream = torch's default stream)."""
-        self._check(self.lib.mde_set_stream(self.ctx, C.c_void_p(int(stream_handle))))
+        self._call("mde_set_stream", C.c_void_p(int(stream_handle)))
 
     def set_tuning(self, digest_variant: int = -1, digest_blocks_per_cu: int = -1, digest_oversub: int = -1):
-        self._check(self.lib.mde_set_tuning(self.ctx, digest_variant, digest_blocks_per_cu, digest_oversub))
+        self._call("mde_set_tuning", digest_variant, digest_blocks_per_cu, digest_oversub)
 
     def set_verify_mode(self, mode: int):
         """0 = fused one-launch verify when it fits (default), 1 = the five-launch chain."""
-        self._check(self.lib.mde_set_verify_mode(self.ctx, mode))
+        self._call("mde_set_verify_mode", mode)
 
     def use_own_stream(self):
-        self._check(self.lib.mde_use_own_stream(self.ctx))
+        self._call("mde_use_own_stream")
 
     def synchronize(self):
-        self._check(self.lib.mde_synchronize(self.ctx))
+        self._call("mde_synchronize")
 
     def device_info(self):
         cus = C.c_int()
         arch = C.create_string_buffer(64)
-        self._check(self.lib.mde_device_info(self.ctx, C.byref(cus), arch, 64))
+        self._call("mde_device_info", C.byref(cus), arch, 64)
         return cus.value, arch.value.decode()
 
     # -- build --------------------------------------------------------------------------------
@@ -269,7 +281,7 @@ class Engine:
             "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
         }
         to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
-        self._check(self.lib.mde_build(self.ctx, C.byref(rec), C.byref(to)))
+        self._call("mde_build", C.byref(rec), C.byref(to))
         return out
 
     def build_streamed(self, values, seg_rec, n_partitions, n_buckets, value_stride=0,
@@ -296,7 +308,7 @@ class Engine:
             "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
         }
         to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
-        self._check(self.lib.mde_build_streamed(self.ctx, C.byref(rec), C.byref(to), chunk_bytes))
+        self._call("mde_build_streamed", C.byref(rec), C.byref(to), chunk_bytes)
         return out
 
     def build_tagged(self, values: np.ndarray, part_rec: np.ndarray, bucket_tag: np.ndarray,
@@ -314,25 +326,25 @@ class Engine:
             "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
         }
         to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
-        self._check(self.lib.mde_build(self.ctx, C.byref(rec), C.byref(to)))
+        self._call("mde_build", C.byref(rec), C.byref(to))
         return out
 
     def build_async(self, rec: Records, out: TreeOut):
-        self._check(self.lib.mde_build_async(self.ctx, C.byref(rec), C.byref(out)))
+        self._call("mde_build_async", C.byref(rec), C.byref(out))
 
     def digest_async(self, rec: Records):
-        self._check(self.lib.mde_digest_async(self.ctx, C.byref(rec)))
+        self._call("mde_digest_async", C.byref(rec))
 
     def tree_async(self, rec: Records, out: TreeOut):
-        self._check(self.lib.mde_tree_async(self.ctx, C.byref(rec), C.byref(out)))
+        self._call("mde_tree_async", C.byref(rec), C.byref(out))
 
     def build_pipelined_async(self, rec: Records, out: TreeOut):
         """One software-pipelined build (mde_build_pipelined_async): this call's digest and the
         previous call's trees in one launch; `out` is complete after the next call or a drain."""
-        self._check(self.lib.mde_build_pipelined_async(self.ctx, C.byref(rec), C.byref(out)))
+        self._call("mde_build_pipelined_async", C.byref(rec), C.byref(out))
 
     def build_pipeline_drain_async(self):
-        self._check(self.lib.mde_build_pipeline_drain_async(self.ctx))
+        self._call("mde_build_pipeline_drain_async")
 
     # -- tree from digests (EpochTreeObjectToMerkleTree) --------------------------------------
     def tree_from_digests(self, digests: np.ndarray, n_buckets: int, want_nodes=True):
@@ -340,13 +352,13 @@ class Engine:
         T = d.size // n_buckets
         root = np.zeros(T * 32, np.uint8)
         nodes = np.zeros(T * tree_internal_nodes(n_buckets) * 32, np.uint8) if want_nodes else None
-        self._check(self.lib.mde_tree_from_digests(self.ctx, T, n_buckets, _ptr(d), _ptr(root),
-                                                   _ptr(nodes)))
+        self._call("mde_tree_from_digests", T, n_buckets, _ptr(d), _ptr(root),
+                                                   _ptr(nodes))
         return root, nodes
 
     def tree_from_digests_async(self, n_trees, n_buckets, digest, root, nodes=None):
-        self._check(self.lib.mde_tree_from_digests_async(self.ctx, n_trees, n_buckets, _ptr(digest),
-                                                         _ptr(root), _ptr(nodes)))
+        self._call("mde_tree_from_digests_async", n_trees, n_buckets, _ptr(digest),
+                                                         _ptr(root), _ptr(nodes))
 
     # -- diff (DifferentMerkleTreeBuckets) ----------------------------------------------------
     def diff(self, ba: int, da: np.ndarray, na: np.ndarray, bb: int, db: np.ndarray,
@@ -357,8 +369,8 @@ class Engine:
         cnt = np.zeros(n_pairs, np.int32)
         da, db = (np.ascontiguousarray(x, dtype=np.uint64) for x in (da, db))
         na, nb = (np.ascontiguousarray(x, dtype=np.uint8) for x in (na, nb))
-        self._check(self.lib.mde_diff(self.ctx, n_pairs, ba, _ptr(da), _ptr(na), bb, _ptr(db),
-                                      _ptr(nb), _ptr(ids), cap, _ptr(cnt)))
+        self._call("mde_diff", n_pairs, ba, _ptr(da), _ptr(na), bb, _ptr(db),
+                                      _ptr(nb), _ptr(ids), cap, _ptr(cnt))
         res = []
         for i in range(n_pairs):
             c = int(cnt[i])
@@ -371,13 +383,13 @@ class Engine:
         ids = np.zeros(n_pairs * cap, np.int32)
         cnt = np.zeros(n_pairs, np.int32)
         da, db = (np.ascontiguousarray(x, dtype=np.uint64) for x in (da, db))
-        self._check(self.lib.mde_diff_digests(self.ctx, n_pairs, ba, _ptr(da), bb, _ptr(db),
-                                              _ptr(ids), cap, _ptr(cnt)))
+        self._call("mde_diff_digests", n_pairs, ba, _ptr(da), bb, _ptr(db),
+                                              _ptr(ids), cap, _ptr(cnt))
         return [int(c) if c < 0 else ids[i * cap:i * cap + int(c)].tolist() for i, c in enumerate(cnt)]
 
     def diff_async(self, n_pairs, ba, da, na, bb, db, nb, out_ids, out_stride, out_count):
-        self._check(self.lib.mde_diff_async(self.ctx, n_pairs, ba, _ptr(da), _ptr(na), bb, _ptr(db),
-                                            _ptr(nb), _ptr(out_ids), out_stride, _ptr(out_count)))
+        self._call("mde_diff_async", n_pairs, ba, _ptr(da), _ptr(na), bb, _ptr(db),
+                                            _ptr(nb), _ptr(out_ids), out_stride, _ptr(out_count))
 
     # -- out-of-sync range extract (StreamBucketsTask) ----------------------------------------
     def extract(self, values, seg_rec, n_partitions, n_buckets, ids, ids_stride, counts,
@@ -407,9 +419,9 @@ class Engine:
         out_rec = np.zeros(rec_cap, np.uint64)
         out_vals = np.zeros(bytes_cap, np.uint8) if want_values else None
         out_voff = np.zeros(rec_cap + 1, np.uint64) if want_values else None
-        self._check(self.lib.mde_extract(self.ctx, C.byref(rec), _ptr(ids), ids_stride, _ptr(counts),
+        self._call("mde_extract", C.byref(rec), _ptr(ids), ids_stride, _ptr(counts),
                                          _ptr(part_off), _ptr(out_rec), rec_cap, _ptr(out_vals),
-                                         _ptr(out_voff), bytes_cap))
+                                         _ptr(out_voff), bytes_cap)
         n = int(part_off[-1])
         if not want_values:
             return part_off, out_rec[:n], None, None
@@ -417,10 +429,10 @@ class Engine:
 
     def extract_async(self, rec: Records, ids, ids_stride, counts, part_off, out_rec, rec_cap,
                       out_values, out_value_off, bytes_cap, status):
-        self._check(self.lib.mde_extract_async(self.ctx, C.byref(rec), _ptr(ids), ids_stride,
+        self._call("mde_extract_async", C.byref(rec), _ptr(ids), ids_stride,
                                                _ptr(counts), _ptr(part_off), _ptr(out_rec), rec_cap,
                                                _ptr(out_values), _ptr(out_value_off), bytes_cap,
-                                               _ptr(status)))
+                                               _ptr(status))
 
     # -- EpochTreeObject wire bytes -----------------------------------------------------------
     def encode_objects(self, n_buckets, digest, size, partition=None, lower=0, upper=0, valid=None,
@@ -437,9 +449,9 @@ class Engine:
         part = None if partition is None else np.ascontiguousarray(partition, dtype=np.int32)
         val = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
         it = None if items is None else np.ascontiguousarray(items, dtype=np.int32)
-        self._check(self.lib.mde_encode_epoch_tree_objects(self.ctx, n, B, _ptr(part), lower, upper,
+        self._call("mde_encode_epoch_tree_objects", n, B, _ptr(part), lower, upper,
                                                            _ptr(digest), _ptr(size), _ptr(val), _ptr(it),
-                                                           _ptr(out), stride, _ptr(ln)))
+                                                           _ptr(out), stride, _ptr(ln))
         return [out[i * stride:i * stride + int(ln[i])].tobytes() for i in range(n)]
 
     def decode_objects(self, objs, cap):
@@ -452,9 +464,9 @@ class Engine:
              "upper": np.zeros(n, np.int64), "digest": np.zeros(n * cap, np.uint64),
              "size": np.zeros(n * cap, np.int32), "valid": np.zeros(n, np.uint8),
              "items": np.zeros(n, np.int32), "n_buckets": np.zeros(n, np.int32)}
-        self._check(self.lib.mde_decode_epoch_tree_objects(
-            self.ctx, n, _ptr(blob), _ptr(off), cap, *(_ptr(o[k]) for k in (
-                "partition", "lower", "upper", "digest", "size", "valid", "items", "n_buckets"))))
+        self._call("mde_decode_epoch_tree_objects",
+            n, _ptr(blob), _ptr(off), cap, *(_ptr(o[k]) for k in (
+                "partition", "lower", "upper", "digest", "size", "valid", "items", "n_buckets")))
         res = []
         for i in range(n):
             nb = int(o["n_buckets"][i])
@@ -497,10 +509,10 @@ class Engine:
         stride = int(self.lib.mde_epoch_tree_object_max_bytes(B)) if want_objects else 0
         objs = np.zeros(max(P * stride, 1), np.uint8) if want_objects else None
         olen = np.zeros(P, np.uint32) if want_objects else None
-        self._check(self.lib.mde_verify_epochs(
-            self.ctx, P, B, _ptr(part), epoch, _ptr(digest), _ptr(size), _ptr(nodes), R, _ptr(blob),
+        self._call("mde_verify_epochs",
+            P, B, _ptr(part), epoch, _ptr(digest), _ptr(size), _ptr(nodes), R, _ptr(blob),
             _ptr(off), replica_count, _ptr(valid), _ptr(vcount), _ptr(ids), _ptr(dcount),
-            _ptr(status), _ptr(objs), stride, _ptr(olen)))
+            _ptr(status), _ptr(objs), stride, _ptr(olen))
         return {
             "valid": [bool(v) for v in valid], "valid_count": vcount.tolist(),
             "diff": [ids[p * B:p * B + int(dcount[p])].tolist() for p in range(P)],
@@ -513,11 +525,11 @@ class Engine:
                             n_peers, peer_bytes, peer_off, replica_count, valid, valid_count,
                             diff_ids, diff_count, peer_status=None, object_out=None,
                             object_stride=0, object_len=None):
-        self._check(self.lib.mde_verify_epochs_async(
-            self.ctx, n_partitions, n_buckets, _ptr(partition), epoch, _ptr(digest), _ptr(size),
+        self._call("mde_verify_epochs_async",
+            n_partitions, n_buckets, _ptr(partition), epoch, _ptr(digest), _ptr(size),
             _ptr(nodes), n_peers, _ptr(peer_bytes), _ptr(peer_off), replica_count, _ptr(valid),
             _ptr(valid_count), _ptr(diff_ids), _ptr(diff_count), _ptr(peer_status),
-            _ptr(object_out), object_stride, _ptr(object_len)))
+            _ptr(object_out), object_stride, _ptr(object_len))
 
     # -- tagging / synthetic workload ---------------------------------------------------------
     def tag_keys(self, keys, n_buckets: int, n_partitions: int):
@@ -527,21 +539,21 @@ class Engine:
         blob = np.frombuffer(b"".join(keys) or b"\0", dtype=np.uint8).copy()
         bk = np.zeros(len(keys), np.uint32)
         pt = np.zeros(len(keys), np.uint32)
-        self._check(self.lib.mde_tag_keys(self.ctx, _ptr(blob), _ptr(offs), len(keys), n_buckets,
-                                          n_partitions, _ptr(bk), _ptr(pt)))
+        self._call("mde_tag_keys", _ptr(blob), _ptr(offs), len(keys), n_buckets,
+                                          n_partitions, _ptr(bk), _ptr(pt))
         return bk, pt
 
     def tag_keys_async(self, keys, key_off, n, n_buckets, n_partitions, bucket, partition):
-        self._check(self.lib.mde_tag_keys_async(self.ctx, _ptr(keys), _ptr(key_off), n, n_buckets,
-                                                n_partitions, _ptr(bucket), _ptr(partition)))
+        self._call("mde_tag_keys_async", _ptr(keys), _ptr(key_off), n, n_buckets,
+                                                n_partitions, _ptr(bucket), _ptr(partition))
 
     def synth_tags_async(self, gids, n, n_partitions, n_buckets, part_mode, kpp, part, bucket):
-        self._check(self.lib.mde_synth_tags_async(self.ctx, _ptr(gids), n, n_partitions, n_buckets,
-                                                  part_mode, kpp, _ptr(part), _ptr(bucket)))
+        self._call("mde_synth_tags_async", _ptr(gids), n, n_partitions, n_buckets,
+                                                  part_mode, kpp, _ptr(part), _ptr(bucket))
 
     def synth_values_async(self, dst, gids, n, value_len, seed):
-        self._check(self.lib.mde_synth_values_async(self.ctx, _ptr(dst), _ptr(gids), n, value_len,
-                                                    seed))
+        self._call("mde_synth_values_async", _ptr(dst), _ptr(gids), n, value_len,
+                                                    seed)
 
 
 class Group:
@@ -599,5 +611,7 @@ class Group:
         else:
             rc = self.lib.mde_multi_build(self.g, C.byref(rec), C.byref(to))
         if rc != MDE_OK:
-            raise MdeError(rc, (self.lib.mde_group_last_error(self.g) or b"").decode())
+            buf = C.create_string_buffer(512)
+            self.lib.mde_group_last_error_copy(self.g, buf, len(buf))
+            raise MdeError(rc, buf.value.decode(errors="replace"))
         return out

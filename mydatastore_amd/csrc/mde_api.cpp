@@ -726,6 +726,23 @@ void mde_destroy(mde_ctx* c) {
 
 const char* mde_last_error(mde_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+namespace {
+uint64_t copy_message(const std::string& m, char* buf, uint64_t cap) {
+  if (buf && cap) {
+    const uint64_t n = std::min<uint64_t>(m.size(), cap - 1);
+    std::memcpy(buf, m.data(), n);
+    buf[n] = 0;
+  }
+  return m.size();
+}
+}  // namespace
+
+uint64_t mde_last_error_copy(mde_ctx* c, char* buf, uint64_t cap) {
+  if (!c) return copy_message("null context", buf, cap);
+  std::lock_guard<std::mutex> lk(c->mu);
+  return copy_message(c->err, buf, cap);
+}
+
 int mde_set_tuning(mde_ctx* c, int digest_variant, int digest_blocks_per_cu, int digest_oversub) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
@@ -1511,6 +1528,7 @@ int mde_memcpy_d2h(mde_ctx* c, void* dst, const void* src, uint64_t bytes) {
 // Device groups: one process driving G GPUs (mde_multi_build).
 struct mde_group {
   std::vector<mde_ctx*> ctx;
+  std::mutex mu;  // held by mde_multi_build[_streamed] for the whole call; guards err
   std::string err;
 };
 
@@ -1545,11 +1563,18 @@ mde_ctx* mde_group_ctx(mde_group* g, uint32_t i) { return g && i < g->ctx.size()
 
 const char* mde_group_last_error(const mde_group* g) { return g ? g->err.c_str() : "null group"; }
 
+uint64_t mde_group_last_error_copy(mde_group* g, char* buf, uint64_t cap) {
+  if (!g) return copy_message("null group", buf, cap);
+  std::lock_guard<std::mutex> lk(g->mu);
+  return copy_message(g->err, buf, cap);
+}
+
 namespace {
 // mde_multi_build / mde_multi_build_streamed: split P partitions into G contiguous blocks and
 // build each on its own device, one host thread per device (streamed: chunk_bytes ring per device).
 int multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o, bool streamed, uint64_t chunk_bytes) {
   if (!g || g->ctx.empty()) return MDE_E_INVAL;
+  std::lock_guard<std::mutex> glk(g->mu);
   g->err.clear();
   mde_ctx* c0 = g->ctx[0];
   {
@@ -1619,7 +1644,9 @@ int multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o, bool 
   for (auto& t : th) t.join();
   for (uint32_t i = 0; i < G; i++)
     if (sh[i].rc != MDE_OK) {
-      g->err = "device " + std::to_string(g->ctx[i]->device) + ": " + g->ctx[i]->err;
+      char m[512];
+      mde_last_error_copy(g->ctx[i], m, sizeof m);
+      g->err = "device " + std::to_string(g->ctx[i]->device) + ": " + m;
       return sh[i].rc;
     }
   return MDE_OK;

@@ -23,8 +23,9 @@ Engine::~Engine() {
 }
 
 Error Engine::error(int rc) const {
-  const char* m = ctx_ ? mde_last_error(ctx_) : "";
-  return std::string(mde_strerror(rc)) + (m && *m ? std::string(": ") + m : std::string());
+  char m[512] = {0};
+  if (ctx_) mde_last_error_copy(ctx_, m, sizeof m);
+  return std::string(mde_strerror(rc)) + (*m ? std::string(": ") + m : std::string());
 }
 
 // ---------------------------------------------------------------- utils/utils.go:67-89

@@ -75,3 +75,16 @@ def test_product_never_uses_oracle():
             src = p.read_text()
             assert "import oracle" not in src and "from oracle" not in src, p
             assert "liboracle" not in src or p.name == "_build.py", p
+
+
+def test_last_error_copy_truncates_and_terminates(lib):
+    """mde_last_error_copy / mde_group_last_error_copy: at most cap-1 bytes + NUL, full length
+    returned (the shared-context-safe way to read a message)."""
+    import ctypes as C
+    buf = C.create_string_buffer(b"\xff" * 8, 8)
+    assert lib.mde_last_error_copy(None, buf, 8) == len(b"null context")
+    assert buf.raw == b"null co\0"
+    assert lib.mde_last_error_copy(None, None, 0) == len(b"null context")
+    big = C.create_string_buffer(64)
+    assert lib.mde_group_last_error_copy(None, big, 64) == len(b"null group")
+    assert big.value == b"null group"

@@ -63,3 +63,38 @@ def test_shared_context_concurrent_build_and_verify(engine):
     # the verdicts themselves: one agreeing peer, one Valid peer differing in one bucket
     for root, v in got:
         assert v["valid"] == [True] and v["valid_count"] == [1] and len(v["diff"][0]) == 1
+
+
+@pytest.mark.gpu
+def test_shared_context_errors_stay_with_their_call(engine):
+    """Threads sharing one context each get the message of THEIR failed call (the binding pairs
+    the call and mde_last_error_copy in one critical section, as the Go shim's mdeCall does)."""
+    import mydatastore_amd as mde
+    values = np.zeros(64, np.uint8)
+    bad_seg = np.array([0, 5, 3, 8], np.uint64)   # decreasing -> "nondecreasing" message
+    long_seg = np.array([0, 100], np.uint64)      # 8 records only -> "exceeds n_records"
+    errors, wrong = [], []
+
+    def worker(t):
+        try:
+            for _ in range(40):
+                try:
+                    if t % 2:
+                        engine.build(values, bad_seg, 1, 3, value_stride=8)
+                    else:
+                        engine.build(values, long_seg, 1, 1, value_stride=8)
+                    wrong.append((t, "no error"))
+                except mde.MdeError as e:
+                    want = "nondecreasing" if t % 2 else "exceeds n_records"
+                    if want not in str(e):
+                        wrong.append((t, str(e)))
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=60)
+    assert not errors, errors[:3]
+    assert not wrong, wrong[:5]
