@@ -113,6 +113,12 @@ int mde_device_info(mde_ctx* ctx, int* cu_count, char* arch_name, int arch_cap);
  * oversubscription (-1 = the built-in defaults). Results are identical for every setting; only
  * speed changes. */
 int mde_set_tuning(mde_ctx* ctx, int digest_variant, int digest_blocks_per_cu, int digest_oversub);
+/* Tuning hook: layout-A digest work split. 0 = one contiguous range per resident wave; N > 0 =
+ * with the interleaved-pieces digest variant, each wave's share cut into pieces of about N bytes,
+ * interleaved across the grid so all waves sweep the arena front to back together (used when a
+ * share is at least 2N bytes); UINT64_MAX (default) = automatic: shares of 4 MiB or more are cut
+ * into 5 pieces. Results are identical for every setting. */
+int mde_set_digest_piece_bytes(mde_ctx* ctx, uint64_t piece_bytes);
 /* Launch shape of mde_verify_epochs[_async]: 0 (default) = one fused launch whenever
  * n_peers <= 64 and mde_verify_peer_capacity(n_buckets) <= 1024, else the five-launch chain;
  * 1 = always the chain. Results are identical; only latency changes. */

@@ -32,7 +32,7 @@ LAYOUT_TAGGED = 1  # layout B: grouped by partition, per-record bucket tags
 EXPORTED_SYMBOLS = (
     "mde_abi_version", "mde_strerror", "mde_create", "mde_destroy", "mde_last_error",
     "mde_last_error_copy", "mde_group_last_error_copy",
-    "mde_set_stream", "mde_use_own_stream", "mde_set_tuning", "mde_set_verify_mode", "mde_get_stream", "mde_synchronize", "mde_device_info", "mde_tree_depth",
+    "mde_set_stream", "mde_use_own_stream", "mde_set_tuning", "mde_set_digest_piece_bytes", "mde_set_verify_mode", "mde_get_stream", "mde_synchronize", "mde_device_info", "mde_tree_depth",
     "mde_tree_internal_nodes", "mde_diff_capacity", "mde_build", "mde_build_async",
     "mde_build_streamed",
     "mde_digest_async", "mde_tree_async", "mde_build_pipelined_async", "mde_build_pipeline_drain_async",
@@ -100,6 +100,7 @@ def load_library() -> C.CDLL:
         "mde_set_stream": (C.c_int, [vp, vp]),
         "mde_use_own_stream": (C.c_int, [vp]),
         "mde_set_tuning": (C.c_int, [vp, C.c_int, C.c_int, C.c_int]),
+        "mde_set_digest_piece_bytes": (C.c_int, [vp, u64]),
         "mde_set_verify_mode": (C.c_int, [vp, C.c_int]),
         "mde_get_stream": (vp, [vp]),
         "mde_synchronize": (C.c_int, [vp]),
@@ -235,6 +236,11 @@ class Engine:
 
     def set_tuning(self, digest_variant: int = -1, digest_blocks_per_cu: int = -1, digest_oversub: int = -1):
         self._call("mde_set_tuning", digest_variant, digest_blocks_per_cu, digest_oversub)
+
+    def set_digest_piece_bytes(self, piece_bytes: int = -1):
+        """Layout-A digest work split: 0 = one range per wave, N = interleaved ~N-byte pieces,
+        -1 = the built-in default."""
+        self._call("mde_set_digest_piece_bytes", (1 << 64) - 1 if piece_bytes < 0 else piece_bytes)
 
     def set_verify_mode(self, mode: int):
         """0 = fused one-launch verify when it fits (default), 1 = the five-launch chain."""

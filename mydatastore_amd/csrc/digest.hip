@@ -98,31 +98,20 @@ __device__ __forceinline__ void load_step(u32x4 (&v)[U], const u32x4* src, uint6
   }
 }
 
-// U = 16-byte loads per lane per step (step = U KiB per wave); NT = nontemporal loads;
-// PIPE = issue the next step's loads before reducing the current one (register double buffer);
-// PIPE = 2 also issues the first step's loads before the bucket search, so the wave's first HBM
-// round trip overlaps the search's dependent seg_rec loads.
-// `block` = this workgroup's index among the digest workgroups of the launch.
-template <int U, bool NT, int PIPE, int PRIO = 0>
-__device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t block) {
+// Streams the arena range [beg, end) of one wave: U = 16-byte loads per lane per step (step = U
+// KiB per wave); NT = nontemporal loads; PIPE = issue the next step's loads before reducing the
+// current one (register double buffer); PIPE = 2 also issues the first step's loads before the
+// bucket search (from bucket s_lo on), so the wave's first HBM round trip overlaps the search's
+// dependent seg_rec loads. Returns the last bucket the range touched.
+template <int U, bool NT, int PIPE>
+__device__ __forceinline__ uint32_t digest_range(const DigestLaunch& a, uint64_t beg, uint64_t end, uint32_t s_lo,
+                                                 int lane) {
   constexpr uint64_t kStep = 1024ull * U;
-  // Streaming waves issue little VALU; when tree waves (back-to-back SHA-256 VALU) share the CU,
-  // a raised priority keeps the loads flowing and the SHA waves take the slack.
-  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave = block * (kThreads / 64) + (threadIdx.x >> 6);
-  if (wave >= a.n_waves) return;
   const SegDesc& d = a.seg;
-  const uint64_t first = segpos(d, 0) & ~15ull;
-  const uint64_t last = segpos(d, d.S);
-  const uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
-  if (beg >= last) return;
-  const uint64_t end = min(beg + a.wave_bytes, last);
-
   const u32x4* lane_base = reinterpret_cast<const u32x4*>(d.base) + lane;
   u32x4 cur[U];
   if (PIPE == 2) load_step<U, NT>(cur, lane_base + (beg >> 4), beg, end, lane, beg + kStep <= end);
-  uint32_t s = seg_search(d, 0u, beg, lane);
+  uint32_t s = seg_search(d, s_lo, beg, lane);
   uint64_t sb = segpos(d, s), se = segpos(d, s + 1);
   uint32_t acc = 0;
   if (PIPE == 1) load_step<U, NT>(cur, lane_base + (beg >> 4), beg, end, lane, beg + kStep <= end);
@@ -167,6 +156,43 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
     }
   }
   flush(a.sums, s, acc);
+  return s;
+}
+
+// One contiguous range of wave_bytes per wave. `block` = this workgroup's index among the digest
+// workgroups of the launch.
+template <int U, bool NT, int PIPE, int PRIO = 0>
+__device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t block) {
+  // Streaming waves issue little VALU; when tree waves (back-to-back SHA-256 VALU) share the CU,
+  // a raised priority keeps the loads flowing and the SHA waves take the slack.
+  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = block * (kThreads / 64) + (threadIdx.x >> 6);
+  if (wave >= a.n_waves) return;
+  const SegDesc& d = a.seg;
+  const uint64_t first = segpos(d, 0) & ~15ull;
+  const uint64_t last = segpos(d, d.S);
+  const uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
+  if (beg >= last) return;
+  digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), 0u, lane);
+}
+
+// Interleaved pieces (DigestLaunch::pieces): the wave streams `pieces` ranges of wave_bytes,
+// piece_stride apart, so the whole grid sweeps the arena front to back together. Each piece is a
+// digest_range (its own bucket search, from the previous piece's last bucket on, and flush).
+template <int U, bool NT, int PIPE, int PRIO = 0>
+__device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32_t block) {
+  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = block * (kThreads / 64) + (threadIdx.x >> 6);
+  if (wave >= a.n_waves) return;
+  const SegDesc& d = a.seg;
+  const uint64_t first = segpos(d, 0) & ~15ull;
+  const uint64_t last = segpos(d, d.S);
+  uint32_t s = 0;
+  uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
+  for (uint32_t j = 0; j < a.pieces && beg < last; j++, beg += a.piece_stride)
+    s = digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), s, lane);
 }
 
 
@@ -362,10 +388,13 @@ __device__ __forceinline__ void digest_body_steal(const DigestLaunch& a, uint32_
   }
 }
 
-template <int U, bool NT, int PIPE, int PRIO = 0, bool STEAL = false>
+// MODE: 0 = one static range per wave, 1 = tail stealing, 2 = interleaved pieces.
+template <int U, bool NT, int PIPE, int PRIO = 0, int MODE = 0>
 __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a) {
-  if (STEAL)
+  if (MODE == 1)
     digest_body_steal<U, NT, PRIO>(a, blockIdx.x);
+  else if (MODE == 2)
+    digest_body_pieces<U, NT, PIPE, PRIO>(a, blockIdx.x);
   else
     digest_body<U, NT, PIPE, PRIO>(a, blockIdx.x);
 }
@@ -381,7 +410,7 @@ __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a)
 // wave per workgroup up to B = 128, the rest exit at once), so the SHA waves spread over many
 // CUs instead of crowding a few; tree workgroups come first so the dispatcher places them before
 // the streaming grid (sized to be fully resident) fills the remaining slots.
-template <int U, bool NT, int PIPE, int PRIO = 0, bool STEAL = false>
+template <int U, bool NT, int PIPE, int PRIO = 0, int MODE = 0>
 __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, TreeLaunch t, uint32_t tree_blocks,
                                                               uint32_t Q) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -401,8 +430,10 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
   }
   const uint32_t db = blockIdx.x - tree_blocks;
 #endif
-  if (STEAL)
+  if (MODE == 1)
     digest_body_steal<U, NT, PRIO>(a, db);
+  else if (MODE == 2)
+    digest_body_pieces<U, NT, PIPE, PRIO>(a, db);
   else
     digest_body<U, NT, PIPE, PRIO>(a, db);
 }
@@ -452,20 +483,21 @@ struct Variant {
   DigestKernel fn;
   StepKernel step;
   int unroll;
-  bool steal;
+  int mode;
 };
 
-#define MDE_VARIANT(U, NT, PIPE, PRIO, STEAL) \
-  { bucket_digest_kernel<U, NT, PIPE, PRIO, STEAL>, build_step_kernel<U, NT, PIPE, PRIO, STEAL>, U, STEAL }
+#define MDE_VARIANT(U, NT, PIPE, PRIO, MODE) \
+  { bucket_digest_kernel<U, NT, PIPE, PRIO, MODE>, build_step_kernel<U, NT, PIPE, PRIO, MODE>, U, MODE }
 
 // Kernel variants (tuning knob mde_set_tuning digest_variant = index; default in mde_api.cpp).
 const Variant kVariants[] = {
-    MDE_VARIANT(8, true, false, 0, false),  MDE_VARIANT(8, false, false, 0, false),
-    MDE_VARIANT(16, true, false, 0, false), MDE_VARIANT(4, true, false, 0, false),
-    MDE_VARIANT(4, true, true, 0, false),   MDE_VARIANT(8, true, true, 0, false),
-    MDE_VARIANT(16, false, false, 0, false), MDE_VARIANT(4, true, true, 2, false),
-    MDE_VARIANT(4, true, true, 3, false),   MDE_VARIANT(4, true, true, 2, true),
-    MDE_VARIANT(8, true, true, 2, true),    MDE_VARIANT(4, true, 2, 2, false),
+    MDE_VARIANT(8, true, false, 0, 0),  MDE_VARIANT(8, false, false, 0, 0),
+    MDE_VARIANT(16, true, false, 0, 0), MDE_VARIANT(4, true, false, 0, 0),
+    MDE_VARIANT(4, true, true, 0, 0),   MDE_VARIANT(8, true, true, 0, 0),
+    MDE_VARIANT(16, false, false, 0, 0), MDE_VARIANT(4, true, true, 2, 0),
+    MDE_VARIANT(4, true, true, 3, 0),   MDE_VARIANT(4, true, true, 2, 1),
+    MDE_VARIANT(8, true, true, 2, 1),    MDE_VARIANT(4, true, 2, 2, 0),
+    MDE_VARIANT(4, true, 2, 2, 2),
 };
 #undef MDE_VARIANT
 
@@ -491,7 +523,8 @@ hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t
   return hipGetLastError();
 }
 
-bool bucket_digest_steals(int v) { return variant(v).steal; }
+bool bucket_digest_steals(int v) { return variant(v).mode == 1; }
+bool bucket_digest_pieces(int v) { return variant(v).mode == 2; }
 
 void plan_steal(uint64_t wave_bytes, uint64_t* head_bytes, uint64_t* chunk_bytes, uint32_t* tail_chunks) {
   // Tail = about 1/6 of each wave range in up to 16 pieces of >= 16 KiB (the max step), at most
@@ -518,12 +551,28 @@ int bucket_digest_blocks_per_cu(int v, int cap) {
 
 // One contiguous range per resident wave: every wave of the grid is co-resident and all ranges
 // are equal, so the launch has no tail of late waves.
-void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, int oversub, uint64_t* wave_bytes,
-                        uint32_t* n_waves) {
+void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, int oversub, uint64_t piece_bytes,
+                        uint64_t* wave_bytes, uint32_t* n_waves, uint32_t* pieces) {
   const uint64_t target_waves = (uint64_t)(cus > 0 ? cus : 256) *
                                 (uint64_t)(blocks_per_cu > 0 ? blocks_per_cu : 4) * (kThreads / 64) *
                                 (uint64_t)(oversub > 0 ? oversub : 1);
   uint64_t wb = (bytes + target_waves - 1) / target_waves;
+  *pieces = 1;
+  if (piece_bytes && oversub <= 1 && wb >= 2 * piece_bytes) {
+    // Interleaved pieces: every resident wave takes k pieces of ~piece_bytes, piece j of wave w at
+    // (j * n_waves + w) * wave_bytes, so the whole grid sweeps the arena front to back together.
+    // Pieces are 1 KiB multiples (one wave-instruction), so the largest share exceeds the mean by
+    // at most k KiB; each piece switch costs one bucket search and one flush.
+    const uint64_t k = (wb + piece_bytes / 2) / piece_bytes;
+    uint64_t c = (bytes + 16 + target_waves * k - 1) / (target_waves * k);
+    c = (c + 1023) / 1024 * 1024;
+    if (c <= kMaxWaveBytes) {
+      *wave_bytes = c;
+      *n_waves = (uint32_t)target_waves;
+      *pieces = (uint32_t)k;
+      return;
+    }
+  }
   if (wb > kMaxStepBytes) {
     wb = (wb + kMaxStepBytes - 1) / kMaxStepBytes * kMaxStepBytes;
     if (wb < 2 * kMaxStepBytes) wb = 2 * kMaxStepBytes;

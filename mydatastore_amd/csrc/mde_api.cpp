@@ -27,6 +27,15 @@ constexpr int kDefaultDigestVariant = 11;  // U=4 nontemporal, register-prefetch
 constexpr int kStaticDigestVariant = 11;  // used when a stealing variant cannot steal
 constexpr int kDefaultDigestCap = 2;      // 2 workgroups (8 waves) per CU
 constexpr int kDefaultDigestOversub = 1;  // grid = resident slots x oversub
+// Interleaved pieces (digest variant 12): by default a wave whose share of
+// the arena is at least kAutoPieceMinShare streams it as kAutoPieces interleaved pieces, so the
+// grid sweeps the arena front to back together (same-box A/B, profiles/r02g_pieces_*.jsonl: C4
+// fused +1.0 %, C3 +3.6 %; the N=8 shard, 0.6 MB per wave, loses 2-10 % to the per-piece search
+// and pipeline drain, so small shares keep one range).
+constexpr uint64_t kAutoPieceBytes = UINT64_MAX;  // digest_piece_bytes value: the policy above
+constexpr uint64_t kAutoPieceMinShare = 4ull << 20;
+constexpr uint64_t kAutoPieces = 5;
+constexpr int kPiecesDigestVariant = 12;
 
 struct mde_ctx {
   int device = 0;
@@ -35,6 +44,7 @@ struct mde_ctx {
   int digest_variant = kDefaultDigestVariant;
   int digest_cap = kDefaultDigestCap;
   int digest_oversub = kDefaultDigestOversub;
+  uint64_t digest_piece_bytes = kAutoPieceBytes;
   char arch[64] = {0};
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
@@ -326,11 +336,27 @@ mde::SegDesc seg_desc(const mde_records* r) {
 }
 
 int plan_digest(mde_ctx* c, uint64_t bytes, mde::DigestLaunch* a) {
-  mde::plan_bucket_digest(bytes, c->cus, c->digest_blocks_per_cu, c->digest_oversub, &a->wave_bytes,
-                          &a->n_waves);
+  uint64_t piece_bytes = 0;
+  if (c->digest_piece_bytes == kAutoPieceBytes) {
+    if (a->variant == kDefaultDigestVariant || mde::bucket_digest_pieces(a->variant)) {
+      const uint64_t waves = (uint64_t)c->cus * (uint64_t)(c->digest_blocks_per_cu > 0 ? c->digest_blocks_per_cu : 4) * 4u *
+                             (uint64_t)(c->digest_oversub > 0 ? c->digest_oversub : 1);
+      const uint64_t share = bytes / waves;
+      if (c->digest_oversub <= 1 && share >= kAutoPieceMinShare) {
+        piece_bytes = share / kAutoPieces;
+        a->variant = kPiecesDigestVariant;
+      }
+    }
+  } else if (mde::bucket_digest_pieces(a->variant)) {
+    piece_bytes = c->digest_piece_bytes;
+  }
+  const bool steals = mde::bucket_digest_steals(a->variant);
+  mde::plan_bucket_digest(bytes, c->cus, c->digest_blocks_per_cu, c->digest_oversub, piece_bytes,
+                          &a->wave_bytes, &a->n_waves, &a->pieces);
+  a->piece_stride = (uint64_t)a->n_waves * a->wave_bytes;
   a->lds_bytes = c->digest_oversub > 1 ? (uint32_t)((160u * 1024u) / (uint32_t)c->digest_blocks_per_cu) & ~255u : 0u;
   // Tail stealing needs fixed-length values and a split range; otherwise the static sibling.
-  if (mde::bucket_digest_steals(a->variant)) {
+  if (steals) {
     mde::plan_steal(a->wave_bytes, &a->head_bytes, &a->chunk_bytes, &a->tail_chunks);
     if (!a->seg.stride || !a->tail_chunks) {
       a->variant = kStaticDigestVariant;
@@ -752,6 +778,13 @@ int mde_set_tuning(mde_ctx* c, int digest_variant, int digest_blocks_per_cu, int
   c->digest_cap = digest_blocks_per_cu < 0 ? kDefaultDigestCap : digest_blocks_per_cu;
   c->digest_oversub = digest_oversub < 0 ? kDefaultDigestOversub : (digest_oversub ? digest_oversub : 1);
   c->digest_blocks_per_cu = 0;  // re-query
+  return MDE_OK;
+}
+
+int mde_set_digest_piece_bytes(mde_ctx* c, uint64_t piece_bytes) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  c->digest_piece_bytes = piece_bytes;  // UINT64_MAX = kAutoPieceBytes
   return MDE_OK;
 }
 

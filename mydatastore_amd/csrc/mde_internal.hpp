@@ -47,14 +47,22 @@ struct DigestLaunch {
   uint64_t head_bytes;        // bytes of each wave range its owner streams
   uint64_t chunk_bytes;       // tail piece size (multiple of the 16 KiB max step)
   uint32_t tail_chunks;       // tail pieces per wave
+  // Interleaved pieces (static variants): wave w streams `pieces` ranges of wave_bytes each,
+  // [first + (j * n_waves + w) * wave_bytes, +wave_bytes) for j < pieces; piece_stride =
+  // n_waves * wave_bytes. pieces = 1 is one contiguous range per wave.
+  uint32_t pieces;
+  uint64_t piece_stride;
 };
 hipError_t launch_bucket_digest(const DigestLaunch& a, hipStream_t st);
 // Waves and wave range for an arena of `bytes` on a device with `cus` CUs.
-void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, int oversub, uint64_t* wave_bytes,
-                        uint32_t* n_waves);
+// piece_bytes > 0 cuts each resident wave's share into pieces of about that size, interleaved
+// across the grid (DigestLaunch::pieces); 0 keeps one contiguous range per wave.
+void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, int oversub, uint64_t piece_bytes,
+                        uint64_t* wave_bytes, uint32_t* n_waves, uint32_t* pieces);
 int bucket_digest_blocks_per_cu(int variant, int cap);
 int bucket_digest_variants();
 bool bucket_digest_steals(int variant);
+bool bucket_digest_pieces(int variant);  // interleaved-pieces variant (DigestLaunch::pieces)
 constexpr uint64_t kStealScratchBytes = 512;
 // Head / tail split of each wave range for tail stealing (tail_chunks = 0: no split).
 void plan_steal(uint64_t wave_bytes, uint64_t* head_bytes, uint64_t* chunk_bytes, uint32_t* tail_chunks);

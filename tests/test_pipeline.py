@@ -239,3 +239,108 @@ def test_stealing_skewed_arena_matches_torch_sums(engine):
                 assert torch.equal(o["root"].cpu(), roots["r"]), (v, rep)
     finally:
         engine.set_tuning(-1, -1)
+
+
+PIECES_VARIANT = 12  # digest.hip kVariants: U = 4, nontemporal, prefetched, interleaved pieces
+
+
+def _skewed_arena(dev, variable, seed=11):
+    """Ragged layout-A arena of ~100-300 MB for the digest work split: empty buckets and an empty
+    partition, a few buckets of tens of MB, the arena start 5 bytes past an allocation. Fixed
+    13-byte records (never 16-byte aligned) or variable lengths 0..40 (value_off). Returns the
+    Records, the per-bucket record counts and the expected digests (torch byte sums mod 999999)."""
+    import torch
+    import mydatastore_amd as mde
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    P, B = 37, 100
+    counts = torch.randint(0, 8_000, (P * B,), generator=g)
+    counts[torch.randint(0, P * B, (900,), generator=g)] = 0
+    counts[5 * B:6 * B] = 0
+    counts[torch.tensor([17, 1234, 3001])] = torch.tensor([3_000_000, 1_500_000, 2_000_000])
+    seg = torch.zeros(P * B + 1, dtype=torch.int64)
+    seg[1:] = torch.cumsum(counts, 0)
+    n = int(seg[-1])
+    keep = []
+    if variable:
+        lens = torch.randint(0, 41, (n,), generator=g)
+        voff = torch.zeros(n + 1, dtype=torch.int64)
+        voff[1:] = torch.cumsum(lens, 0)
+        nbytes = int(voff[-1])
+        stride = 0
+    else:
+        nbytes, stride = n * 13, 13
+    buf = torch.randint(0, 256, (nbytes + 32,), dtype=torch.uint8, device=dev)
+    vals = buf[5:5 + nbytes]
+    cb = torch.zeros(nbytes + 1, dtype=torch.int64, device=dev)
+    cb[1:] = torch.cumsum(vals.to(torch.int64), 0)
+    if variable:
+        dvoff = voff.to(dev)
+        bpos = dvoff[seg.to(dev)]
+        keep.append(dvoff)
+    else:
+        bpos = seg.to(dev) * 13
+    want = ((cb[bpos[1:]] - cb[bpos[:-1]]) % 999999).cpu()
+    dseg = seg.to(dev)
+    keep += [buf, dseg]
+    rec = mde.Records(vals.data_ptr(), nbytes, stride, mde.LAYOUT_SORTED,
+                      keep[0].data_ptr() if variable else 0, n, P, B, dseg.data_ptr())
+    return rec, counts, want, keep, (P, B)
+
+
+@pytest.mark.parametrize("variable", [False, True])
+def test_digest_pieces_ragged_arena_matches_torch_sums(engine, variable):
+    """Interleaved digest pieces (mde_set_digest_piece_bytes) from 1 KiB (a piece switch every
+    few steps, pieces ending inside records and buckets) to 1 MiB, and one range per wave: the
+    digests equal torch byte sums and the sizes the record counts, standalone and fused."""
+    import torch
+    import mydatastore_amd as mde
+    dev = torch.device("cuda:0")
+    engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    rec, counts, want, keep, (P, B) = _skewed_arena(dev, variable)
+    roots = {}
+    engine.set_tuning(PIECES_VARIANT, -1)
+    try:
+        for pb in (0, 1024, 3072, 16384, 65536, 1 << 20):
+            engine.set_digest_piece_bytes(pb)
+            for rep in range(2):
+                o = {"digest": torch.zeros(P * B, dtype=torch.int64, device=dev),
+                     "size": torch.zeros(P * B, dtype=torch.int32, device=dev),
+                     "items": torch.zeros(P, dtype=torch.int32, device=dev),
+                     "root": torch.zeros(P * 32, dtype=torch.uint8, device=dev)}
+                to = mde.TreeOut(o["digest"].data_ptr(), o["size"].data_ptr(), o["items"].data_ptr(),
+                                 o["root"].data_ptr(), 0)
+                if rep == 0:
+                    engine.build_async(rec, to)
+                else:
+                    engine.build_pipelined_async(rec, to)
+                    engine.build_pipeline_drain_async()
+                engine.synchronize()
+                assert torch.equal(o["digest"].cpu(), want), (pb, rep)
+                assert torch.equal(o["size"].cpu().to(torch.int64), counts), (pb, rep)
+                roots.setdefault("r", o["root"].cpu())
+                assert torch.equal(o["root"].cpu(), roots["r"]), (pb, rep)
+    finally:
+        engine.set_digest_piece_bytes(-1)
+        engine.set_tuning(-1, -1)
+
+
+def test_digest_pieces_full_size(engine):
+    """C4 at N=1 and the N=8 shard: every piece size gives the roots of one range per wave."""
+    import torch
+    from mydatastore_amd.workload import make_workload
+    for world in (8, 1):
+        w = make_workload(engine, n_partitions=1024, n_buckets=64, value_len=1024, part_mode="mod",
+                          n_keys=10_000_000, rank=0, world=world)
+        try:
+            engine.set_digest_piece_bytes(0)
+            ref = w.build()  # default variant, one range per wave
+            for v, pb in [(-1, -1)] + [(PIECES_VARIANT, x) for x in (0, 65536, 262144, 1 << 20, 4 << 20)]:
+                engine.set_tuning(v, -1)  # (-1, -1): the defaults, automatic pieces
+                engine.set_digest_piece_bytes(pb)
+                o = w.build()
+                for k in ("digest", "size", "root"):
+                    assert torch.equal(o[k], ref[k]), (world, pb, k)
+        finally:
+            engine.set_digest_piece_bytes(-1)
+            engine.set_tuning(-1, -1)
+        del w

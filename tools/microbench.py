@@ -113,6 +113,56 @@ def bench_ab(eng, variants, worlds=(1, 8), reps=5, cap=2):
     return res
 
 
+def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
+    """Interleaved A/B of the layout-A digest work split: the defaults ("d", automatic pieces),
+    the default variant with one contiguous range per wave ("x") and the interleaved-pieces
+    variant at N-byte pieces (0 = its loop with one piece per wave). Per setting: the standalone
+    digest kernel and a run of fused pipelined builds (build_step_kernel), median over reps;
+    every setting's roots must equal the first setting's."""
+    import torch
+    from mydatastore_amd.workload import make_workload
+    shape_args = {"c4": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1),
+                  "c4/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8),
+                  "c3": dict(n_partitions=64, n_keys=64_000_000, part_mode="block", world=1)}
+    res = []
+    for shape in shapes:
+        w = make_workload(eng, n_buckets=64, value_len=1024, rank=0, **shape_args[shape])
+        sets = [w._outs() for _ in range(2)]
+        n_steps = 10
+
+        def fused():
+            for i in range(n_steps):
+                eng.build_pipelined_async(w.rec, sets[i % 2][1])
+            eng.build_pipeline_drain_async()
+
+        ref = None
+        td = {p: [] for p in pieces}
+        tf = {p: [] for p in pieces}
+        for _ in range(reps):
+            for p in pieces:
+                # "d": the defaults (automatic pieces); "x": the default variant with one range per
+                # wave; a number: the interleaved-pieces variant at that piece size
+                eng.set_tuning(-1 if p in ("d", "x") else 12, -1)
+                eng.set_digest_piece_bytes({"d": -1, "x": 0}.get(p, None) if p in ("d", "x") else int(p))
+                td[p].append(timeit(w.digest_async, reps=10, warm=2))
+                tf[p].append(timeit(fused, reps=1, warm=1) / n_steps)
+                o = w.build()
+                if ref is None:
+                    ref = o["root"].cpu()
+                assert bool((o["root"].cpu() == ref).all()), f"pieces {p}: roots differ"
+        eng.set_digest_piece_bytes(-1)
+        eng.set_tuning(-1, -1)
+        for p in pieces:
+            md, mf = float(np.median(td[p])), float(np.median(tf[p]))
+            res.append({"shape": shape, "piece_bytes": p, "bytes": w.value_bytes, "digest_us": round(md, 2),
+                        "digest_GBps": round(w.value_bytes / md / 1e3, 1), "fused_us_per_build": round(mf, 2),
+                        "fused_GBps": round(w.value_bytes / mf / 1e3, 1)})
+            print(json.dumps(res[-1]), flush=True)
+        del w, sets
+        torch.cuda.empty_cache()
+    return res
+
+
 def bench_verify(eng, P=1024, B=64, R=2, mode=0):
     """VerifyEpoch decision step (mde_verify_epochs) for P partitions x R peer objects: peer 0
     agrees, peer 1 differs in one bucket. Device-resident call timed with HIP events; the
@@ -217,6 +267,10 @@ def main():
     for w in what:
         if w.startswith("ab:"):
             out["ab"] = bench_ab(eng, [int(x) for x in w.split(":")[1].split(",")])
+        if w.startswith("pieces:"):  # pieces:0,262144,1048576[:c4,c3]
+            parts = w.split(":")
+            shapes = tuple(parts[2].split(",")) if len(parts) > 2 else ("c4", "c4/8", "c3")
+            out["pieces"] = bench_pieces(eng, parts[1].split(","), shapes)
         if w.startswith("digest:"):
             out["digest"] = bench_digest(eng, [int(x) for x in w.split(":")[1].split(",")])
     Path("gpurun_out").mkdir(exist_ok=True)

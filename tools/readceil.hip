@@ -120,6 +120,47 @@ __global__ __launch_bounds__(64 * W) void read_wgcontig(const u32x4* __restrict_
   if (lane == 0) atomicAdd(out, s);
 }
 
+// Chunked grid-stride: the buffer is cut into chunks of C16 16-B vectors; wave w streams chunks
+// w, w + nw, w + 2nw, ... front to back (U KiB steps, next step's loads issued before the current
+// step is reduced). All waves sweep the buffer together in a window of nw * C bytes, as the
+// grid-stride shape does, while each wave still reads C contiguous bytes at a time.
+template <int U>
+__global__ __launch_bounds__(256) void read_chunk(const u32x4* __restrict__ buf, uint64_t n16, uint64_t c16,
+                                                  unsigned long long* out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  constexpr uint64_t kStep = 64ull * U;
+  const uint64_t nchunks = (n16 + c16 - 1) / c16;
+  uint32_t acc = 0;
+  for (uint64_t c = wave; c < nchunks; c += nw) {
+    const uint64_t beg = c * c16, end = std::min(beg + c16, n16) / kStep * kStep;
+    if (beg >= end) break;
+    u32x4 cur[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) cur[u] = __builtin_nontemporal_load(buf + beg + u * 64 + lane);
+    for (uint64_t p = beg; p < end; p += kStep) {
+      u32x4 v[U], nx[U];
+      if (p + kStep < end) {
+#pragma unroll
+        for (int u = 0; u < U; u++) nx[u] = __builtin_nontemporal_load(buf + p + kStep + u * 64 + lane);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) { v[u] = cur[u]; cur[u] = nx[u]; }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
+      }
+    }
+  }
+  unsigned long long s = acc;
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) atomicAdd(out, s);
+}
+
 __global__ void fill(uint32_t* p, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     p[i] = (uint32_t)(i * 2654435761u);
@@ -198,6 +239,35 @@ int main(int argc, char** argv) {
            wg_per_cu, (unsigned long long)bytes, ms, bytes / (ms * 1e-3) / 1e9);
     fflush(stdout);
   };
+  if (argc > 2 && std::string(argv[2]) == "chunk") {
+    // chunked grid-stride vs the two end points (contiguous range per wave, plain grid-stride);
+    // chunk sizes divide the byte count only approximately: the reported rate uses the bytes read
+    for (int wpc : {1, 2, 3}) {
+      const uint64_t waves = (uint64_t)cus * wpc * 4;
+      uint64_t per = (n16 + waves - 1) / waves;
+      per = (per + 255) / 256 * 256;
+      const uint32_t blocks = (uint32_t)((n16 + per * 4 - 1) / (per * 4));
+      report("contig U4 nt pipe", wpc, time_it([&] {
+               hipLaunchKernelGGL((read_contig<4, true, true>), dim3(blocks), dim3(256), 0, 0, buf, n16, per, out);
+             }));
+      report("stride U4 nt", wpc, time_it([&] {
+               hipLaunchKernelGGL((read_stride<4, true>), dim3(cus * wpc), dim3(256), 0, 0, buf, n16, out);
+             }));
+      // k pieces per wave: the wave's share cut into k chunks placed k grid-strides apart
+      for (uint64_t k : {2ull, 4ull, 16ull, 64ull, 256ull}) {
+        uint64_t c16 = (n16 + waves * k - 1) / (waves * k);
+        c16 = (c16 + 255) / 256 * 256;
+        const float ms = time_it([&] {
+          hipLaunchKernelGGL((read_chunk<4>), dim3(cus * wpc), dim3(256), 0, 0, buf, n16, c16, out);
+        });
+        printf("{\"shape\": \"chunk k%llu (%llu KiB) U4 nt pipe\", \"wg_per_cu\": %d, \"bytes\": %llu, "
+               "\"ms\": %.4f, \"GBps\": %.1f}\n", (unsigned long long)k, (unsigned long long)(c16 / 64), wpc,
+               (unsigned long long)bytes, ms, bytes / (ms * 1e-3) / 1e9);
+        fflush(stdout);
+      }
+    }
+    return 0;
+  }
 
   for (int wpc : {1, 2, 3, 4, 8}) {
     const uint64_t waves = (uint64_t)cus * wpc * 4;
