@@ -12,7 +12,8 @@ tree passes. For N > 1 a step also carries the RCCL all-gather of the per-partit
 exchange step of the path), bucketed 8 builds per collective on a side stream. --config c5 (BASELINE config 5): build replicas A and B,
 device DFS-order diff of every partition, out-of-sync range extract of B's differing buckets;
 value counts the bytes of both builds. Default workload = BASELINE config 4: 10M keys x 1 KiB values
-over 1024 partitions, partition p on GPU p % N (total work fixed: strong scaling). The output is
+over 1024 partitions per GPU, partition p on GPU p % N (weak scaling: per-GPU work fixed; --scaling
+strong splits the config's 10M keys over the N GPUs instead). The output is
 one JSON line on rank 0 with `roofline` (the dominant kernel, HIP events on the launch stream) and
 `cpu_baseline` (the C restatement on the host cores, rank 0 at N = 1 only).
 """
@@ -73,49 +74,54 @@ def parse():
                          "(mde_build_pipelined_async; the default, except layout b at N=1); streams: "
                          "tree kernel on a second stream; off: digest + tree serially")
     ap.add_argument("--tuning", default="", help="digest kernel 'variant,workgroups_per_cu' (A/B only)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak (default): every rank holds the config's full workload (N x the "
+                         "partitions and keys in all, partition p on rank p %% N); strong: the "
+                         "config's total split over the ranks (BASELINE config 4 as stated)")
     return ap.parse_args()
 
 
-def cpu_baseline(cfg, seconds: float):
+def cpu_baseline(cfg, seconds: float, part_ids):
     """The C restatement of RawPartitionMerkleTree (oracle/, kind "port") timed on the host on a
-    bounded sample of the same workload: the first partitions of the config, generated on the
-    host with the same generator, built repeatedly for ~`seconds`."""
+    bounded sample of the same workload: the first (up to 32) partitions this rank holds,
+    generated on the host with the same generator, built repeatedly for ~`seconds`. Also returns
+    the oracle's digests, sizes and roots of that sample (the checker for the timed device build)."""
     from tests.oracle_c import COracle
     n_keys, P, V, B, mode, _ = cfg
     co = COracle()
-    sample_parts = min(P, 32)
+    sample = np.asarray(part_ids[:32], dtype=np.int64)
+    kpp = -(-n_keys // P)
     if mode == "mod":
         per = -(-n_keys // P)
-        g = (np.arange(per, dtype=np.uint64)[None, :] * np.uint64(P) +
-             np.arange(sample_parts, dtype=np.uint64)[:, None]).reshape(-1)
+        g = (np.arange(per, dtype=np.uint64)[None, :] * np.uint64(P) + sample.astype(np.uint64)[:, None]).reshape(-1)
         g = np.sort(g[g < n_keys])
     else:
-        kpp = -(-n_keys // P)
-        g = np.arange(min(n_keys, sample_parts * kpp), dtype=np.uint64)
-    kpp = -(-n_keys // P)
+        g = np.concatenate([np.arange(p * kpp, min((p + 1) * kpp, n_keys), dtype=np.uint64) for p in sample])
     part, bk = co.synth_tags(g, P, B, {"block": 0, "mod": 1}[mode], kpp)
-    order, seg = co.layout_a(part, bk, P, B)
-    seg = seg[:sample_parts * B + 1]
+    slot = np.full(P, -1, np.int64)
+    slot[sample] = np.arange(sample.size)
+    order, seg = co.layout_a(slot[part].astype(np.uint32), bk, int(sample.size), B)
     values = co.synth_values(g[order], V, 0x4D445354)
     threads = max(1, min(16, os.cpu_count() or 1))
     res = {}
     for t in sorted({1, threads}):
         reps, t0 = 0, time.perf_counter()
         while True:
-            co.build(values, seg, sample_parts, B, V, threads=t, want_nodes=False)
+            co.build(values, seg, int(sample.size), B, V, threads=t, want_nodes=False)
             reps += 1
             el = time.perf_counter() - t0
             if el >= seconds / 2 or reps >= 1000:
                 break
         res[t] = values.nbytes * reps / el / 2**30
+    ref = co.build(values, seg, int(sample.size), B, V, threads=threads, want_nodes=False)
     return {
         "value": round(res[threads], 3), "unit": "GiB/s", "cores": threads, "kind": "port",
         "single_thread_value": round(res[1], 3),
-        "sample": f"{sample_parts} of {P} partitions ({len(g)} records x {V} B = "
+        "sample": f"{sample.size} of {P} partitions ({len(g)} records x {V} B = "
                   f"{values.nbytes / 2**20:.0f} MiB), oracle/mde_oracle.c oracle_build with "
                   f"{threads} threads (1-thread value in single_thread_value); Badger iteration "
                   f"excluded, so an upper bound on the reference Go CPU rate",
-    }
+    }, ref
 
 
 def pmc_traffic(config_name: str, local_bytes: int):
@@ -196,7 +202,7 @@ def main():
     import torch
     import torch.distributed as dist
     import mydatastore_amd as mde
-    from mydatastore_amd.dist import RootGather
+    from mydatastore_amd.dist import RootGather, weak_totals
     from mydatastore_amd.workload import Workload, make_workload
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -228,6 +234,14 @@ def main():
         eng.set_tuning(*map(int, args.tuning.split(",")))
     kpp = -(-n_keys // P)
     shard_world = args.simulate_world if (args.simulate_world and world == 1) else world
+    # Partitions are independent units. Weak scaling: each rank holds the
+    # config's per-GPU workload, so N ranks build N x P partitions of N x n_keys keys (partition p
+    # on rank p % N, p = gid % (N x P) for round-robin configs); every rank's shard then has
+    # exactly the N = 1 shape. Strong: the config's total is split (--simulate-world models it).
+    weak = args.scaling == "weak" and not args.simulate_world
+    if weak and world > 1:
+        n_keys, P = weak_totals(n_keys, P, world)
+        desc = desc + f"; weak scaling: x{world} in all, the N=1 workload on every GPU"
     if c5 and args.layout != "a":
         raise SystemExit("--config c5 uses layout a (the extract gathers bucket runs)")
     w = make_workload(eng, n_partitions=P, n_buckets=B, value_len=V, part_mode=mode,
@@ -291,6 +305,7 @@ def main():
     ev_built = [torch.cuda.Event() for _ in range(2)]
     ev_gathered = [torch.cuda.Event() for _ in range(2)]
     n_step = [0]
+    last_out = [None]  # the output set (replica A) the latest step writes
 
     def gather_bucket(last):  # RCCL gather of the bucket holding build `last` (its last build)
         b = last // bucket
@@ -314,6 +329,7 @@ def main():
         if ev_a is not None:
             ev_a.record(stream)
         eng.build_pipelined_async(w.rec, outs[L % (2 * bucket)][1])
+        last_out[0] = outs[L % (2 * bucket)][0]
         if ev_b is not None:
             ev_b.record(stream)
         if use_dist and L >= 1 and L % bucket == 0:
@@ -343,6 +359,7 @@ def main():
         if use_dist:
             stream.wait_event(ev_gathered[L % 2])
         eng.build_pipelined_async(w.rec, outs[L % 2][1])
+        last_out[0] = outs[L % 2][0]
         if L >= 1:
             c5_compare(L - 1)
         eng.build_pipelined_async(wb.rec, outs_b[L % 2][1])
@@ -355,6 +372,7 @@ def main():
         i = n_step[0] % 2
         n_step[0] += 1
         o, to = outs[i]
+        last_out[0] = o
         if use_dist and not pipeline:
             stream.wait_event(ev_gathered[i])
         if pipeline:
@@ -523,7 +541,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms, 5),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if weak else "strong",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (device-generated splitmix64 values, 'k%016x' keys, SHA-256 bucket tags)",
@@ -555,7 +573,16 @@ def main():
                          "off": None}[mode],
         }
         if world == 1 and not args.no_cpu_baseline and not args.profile:
-            result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_baseline_seconds)
+            result["cpu_baseline"], ref = cpu_baseline(cfg, args.cpu_baseline_seconds, w.partition_ids)
+            # the oracle is the checker of the timed kernel: the last timed build's digests,
+            # sizes and roots of the sampled partitions (local slots 0..n-1) equal the C restatement's
+            n = ref["items"].size
+            o = {k: v.cpu().numpy() for k, v in last_out[0].items() if k in ("digest", "size", "root")}
+            ok = (np.array_equal(o["digest"][:n * B].view(np.uint64), ref["digest"]) and
+                  np.array_equal(o["size"][:n * B], ref["size"]) and np.array_equal(o["root"][:n * 32], ref["root"]))
+            parity["oracle_sample_partitions"] = int(n)
+            parity["timed_build_equals_c_oracle_on_sample"] = bool(ok)
+            parity["all_ranks_ok"] = bool(parity["all_ranks_ok"] and ok)
         else:
             result["cpu_baseline"] = None
         if world == 1 and not args.no_e2e and not args.profile and not c5:

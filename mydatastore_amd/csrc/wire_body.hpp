@@ -257,11 +257,47 @@ struct Cursor {
 
 // protowire.consumeFieldValueD for an unknown group (start tag `num` already read): nested
 // fields are skipped by wire type until the end tag of the same number; inner tags need a number
-// in [1, MaxInt32]. The open groups' numbers live in gstack (wave-uniform LDS, kWireGroupDepth
-// words): groups nested deeper than that fail, where protobuf-go allows 10,000 levels.
+// in [1, MaxInt32]. protobuf-go enters a group only while its depth budget
+// (protowire.DefaultRecursionLimit = 10,000, one less per level) is >= 0, so up to 10,001 levels
+// nest and the 10,002nd fails.
+// The open groups' numbers live in gstack, a ring of the kWireGroupDepth deepest levels
+// (wave-uniform LDS): level k at gstack[(k - 1) % kWireGroupDepth], valid for levels
+// [lo, depth]. An end tag below lo (only after more than kWireGroupDepth levels) refills the ring
+// by rescanning the group from its first byte: the last start tag seen at level k before the end
+// tag is the open level-k group. Objects nested no deeper than the ring never rescan.
 constexpr uint32_t kWireGroupDepth = 64;
+constexpr uint32_t kWireGroupMaxNest = 10001;
+__device__ __forceinline__ void group_refill(const Cursor& c, uint64_t start, uint64_t stop, uint32_t depth,
+                                             uint32_t num, uint32_t* gstack) {
+  const uint32_t lo = depth > kWireGroupDepth ? depth - kWireGroupDepth + 1 : 1u;
+  if (lo == 1) gstack[0] = num;  // level 1's start tag precedes `start`
+  // bytes [start, stop) were parsed once (well formed); the last is the end tag being matched,
+  // which only lowers d
+  Cursor r{c.p, stop, start, true};
+  uint32_t d = 1;
+  while (r.pos < stop) {
+    const uint64_t key = r.varint();
+    const uint32_t w = (uint32_t)(key & 7);
+    if (w == 3) {
+      if (++d >= lo && d <= depth) gstack[(d - 1) % kWireGroupDepth] = (uint32_t)(key >> 3);
+    } else if (w == 4) {
+      d--;
+    } else if (w == 0) {
+      r.varint();
+    } else if (w == 1) {
+      r.pos += 8;
+    } else if (w == 5) {
+      r.pos += 4;
+    } else {
+      const uint64_t len = r.varint();
+      r.pos += len;
+    }
+  }
+}
+
 __device__ __forceinline__ void skip_group(Cursor& c, uint64_t num, uint32_t* gstack) {
-  uint32_t depth = 1;
+  const uint64_t start = c.pos;  // first byte inside the outermost group (level 1)
+  uint32_t depth = 1, lo = 1;
   gstack[0] = (uint32_t)num;
   while (c.ok) {
     const uint64_t key = c.varint();
@@ -270,13 +306,18 @@ __device__ __forceinline__ void skip_group(Cursor& c, uint64_t num, uint32_t* gs
     const uint32_t w = (uint32_t)(key & 7);
     if (n2 < 1 || n2 > 0x7FFFFFFFull) { c.ok = false; return; }
     if (w == 4) {
-      if ((uint32_t)n2 != gstack[depth - 1]) { c.ok = false; return; }
+      if (depth < lo) {  // this level's number left the ring: rescan up to this end tag
+        group_refill(c, start, c.pos, depth, (uint32_t)num, gstack);
+        lo = depth > kWireGroupDepth ? depth - kWireGroupDepth + 1 : 1u;
+      }
+      if ((uint32_t)n2 != gstack[(depth - 1) % kWireGroupDepth]) { c.ok = false; return; }
       if (--depth == 0) return;
       continue;
     }
     if (w == 3) {
-      if (depth == kWireGroupDepth) { c.ok = false; return; }
-      gstack[depth++] = (uint32_t)n2;
+      if (depth == kWireGroupMaxNest) { c.ok = false; return; }  // errCodeRecursion
+      gstack[depth++ % kWireGroupDepth] = (uint32_t)n2;
+      if (depth - lo >= kWireGroupDepth) lo = depth - kWireGroupDepth + 1;
       continue;
     }
     if (w == 0) { c.varint(); continue; }

@@ -12,6 +12,14 @@ from __future__ import annotations
 import numpy as np
 
 
+def weak_totals(n_keys: int, n_partitions: int, world: int) -> tuple[int, int]:
+    """Weak scaling (bench.py default): every rank holds a workload of the per-GPU shape
+    (n_partitions partitions, n_keys keys), so the job has world x both. With partition p on rank
+    p % world and round-robin (p = gid % P) or block (p = gid // keys_per_partition) tagging, each
+    rank's shard has exactly the single-GPU per-partition record counts."""
+    return n_keys * world, n_partitions * world
+
+
 def partition_rank(p: int, world: int) -> int:
     return p % world
 

@@ -109,15 +109,23 @@ def _skip(b, pos, num, typ, depth):
             raise WireError("truncated bytes")
         return pos + n
     if typ == 3:
-        if depth < 0:
-            raise WireError("recursion")
-        while True:
+        # consumeFieldValueD's recursion, unrolled onto an explicit stack (Python's own stack is
+        # shallower than the 10,000 levels Go allows): each open group keeps (number, depth); a
+        # group is entered only with depth >= 0, so at most RECURSION_LIMIT + 1 levels nest
+        stack = [(num, depth)]
+        while stack:
+            if stack[-1][1] < 0:
+                raise WireError("recursion")
             num2, typ2, pos = _tag(b, pos)
             if typ2 == 4:
-                if num2 != num:
+                if num2 != stack[-1][0]:
                     raise WireError("end group mismatch")
-                return pos
-            pos = _skip(b, pos, num2, typ2, depth - 1)
+                stack.pop()
+            elif typ2 == 3:
+                stack.append((num2, stack[-1][1] - 1))
+            else:
+                pos = _skip(b, pos, num2, typ2, 0)
+        return pos
     raise WireError("end group / reserved wire type")
 
 

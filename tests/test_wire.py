@@ -152,6 +152,17 @@ def test_decode_wave_runs_and_hostile_lengths(engine):
     for B, cap in ((65, 64), (129, 100), (700, 640), (64, 64)):
         r = engine.decode_objects([objs[(63, 64, 65, 127, 128, 129, 700, 1000).index(B)]], cap=cap)[0]
         assert (r == mde.MDE_E_CAPACITY) if B > cap else isinstance(r, dict)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [16, 1024])
+def test_decode_split_run_and_malformed_varints(engine, cap):
+    """Both decode_kernel instantiations (64-wide windows for cap <= 64, 256-wide above): a
+    bucket run split by a non-canonical entry, and the malformed varints and wrapping lengths
+    that must fail."""
+    import mydatastore_amd as mde
+    rng = np.random.default_rng(64)
+    cls = wire_pb.epoch_tree_object_class()
     # a run split by a non-canonical entry: overlong key varint 0xA2 0x00 (= field 4, wire type 2)
     ent = [int(x) for x in rng.integers(0, 999999, 6)]
     body = b"".join(b"\x22\x08" + v.to_bytes(8, "little") for v in ent[:3])
@@ -159,7 +170,7 @@ def test_decode_wave_runs_and_hostile_lengths(engine):
     body += b"".join(b"\x22\x08" + v.to_bytes(8, "little") for v in ent[4:])
     pk = b"".join(_varint(x) for x in (1, 300, 2**32 - 1))
     split = body + b"\x2a" + _varint(len(pk)) + pk
-    g = engine.decode_objects([split], cap=16)[0]
+    g = engine.decode_objects([split], cap=cap)[0]
     assert g["digest"] == ent and g["size"] == [1, 300, -1, 0, 0, 0]
     assert [int.from_bytes(x, "little") for x in cls.FromString(split).buckets] == ent
     # failures: 11-byte size varint, a varint crossing the packed run's end, wrapping lengths
@@ -168,7 +179,7 @@ def test_decode_wave_runs_and_hostile_lengths(engine):
     wrap_unknown = b"\x08\x01\x0a" + _varint(2**64 - 12)  # field 1, wire type 2: skipped
     wrap_bucket = b"\x22" + _varint(2**64 - 1)
     wrap_packed = b"\x2a" + _varint(2**64 - 11) + b"\x01"
-    res = engine.decode_objects([eleven, cross, wrap_unknown, wrap_bucket, wrap_packed], cap=16)
+    res = engine.decode_objects([eleven, cross, wrap_unknown, wrap_bucket, wrap_packed], cap=cap)
     assert res == [mde.MDE_E_DECODE] * 5
 
 
@@ -203,6 +214,14 @@ def test_oracle_unmarshal_go_rules():
             got = False
         assert got == ok, name
     assert wire_pb.unmarshal(GO_RULE_CASES["unknown_group"][0]).partition == 5
+    # protowire.DefaultRecursionLimit: 10,001 nested unknown groups skip, 10,002 fail
+    for d, ok in ((10001, True), (10002, False)):
+        deep = b"\x4b" * d + b"\x4c" * d + b"\x08\x05"
+        try:
+            got = wire_pb.unmarshal(deep).partition == 5
+        except wire_pb.WireError:
+            got = False
+        assert got == ok, d
     assert wire_pb.unmarshal(GO_RULE_CASES["bool_2"][0]).valid
     rng = np.random.default_rng(9)
     for B in (0, 1, 2, 7, 64, 129):
@@ -253,15 +272,17 @@ def _mutate(rng, b):
 
 
 @pytest.mark.gpu
-def test_decode_follows_go_unmarshal(engine):
+@pytest.mark.parametrize("cap", [64, 1024])
+def test_decode_follows_go_unmarshal(engine, cap):
     """Device decoder vs the protobuf-go restatement: the wire-rule cases, then 3,000 seeded
     mutations (byte overwrites, insertions, deletions, truncations, continuation-bit flips,
-    spliced edge cases) of valid objects -- same error class or the same decoded fields."""
-    rng = np.random.default_rng(2024)
-    cap = 64
+    spliced edge cases) of valid objects -- same error class or the same decoded fields. Both
+    decode_kernel instantiations: cap 64 (64-wide windows) and cap 1024 (256-wide windows, with
+    objects of up to 700 buckets among the mutated bases)."""
+    rng = np.random.default_rng(2024 + cap)
     objs = [b for b, _ in GO_RULE_CASES.values()]
     base = []
-    for B in (1, 3, 30, 64, 70):
+    for B in (1, 3, 30, 64, 70) + ((130, 300, 700) if cap > 64 else ()):
         d = rng.integers(0, 999999, B).tolist()
         s = rng.integers(-2**31, 2**31, B).tolist() if B % 2 else rng.integers(0, 300, B).tolist()
         base.append(wire_pb.marshal(int(rng.integers(-9, 9)), 6, 7, d, s, bool(B % 2)))
@@ -272,3 +293,72 @@ def test_decode_follows_go_unmarshal(engine):
     assert not bad, bad[:5]
     n_err = sum(1 for g in got if not isinstance(g, dict))
     assert 300 < n_err < 2900  # the mutations exercise both outcomes
+
+
+def _tagb(num, wt):
+    return _varint((num << 3) | wt)
+
+
+def _group_walk(rng, targets, sib=0.3, big_numbers=True):
+    """Unknown-group nesting that walks through the depths in `targets` (down and up again),
+    with random sibling fields (varint, fixed32/64, length-delimited, small closed groups) between
+    the tags; returns the bytes (all groups closed when the walk ends at 0) and the open stack."""
+    out, stack = bytearray(), []
+
+    def sibling():
+        k = int(rng.integers(0, 5))
+        n = int(rng.integers(8, 40))
+        if k == 0:
+            return _tagb(n, 0) + _varint(int(rng.integers(0, 2**40)))
+        if k == 1:
+            return _tagb(n, 1) + bytes(8)
+        if k == 2:
+            return _tagb(n, 5) + bytes(4)
+        if k == 3:
+            return _tagb(n, 2) + _varint(3) + b"abc"
+        return _tagb(n, 3) + _tagb(9, 0) + b"\x01" + _tagb(n, 4)
+
+    for t in targets:
+        while len(stack) < t:
+            if rng.random() < sib:
+                out += sibling()
+            n = int(rng.integers(1, 2**31)) if (big_numbers and rng.random() < 0.2) else int(rng.integers(1, 16))
+            out += _tagb(n, 3)
+            stack.append(n)
+        while len(stack) > t:
+            if rng.random() < sib:
+                out += sibling()
+            out += _tagb(stack.pop(), 4)
+    return bytes(out), stack
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [64, 1024])
+def test_decode_deep_unknown_groups_follow_go(engine, cap):
+    """Unknown groups nested beyond the decoder's 64-level ring: protobuf-go skips up to 10,001
+    levels (protowire.DefaultRecursionLimit) and rejects the 10,002nd; an end tag whose number
+    left the ring is matched after a rescan. Straight nests, zig-zag walks with siblings and
+    multi-byte field numbers, deep end-number mismatches and truncations: the device decode
+    equals the protobuf-go restatement (oracle/wire_pb.py) for both decode_kernel shapes."""
+    import mydatastore_amd as mde
+    rng = np.random.default_rng(10001 + cap)
+    tail = b"\x08\x05\x10\x06\x22\x08" + (1234).to_bytes(8, "little")  # partition 5, lower 6, one bucket
+    objs = []
+    for d in (63, 64, 65, 129, 1000, 10001, 10002):
+        objs.append(_group_walk(rng, [d, 0], sib=0.0, big_numbers=False)[0] + tail)
+    for targets in ([200, 50, 300, 0], [70, 3, 140, 65, 66, 0], [5000, 4000, 9000, 100, 0],
+                    [10001, 9000, 10001, 0], [10001, 10000, 10002, 0]):
+        objs.append(_group_walk(rng, targets)[0] + tail)
+    good = [o for o in objs if isinstance(_expect_decode(o, cap), dict)]
+    for o in good[:4]:  # a wrong end number deep inside (after a refill) and a truncation
+        b = bytearray(o)
+        ends = [i for i in range(len(b) - len(tail)) if b[i] & 7 == 4 and b[i] < 0x80 and (i == 0 or b[i - 1] < 0x80)]
+        b[ends[len(ends) // 3]] ^= 0x08  # end tag of another number (or field 0)
+        objs.append(bytes(b))
+        objs.append(o[: len(o) // 2])
+    exp = [_expect_decode(o, cap) for o in objs]
+    assert sum(isinstance(e, dict) for e in exp) >= 8 and sum(e == mde.MDE_E_DECODE for e in exp) >= 4
+    got = engine.decode_objects(objs, cap=cap)
+    bad = [(i, len(objs[i]), g if not isinstance(g, dict) else "ok", e if not isinstance(e, dict) else "ok")
+           for i, (g, e) in enumerate(zip(got, exp)) if g != e]
+    assert not bad, bad
