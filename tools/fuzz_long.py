@@ -15,7 +15,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 def main(seeds=4, n_dec=20000, n_ver=300):
     import mydatastore_amd as mde
     from oracle import wire_pb
-    from tests.test_wire import GO_RULE_CASES, _expect_decode, _mutate
+    from tests.test_wire import GO_RULE_CASES, _expect_decode, _group_walk, _mutate
     from tests.test_verify import STATUS, _oracle_verify
     eng = mde.Engine(0)
     for seed in range(seeds):
@@ -26,6 +26,9 @@ def main(seeds=4, n_dec=20000, n_ver=300):
             s = rng.integers(-2**31, 2**31, B).tolist() if B % 3 else rng.integers(0, 300, B).tolist()
             base.append(wire_pb.marshal(int(rng.integers(-9, 9)), int(rng.integers(0, 2**40)), 7, d, s,
                                         bool(B % 2)))
+        # unknown groups nested past the decoder's 64-level ring (rescans) ahead of valid objects
+        for t in ([70, 0], [130, 20, 200, 0], [65, 64, 66, 0]):
+            base.append(_group_walk(rng, t)[0] + base[int(rng.integers(0, 10))])
         objs = [_mutate(rng, base[int(rng.integers(0, len(base)))]) for _ in range(n_dec)]
         objs += [b for b, _ in GO_RULE_CASES.values()]
         for cap in (64, 512):
