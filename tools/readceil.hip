@@ -161,6 +161,47 @@ __global__ __launch_bounds__(256) void read_chunk(const u32x4* __restrict__ buf,
   if (lane == 0) atomicAdd(out, s);
 }
 
+// Contiguous range per wave through buffer loads with cache-policy bits AUX (gfx950: 1 = sc0,
+// 2 = nt, 16 = sc1): one descriptor per wave based at its range (ranges < 4 GiB).
+template <int AUX>
+__global__ __launch_bounds__(256) void read_buf(const u32x4* __restrict__ buf, uint64_t n16, uint64_t per_wave16,
+                                                unsigned long long* out) {
+  constexpr int U = 4;
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t beg = wave * per_wave16, end = std::min(beg + per_wave16, n16);
+  uint32_t acc = 0;
+  if (beg < end) {
+    const uint32_t nbytes = (uint32_t)((end - beg) * 16);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(buf + beg), (short)0, (int)nbytes, 0x00020000);
+    const uint32_t steps = (uint32_t)((end - beg) / (64 * U));
+    u32x4 cur[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      cur[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u * 64 + lane) * 16, 0, AUX));
+    for (uint32_t t = 0; t < steps; t++) {
+      u32x4 v[U], nx[U];
+      if (t + 1 < steps) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          nx[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((t + 1) * 64 * U + u * 64 + lane) * 16, 0, AUX));
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) { v[u] = cur[u]; cur[u] = nx[u]; }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
+      }
+    }
+  }
+  unsigned long long s = acc;
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) atomicAdd(out, s);
+}
+
 __global__ void fill(uint32_t* p, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     p[i] = (uint32_t)(i * 2654435761u);
@@ -239,6 +280,25 @@ int main(int argc, char** argv) {
            wg_per_cu, (unsigned long long)bytes, ms, bytes / (ms * 1e-3) / 1e9);
     fflush(stdout);
   };
+  if (argc > 2 && std::string(argv[2]) == "policy") {
+    // cache-policy bits of the streaming loads: buffer loads with aux = sc0 / nt / sc1 combos
+    for (int wpc : {1, 2}) {
+      const uint64_t waves = (uint64_t)cus * wpc * 4;
+      uint64_t per = (n16 + waves - 1) / waves;
+      per = (per + 255) / 256 * 256;
+      const uint32_t blocks = (uint32_t)((n16 + per * 4 - 1) / (per * 4));
+      report("contig U4 nt pipe (global)", wpc, time_it([&] {
+               hipLaunchKernelGGL((read_contig<4, true, true>), dim3(blocks), dim3(256), 0, 0, buf, n16, per, out);
+             }));
+#define RB(AUX)                                                                                         \
+  report("buffer U4 pipe aux " #AUX, wpc, time_it([&] {                                                 \
+           hipLaunchKernelGGL((read_buf<AUX>), dim3(blocks), dim3(256), 0, 0, buf, n16, per, out);     \
+         }));
+      RB(0) RB(1) RB(2) RB(3) RB(16) RB(17) RB(18) RB(19)
+#undef RB
+    }
+    return 0;
+  }
   if (argc > 2 && std::string(argv[2]) == "chunk") {
     // chunked grid-stride vs the two end points (contiguous range per wave, plain grid-stride);
     // chunk sizes divide the byte count only approximately: the reported rate uses the bytes read
