@@ -123,7 +123,9 @@ def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
     from mydatastore_amd.workload import make_workload
     shape_args = {"c4": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1),
                   "c4/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8),
-                  "c3": dict(n_partitions=64, n_keys=64_000_000, part_mode="block", world=1)}
+                  "c3": dict(n_partitions=64, n_keys=64_000_000, part_mode="block", world=1),
+                  "c4b": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1, layout="b"),
+                  "c4b/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8, layout="b")}
     res = []
     for shape in shapes:
         w = make_workload(eng, n_buckets=64, value_len=1024, rank=0, **shape_args[shape])
