@@ -110,8 +110,10 @@ void* mde_get_stream(mde_ctx* ctx);
 int mde_synchronize(mde_ctx* ctx);
 int mde_device_info(mde_ctx* ctx, int* cu_count, char* arch_name, int arch_cap);
 /* Tuning hook for benchmarks: digest-kernel variant, resident workgroups per CU, and grid
- * oversubscription (-1 = the built-in defaults). Results are identical for every setting; only
- * speed changes. */
+ * oversubscription (-1 = the built-in defaults: the variant is then chosen per build -- the
+ * register-window kernel when buckets average under 64 KiB, e.g. the reference's default
+ * B = 1000 -- with interleaved pieces for large shares). Results are identical for every setting;
+ * only speed changes. */
 int mde_set_tuning(mde_ctx* ctx, int digest_variant, int digest_blocks_per_cu, int digest_oversub);
 /* Tuning hook: layout-A digest work split. 0 = one contiguous range per resident wave; N > 0 =
  * with the interleaved-pieces digest variant, each wave's share cut into pieces of about N bytes,

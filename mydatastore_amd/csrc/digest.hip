@@ -58,6 +58,26 @@ __device__ __forceinline__ uint32_t seg_next(const SegDesc& d, uint32_t s, uint6
   return seg_search(d, s + 64u, x, lane);
 }
 
+// Register window over the bucket starts: lane i holds segpos(base + i) (~0 past S), so the 63
+// buckets base .. base + 62 have their bounds in registers. A bucket boundary inside the window is
+// then a ballot and two readlanes instead of two dependent seg_rec round trips (seg_next + the
+// new bucket's bounds); the window reloads once per 63 buckets.
+struct SegWindow {
+  uint32_t base;
+  uint64_t start;  // this lane's segpos(base + lane)
+  __device__ __forceinline__ void load(const SegDesc& d, uint32_t b, int lane) {
+    base = b;
+    const uint32_t idx = b + (uint32_t)lane;
+    start = idx <= d.S ? segpos(d, idx) : ~0ull;
+  }
+};
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint32_t byte_mask(int lo, int hi) {  // bytes [lo, hi) of a dword
   const uint32_t mh = hi >= 4 ? 0xffffffffu : ((1u << (8 * hi)) - 1u);
   const uint32_t ml = lo >= 4 ? 0xffffffffu : ((1u << (8 * lo)) - 1u);
@@ -77,10 +97,18 @@ __device__ __forceinline__ uint32_t masked_sum16(u32x4 v, int64_t a, int64_t b, 
 }
 
 __device__ __forceinline__ void flush(unsigned long long* sums, uint32_t s, uint32_t acc) {
+#ifdef MDE_PROBE_NO_REDUCE  // A/B probe only (wrong sums): the lane-0 partial, no cross-lane sum
+  const unsigned long long v = acc;
+#else
   unsigned long long v = acc;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+#endif
+#ifdef MDE_PROBE_NO_ATOMIC  // A/B probe only (wrong sums): the reduction without its atomic
+  if ((threadIdx.x & 63) == 0 && v == 0x123456789abcdefull) atomicAdd(sums + s, v);
+#else
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(sums + s, v);
+#endif
 }
 
 template <int U, bool NT>
@@ -159,9 +187,141 @@ __device__ __forceinline__ uint32_t digest_range(const DigestLaunch& a, uint64_t
   return s;
 }
 
+// Sum of the 64 lanes' u32 values, exact when it fits 32 bits: DPP within each row of 16 lanes
+// (no LDS round trips), then the four row sums by readlane. Call with all 64 lanes active.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, true);   // quad_perm [1,0,3,2]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, true);   // quad_perm [2,3,0,1]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, true);  // row_half_mirror
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, true);  // row_mirror
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
+// digest_range for many short buckets (the reference's default B = 1000 puts a bucket boundary
+// every few KiB):
+//   * a true register double buffer: the loop is unrolled by two over buffers A and B and every
+//     step issues its U loads unconditionally (addresses past `end` clamp to the last vector), so
+//     the compiler's vmcnt bookkeeping waits for the current buffer only and the next step's
+//     loads stay in flight across the reduction (digest_range's single-buffer swap makes hipcc
+//     wait for both before the register moves);
+//   * the bucket bounds come from a SegWindow: no dependent seg_rec loads per boundary;
+//   * a step that crosses boundaries byte-sums each vector once and attributes whole vectors to
+//     buckets by two compares (only a vector holding a boundary takes byte masks);
+//   * a finished bucket's sum is a DPP wave reduction (u64 shuffles when this wave streamed more
+//     than 16 MiB of it), parked in the window lane of that bucket; the window's sums go out as
+//     ONE coalesced atomic per 63 buckets, not one atomic (and its vmcnt stall) per bucket.
+// Bytes past `end` are loaded but never counted: whole-vector sums are used only for vectors
+// inside [lo, hi) and the vector holding `end` is masked.
+template <int U, bool NT>
+__device__ __forceinline__ void load_step_clamped(u32x4 (&v)[U], const u32x4* base16, uint64_t p, uint64_t lastvec,
+                                                  int lane) {
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint64_t x = min(p + (uint64_t)u * 1024u + (uint64_t)lane * 16u, lastvec);
+    v[u] = NT ? __builtin_nontemporal_load(base16 + (x >> 4)) : base16[x >> 4];
+  }
+}
+
+template <int U, bool NT, int PIPE>
+__device__ __forceinline__ uint32_t digest_range_win(const DigestLaunch& a, uint64_t beg, uint64_t end, uint32_t s_lo,
+                                                     int lane) {
+  constexpr uint64_t kStep = 1024ull * U;
+  const SegDesc& d = a.seg;
+  const u32x4* base16 = reinterpret_cast<const u32x4*>(d.base);
+  const uint64_t lastvec = (end - 1) & ~15ull;  // the vector holding the range's last byte
+  u32x4 va[U], vb[U];
+  load_step_clamped<U, NT>(va, base16, beg, lastvec, lane);
+  uint32_t s = seg_search(d, s_lo, beg, lane);
+  SegWindow win;
+  win.load(d, s, lane);
+  uint64_t sb = readlane64(win.start, 0), se = readlane64(win.start, 1);
+  uint64_t wsum = 0;     // this lane's window bucket (win.base + lane): its finished sum
+  uint64_t bfrom = beg;  // where this wave entered bucket s
+  uint32_t acc = 0;
+
+  // the bucket being left: its sum into its window lane
+  auto retire = [&](uint64_t upto) {
+    uint64_t v;
+    if (upto - bfrom <= (16ull << 20)) {
+      v = wave_sum_u32(acc);  // <= 255 x 16 MiB < 2^32
+    } else {
+      v = acc;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    }
+    if ((uint32_t)lane == s - win.base) wsum = v;
+    acc = 0;
+  };
+  auto window_out = [&]() {  // one coalesced atomic for the window's finished buckets
+    if (wsum) atomicAdd(a.sums + win.base + (uint32_t)lane, (unsigned long long)wsum);
+    wsum = 0;
+  };
+  auto process = [&](const u32x4 (&v)[U], uint64_t p) {
+    if (p + kStep <= end && sb <= p && p + kStep <= se) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
+      }
+      return;
+    }
+    uint32_t fs[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint32_t t = __builtin_amdgcn_sad_u8(v[u].x, 0u, 0u);
+      t = __builtin_amdgcn_sad_u8(v[u].y, 0u, t);
+      t = __builtin_amdgcn_sad_u8(v[u].z, 0u, t);
+      fs[u] = __builtin_amdgcn_sad_u8(v[u].w, 0u, t);
+    }
+    const uint64_t q = min(p + kStep, end);
+    for (;;) {
+      const uint64_t lo = max(sb, p), hi = min(se, q);
+      if (lo < hi) {
+        const int a32 = (int)(lo - p), b32 = (int)(hi - p);  // within [0, kStep]
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int off = u * 1024 + lane * 16;
+          const bool inside = off >= a32 && off + 16 <= b32;
+          acc += inside ? fs[u] : 0u;
+          if (!inside && off < b32 && off + 16 > a32)  // this vector holds a boundary
+            acc = masked_sum16(v[u], (int64_t)(a32 - off), (int64_t)(b32 - off), acc);
+        }
+      }
+      if (se >= q) break;
+      retire(se);
+      bfrom = se;
+      // the bucket holding position se (empty buckets skipped), through the window
+      uint32_t c = (uint32_t)__popcll(__ballot(win.start <= se));
+      while (c == 64u) {  // past the window: its sums go out, the next 63 buckets come in
+        window_out();
+        win.load(d, win.base + 63u, lane);
+        c = (uint32_t)__popcll(__ballot(win.start <= se));
+      }
+      s = win.base + c - 1u;
+      sb = readlane64(win.start, c - 1u);
+      se = readlane64(win.start, c);
+    }
+  };
+
+  for (uint64_t p = beg;; p += 2 * kStep) {
+    load_step_clamped<U, NT>(vb, base16, p + kStep, lastvec, lane);  // always issued (see above)
+    process(va, p);
+    if (p + kStep >= end) break;
+    load_step_clamped<U, NT>(va, base16, p + 2 * kStep, lastvec, lane);
+    process(vb, p + kStep);
+    if (p + 2 * kStep >= end) break;
+  }
+  retire(min(se, end));
+  window_out();
+  return s;
+}
+
 // One contiguous range of wave_bytes per wave. `block` = this workgroup's index among the digest
 // workgroups of the launch.
-template <int U, bool NT, int PIPE, int PRIO = 0>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false>
 __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t block) {
   // Streaming waves issue little VALU; when tree waves (back-to-back SHA-256 VALU) share the CU,
   // a raised priority keeps the loads flowing and the SHA waves take the slack.
@@ -174,13 +334,16 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
   const uint64_t last = segpos(d, d.S);
   const uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
   if (beg >= last) return;
-  digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), 0u, lane);
+  if (WIN)
+    digest_range_win<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), 0u, lane);
+  else
+    digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), 0u, lane);
 }
 
 // Interleaved pieces (DigestLaunch::pieces): the wave streams `pieces` ranges of wave_bytes,
 // piece_stride apart, so the whole grid sweeps the arena front to back together. Each piece is a
 // digest_range (its own bucket search, from the previous piece's last bucket on, and flush).
-template <int U, bool NT, int PIPE, int PRIO = 0>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false>
 __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32_t block) {
   if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const int lane = threadIdx.x & 63;
@@ -192,7 +355,8 @@ __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32
   uint32_t s = 0;
   uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
   for (uint32_t j = 0; j < a.pieces && beg < last; j++, beg += a.piece_stride)
-    s = digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), s, lane);
+    s = WIN ? digest_range_win<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), s, lane)
+            : digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), s, lane);
 }
 
 
@@ -388,15 +552,21 @@ __device__ __forceinline__ void digest_body_steal(const DigestLaunch& a, uint32_
   }
 }
 
-// MODE: 0 = one static range per wave, 1 = tail stealing, 2 = interleaved pieces.
+// MODE: 0 = one static range per wave, 1 = tail stealing, 2 = interleaved pieces; 3 and 4 = 0 and
+// 2 with the bucket bounds in a register window (SegWindow).
+template <int U, bool NT, int PIPE, int PRIO, int MODE>
+__device__ __forceinline__ void digest_dispatch(const DigestLaunch& a, uint32_t block) {
+  if (MODE == 1)
+    digest_body_steal<U, NT, PRIO>(a, block);
+  else if (MODE == 2 || MODE == 4)
+    digest_body_pieces<U, NT, PIPE, PRIO, MODE == 4>(a, block);
+  else
+    digest_body<U, NT, PIPE, PRIO, MODE == 3>(a, block);
+}
+
 template <int U, bool NT, int PIPE, int PRIO = 0, int MODE = 0>
 __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a) {
-  if (MODE == 1)
-    digest_body_steal<U, NT, PRIO>(a, blockIdx.x);
-  else if (MODE == 2)
-    digest_body_pieces<U, NT, PIPE, PRIO>(a, blockIdx.x);
-  else
-    digest_body<U, NT, PIPE, PRIO>(a, blockIdx.x);
+  digest_dispatch<U, NT, PIPE, PRIO, MODE>(a, blockIdx.x);
 }
 
 
@@ -430,12 +600,7 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
   }
   const uint32_t db = blockIdx.x - tree_blocks;
 #endif
-  if (MODE == 1)
-    digest_body_steal<U, NT, PRIO>(a, db);
-  else if (MODE == 2)
-    digest_body_pieces<U, NT, PIPE, PRIO>(a, db);
-  else
-    digest_body<U, NT, PIPE, PRIO>(a, db);
+  digest_dispatch<U, NT, PIPE, PRIO, MODE>(a, db);
 }
 
 // One-launch build of a small arena (the synchronous one-partition calls of VerifyEpoch). Digest
@@ -497,7 +662,8 @@ const Variant kVariants[] = {
     MDE_VARIANT(16, false, false, 0, 0), MDE_VARIANT(4, true, true, 2, 0),
     MDE_VARIANT(4, true, true, 3, 0),   MDE_VARIANT(4, true, true, 2, 1),
     MDE_VARIANT(8, true, true, 2, 1),    MDE_VARIANT(4, true, 2, 2, 0),
-    MDE_VARIANT(4, true, 2, 2, 2),
+    MDE_VARIANT(4, true, 2, 2, 2),      MDE_VARIANT(4, true, 2, 2, 3),
+    MDE_VARIANT(4, true, 2, 2, 4),
 };
 #undef MDE_VARIANT
 
@@ -524,7 +690,14 @@ hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t
 }
 
 bool bucket_digest_steals(int v) { return variant(v).mode == 1; }
-bool bucket_digest_pieces(int v) { return variant(v).mode == 2; }
+bool bucket_digest_pieces(int v) { return variant(v).mode == 2 || variant(v).mode == 4; }
+int bucket_digest_pieces_sibling(int v) {  // the same kernel with interleaved pieces
+  switch (v) {
+    case 11: return 12;
+    case 13: return 14;
+    default: return v;
+  }
+}
 
 void plan_steal(uint64_t wave_bytes, uint64_t* head_bytes, uint64_t* chunk_bytes, uint32_t* tail_chunks) {
   // Tail = about 1/6 of each wave range in up to 16 pieces of >= 16 KiB (the max step), at most

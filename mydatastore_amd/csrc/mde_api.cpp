@@ -35,13 +35,15 @@ constexpr int kDefaultDigestOversub = 1;  // grid = resident slots x oversub
 constexpr uint64_t kAutoPieceBytes = UINT64_MAX;  // digest_piece_bytes value: the policy above
 constexpr uint64_t kAutoPieceMinShare = 4ull << 20;
 constexpr uint64_t kAutoPieces = 5;
-constexpr int kPiecesDigestVariant = 12;
+constexpr int kWindowDigestVariant = 13;                 // SegWindow + true double buffer (plan_digest)
+constexpr uint64_t kWindowMaxAvgBucketBytes = 64ull << 10;  // average bucket bytes below which it runs
 
 struct mde_ctx {
   int device = 0;
   int cus = 256;
   int digest_blocks_per_cu = 0;  // resident workgroups per CU for the digest kernel (queried)
   int digest_variant = kDefaultDigestVariant;
+  bool digest_auto = true;  // no explicit variant: plan_digest picks the window / pieces forms
   int digest_cap = kDefaultDigestCap;
   int digest_oversub = kDefaultDigestOversub;
   uint64_t digest_piece_bytes = kAutoPieceBytes;
@@ -336,15 +338,24 @@ mde::SegDesc seg_desc(const mde_records* r) {
 }
 
 int plan_digest(mde_ctx* c, uint64_t bytes, mde::DigestLaunch* a) {
+  // Short buckets (a boundary every few KiB, e.g. the reference's default B = 1000): the
+  // register-window kernel (variant 13). Same-box A/B (profiles/r02u_window.jsonl): C4 at
+  // B = 1000 (10 KiB buckets) 2,685 -> 1,493 us, its N=8 shard 376 -> 192 us; at B = 64 (156 KiB
+  // buckets) it costs 0.3-0.8 %, so longer buckets keep variant 11.
+  if (c->digest_auto && a->seg.S && bytes / a->seg.S < kWindowMaxAvgBucketBytes)
+    a->variant = kWindowDigestVariant;
   uint64_t piece_bytes = 0;
   if (c->digest_piece_bytes == kAutoPieceBytes) {
-    if (a->variant == kDefaultDigestVariant || mde::bucket_digest_pieces(a->variant)) {
+    // automatic pieces: the default's (or an explicitly chosen pieces variant's) pieces form
+    const int sib = c->digest_auto || mde::bucket_digest_pieces(a->variant)
+                        ? mde::bucket_digest_pieces_sibling(a->variant) : a->variant;
+    if (mde::bucket_digest_pieces(sib)) {
       const uint64_t waves = (uint64_t)c->cus * (uint64_t)(c->digest_blocks_per_cu > 0 ? c->digest_blocks_per_cu : 4) * 4u *
                              (uint64_t)(c->digest_oversub > 0 ? c->digest_oversub : 1);
       const uint64_t share = bytes / waves;
       if (c->digest_oversub <= 1 && share >= kAutoPieceMinShare) {
         piece_bytes = share / kAutoPieces;
-        a->variant = kPiecesDigestVariant;
+        a->variant = sib;
       }
     }
   } else if (mde::bucket_digest_pieces(a->variant)) {
@@ -775,6 +786,7 @@ int mde_set_tuning(mde_ctx* c, int digest_variant, int digest_blocks_per_cu, int
   if (digest_variant >= mde::bucket_digest_variants())
     return set_err(c, MDE_E_INVAL, "digest variant %d out of range", digest_variant);
   c->digest_variant = digest_variant < 0 ? kDefaultDigestVariant : digest_variant;
+  c->digest_auto = digest_variant < 0;
   c->digest_cap = digest_blocks_per_cu < 0 ? kDefaultDigestCap : digest_blocks_per_cu;
   c->digest_oversub = digest_oversub < 0 ? kDefaultDigestOversub : (digest_oversub ? digest_oversub : 1);
   c->digest_blocks_per_cu = 0;  // re-query

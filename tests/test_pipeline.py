@@ -242,9 +242,10 @@ def test_stealing_skewed_arena_matches_torch_sums(engine):
 
 
 PIECES_VARIANT = 12  # digest.hip kVariants: U = 4, nontemporal, prefetched, interleaved pieces
+WINDOW_VARIANTS = (13, 14)  # the same with the bucket bounds in a register window (14: + pieces)
 
 
-def _skewed_arena(dev, variable, seed=11):
+def _skewed_arena(dev, variable, seed=11, P=37, B=100, max_count=8_000, big=(3_000_000, 1_500_000, 2_000_000)):
     """Ragged layout-A arena of ~100-300 MB for the digest work split: empty buckets and an empty
     partition, a few buckets of tens of MB, the arena start 5 bytes past an allocation. Fixed
     13-byte records (never 16-byte aligned) or variable lengths 0..40 (value_off). Returns the
@@ -252,11 +253,10 @@ def _skewed_arena(dev, variable, seed=11):
     import torch
     import mydatastore_amd as mde
     g = torch.Generator(device="cpu").manual_seed(seed)
-    P, B = 37, 100
-    counts = torch.randint(0, 8_000, (P * B,), generator=g)
-    counts[torch.randint(0, P * B, (900,), generator=g)] = 0
+    counts = torch.randint(0, max_count, (P * B,), generator=g)
+    counts[torch.randint(0, P * B, (P * B // 4,), generator=g)] = 0
     counts[5 * B:6 * B] = 0
-    counts[torch.tensor([17, 1234, 3001])] = torch.tensor([3_000_000, 1_500_000, 2_000_000])
+    counts[torch.tensor([17, 1234, 3001])] = torch.tensor(list(big))
     seg = torch.zeros(P * B + 1, dtype=torch.int64)
     seg[1:] = torch.cumsum(counts, 0)
     n = int(seg[-1])
@@ -287,8 +287,9 @@ def _skewed_arena(dev, variable, seed=11):
     return rec, counts, want, keep, (P, B)
 
 
+@pytest.mark.parametrize("variant", [PIECES_VARIANT, WINDOW_VARIANTS[1]])
 @pytest.mark.parametrize("variable", [False, True])
-def test_digest_pieces_ragged_arena_matches_torch_sums(engine, variable):
+def test_digest_pieces_ragged_arena_matches_torch_sums(engine, variable, variant):
     """Interleaved digest pieces (mde_set_digest_piece_bytes) from 1 KiB (a piece switch every
     few steps, pieces ending inside records and buckets) to 1 MiB, and one range per wave: the
     digests equal torch byte sums and the sizes the record counts, standalone and fused."""
@@ -298,7 +299,7 @@ def test_digest_pieces_ragged_arena_matches_torch_sums(engine, variable):
     engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     rec, counts, want, keep, (P, B) = _skewed_arena(dev, variable)
     roots = {}
-    engine.set_tuning(PIECES_VARIANT, -1)
+    engine.set_tuning(variant, -1)
     try:
         for pb in (0, 1024, 3072, 16384, 65536, 1 << 20):
             engine.set_digest_piece_bytes(pb)
@@ -370,3 +371,72 @@ def test_tagged_equals_layout_a_full_size(engine, value_len, n_keys, world):
             o = wb.build()
         for k in ("digest", "size", "items", "root"):
             assert torch.equal(o[k], ref[k]), (fused, k)
+
+
+@pytest.mark.parametrize("variable", [False, True])
+def test_many_small_buckets_every_static_variant(engine, variable):
+    """The reference's default PartitionBuckets = 1000 (config/default-config.yaml:8) with a few
+    records per bucket: a wave crosses a bucket boundary every few hundred bytes, so every window
+    reload and every crossing inside a 16-byte vector is exercised. 64 partitions x 1000 buckets,
+    0-19 records of 13 bytes (or 0-40-byte variable records) per bucket, a quarter empty, an empty
+    partition and three buckets of a few MB: every static variant (one range, pieces, register
+    window, both; pieces from 1 KiB) equals torch byte sums, standalone and fused."""
+    import torch
+    import mydatastore_amd as mde
+    dev = torch.device("cuda:0")
+    engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    rec, counts, want, keep, (P, B) = _skewed_arena(dev, variable, seed=5, P=64, B=1000, max_count=20,
+                                                    big=(300_000, 200_000, 250_000))
+    try:
+        for v in (11, PIECES_VARIANT) + WINDOW_VARIANTS:
+            engine.set_tuning(v, -1)
+            for pb in ((-1, 1024, 8192) if v in (PIECES_VARIANT, WINDOW_VARIANTS[1]) else (-1,)):
+                engine.set_digest_piece_bytes(pb)
+                for fused in (False, True):
+                    o = {"digest": torch.zeros(P * B, dtype=torch.int64, device=dev),
+                         "size": torch.zeros(P * B, dtype=torch.int32, device=dev),
+                         "items": torch.zeros(P, dtype=torch.int32, device=dev),
+                         "root": torch.zeros(P * 32, dtype=torch.uint8, device=dev)}
+                    to = mde.TreeOut(o["digest"].data_ptr(), o["size"].data_ptr(), o["items"].data_ptr(),
+                                     o["root"].data_ptr(), 0)
+                    if fused:
+                        engine.build_pipelined_async(rec, to)
+                        engine.build_pipeline_drain_async()
+                    else:
+                        engine.build_async(rec, to)
+                    engine.synchronize()
+                    assert torch.equal(o["digest"].cpu(), want), (v, pb, fused)
+                    assert torch.equal(o["size"].cpu().to(torch.int64), counts), (v, pb, fused)
+    finally:
+        engine.set_digest_piece_bytes(-1)
+        engine.set_tuning(-1, -1)
+
+
+@pytest.mark.parametrize("world", [1, 8])
+def test_default_variant_choice_b1000_full_size(engine, world):
+    """C4 with the reference's default PartitionBuckets = 1000 (10 KiB buckets): the automatic
+    choice (the register-window kernel, pieces at N=1) gives exactly what the round-1 kernel
+    (variant 11, one range per wave) gives, standalone and fused."""
+    import torch
+    from mydatastore_amd.workload import make_workload
+    w = make_workload(engine, n_partitions=1024, n_buckets=1000, value_len=1024, part_mode="mod",
+                      n_keys=10_000_000, rank=0, world=world)
+    try:
+        engine.set_tuning(11, -1)
+        engine.set_digest_piece_bytes(0)
+        ref = w.build()
+        engine.set_tuning(-1, -1)
+        engine.set_digest_piece_bytes(-1)
+        for fused in (False, True):
+            if fused:
+                o, to = w._outs()
+                engine.build_pipelined_async(w.rec, to)
+                engine.build_pipeline_drain_async()
+                engine.synchronize()
+            else:
+                o = w.build()
+            for k in ("digest", "size", "items", "root", "nodes"):
+                assert torch.equal(o[k], ref[k]), (fused, k)
+    finally:
+        engine.set_tuning(-1, -1)
+        engine.set_digest_piece_bytes(-1)

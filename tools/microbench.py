@@ -125,10 +125,13 @@ def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
                   "c4/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8),
                   "c3": dict(n_partitions=64, n_keys=64_000_000, part_mode="block", world=1),
                   "c4b": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1, layout="b"),
-                  "c4b/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8, layout="b")}
+                  "c4b/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8, layout="b"),
+                  # the reference's default PartitionBuckets (config/default-config.yaml:8)
+                  "c4k": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1, n_buckets=1000),
+                  "c4k/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8, n_buckets=1000)}
     res = []
     for shape in shapes:
-        w = make_workload(eng, n_buckets=64, value_len=1024, rank=0, **shape_args[shape])
+        w = make_workload(eng, **{"n_buckets": 64, "value_len": 1024, "rank": 0, **shape_args[shape]})
         sets = [w._outs() for _ in range(2)]
         n_steps = 10
 
@@ -140,14 +143,23 @@ def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
         ref = None
         td = {p: [] for p in pieces}
         tf = {p: [] for p in pieces}
+        tt = {p: [] for p in pieces}
         for _ in range(reps):
             for p in pieces:
-                # "d": the defaults (automatic pieces); "x": the default variant with one range per
-                # wave; a number: the interleaved-pieces variant at that piece size
-                eng.set_tuning(-1 if p in ("d", "x") else 12, -1)
-                eng.set_digest_piece_bytes({"d": -1, "x": 0}.get(p, None) if p in ("d", "x") else int(p))
+                # "d": the defaults (automatic variant and pieces); "x": variant 11 (round 1's
+                # default) with one range per wave; a number: the interleaved-pieces variant at that piece size; "v13d",
+                # "v13x", "v14_1048576": variant 13 / 14 with the same piece settings
+                v, rest = (11 if p == "x" else -1), p
+                if p.startswith("v"):
+                    num = "".join(ch for ch in p[1:] if ch.isdigit())
+                    v, rest = int(num), p[1 + len(num):].lstrip("_")
+                elif p not in ("d", "x"):
+                    v = 12
+                eng.set_tuning(v, -1)
+                eng.set_digest_piece_bytes({"d": -1, "x": 0}[rest] if rest in ("d", "x") else int(rest))
                 td[p].append(timeit(w.digest_async, reps=10, warm=2))
                 tf[p].append(timeit(fused, reps=1, warm=1) / n_steps)
+                tt[p].append(timeit(w.tree_async, reps=5, warm=1))
                 o = w.build()
                 if ref is None:
                     ref = o["root"].cpu()
@@ -158,7 +170,8 @@ def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
             md, mf = float(np.median(td[p])), float(np.median(tf[p]))
             res.append({"shape": shape, "piece_bytes": p, "bytes": w.value_bytes, "digest_us": round(md, 2),
                         "digest_GBps": round(w.value_bytes / md / 1e3, 1), "fused_us_per_build": round(mf, 2),
-                        "fused_GBps": round(w.value_bytes / mf / 1e3, 1)})
+                        "fused_GBps": round(w.value_bytes / mf / 1e3, 1),
+                        "tree_us": round(float(np.median(tt[p])), 2)})
             print(json.dumps(res[-1]), flush=True)
         del w, sets
         torch.cuda.empty_cache()
