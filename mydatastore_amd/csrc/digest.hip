@@ -187,6 +187,19 @@ __device__ __forceinline__ uint32_t digest_range(const DigestLaunch& a, uint64_t
   return s;
 }
 
+// Inclusive prefix sum over the 64 lanes (lane order), exact when the total fits 32 bits: DPP
+// row shifts within each row of 16 lanes, then row_bcast:15 / row_bcast:31 across rows (gfx9).
+// Call with all 64 lanes active.
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
 // Sum of the 64 lanes' u32 values, exact when it fits 32 bits: DPP within each row of 16 lanes
 // (no LDS round trips), then the four row sums by readlane. Call with all 64 lanes active.
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
@@ -277,6 +290,73 @@ __device__ __forceinline__ uint32_t digest_range_win(const DigestLaunch& a, uint
       fs[u] = __builtin_amdgcn_sad_u8(v[u].w, 0u, t);
     }
     const uint64_t q = min(p + kStep, end);
+    // Two or more bucket starts inside the step (buckets of a few hundred bytes, e.g. 8-byte
+    // timestamps at B = 1,000): segmented sums by a prefix scan instead of one pass per bucket.
+    // E[u] = bytes of the step before vector (u, lane) in address order; window lane i reads
+    // F(y_i) = bytes before its bucket's start y_i (clamped to the step), so bucket i's bytes in
+    // the step are F(y_{i+1}) - F(y_i): one scan, a few shuffles and one reduction per step,
+    // whatever the number of buckets.
+    if (__popcll(__ballot(win.start > p && win.start < q)) >= 2) {
+      uint32_t E[U];
+      uint32_t total = 0;
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t incl = wave_incl_scan_u32(fs[u]);
+        E[u] = total + incl - fs[u];
+        total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      }
+      const uint32_t qrel = (uint32_t)(q - p);
+      for (;;) {
+        const uint64_t st = win.start;
+        const uint32_t y = st <= p ? 0u : (st >= q ? qrel : (uint32_t)(st - p));
+        const uint32_t vi = y >> 4, ui = vi >> 6, li = vi & 63u, boff = y & 15u;
+        uint32_t e = 0;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint32_t eu = (uint32_t)__shfl((int)E[u], (int)li);
+          e = ui == (uint32_t)u ? eu : e;
+        }
+        if (__ballot(boff != 0u)) {  // some bucket starts inside a vector: add its leading bytes
+          u32x4 w = {0u, 0u, 0u, 0u};
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const u32x4 g = {(uint32_t)__shfl((int)v[u].x, (int)li), (uint32_t)__shfl((int)v[u].y, (int)li),
+                             (uint32_t)__shfl((int)v[u].z, (int)li), (uint32_t)__shfl((int)v[u].w, (int)li)};
+            if (ui == (uint32_t)u) w = g;
+          }
+          e = masked_sum16(w, 0, (int64_t)boff, e);
+        }
+        const uint32_t F = vi >= (uint32_t)(kStep / 16) ? total : e;
+        const uint32_t c = (uint32_t)__shfl_down((int)F, 1) - F;  // bucket base + lane, lanes 0..62
+        const uint32_t k = s - win.base;
+        const uint32_t cnt = (uint32_t)__popcll(__ballot(st < q));
+        const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)k);
+        if (lane == 0) acc += ck;
+        if (cnt == 64u) {  // the step runs past the window: buckets k..62 all end inside it
+          retire(readlane64(st, k + 1u));
+          if ((uint32_t)lane > k && lane < 63) wsum = c;
+          window_out();
+          win.load(d, win.base + 63u, lane);
+          s = win.base;
+          sb = readlane64(win.start, 0);
+          se = readlane64(win.start, 1);
+          bfrom = sb;
+          continue;
+        }
+        const uint32_t m = cnt - 1u;  // the last bucket starting before q: it runs on past q
+        if (m > k) {
+          retire(readlane64(st, k + 1u));
+          if ((uint32_t)lane > k && (uint32_t)lane < m) wsum = c;
+          s = win.base + m;
+          sb = readlane64(st, m);
+          se = readlane64(st, m + 1u);
+          bfrom = sb;
+          const uint32_t cm = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)m);
+          acc = lane == 0 ? cm : 0u;
+        }
+        return;
+      }
+    }
     for (;;) {
       const uint64_t lo = max(sb, p), hi = min(se, q);
       if (lo < hi) {

@@ -412,15 +412,19 @@ def test_many_small_buckets_every_static_variant(engine, variable):
         engine.set_tuning(-1, -1)
 
 
-@pytest.mark.parametrize("world", [1, 8])
-def test_default_variant_choice_b1000_full_size(engine, world):
-    """C4 with the reference's default PartitionBuckets = 1000 (10 KiB buckets): the automatic
-    choice (the register-window kernel, pieces at N=1) gives exactly what the round-1 kernel
-    (variant 11, one range per wave) gives, standalone and fused."""
+@pytest.mark.parametrize("value_len,n_keys,n_buckets,world", [
+    (1024, 10_000_000, 1000, 1), (1024, 10_000_000, 1000, 8), (8, 20_000_000, 1000, 1),
+    (8, 20_000_000, 64, 1), (64, 4_000_000, 1000, 1), (13, 6_000_000, 1000, 1)])
+def test_default_variant_choice_b1000_full_size(engine, value_len, n_keys, n_buckets, world):
+    """The reference's default PartitionBuckets = 1000 (C4: 10 KiB buckets) and production-sized
+    values (8-byte timestamps: ~160 B buckets, several bucket starts per step, the prefix-scan
+    path; 13-byte records: starts inside vectors): the automatic choice (the register-window
+    kernel, pieces for large shares) gives exactly what the round-1 kernel (variant 11, one range
+    per wave) gives, standalone and fused."""
     import torch
     from mydatastore_amd.workload import make_workload
-    w = make_workload(engine, n_partitions=1024, n_buckets=1000, value_len=1024, part_mode="mod",
-                      n_keys=10_000_000, rank=0, world=world)
+    w = make_workload(engine, n_partitions=1024, n_buckets=n_buckets, value_len=value_len, part_mode="mod",
+                      n_keys=n_keys, rank=0, world=world)
     try:
         engine.set_tuning(11, -1)
         engine.set_digest_piece_bytes(0)

@@ -128,7 +128,13 @@ def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
                   "c4b/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8, layout="b"),
                   # the reference's default PartitionBuckets (config/default-config.yaml:8)
                   "c4k": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1, n_buckets=1000),
-                  "c4k/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8, n_buckets=1000)}
+                  "c4k/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8, n_buckets=1000),
+                  # production values: the 8-byte LE write timestamp (main/manager.go:816)
+                  "ts8": dict(n_partitions=1024, n_keys=100_000_000, part_mode="mod", world=1, value_len=8),
+                  "ts8k": dict(n_partitions=1024, n_keys=100_000_000, part_mode="mod", world=1, value_len=8,
+                               n_buckets=1000),
+                  "v64k": dict(n_partitions=1024, n_keys=20_000_000, part_mode="mod", world=1, value_len=64,
+                               n_buckets=1000)}
     res = []
     for shape in shapes:
         w = make_workload(eng, **{"n_buckets": 64, "value_len": 1024, "rank": 0, **shape_args[shape]})
