@@ -44,6 +44,9 @@ CONFIGS = {
     "c3": (64_000_000, 64, 1024, 64, "block",
            "C3: 64 partitions x 1M keys x 1 KiB values, B=64"),
     "c1": (1_000, 1, 64, 64, "block", "C1: 1 partition x 1k keys x 64 B values, B=64"),
+    # not a BASELINE config: C4 at the reference's default PartitionBuckets (config/default-config.yaml:8)
+    "c4k": (10_000_000, 1024, 1024, 1000, "mod",
+            "C4 at B=1000 (the reference's default PartitionBuckets): 10M keys x 1 KiB values, 1024 partitions"),
 }
 
 
