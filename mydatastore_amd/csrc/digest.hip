@@ -97,18 +97,10 @@ __device__ __forceinline__ uint32_t masked_sum16(u32x4 v, int64_t a, int64_t b, 
 }
 
 __device__ __forceinline__ void flush(unsigned long long* sums, uint32_t s, uint32_t acc) {
-#ifdef MDE_PROBE_NO_REDUCE  // A/B probe only (wrong sums): the lane-0 partial, no cross-lane sum
-  const unsigned long long v = acc;
-#else
   unsigned long long v = acc;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-#endif
-#ifdef MDE_PROBE_NO_ATOMIC  // A/B probe only (wrong sums): the reduction without its atomic
-  if ((threadIdx.x & 63) == 0 && v == 0x123456789abcdefull) atomicAdd(sums + s, v);
-#else
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(sums + s, v);
-#endif
 }
 
 template <int U, bool NT>
