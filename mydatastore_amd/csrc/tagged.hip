@@ -165,26 +165,73 @@ __device__ __forceinline__ void tagged_body(const TaggedLaunch& a, uint32_t bloc
   const uint32_t vsh = V >= kStep / 64 && (V & (V - 1)) == 0 ? (uint32_t)__builtin_ctzll(V) : 0u;
   const uint32_t vmask = (uint32_t)V - 1u;
   const bool fast_ok = vsh != 0 && !straddles && w.sum != nullptr && start == beg;
+  // Small records (8 or 16 bytes: production values are 8-byte timestamps,
+  // main/manager.go:816), each vector holding 16 / V whole records: every lane bins its own
+  // records, whose tags it prefetches with the step (16 / V u16 loads per vector).
+  const uint32_t ssh = (V == 8 || V == 16) ? (uint32_t)__builtin_ctzll(V) : 0u;
+  const bool small = ssh != 0 && (a.shift & (V - 1)) == 0 && w.sum != nullptr && start == beg;
   const uint64_t r_last = r_hi - 1;
   auto load_tags = [&](uint64_t p, uint64_t& r_first) -> uint32_t {
     r_first = rec_at(max(p, start));
     return a.tag[min(r_first + (uint64_t)lane, r_last)];
   };
+  constexpr int kR = 2;  // tags per vector kept per lane (16 / V <= 2)
+  auto load_small_tags = [&](uint64_t p, uint32_t (&t)[kU][kR]) {
+    const uint32_t per = 16u >> ssh;
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const uint64_t rv = r0 + (((p - pos0) + (uint64_t)u * 1024u + (uint64_t)lane * 16u) >> ssh);
+#pragma unroll
+      for (int j = 0; j < kR; j++)
+        t[u][j] = (uint32_t)j < per ? (uint32_t)a.tag[min(rv + (uint64_t)j, r_last)] : 0u;
+    }
+  };
   u32x4 cur[kU], nxt[kU];
+  uint32_t ctag[kU][kR], ntag[kU][kR];
   uint64_t cur_r0 = 0, nxt_r0 = 0;
-  uint32_t cur_tags = load_tags(beg, cur_r0), nxt_tags = 0;
+  uint32_t cur_tags = 0, nxt_tags = 0;
+  if (small)
+    load_small_tags(beg, ctag);
+  else
+    cur_tags = load_tags(beg, cur_r0);
   load_step(cur, lane_base, beg, end, lane);
   for (uint64_t p = beg; p < end; p += kStep) {
     const uint64_t pn = p + kStep;
     if (pn < end) {
-      nxt_tags = load_tags(pn, nxt_r0);
+      if (small)
+        load_small_tags(pn, ntag);
+      else
+        nxt_tags = load_tags(pn, nxt_r0);
       load_step(nxt, lane_base, pn, end, lane);
     }
-    // Fast step (wave-uniform): power-of-two records of >= kStep/64 B on 16-byte boundaries, the whole
-    // step inside [start, end) and inside partition q. Every vector then lies in one record, the
-    // record index is a shift, and a step holds <= 64 records (tags by shuffle): per vector 4
-    // v_sad_u8 + one ds_add, in 32-bit arithmetic.
-    if (fast_ok && pn <= end && r0 + ((pn - 1 - pos0) >> vsh) < q_end) {
+    // Small-record step: the whole step inside [start, end) and inside partition q; per vector
+    // 16 / V byte sums of V bytes (v_sad_u8 per dword), each binned with its own tag.
+    if (small && pn <= end && r0 + ((pn - 1 - pos0) >> ssh) < q_end) {
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const uint32_t d0 = __builtin_amdgcn_sad_u8(cur[u].x, 0u, 0u), d1 = __builtin_amdgcn_sad_u8(cur[u].y, 0u, 0u);
+        const uint32_t d2 = __builtin_amdgcn_sad_u8(cur[u].z, 0u, 0u), d3 = __builtin_amdgcn_sad_u8(cur[u].w, 0u, 0u);
+        uint32_t sj[kR];
+        if (ssh == 4) {
+          sj[0] = d0 + d1 + d2 + d3;
+          sj[1] = 0u;
+        } else {
+          sj[0] = d0 + d1;
+          sj[1] = d2 + d3;
+        }
+#pragma unroll
+        for (int j = 0; j < kR; j++) {
+          if ((uint32_t)j >= (16u >> ssh)) break;
+          const uint32_t b = min(ctag[u][j], a.B - 1);
+          atomicAdd(w.sum + b * L + slot, sj[j]);
+          atomicAdd(w.cnt + b, 1u);
+        }
+      }
+    } else if (fast_ok && pn <= end && r0 + ((pn - 1 - pos0) >> vsh) < q_end) {
+      // Fast step (wave-uniform): power-of-two records of >= kStep/64 B on 16-byte boundaries, the
+      // whole step inside [start, end) and inside partition q. Every vector then lies in one
+      // record, the record index is a shift, and a step holds <= 64 records (tags by shuffle):
+      // per vector 4 v_sad_u8 + one ds_add, in 32-bit arithmetic.
       const uint32_t xr0 = (uint32_t)(p - pos0) + (uint32_t)lane * 16u;
       const uint32_t k0 = (uint32_t)(cur_r0 - r0);
 #pragma unroll
@@ -215,7 +262,8 @@ __device__ __forceinline__ void tagged_body(const TaggedLaunch& a, uint32_t bloc
         const uint32_t s = (c0 == x && c1 == x + 16) ? full_sum16(cur[u])
                                                       : masked_sum16(cur[u], (int)(c0 - x), (int)(c1 - x));
         const uint32_t cnt = rs >= lo ? 1u : 0u;  // this lane holds the record's first byte
-        const uint32_t tg = (j == 0 && k < 64) ? t0 : (j == 1 && k + 1 < 64) ? t1 : (uint32_t)a.tag[r];
+        // (small-record mode prefetches per-lane tags, not the step's first 64: load directly)
+        const uint32_t tg = (!small && j == 0 && k < 64) ? t0 : (!small && j == 1 && k + 1 < 64) ? t1 : (uint32_t)a.tag[r];
         const uint32_t b = min(tg, a.B - 1);  // bad tags never fault (the host API rejects them)
         if (w.sum && r < q_end) {
           if (s) atomicAdd(w.sum + (uint64_t)b * L + slot, s);
@@ -236,7 +284,11 @@ __device__ __forceinline__ void tagged_body(const TaggedLaunch& a, uint32_t bloc
       q_end = a.part_rec[q + 1];
     }
 #pragma unroll
-    for (int u = 0; u < kU; u++) cur[u] = nxt[u];
+    for (int u = 0; u < kU; u++) {
+      cur[u] = nxt[u];
+#pragma unroll
+      for (int j = 0; j < kR; j++) ctag[u][j] = ntag[u][j];
+    }
     cur_tags = nxt_tags;
     cur_r0 = nxt_r0;
   }

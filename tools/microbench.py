@@ -133,6 +133,10 @@ def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
                   "ts8": dict(n_partitions=1024, n_keys=100_000_000, part_mode="mod", world=1, value_len=8),
                   "ts8k": dict(n_partitions=1024, n_keys=100_000_000, part_mode="mod", world=1, value_len=8,
                                n_buckets=1000),
+                  "c4bk": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1, layout="b",
+                               n_buckets=1000),
+                  "ts8bk": dict(n_partitions=1024, n_keys=100_000_000, part_mode="mod", world=1, value_len=8,
+                                n_buckets=1000, layout="b"),
                   "v64k": dict(n_partitions=1024, n_keys=20_000_000, part_mode="mod", world=1, value_len=64,
                                n_buckets=1000)}
     res = []
