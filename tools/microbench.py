@@ -113,6 +113,27 @@ def bench_ab(eng, variants, worlds=(1, 8), reps=5, cap=2):
     return res
 
 
+# Workload shapes for the digest probes (make_workload arguments over the C4 defaults).
+SHAPES = {"c4": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1),
+              "c4/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8),
+              "c3": dict(n_partitions=64, n_keys=64_000_000, part_mode="block", world=1),
+              "c4b": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1, layout="b"),
+              "c4b/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8, layout="b"),
+              # the reference's default PartitionBuckets (config/default-config.yaml:8)
+              "c4k": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1, n_buckets=1000),
+              "c4k/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8, n_buckets=1000),
+              # production values: the 8-byte LE write timestamp (main/manager.go:816)
+              "ts8": dict(n_partitions=1024, n_keys=100_000_000, part_mode="mod", world=1, value_len=8),
+              "ts8k": dict(n_partitions=1024, n_keys=100_000_000, part_mode="mod", world=1, value_len=8,
+                           n_buckets=1000),
+              "c4bk": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1, layout="b",
+                           n_buckets=1000),
+              "ts8bk": dict(n_partitions=1024, n_keys=100_000_000, part_mode="mod", world=1, value_len=8,
+                            n_buckets=1000, layout="b"),
+              "v64k": dict(n_partitions=1024, n_keys=20_000_000, part_mode="mod", world=1, value_len=64,
+                           n_buckets=1000)}
+
+
 def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
     """Interleaved A/B of the layout-A digest work split: the defaults ("d", automatic pieces),
     the default variant with one contiguous range per wave ("x") and the interleaved-pieces
@@ -121,27 +142,9 @@ def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
     every setting's roots must equal the first setting's."""
     import torch
     from mydatastore_amd.workload import make_workload
-    shape_args = {"c4": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1),
-                  "c4/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8),
-                  "c3": dict(n_partitions=64, n_keys=64_000_000, part_mode="block", world=1),
-                  "c4b": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1, layout="b"),
-                  "c4b/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8, layout="b"),
-                  # the reference's default PartitionBuckets (config/default-config.yaml:8)
-                  "c4k": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1, n_buckets=1000),
-                  "c4k/8": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=8, n_buckets=1000),
-                  # production values: the 8-byte LE write timestamp (main/manager.go:816)
-                  "ts8": dict(n_partitions=1024, n_keys=100_000_000, part_mode="mod", world=1, value_len=8),
-                  "ts8k": dict(n_partitions=1024, n_keys=100_000_000, part_mode="mod", world=1, value_len=8,
-                               n_buckets=1000),
-                  "c4bk": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", world=1, layout="b",
-                               n_buckets=1000),
-                  "ts8bk": dict(n_partitions=1024, n_keys=100_000_000, part_mode="mod", world=1, value_len=8,
-                                n_buckets=1000, layout="b"),
-                  "v64k": dict(n_partitions=1024, n_keys=20_000_000, part_mode="mod", world=1, value_len=64,
-                               n_buckets=1000)}
     res = []
     for shape in shapes:
-        w = make_workload(eng, **{"n_buckets": 64, "value_len": 1024, "rank": 0, **shape_args[shape]})
+        w = make_workload(eng, **{"n_buckets": 64, "value_len": 1024, "rank": 0, **SHAPES[shape]})
         sets = [w._outs() for _ in range(2)]
         n_steps = 10
 
@@ -186,6 +189,18 @@ def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
         del w, sets
         torch.cuda.empty_cache()
     return res
+
+
+def bench_digest_only(eng, shape, reps=5):
+    """The default digest kernel alone on one workload shape, `reps` launches (for rocprofv3 PMC
+    passes: no other kernels between the workload build and the launches but its own)."""
+    from mydatastore_amd.workload import make_workload
+    w = make_workload(eng, **{"n_buckets": 64, "value_len": 1024, "rank": 0, **SHAPES[shape]})
+    us = timeit(w.digest_async, reps=reps, warm=1)
+    r = {"shape": shape, "bytes": w.value_bytes, "digest_us": round(us, 2),
+         "digest_GBps": round(w.value_bytes / us / 1e3, 1)}
+    print(json.dumps(r), flush=True)
+    return r
 
 
 def bench_verify(eng, P=1024, B=64, R=2, mode=0):
@@ -296,6 +311,9 @@ def main():
             parts = w.split(":")
             shapes = tuple(parts[2].split(",")) if len(parts) > 2 else ("c4", "c4/8", "c3")
             out["pieces"] = bench_pieces(eng, parts[1].split(","), shapes)
+        if w.startswith("digestonly:"):  # digestonly:ts8k[:reps] -- the digest kernel alone (PMC runs)
+            parts = w.split(":")
+            out["digestonly"] = bench_digest_only(eng, parts[1], int(parts[2]) if len(parts) > 2 else 5)
         if w.startswith("digest:"):
             out["digest"] = bench_digest(eng, [int(x) for x in w.split(":")[1].split(",")])
     Path("gpurun_out").mkdir(exist_ok=True)
