@@ -848,28 +848,43 @@ hipError_t launch_bucket_digest(const DigestLaunch& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Partitions per tree wave in the fused step: up to 16, as many as the LDS budget holds.
+// Partitions per tree wave in the fused step: up to 8, as many as the LDS budget holds. A packed
+// tree wave's critical path grows with Q (B = 64: 8.4 node-hash passes at Q = 8, 13.8 at Q = 16);
+// on small arenas it outlasts the stream: 800 MB of 8-byte values at B = 64 took 137-141 us per
+// fused build at Q = 2-8 vs 165-167 at Q = 16, C4 and its N = 8 shard unchanged within noise
+// (profiles/r02af_treeq.jsonl).
 uint32_t build_step_tree_q(uint32_t B) {
   const uint32_t n1 = (B + 1) / 2;
   const uint32_t per = (n1 + (n1 + 1) / 2) * 8u * 4u;  // bytes of level buffers per partition
   const uint32_t q = (kStepTreeLdsMax - 64u) / per;
 #ifndef MDE_STEP_TREE_QMAX
-#define MDE_STEP_TREE_QMAX 16u
+#define MDE_STEP_TREE_QMAX 8u
 #endif
   return q > MDE_STEP_TREE_QMAX ? MDE_STEP_TREE_QMAX : q;
 }
 
 bool build_step_fusable(uint32_t B) { return B >= 1 && build_step_tree_q(B) >= 1; }
 
+void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint32_t* lds_bytes) {
+  // Measured and rejected for Q = 1 (B > 128): a whole 4-wave workgroup per partition
+  // (tree_body), whose critical path is 10 node-hash passes instead of 18 at B = 1,000. 800 MB of
+  // 8-byte values at B = 1,000 went 247 -> 235 us per fused build, but C4 at B = 1,000 went
+  // 1,620 -> 1,657 us and its N = 8 shard 220 -> 223 us (profiles/r02af_treewide.jsonl).
+  const uint32_t q = build_step_tree_q(B);
+  *Q = q;
+  *blocks = q ? (P + q - 1) / q : 0;
+  *lds_bytes = packed_tree_lds_words(B, q) * 4u;
+}
+
 hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st) {
   uint32_t tree_blocks = 0, Q = 0, lds = a.lds_bytes;
   if (t && t->P) {
     if (!build_step_fusable(t->B) || !t->sums_in) return hipErrorInvalidValue;
-    Q = build_step_tree_q(t->B);
-    tree_blocks = (t->P + Q - 1) / Q;
+    uint32_t tree_lds = 0;
+    plan_step_trees(t->B, t->P, &Q, &tree_blocks, &tree_lds);
     // every workgroup of the dispatch reserves the tree waves' LDS; kStepTreeLdsMax keeps the
     // streaming grid fully resident
-    lds = std::max<uint32_t>(lds, packed_tree_lds_words(t->B, Q) * 4u);
+    lds = std::max<uint32_t>(lds, tree_lds);
   }
   const uint32_t digest_blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);
   if (tree_blocks + digest_blocks == 0) return hipSuccess;

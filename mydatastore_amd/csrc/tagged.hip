@@ -301,9 +301,9 @@ __global__ __launch_bounds__(kThreads) void tagged_digest_kernel(TaggedLaunch a)
 }
 
 // Fused build step for layout B (see build_step_kernel in digest.hip): the binning workgroups
-// come first, then tree_blocks workgroups build the previous build's trees (tree_body_packed,
-// first wave only). Both roles share one LDS reservation, the bins of two waves (33 KiB at
-// B = 64), so four binning workgroups fill a CU's LDS: tree workgroups placed first would each
+// come first, then tree_blocks workgroups build the previous build's trees (tree_body_packed). Both
+// roles share one LDS reservation, the bins of two waves (33 KiB at B = 64), so four binning
+// workgroups fill a CU's LDS: tree workgroups placed first would each
 // hold back a binning workgroup until the tree is done (measured: 1.584 vs 1.551 ms at C4 with
 // the trees last); placed last they start in LDS left over and in the first slots that free up.
 __global__ __launch_bounds__(kThreads) void tagged_step_kernel(TaggedLaunch a, TreeLaunch t, uint32_t tree_blocks,
@@ -353,9 +353,9 @@ hipError_t launch_tagged_step(TaggedLaunch& a, const TreeLaunch* t, hipStream_t 
   size_t lds = bins;
   if (t && t->P) {
     if (!build_step_fusable(t->B) || !t->sums_in) return hipErrorInvalidValue;
-    Q = build_step_tree_q(t->B);
-    tree_blocks = (t->P + Q - 1) / Q;
-    lds = std::max<size_t>(lds, (size_t)packed_tree_lds_words(t->B, Q) * 4u);
+    uint32_t tree_lds = 0;
+    plan_step_trees(t->B, t->P, &Q, &tree_blocks, &tree_lds);
+    lds = std::max<size_t>(lds, (size_t)tree_lds);
   }
   const uint32_t blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);
   if (tree_blocks + blocks == 0) return hipSuccess;
