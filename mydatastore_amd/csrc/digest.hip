@@ -228,7 +228,7 @@ __device__ __forceinline__ void load_step_clamped(u32x4 (&v)[U], const u32x4* ba
   }
 }
 
-template <int U, bool NT, int PIPE>
+template <int U, bool NT, int PIPE, bool A8>
 __device__ __forceinline__ uint32_t digest_range_win(const DigestLaunch& a, uint64_t beg, uint64_t end, uint32_t s_lo,
                                                      int lane) {
   constexpr uint64_t kStep = 1024ull * U;
@@ -309,14 +309,29 @@ __device__ __forceinline__ uint32_t digest_range_win(const DigestLaunch& a, uint
           e = ui == (uint32_t)u ? eu : e;
         }
         if (__ballot(boff != 0u)) {  // some bucket starts inside a vector: add its leading bytes
-          u32x4 w = {0u, 0u, 0u, 0u};
+          if (A8 && !__ballot(boff & 7u)) {
+            // every such start 8 bytes in (8-byte records): the vector's first two dwords, summed
+            // at the owner lane. Standalone digest kernel only (A8): in the fused step's kernel
+            // the extra registers (95 -> 99 VGPRs) cost 64-byte values at B = 1,000 ~5 % per
+            // build, and there the trees, not the digest, bound 8-byte values at B = 1,000.
+            uint32_t h = 0;
 #pragma unroll
-          for (int u = 0; u < U; u++) {
-            const u32x4 g = {(uint32_t)__shfl((int)v[u].x, (int)li), (uint32_t)__shfl((int)v[u].y, (int)li),
-                             (uint32_t)__shfl((int)v[u].z, (int)li), (uint32_t)__shfl((int)v[u].w, (int)li)};
-            if (ui == (uint32_t)u) w = g;
+            for (int u = 0; u < U; u++) {
+              const uint32_t lo8 = __builtin_amdgcn_sad_u8(v[u].y, 0u, __builtin_amdgcn_sad_u8(v[u].x, 0u, 0u));
+              const uint32_t hu = (uint32_t)__shfl((int)lo8, (int)li);
+              h = ui == (uint32_t)u ? hu : h;
+            }
+            e += boff ? h : 0u;
+          } else {
+            u32x4 w = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+              const u32x4 g = {(uint32_t)__shfl((int)v[u].x, (int)li), (uint32_t)__shfl((int)v[u].y, (int)li),
+                               (uint32_t)__shfl((int)v[u].z, (int)li), (uint32_t)__shfl((int)v[u].w, (int)li)};
+              if (ui == (uint32_t)u) w = g;
+            }
+            e = masked_sum16(w, 0, (int64_t)boff, e);
           }
-          e = masked_sum16(w, 0, (int64_t)boff, e);
         }
         const uint32_t F = vi >= (uint32_t)(kStep / 16) ? total : e;
         const uint32_t c = (uint32_t)__shfl_down((int)F, 1) - F;  // bucket base + lane, lanes 0..62
@@ -393,7 +408,7 @@ __device__ __forceinline__ uint32_t digest_range_win(const DigestLaunch& a, uint
 
 // One contiguous range of wave_bytes per wave. `block` = this workgroup's index among the digest
 // workgroups of the launch.
-template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false>
 __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t block) {
   // Streaming waves issue little VALU; when tree waves (back-to-back SHA-256 VALU) share the CU,
   // a raised priority keeps the loads flowing and the SHA waves take the slack.
@@ -407,7 +422,7 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
   const uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
   if (beg >= last) return;
   if (WIN)
-    digest_range_win<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), 0u, lane);
+    digest_range_win<U, NT, PIPE, A8>(a, beg, min(beg + a.wave_bytes, last), 0u, lane);
   else
     digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), 0u, lane);
 }
@@ -415,7 +430,7 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
 // Interleaved pieces (DigestLaunch::pieces): the wave streams `pieces` ranges of wave_bytes,
 // piece_stride apart, so the whole grid sweeps the arena front to back together. Each piece is a
 // digest_range (its own bucket search, from the previous piece's last bucket on, and flush).
-template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false>
 __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32_t block) {
   if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const int lane = threadIdx.x & 63;
@@ -427,7 +442,7 @@ __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32
   uint32_t s = 0;
   uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
   for (uint32_t j = 0; j < a.pieces && beg < last; j++, beg += a.piece_stride)
-    s = WIN ? digest_range_win<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), s, lane)
+    s = WIN ? digest_range_win<U, NT, PIPE, A8>(a, beg, min(beg + a.wave_bytes, last), s, lane)
             : digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), s, lane);
 }
 
@@ -626,19 +641,19 @@ __device__ __forceinline__ void digest_body_steal(const DigestLaunch& a, uint32_
 
 // MODE: 0 = one static range per wave, 1 = tail stealing, 2 = interleaved pieces; 3 and 4 = 0 and
 // 2 with the bucket bounds in a register window (SegWindow).
-template <int U, bool NT, int PIPE, int PRIO, int MODE>
+template <int U, bool NT, int PIPE, int PRIO, int MODE, bool A8>
 __device__ __forceinline__ void digest_dispatch(const DigestLaunch& a, uint32_t block) {
   if (MODE == 1)
     digest_body_steal<U, NT, PRIO>(a, block);
   else if (MODE == 2 || MODE == 4)
-    digest_body_pieces<U, NT, PIPE, PRIO, MODE == 4>(a, block);
+    digest_body_pieces<U, NT, PIPE, PRIO, MODE == 4, A8>(a, block);
   else
-    digest_body<U, NT, PIPE, PRIO, MODE == 3>(a, block);
+    digest_body<U, NT, PIPE, PRIO, MODE == 3, A8>(a, block);
 }
 
 template <int U, bool NT, int PIPE, int PRIO = 0, int MODE = 0>
 __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a) {
-  digest_dispatch<U, NT, PIPE, PRIO, MODE>(a, blockIdx.x);
+  digest_dispatch<U, NT, PIPE, PRIO, MODE, true>(a, blockIdx.x);
 }
 
 
@@ -672,7 +687,7 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
   }
   const uint32_t db = blockIdx.x - tree_blocks;
 #endif
-  digest_dispatch<U, NT, PIPE, PRIO, MODE>(a, db);
+  digest_dispatch<U, NT, PIPE, PRIO, MODE, false>(a, db);
 }
 
 // One-launch build of a small arena (the synchronous one-partition calls of VerifyEpoch). Digest
