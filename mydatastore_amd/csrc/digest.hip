@@ -674,14 +674,14 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
 #ifdef MDE_STEP_TREES_LAST
   const uint32_t digest_blocks = gridDim.x - tree_blocks;
   if (blockIdx.x >= digest_blocks) {
-    tree_body_packed(t, Q, blockIdx.x - digest_blocks, lds);
+    step_trees(t, Q, blockIdx.x - digest_blocks, lds);
     return;
   }
   const uint32_t db = blockIdx.x;
 #else
   if (blockIdx.x < tree_blocks) {
 #ifndef MDE_STEP_SKIP_TREES  // probe only: the dispatch shape without the tree work
-    tree_body_packed(t, Q, blockIdx.x, lds);
+    step_trees(t, Q, blockIdx.x, lds);
 #endif
     return;
   }
@@ -881,11 +881,21 @@ uint32_t build_step_tree_q(uint32_t B) {
 bool build_step_fusable(uint32_t B) { return B >= 1 && build_step_tree_q(B) >= 1; }
 
 void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint32_t* lds_bytes) {
-  // Measured and rejected for Q = 1 (B > 128): a whole 4-wave workgroup per partition
-  // (tree_body), whose critical path is 10 node-hash passes instead of 18 at B = 1,000. 800 MB of
-  // 8-byte values at B = 1,000 went 247 -> 235 us per fused build, but C4 at B = 1,000 went
-  // 1,620 -> 1,657 us and its N = 8 shard 220 -> 223 us (profiles/r02af_treewide.jsonl).
+  // One packed tree wave per partition (Q = 1, B > 128) has a critical path of 34 dependent
+  // compressions at B = 1,000; two waves per partition (tree_body over 128 threads) cut it to 24.
+  // With many partitions the trees, not the stream, bound a small arena: 800 MB of 8-byte values
+  // at B = 1,000 over 1,024 partitions went 248 -> 234 us per fused build, C4 at B = 1,000 and
+  // 64-byte values unchanged; with few partitions the packed wave hides behind the stream (the
+  // N = 8 shard at B = 1,000, 128 partitions: 218 vs 221 us), hence the partition threshold
+  // (profiles/r02ak_half.jsonl). Four waves per partition measured worse at C4 (1,645 vs
+  // 1,615 us; r02af_treewide.jsonl).
   const uint32_t q = build_step_tree_q(B);
+  if (q == 1 && (B + 1) / 2 > 64 && P >= kStepTreeWideMinPartitions) {
+    *Q = 0;
+    *blocks = P;
+    *lds_bytes = tree_lds_words(B) * 4u;
+    return;
+  }
   *Q = q;
   *blocks = q ? (P + q - 1) / q : 0;
   *lds_bytes = packed_tree_lds_words(B, q) * 4u;

@@ -127,7 +127,10 @@ constexpr uint32_t kStepTreeLdsMax = 24u * 1024u + 64u;
 bool build_step_fusable(uint32_t B);
 uint32_t build_step_tree_q(uint32_t B);  // partitions per packed tree wave
 // The tree workgroups of a fused step for P partitions of B buckets: Q partitions per packed tree
-// wave, blocks = tree workgroups, lds_bytes = their LDS.
+// wave (Q >= 1), or Q = 0 for one partition per two-wave group (kStepTreeWideThreads threads of
+// tree_body); blocks = tree workgroups, lds_bytes = their LDS.
+constexpr uint32_t kStepTreeWideThreads = 128;
+constexpr uint32_t kStepTreeWideMinPartitions = 512;
 void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint32_t* lds_bytes);
 hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st);
 // One-launch build of a small layout-A arena (digest.hip small_build_kernel); t.sums_in is the

@@ -301,7 +301,7 @@ __global__ __launch_bounds__(kThreads) void tagged_digest_kernel(TaggedLaunch a)
 }
 
 // Fused build step for layout B (see build_step_kernel in digest.hip): the binning workgroups
-// come first, then tree_blocks workgroups build the previous build's trees (tree_body_packed). Both
+// come first, then tree_blocks workgroups build the previous build's trees (step_trees). Both
 // roles share one LDS reservation, the bins of two waves (33 KiB at B = 64), so four binning
 // workgroups fill a CU's LDS: tree workgroups placed first would each
 // hold back a binning workgroup until the tree is done (measured: 1.584 vs 1.551 ms at C4 with
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(kThreads) void tagged_step_kernel(TaggedLaunch a, T
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t digest_blocks = gridDim.x - tree_blocks;
   if (blockIdx.x >= digest_blocks) {
-    tree_body_packed(t, Q, blockIdx.x - digest_blocks, smem);
+    step_trees(t, Q, blockIdx.x - digest_blocks, smem);
     return;
   }
   tagged_body(a, blockIdx.x, smem);

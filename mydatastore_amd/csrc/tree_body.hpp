@@ -216,4 +216,20 @@ __device__ __forceinline__ void tree_body_packed(const TreeLaunch& a, uint32_t Q
     for (uint32_t i = lane; i < nq; i += 64) a.items_out[p0 + i] = (int32_t)cnt[i];
 }
 
+// LDS words of one tree_body group for B buckets (counter slot + the two level buffers).
+__host__ __device__ inline uint32_t tree_lds_words(uint32_t B) {
+  const uint32_t n1 = (B + 1) / 2;
+  return 4u + (n1 + (n1 + 1) / 2) * 8u;
+}
+
+// A tree workgroup of a fused build step (plan_step_trees): Q > 0 -> its first wave builds Q
+// partitions (tree_body_packed); Q == 0 -> its first kStepTreeWideThreads threads (two waves)
+// build one partition (tree_body; the other waves leave at once).
+__device__ __forceinline__ void step_trees(const TreeLaunch& t, uint32_t Q, uint32_t block, uint32_t* lds) {
+  if (Q)
+    tree_body_packed(t, Q, block, lds);
+  else
+    tree_body<true>(t, kStepTreeWideThreads, tree_lds_words(t.B), block, lds, kStepTreeWideThreads);
+}
+
 }  // namespace mde

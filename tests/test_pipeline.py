@@ -376,6 +376,28 @@ def test_tagged_equals_layout_a_full_size(engine, value_len, n_keys, world, n_bu
             assert torch.equal(o[k], ref[k]), (fused, k)
 
 
+@pytest.mark.parametrize("layout,n_buckets,world", [
+    ("a", 1000, 1), ("b", 1000, 1), ("a", 1000, 8), ("b", 1000, 8), ("a", 64, 1), ("b", 64, 1)])
+def test_fused_step_trees_many_builds(engine, layout, n_buckets, world):
+    """Runs of pipelined builds, where every build but the last gets its trees from the NEXT
+    build's launch (the fused step's tree workgroups): 1,024 partitions (two-wave trees at
+    B = 1,000) and the 128-partition N = 8 shard (packed tree waves), 8-byte values, both layouts.
+    Every build of the run equals the standalone build, nodes included."""
+    import torch
+    from mydatastore_amd.workload import make_workload
+    w = make_workload(engine, n_partitions=1024, n_buckets=n_buckets, value_len=8, part_mode="mod",
+                      n_keys=20_000_000, rank=0, world=world, layout=layout)
+    ref = w.build()
+    sets = [w._outs() for _ in range(3)]
+    for o, to in sets:
+        engine.build_pipelined_async(w.rec, to)
+    engine.build_pipeline_drain_async()
+    engine.synchronize()
+    for i, (o, _) in enumerate(sets):
+        for k in ("digest", "size", "items", "root", "nodes"):
+            assert torch.equal(o[k], ref[k]), (i, k)
+
+
 @pytest.mark.parametrize("variable", [False, True])
 def test_many_small_buckets_every_static_variant(engine, variable):
     """The reference's default PartitionBuckets = 1000 (config/default-config.yaml:8) with a few
