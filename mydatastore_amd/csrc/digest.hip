@@ -889,6 +889,13 @@ void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint
   // N = 8 shard at B = 1,000, 128 partitions: 218 vs 221 us), hence the partition threshold
   // (profiles/r02ak_half.jsonl). Four waves per partition measured worse at C4 (1,645 vs
   // 1,615 us; r02af_treewide.jsonl).
+  // r02, rejected: the pair shape of the standalone tree kernel (tree_body_pair: two partitions
+  // per workgroup, 28 instead of 34 wave-compressions per partition at B = 1,000, the same
+  // critical path). Beside the stream it bought nothing: 8-byte values at B = 1,000 230-233 vs
+  // 233 us per fused build, 64-byte values 269-271 vs 266-267, C4 at B = 1,000 within noise
+  // (profiles/r02an_pair_trees.jsonl). Stopping every tree at its first level of <= 64 nodes
+  // (a probe, wrong roots) took 8-byte values to 193-197 us: the top levels' six dependent node
+  // hashes, not their instruction count, hold the step.
   const uint32_t q = build_step_tree_q(B);
   if (q == 1 && (B + 1) / 2 > 64 && P >= kStepTreeWideMinPartitions) {
     *Q = 0;
@@ -904,7 +911,8 @@ void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint
 hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st) {
   uint32_t tree_blocks = 0, Q = 0, lds = a.lds_bytes;
   if (t && t->P) {
-    if (!build_step_fusable(t->B) || !t->sums_in) return hipErrorInvalidValue;
+    // every partition of a fused step has t->B buckets (no per-tree n_in)
+    if (!build_step_fusable(t->B) || !t->sums_in || t->n_in) return hipErrorInvalidValue;
     uint32_t tree_lds = 0;
     plan_step_trees(t->B, t->P, &Q, &tree_blocks, &tree_lds);
     // every workgroup of the dispatch reserves the tree waves' LDS; kStepTreeLdsMax keeps the

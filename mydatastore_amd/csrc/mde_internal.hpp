@@ -110,6 +110,8 @@ struct TreeLaunch {
   const int32_t* n_in;
 };
 constexpr uint32_t kTreeLdsMaxBuckets = 4096;
+constexpr uint32_t kTreePairLdsMax = 64u * 1024u;  // standalone pair-shape trees (B <= 2,728)
+constexpr uint32_t kTreePairMinPartitions = 512;
 hipError_t launch_tree(const TreeLaunch& a, hipStream_t st);
 struct TreeGeometry {
   uint32_t G, threads, groups, words, lds_bytes;

@@ -352,7 +352,7 @@ hipError_t launch_tagged_step(TaggedLaunch& a, const TreeLaunch* t, hipStream_t 
   uint32_t tree_blocks = 0, Q = 0;
   size_t lds = bins;
   if (t && t->P) {
-    if (!build_step_fusable(t->B) || !t->sums_in) return hipErrorInvalidValue;
+    if (!build_step_fusable(t->B) || !t->sums_in || t->n_in) return hipErrorInvalidValue;
     uint32_t tree_lds = 0;
     plan_step_trees(t->B, t->P, &Q, &tree_blocks, &tree_lds);
     lds = std::max<size_t>(lds, (size_t)tree_lds);

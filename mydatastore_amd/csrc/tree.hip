@@ -14,6 +14,13 @@ __global__ __launch_bounds__(256) void tree_kernel(TreeLaunch a, uint32_t G, uin
   tree_body<kLds>(a, G, lds_words, blockIdx.x, lds, blockDim.x);
 }
 
+// Two wide trees per workgroup (tree_body_pair): used for many partitions, where the trees are
+// bound by wave-instructions rather than by their critical path.
+__global__ __launch_bounds__(256) void tree_pair_kernel(TreeLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  tree_body_pair(a, blockIdx.x, lds);
+}
+
 }  // namespace
 
 uint32_t tree_levels(uint32_t B, uint32_t* sizes) {
@@ -60,6 +67,13 @@ bool tree_geometry(uint32_t B, TreeGeometry* g) {
 
 hipError_t launch_tree(const TreeLaunch& a, hipStream_t st) {
   if (a.P == 0) return hipSuccess;
+  // Wide trees of many partitions: two per workgroup. 1,024 partitions at B = 1,000: 142 -> 119.5 us
+  // (-16 %); at 128 partitions the 4-wave tree_body's shorter critical path wins, 61.5 vs 73 us
+  // (profiles/r02an_pair_trees.jsonl, `tree_us`).
+  if ((a.B + 1) / 2 > 64 && !a.n_in && a.P >= kTreePairMinPartitions && pair_tree_lds_words(a.B) * 4u <= kTreePairLdsMax) {
+    hipLaunchKernelGGL(tree_pair_kernel, dim3((a.P + 1) / 2), dim3(256), pair_tree_lds_words(a.B) * 4u, st, a);
+    return hipGetLastError();
+  }
   TreeGeometry g;
   const bool lds = tree_geometry(a.B, &g);
   const uint32_t blocks = (a.P + g.groups - 1) / g.groups;

@@ -216,6 +216,131 @@ __device__ __forceinline__ void tree_body_packed(const TreeLaunch& a, uint32_t Q
     for (uint32_t i = lane; i < nq; i += 64) a.items_out[p0 + i] = (int32_t)cnt[i];
 }
 
+// Pair shape for wide trees (level 1 > 64 nodes) with one B for every partition (byte-sum or
+// digest input, no n_in): a 256-thread workgroup builds partitions 2*block and 2*block+1, 128
+// threads (two waves) each, until a level has <= 64 nodes; then ONE wave finishes both trees,
+// their nodes spread over its 64 lanes. tree_body's shape runs those top levels (six at
+// B = 1,000) one wave per partition with 32 lanes or fewer busy: 12 of its 34 wave-compressions
+// per partition at B = 1,000, here 6, for the same critical path (24 dependent compressions).
+// Level 1 never reaches LDS: a thread hashes the two level-1 nodes under its level-2 node and
+// that node from registers, which halves the LDS (two trees in 24 KiB at B <= 1,024).
+// Used by the standalone tree kernel for >= 512 partitions (tree.hip launch_tree); in the fused
+// build step it measured no better than tree_body's two-wave trees (digest.hip plan_step_trees).
+// LDS per partition: a 4-word counter slot, then level buffers of n2 and ceil(n2 / 2) nodes.
+__host__ __device__ inline uint32_t pair_tree_region_words(uint32_t B) {
+  const uint32_t n1 = (B + 1) / 2, n2 = (n1 + 1) / 2;
+  return 4u + (n2 + (n2 + 1) / 2) * 8u;
+}
+__host__ __device__ inline uint32_t pair_tree_lds_words(uint32_t B) { return 2u * pair_tree_region_words(B); }
+
+// Level-1 node j of a tree over B leaves (leaves 2j, 2j+1; the odd last leaf pairs with itself).
+__device__ __forceinline__ void tree_level1(const TreeLaunch& a, uint64_t s0, uint32_t B, uint32_t j,
+                                            uint32_t& items, uint32_t st[8]) {
+  const uint32_t bl = 2 * j, br = (2 * j + 1 < B) ? 2 * j + 1 : 2 * j;
+  uint32_t szl = 0, szr = 0;
+  const uint64_t dl = tree_leaf(a, s0 + bl, items, szl);
+  const uint64_t dr = (br != bl) ? tree_leaf(a, s0 + br, items, szr) : dl;
+  if (br == bl) items += szl;  // odd B: the duplicate leaf's size counts again (tree.Leafs walk)
+  sha256_leaf_pair(dl, dr, st);
+}
+
+constexpr uint32_t kPairTreeThreads = 128;  // threads per partition in the wide phase
+
+__device__ __forceinline__ void tree_body_pair(const TreeLaunch& a, uint32_t block, uint32_t* lds) {
+  const uint32_t half = threadIdx.x / kPairTreeThreads, tid = threadIdx.x % kPairTreeThreads;
+  const uint32_t p0 = block * 2u;
+  const uint32_t p = p0 + half;
+  const bool live = p < a.P;
+  const uint32_t B = a.B;
+  const uint32_t n1 = (B + 1) / 2, n2 = (n1 + 1) / 2;
+  const uint32_t rw = pair_tree_region_words(B);
+  uint32_t* region = lds + half * rw;
+  uint32_t* cur = region + 4;
+  uint32_t* nxt = cur + (uint64_t)n2 * 8;
+  uint32_t* node_base = (a.nodes_out && live)
+                            ? reinterpret_cast<uint32_t*>(a.nodes_out + (uint64_t)p * a.n_int * 32)
+                            : nullptr;
+  if (tid == 0) region[0] = 0;
+  __syncthreads();
+
+  // Leaves, level 1 and level 2 in registers.
+  uint32_t items = 0;
+  if (live) {
+    const uint64_t s0 = (uint64_t)p * B;
+    for (uint32_t j = tid; j < n2; j += kPairTreeThreads) {
+      const uint32_t l = 2 * j, r = (2 * j + 1 < n1) ? 2 * j + 1 : 2 * j;
+      uint32_t hl[8], hr[8], st[8];
+      tree_level1(a, s0, B, l, items, hl);
+      if (node_base) store_node(node_base + (uint64_t)l * 8, hl);
+      if (r != l) {
+        tree_level1(a, s0, B, r, items, hr);
+        if (node_base) store_node(node_base + (uint64_t)r * 8, hr);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) hr[k] = hl[k];
+      }
+      sha256_node_pair(hl, hr, st);
+      store_node(cur + (uint64_t)j * 8, st);
+      if (node_base) store_node(node_base + (uint64_t)(n1 + j) * 8, st);
+    }
+  }
+  if (items) atomicAdd(region, items);
+
+  // Wide levels, two waves per partition, down to a level of <= 64 nodes.
+  uint32_t n = n2;
+  uint64_t level_off = n1;  // node index of the current level's first node
+  while (n > 64) {
+    __syncthreads();
+    const uint32_t m = (n + 1) / 2;
+    if (live) {
+      for (uint32_t j = tid; j < m; j += kPairTreeThreads) {
+        const uint32_t l = 2 * j, r = (2 * j + 1 < n) ? 2 * j + 1 : 2 * j;
+        uint32_t hl[8], hr[8], st[8];
+        load_node(cur + (uint64_t)l * 8, hl);
+        load_node(cur + (uint64_t)r * 8, hr);
+        sha256_node_pair(hl, hr, st);
+        store_node(nxt + (uint64_t)j * 8, st);
+        if (node_base) store_node(node_base + (level_off + n + j) * 8, st);
+      }
+    }
+    level_off += n;
+    n = m;
+    uint32_t* t = cur; cur = nxt; nxt = t;
+  }
+  __syncthreads();
+
+  // Top levels: wave 0 finishes both trees (the other waves leave; s_barrier counts live waves).
+  if (threadIdx.x >= 64) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t nq = p0 >= a.P ? 0u : min(2u, a.P - p0);
+  while (n > 1) {
+    const uint32_t m = (n + 1) / 2;
+    for (uint32_t i = lane; i < nq * m; i += 64) {
+      const uint32_t q = i >= m ? 1u : 0u, j = i - q * m;
+      const uint32_t l = 2 * j, r = (2 * j + 1 < n) ? 2 * j + 1 : 2 * j;
+      const uint32_t* c = cur + q * rw;
+      uint32_t hl[8], hr[8], st[8];
+      load_node(c + (uint64_t)l * 8, hl);
+      load_node(c + (uint64_t)r * 8, hr);
+      sha256_node_pair(hl, hr, st);
+      store_node(nxt + q * rw + (uint64_t)j * 8, st);
+      if (a.nodes_out)
+        store_node(reinterpret_cast<uint32_t*>(a.nodes_out + ((uint64_t)(p0 + q) * a.n_int + level_off + n + j) * 32),
+                   st);
+    }
+    level_off += n;
+    n = m;
+    uint32_t* t = cur; cur = nxt; nxt = t;
+    __syncthreads();
+  }
+  for (uint32_t i = lane; i < nq * 8; i += 64) {
+    const uint32_t q = i / 8, w = i % 8;
+    reinterpret_cast<uint32_t*>(a.root_out + (uint64_t)(p0 + q) * 32)[w] = cur[q * rw + w];
+  }
+  if (a.items_out)
+    for (uint32_t i = lane; i < nq; i += 64) a.items_out[p0 + i] = (int32_t)lds[i * rw];
+}
+
 // LDS words of one tree_body group for B buckets (counter slot + the two level buffers).
 __host__ __device__ inline uint32_t tree_lds_words(uint32_t B) {
   const uint32_t n1 = (B + 1) / 2;

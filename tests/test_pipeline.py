@@ -398,6 +398,34 @@ def test_fused_step_trees_many_builds(engine, layout, n_buckets, world):
             assert torch.equal(o[k], ref[k]), (i, k)
 
 
+@pytest.mark.parametrize("n_buckets", [129, 257, 999, 1000, 1024])
+def test_pair_trees_odd_shapes_match_oracle(engine, coracle, n_buckets):
+    """Wide trees of >= 512 partitions: the standalone tree kernel's pair shape (two partitions
+    per workgroup) and the fused step's two-wave trees. An odd partition count (the last pair
+    workgroup holds one live tree), odd B (duplicate leaf, self-paired nodes), B whose level 2
+    already fits one wave (129) or needs one wide level (257), and the fused step's LDS limit
+    (1,024). The standalone build and a pipelined run equal the C oracle, nodes included."""
+    import numpy as np
+    import torch
+    from mydatastore_amd.workload import make_workload
+    P, V = 515, 8
+    w = make_workload(engine, n_partitions=P, n_buckets=n_buckets, value_len=V, part_mode="mod",
+                      n_keys=1_500_000, rank=0, world=1, layout="a")
+    exp = coracle.build(w.values.cpu().numpy(), w.seg_rec.cpu().numpy().view(np.uint64), P, n_buckets,
+                        stride=V, threads=8)
+    outs = [w.build()]
+    sets = [w._outs() for _ in range(2)]
+    for o, to in sets:
+        engine.build_pipelined_async(w.rec, to)
+    engine.build_pipeline_drain_async()
+    engine.synchronize()
+    outs += [o for o, _ in sets]
+    for i, o in enumerate(outs):
+        for k in ("digest", "size", "items", "root", "nodes"):
+            got = o[k].cpu().numpy().view(exp[k].dtype).reshape(-1)
+            assert np.array_equal(got, exp[k].reshape(-1)), (i, k)
+
+
 @pytest.mark.parametrize("variable", [False, True])
 def test_many_small_buckets_every_static_variant(engine, variable):
     """The reference's default PartitionBuckets = 1000 (config/default-config.yaml:8) with a few
