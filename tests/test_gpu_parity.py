@@ -152,6 +152,15 @@ def test_tree_from_digests_matches_oracle(engine, coracle):
             r, n = coracle.tree(d[t * B:(t + 1) * B], B)
             assert root[32 * t:32 * t + 32].tobytes() == r, B
             assert nodes[t * ni:(t + 1) * ni].tobytes() == n, B
+    # >= 512 wide trees: the tree kernel's pair shape (two trees per workgroup), odd tree counts
+    for B, T in ((257, 515), (1000, 513)):
+        d = rng.integers(0, 2**63, T * B, dtype=np.int64).astype(np.uint64)
+        root, nodes = engine.tree_from_digests(d, B)
+        ni = O.n_internal_nodes(B) * 32
+        for t in range(T):
+            r, n = coracle.tree(d[t * B:(t + 1) * B], B)
+            assert root[32 * t:32 * t + 32].tobytes() == r, (B, t)
+            assert nodes[t * ni:(t + 1) * ni].tobytes() == n, (B, t)
 
 
 def test_tag_kernels(engine, golden, coracle):
