@@ -264,7 +264,9 @@ def main():
         # layout B on a whole C4 arena: the tree kernel on a second stream costs 0.4 % over bare
         # binning, the fused step 1.5 %; on an N=8 shard fused costs 1 %, two streams 6 %
         # (profiles/r01f_pipeline_modes_layout_b.jsonl)
-        mode = "fused" if (args.layout == "a" or shard_world > 1) else "streams"
+        # layout B at B = 1,000, N = 1: fused 1.72 ms per step vs 2.38 with two streams, the N = 8
+        # shard 0.33-0.34 vs 0.36 (profiles/r02at_layoutb_modes.jsonl)
+        mode = "fused" if (args.layout == "a" or shard_world > 1 or B > 128) else "streams"
     fused = mode == "fused"
     pipeline = mode == "streams"
     engines = [eng]
