@@ -205,7 +205,7 @@ def main():
     import torch
     import torch.distributed as dist
     import mydatastore_amd as mde
-    from mydatastore_amd.dist import RootGather, weak_totals
+    from mydatastore_amd.dist import RootGather, local_partitions, weak_totals
     from mydatastore_amd.workload import Workload, make_workload
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -296,6 +296,10 @@ def main():
         out_vals = torch.zeros(bytes_cap, dtype=torch.uint8, device=dev)
         out_voff = torch.zeros(rec_cap + 1, dtype=torch.int64, device=dev)
         status = torch.zeros(1, dtype=torch.int32, device=dev)
+        # N > 1: each step's per-partition diff counts travel with the roots (SURVEY.md section 8e:
+        # C5 also gathers the diff results); staged per output set, as diff_cnt is rewritten by
+        # the next step's diff while the gather may still be in flight
+        cnt_stage = [torch.zeros(Pl, dtype=torch.int32, device=dev) for _ in range(2)]
 
     # Two output sets and two gather slabs: the RCCL root gather of build i runs on a side stream
     # and overlaps build i+1 (the exchange step overlapped with compute); a build's output set is
@@ -305,7 +309,7 @@ def main():
     bucket = GATHER_BUCKET if (fused and use_dist and not c5) else 1
     outs = [(w.out, w.tree_out)] + [w._outs() for _ in range(2 * bucket - 1)]
     outs_b = [(wb.out, wb.tree_out), wb._outs()] if c5 else None
-    gather = RootGather(P, world, dev, width=64 if c5 else 32, batch=bucket) if use_dist else None
+    gather = RootGather(P, world, dev, width=68 if c5 else 32, batch=bucket) if use_dist else None
     side = torch.cuda.Stream(dev) if use_dist else None
     ev_built = [torch.cuda.Event() for _ in range(2)]
     ev_gathered = [torch.cuda.Event() for _ in range(2)]
@@ -347,7 +351,8 @@ def main():
         eng.extract_async(wb.rec, diff_ids, cap, diff_cnt, part_off, out_rec, rec_cap, out_vals,
                           out_voff, bytes_cap, status)
         if use_dist:
-            roots = torch.cat([o["root"], ob["root"]])
+            cnt_stage[k].copy_(diff_cnt)
+            roots = torch.cat([o["root"], ob["root"], cnt_stage[k].view(torch.uint8)])
             ev_built[k].record(stream)
             side.wait_event(ev_built[k])
             with torch.cuda.stream(side):
@@ -413,7 +418,9 @@ def main():
             eng.diff_async(Pl, B, o["digest"], o["nodes"], B, ob["digest"], ob["nodes"], diff_ids, cap, diff_cnt)
             eng.extract_async(wb.rec, diff_ids, cap, diff_cnt, part_off, out_rec, rec_cap, out_vals,
                               out_voff, bytes_cap, status)
-            roots = torch.cat([o["root"], ob["root"]]) if use_dist else None
+            if use_dist:
+                cnt_stage[i].copy_(diff_cnt)
+                roots = torch.cat([o["root"], ob["root"], cnt_stage[i].view(torch.uint8)])
         if use_dist:
             ev_built[i].record(build_stream)
             side.wait_event(ev_built[i])
@@ -462,6 +469,12 @@ def main():
             got = out_vals[:want * V].view(want, V).cpu().numpy()[:: max(1, len(r) // 64)]
             src = vb.view(-1, V)[torch.from_numpy(samp).to(dev)].cpu().numpy()
             ok_ex = bool(np.array_equal(got, src))
+        if use_dist:  # step 0's gather (slab 0): [A roots | B roots | diff counts] per rank
+            slabs = gather.recv[0].view(world, -1).cpu().numpy()
+            counts = [slabs[r][len(local_partitions(P, r, world)) * 64:
+                               len(local_partitions(P, r, world)) * 68].view(np.int32) for r in range(world)]
+            parity["c5_gathered_diff_counts"] = bool(np.array_equal(counts[rank], cnt) and
+                                                     all(((c == 0) | (c == 1)).all() for c in counts))
         parity["c5_diff_is_exactly_the_perturbed_bucket"] = bool(ok)
         parity["c5_extract_records_and_bytes"] = bool(ok_ex)
         parity["c5_extracted_records_per_step"] = want
