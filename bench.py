@@ -567,8 +567,12 @@ def main():
                        else "B (arrival order + bucket tags, binned on device)", "n_keys": n_keys, "value_len": V, "n_partitions": P,
                        "n_buckets": B, "bytes_hashed_per_step": total_bytes,
                        "partitions_per_gpu": Pl, "parallelism": f"partition-shard x{world}",
-                       "root_gather": ("rccl all_gather_into_tensor of ceil(P/N) x 32 B slabs on a side "
-                                       "stream, overlapped with the next build") if use_dist else None},
+                       "root_gather": (("gloo all_gather (rehearsal, staged through the host)" if args.rehearse
+                                        else "rccl all_gather_into_tensor")
+                                       + f" of ceil(P/N) x {68 if c5 else 32} B slabs on a side stream, "
+                                       + ("one per step (C5: both replicas' roots + diff counts)" if c5 else
+                                          f"one per {bucket} builds") + ", overlapped with the next build")
+                       if use_dist else None},
             "roofline": {"bound": "hbm",
                          "kernel": ("build_step_kernel" if fused else "bucket_digest_kernel")
                          if args.layout == "a" else ("tagged_step_kernel" if fused else "tagged_digest_kernel"),
