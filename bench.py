@@ -9,13 +9,16 @@ every bucket and the SHA-256 tree of every partition. By default (--pipeline fus
 one build_step_kernel launch that streams this build's arena and builds the previous build's
 trees; the timed region drains the pipeline on both sides, so it holds exactly K digests and K
 tree passes. For N > 1 a step also carries the RCCL all-gather of the per-partition roots (the one
-exchange step of the path), bucketed 8 builds per collective on a side stream. --config c5 (BASELINE config 5): build replicas A and B,
-device DFS-order diff of every partition, out-of-sync range extract of B's differing buckets;
-value counts the bytes of both builds. Default workload = BASELINE config 4: 10M keys x 1 KiB values
-over 1024 partitions per GPU, partition p on GPU p % N (weak scaling: per-GPU work fixed; --scaling
-strong splits the config's 10M keys over the N GPUs instead). The output is
-one JSON line on rank 0 with `roofline` (the dominant kernel, HIP events on the launch stream) and
-`cpu_baseline` (the C restatement on the host cores, rank 0 at N = 1 only).
+exchange step of the path), bucketed 8 builds per collective on a side stream; the same run then
+times the builds again with ONE collective per build (`root_gather_per_build`, the per-build RCCL
+cost). --config c5 (BASELINE config 5): build replicas A and B, device DFS-order diff of every
+partition, out-of-sync range extract of B's differing buckets; value counts the bytes of both
+builds. Default workload = BASELINE config 4 as stated: 10M keys x 1 KiB values over 1024
+partitions IN TOTAL, partition p on GPU p % N (strong scaling: the job is fixed, 128 partitions
+per GPU at N = 8); --scaling weak gives every GPU the N = 1 workload instead. The output is one
+JSON line on rank 0 with `roofline` (the dominant kernel, HIP events on the launch stream),
+`cpu_baseline` (the C restatement on the host cores, rank 0 at N = 1 only) and `parity` (every
+rank's timed build against the C oracle on host-regenerated records of a partition sample).
 """
 from __future__ import annotations
 
@@ -77,54 +80,101 @@ def parse():
                          "(mde_build_pipelined_async; the default, except layout b at N=1); streams: "
                          "tree kernel on a second stream; off: digest + tree serially")
     ap.add_argument("--tuning", default="", help="digest kernel 'variant,workgroups_per_cu' (A/B only)")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak (default): every rank holds the config's full workload (N x the "
-                         "partitions and keys in all, partition p on rank p %% N); strong: the "
-                         "config's total split over the ranks (BASELINE config 4 as stated)")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong (default): the config's total split over the ranks (BASELINE "
+                         "config 4 as stated: 10M keys over 1024 partitions in all, partition p on "
+                         "rank p %% N); weak: every rank holds the config's full workload (N x the "
+                         "partitions and keys in all)")
+    ap.add_argument("--no-gather-per-build", action="store_true",
+                    help="N > 1: skip the second timed run with one root-gather collective per build")
     return ap.parse_args()
 
 
-def cpu_baseline(cfg, seconds: float, part_ids):
-    """The C restatement of RawPartitionMerkleTree (oracle/, kind "port") timed on the host on a
-    bounded sample of the same workload: the first (up to 32) partitions this rank holds,
-    generated on the host with the same generator, built repeatedly for ~`seconds`. Also returns
-    the oracle's digests, sizes and roots of that sample (the checker for the timed device build)."""
+SAMPLE_MAX_BYTES = 512 << 20  # host-regenerated oracle sample per rank (at least one partition)
+
+
+def host_cpu_info():
+    """The host the CPU baseline runs on (report nproc and the CPU model),
+    and the CPU share this job may use: a gpurun box exports OMP_NUM_THREADS = its share (16 per
+    GPU) although nproc / os.cpu_count() show every CPU of the machine."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity_cpus"] = None
+    info["cpu_model"] = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["cpu_model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    info["cgroup_cpu_quota"] = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            info["cgroup_cpu_quota"] = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    info["omp_num_threads"] = int(omp) if omp.isdigit() else None
+    return info
+
+
+def cpu_share(info, world: int = 1) -> int:
+    """Threads the C restatement may use: every CPU this process may run on, capped by the cgroup
+    quota and by the job's declared CPU share (OMP_NUM_THREADS), split over the ranks."""
+    n = info.get("affinity_cpus") or info.get("nproc") or 1
+    for cap in (info.get("cgroup_cpu_quota"), info.get("omp_num_threads")):
+        if cap:
+            n = min(n, max(1, int(cap)))
+    return max(1, min(n // max(world, 1), 256))
+
+
+def oracle_sample(cfg, part_ids, threads):
+    """The checker of the timed build: the C restatement (oracle/, test infrastructure) builds a
+    sample of the partitions this rank holds -- the first up to 32, at most SAMPLE_MAX_BYTES --
+    from records REGENERATED ON THE HOST by its own generator (tests/sample.py). Returns the
+    sample's host arrays and the oracle's digests, sizes, items and roots."""
     from tests.oracle_c import COracle
+    from tests.sample import host_sample
     n_keys, P, V, B, mode, _ = cfg
+    per_part = -(-n_keys // P) * V
+    k = int(max(1, min(32, len(part_ids), SAMPLE_MAX_BYTES // max(per_part, 1))))
     co = COracle()
-    sample = np.asarray(part_ids[:32], dtype=np.int64)
-    kpp = -(-n_keys // P)
-    if mode == "mod":
-        per = -(-n_keys // P)
-        g = (np.arange(per, dtype=np.uint64)[None, :] * np.uint64(P) + sample.astype(np.uint64)[:, None]).reshape(-1)
-        g = np.sort(g[g < n_keys])
-    else:
-        g = np.concatenate([np.arange(p * kpp, min((p + 1) * kpp, n_keys), dtype=np.uint64) for p in sample])
-    part, bk = co.synth_tags(g, P, B, {"block": 0, "mod": 1}[mode], kpp)
-    slot = np.full(P, -1, np.int64)
-    slot[sample] = np.arange(sample.size)
-    order, seg = co.layout_a(slot[part].astype(np.uint32), bk, int(sample.size), B)
-    values = co.synth_values(g[order], V, 0x4D445354)
-    threads = max(1, min(16, os.cpu_count() or 1))
+    values, seg, n, _ = host_sample(co, n_keys, P, V, B, mode, np.asarray(part_ids[:k]))
+    ref = co.build(values, seg, n, B, V, threads=threads, want_nodes=False)
+    return co, values, seg, n, ref
+
+
+def cpu_baseline(co, values, seg, n, cfg, seconds: float, threads: int, info):
+    """The C restatement of RawPartitionMerkleTree (kind "port": per partition, per bucket, per
+    record Add then % 999999, then a host SHA-256 tree, main/merkle_tree.go:86-116) timed on the
+    oracle sample for ~`seconds`, on 1 thread and on `threads` threads."""
+    _, P, V, B, _, _ = cfg
     res = {}
     for t in sorted({1, threads}):
         reps, t0 = 0, time.perf_counter()
         while True:
-            co.build(values, seg, int(sample.size), B, V, threads=t, want_nodes=False)
+            co.build(values, seg, n, B, V, threads=t, want_nodes=False)
             reps += 1
             el = time.perf_counter() - t0
             if el >= seconds / 2 or reps >= 1000:
                 break
         res[t] = values.nbytes * reps / el / 2**30
-    ref = co.build(values, seg, int(sample.size), B, V, threads=threads, want_nodes=False)
     return {
         "value": round(res[threads], 3), "unit": "GiB/s", "cores": threads, "kind": "port",
         "single_thread_value": round(res[1], 3),
-        "sample": f"{sample.size} of {P} partitions ({len(g)} records x {V} B = "
-                  f"{values.nbytes / 2**20:.0f} MiB), oracle/mde_oracle.c oracle_build with "
-                  f"{threads} threads (1-thread value in single_thread_value); Badger iteration "
-                  f"excluded, so an upper bound on the reference Go CPU rate",
-    }, ref
+        "host": info,
+        "sample": f"{n} of {P} partitions ({values.nbytes // V} records x {V} B = "
+                  f"{values.nbytes / 2**20:.0f} MiB, regenerated on the host), oracle/mde_oracle.c "
+                  f"oracle_build with {threads} threads = this job's CPU share (cpu_share(): "
+                  f"affinity, cgroup quota, OMP_NUM_THREADS; nproc and the model in `host`); "
+                  f"1-thread value in single_thread_value; Badger iteration excluded, so an upper "
+                  f"bound on the reference Go CPU rate",
+    }
 
 
 def pmc_traffic(config_name: str, local_bytes: int):
@@ -180,33 +230,13 @@ def end_to_end(torch, eng, w, B, reps=3):
     return res
 
 
-def perturb_replica(torch, w, n_buckets):
-    """Replica B of SURVEY.md section 8d config 5: A with one record per partition changed -- the
-    first record of bucket (p*37) % 64 (global partition id p) gets its first value byte +1 mod
-    256, which always changes that bucket's digest. Returns {local partition: bucket}."""
-    vb = w.values.clone()
-    seg = w.seg_rec.cpu().numpy()
-    touched = {}
-    idx = []
-    for lp, gp in enumerate(w.partition_ids):
-        b = int(gp * 37) % n_buckets
-        r0, r1 = int(seg[lp * n_buckets + b]), int(seg[lp * n_buckets + b + 1])
-        if r1 > r0:
-            touched[lp] = b
-            idx.append(r0 * w.value_len)
-    if idx:
-        ii = torch.tensor(idx, dtype=torch.int64, device=vb.device)
-        vb[ii] = ((vb[ii].to(torch.int32) + 1) % 256).to(torch.uint8)
-    return vb, touched
-
-
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
     import mydatastore_amd as mde
     from mydatastore_amd.dist import RootGather, local_partitions, weak_totals
-    from mydatastore_amd.workload import Workload, make_workload
+    from mydatastore_amd.workload import Workload, make_workload, perturb_replica
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -237,14 +267,18 @@ def main():
         eng.set_tuning(*map(int, args.tuning.split(",")))
     kpp = -(-n_keys // P)
     shard_world = args.simulate_world if (args.simulate_world and world == 1) else world
-    # Partitions are independent units. Weak scaling: each rank holds the
-    # config's per-GPU workload, so N ranks build N x P partitions of N x n_keys keys (partition p
-    # on rank p % N, p = gid % (N x P) for round-robin configs); every rank's shard then has
-    # exactly the N = 1 shape. Strong: the config's total is split (--simulate-world models it).
+    # Partitions are independent units, partition p on rank p % N. Strong
+    # scaling (default): the config's total is split, so at N = 8 each rank builds 128 of C4's
+    # 1024 partitions (--simulate-world models one rank's shard). Weak: each rank holds the
+    # config's per-GPU workload, N x P partitions of N x n_keys keys in all (p = gid % (N x P)
+    # for round-robin configs), so every rank's shard has exactly the N = 1 shape.
     weak = args.scaling == "weak" and not args.simulate_world
     if weak and world > 1:
         n_keys, P = weak_totals(n_keys, P, world)
         desc = desc + f"; weak scaling: x{world} in all, the N=1 workload on every GPU"
+    elif shard_world > 1:
+        desc = desc + f"; strong scaling: the config's total over {shard_world} GPUs"
+    cfg = (n_keys, P, V, B, mode, desc)
     if c5 and args.layout != "a":
         raise SystemExit("--config c5 uses layout a (the extract gathers bucket runs)")
     w = make_workload(eng, n_partitions=P, n_buckets=B, value_len=V, part_mode=mode,
@@ -284,7 +318,7 @@ def main():
     if c5:
         desc = ("C5: C4 data as replica A + replica B with one bucket per partition perturbed; "
                 "build both, device DFS-order diff, out-of-sync range extract of B")
-        vb, touched = perturb_replica(torch, w, B)
+        vb, touched = perturb_replica(w)
         wb = Workload(eng, vb, w.seg_rec, Pl, B, w.n_records, V, w.partition_ids)
         cap = mde.diff_capacity(B, B)
         diff_ids = torch.zeros(Pl * cap, dtype=torch.int32, device=dev)
@@ -480,72 +514,128 @@ def main():
         parity["c5_extracted_records_per_step"] = want
     parity_ok = all(v for k, v in parity.items() if isinstance(v, bool))
 
-    for _ in range(args.warmup):
-        step()
-    join()  # the timed region runs exactly K digests and K trees (its last trees in its own join)
-    n_ev = args.steps
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    # Kernel time for the roofline, from HIP events on the launch stream. Fused mode: one event
-    # pair brackets the K back-to-back build_step_kernel launches (no per-launch events: a timing
-    # event between two launches on ROCm costs a visible gap and slows the next launch's start,
-    # measured 10-55 us per step); the kernel trace shows these launches with no gaps, so the
-    # bracket / K is the average launch duration (the drain's tree launch is outside it).
-    # Other modes: one event pair around each digest launch.
-    bracket = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-    ev_joined = torch.cuda.Event(enable_timing=True)
-    if fused:
-        bracket[0].record(stream)
-    for i in range(args.steps):
-        step(*(() if fused else evs[i]))
-    t_enq = time.perf_counter()
-    if fused:
-        bracket[1].record(stream)
-    join()
-    ev_joined.record(stream)
-    t_join = time.perf_counter()
-    torch.cuda.synchronize(dev)
-    t_sync = time.perf_counter()
-    if use_dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    # where the wall time of the timed region went (host clock; the drain on the device clock)
-    host_timing = {"enqueue_ms": round((t_enq - t0) * 1e3, 3), "join_ms": round((t_join - t_enq) * 1e3, 3),
-                   "sync_wait_ms": round((t_sync - t_join) * 1e3, 3), "barrier_ms": round((t1 - t_sync) * 1e3, 3),
-                   "wall_ms": round((t1 - t0) * 1e3, 3)}
-    if fused:
-        host_timing["bracket_ms"] = round(bracket[0].elapsed_time(bracket[1]), 3)
-        host_timing["drain_ms"] = round(bracket[1].elapsed_time(ev_joined), 3)
-    eng.set_stream(stream.cuda_stream)
-    ms = (t1 - t0) * 1e3 / args.steps
-    if use_dist and fused and not c5 and args.steps > 0:
-        # the last build of the timed run, as gathered: this rank's rows equal its own roots
-        last = args.steps - 1
+    def timed_run(steps, warmup):
+        """W untimed steps, then exactly K timed steps between barrier + synchronize on both sides.
+        Returns (wall ms per step, dominant-kernel ms per launch, host timing split)."""
+        for _ in range(warmup):
+            step()
+        join()  # the timed region runs exactly K digests and K trees (its last trees in its own join)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        if use_dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        # Kernel time for the roofline, from HIP events on the launch stream. Fused mode: one event
+        # pair brackets the K back-to-back build_step_kernel launches (no per-launch events: a timing
+        # event between two launches on ROCm costs a visible gap and slows the next launch's start,
+        # measured 10-55 us per step); the kernel trace shows these launches with no gaps, so the
+        # bracket / K is the average launch duration (the drain's tree launch is outside it).
+        # Other modes: one event pair around each digest launch.
+        bracket = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev_joined = torch.cuda.Event(enable_timing=True)
+        if fused:
+            bracket[0].record(stream)
+        for i in range(steps):
+            step(*(() if fused else evs[i]))
+        t_enq = time.perf_counter()
+        if fused:
+            bracket[1].record(stream)
+        join()
+        ev_joined.record(stream)
+        t_join = time.perf_counter()
+        torch.cuda.synchronize(dev)
+        t_sync = time.perf_counter()
+        if use_dist:
+            dist.barrier()
+        t1 = time.perf_counter()
+        # where the wall time of the timed region went (host clock; the drain on the device clock)
+        ht = {"enqueue_ms": round((t_enq - t0) * 1e3, 3), "join_ms": round((t_join - t_enq) * 1e3, 3),
+              "sync_wait_ms": round((t_sync - t_join) * 1e3, 3), "barrier_ms": round((t1 - t_sync) * 1e3, 3),
+              "wall_ms": round((t1 - t0) * 1e3, 3)}
+        if fused:
+            ht["bracket_ms"] = round(bracket[0].elapsed_time(bracket[1]), 3)
+            ht["drain_ms"] = round(bracket[1].elapsed_time(ev_joined), 3)
+        # C5 fused: two build_step_kernel launches + the compare kernels per step inside the bracket;
+        # the per-launch figure is bracket / 2K (the compare kernels counted against it, conservative)
+        km = (bracket[0].elapsed_time(bracket[1]) / steps / (2 if c5 else 1) if fused
+              else float(np.mean([x.elapsed_time(y) for x, y in evs])))
+        return (t1 - t0) * 1e3 / steps, km, ht
+
+    def max_over_ranks(*vals):
+        if not use_dist:
+            return vals
+        t = torch.tensor(vals, dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return tuple(float(x) for x in t)
+
+    def last_gathered_ok(steps):  # the last build of a timed run, as gathered: this rank's rows
+        last = steps - 1
         allr = gather.assemble((last // bucket) % 2, last % bucket)
-        parity["gathered_roots_match_after_run"] = bool(np.array_equal(
-            allr[w.partition_ids].reshape(-1), outs[last % (2 * bucket)][0]["root"].cpu().numpy()))
+        return bool(np.array_equal(allr[w.partition_ids].reshape(-1),
+                                   outs[last % (2 * bucket)][0]["root"].cpu().numpy()))
+
+    ms, kern_ms, host_timing = timed_run(args.steps, args.warmup)
+    eng.set_stream(stream.cuda_stream)
+    if use_dist and fused and not c5 and args.steps > 0:
+        parity["gathered_roots_match_after_run"] = last_gathered_ok(args.steps)
         parity_ok = parity_ok and parity["gathered_roots_match_after_run"]
-    # C5 fused: two build_step_kernel launches + the compare kernels per step inside the bracket;
-    # the per-launch figure is bracket / 2K (the compare kernels counted against it, conservative)
-    kern_ms = (bracket[0].elapsed_time(bracket[1]) / args.steps / (2 if c5 else 1) if fused
-               else float(np.mean([a.elapsed_time(b) for a, b in evs])))
+
+    # The checker of the headline number, on every rank: the digests, sizes, items and roots of the
+    # last timed build (replica A for C5) on a sample of this rank's partitions equal the C
+    # restatement's build of the same partitions' records regenerated on the host.
+    info = host_cpu_info()
+    threads = cpu_share(info, world)
+    co, s_vals, s_seg, s_n, ref = oracle_sample(cfg, w.partition_ids, threads)
+    got = {k: v.cpu().numpy() for k, v in last_out[0].items() if k in ("digest", "size", "items", "root")}
+    ok = (np.array_equal(got["digest"][:s_n * B].view(np.uint64), ref["digest"]) and
+          np.array_equal(got["size"][:s_n * B], ref["size"]) and np.array_equal(got["items"][:s_n], ref["items"]) and
+          np.array_equal(got["root"][:s_n * 32], ref["root"]))
+    parity["oracle_sample_partitions"] = int(s_n)
+    parity["timed_build_equals_c_oracle_on_sample"] = bool(ok)
+    parity_ok = parity_ok and ok
+
+    # N > 1: the same builds with ONE root-gather collective per build (no bucketing): the per-build
+    # RCCL cost the >= 6x target at 8 GPUs depends on (SURVEY.md section 8e), measured, not hidden
+    # in a bucket. Plus K bare collectives of the same slab on the side stream (no builds).
+    per_build = None
+    if use_dist and fused and not c5 and not args.no_gather_per_build and args.steps > 0:
+        bucket = 1
+        gather = RootGather(P, world, dev, width=32, batch=1)
+        ms1, km1, ht1 = timed_run(args.steps, 1)
+        ok1 = last_gathered_ok(args.steps)
+        eng.set_stream(stream.cuda_stream)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        g0 = torch.cuda.Event(enable_timing=True)
+        g1 = torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(side):
+            gather.gather(w.out["root"], 0)
+            g0.record(side)
+            for _ in range(args.steps):
+                gather.gather(w.out["root"], 0)
+            g1.record(side)
+        torch.cuda.synchronize(dev)
+        g_ms = g0.elapsed_time(g1) / args.steps
+        ms1, g_ms = max_over_ranks(ms1, g_ms)
+        per_build = {"ms_per_step": round(ms1, 5), "gathers_per_step": 1,
+                     "bare_gather_ms": round(g_ms, 5), "gathered_roots_match_after_run": ok1,
+                     "host_timing": ht1}
+        parity_ok = parity_ok and ok1
+
     hashed = w.value_bytes * (2 if c5 else 1)
     if use_dist:
-        t = torch.tensor([ms, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms = float(t[0])
+        ms, kern_ms = max_over_ranks(ms, kern_ms)
         tot = torch.tensor([hashed], dtype=torch.int64, device=dev)
         dist.all_reduce(tot)
         total_bytes = int(tot.item())
-        ok = torch.tensor([int(parity_ok)], dtype=torch.int32, device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        parity_ok = bool(ok.item())
+        okt = torch.tensor([int(parity_ok)], dtype=torch.int32, device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        parity_ok = bool(okt.item())
     else:
         total_bytes = hashed
     parity["all_ranks_ok"] = parity_ok
+    if per_build is not None:
+        per_build["value"] = round(total_bytes / 2**30 / (per_build["ms_per_step"] * 1e-3), 3)
 
     if rank == 0:
         local_bytes = w.value_bytes
@@ -559,7 +649,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms, 5),
             "higher_is_better": True,
-            "scaling": "weak" if weak else "strong",
+            "scaling": "weak" if (weak and world > 1) else "strong",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (device-generated splitmix64 values, 'k%016x' keys, SHA-256 bucket tags)",
@@ -571,7 +661,7 @@ def main():
                                         else "rccl all_gather_into_tensor")
                                        + f" of ceil(P/N) x {68 if c5 else 32} B slabs on a side stream, "
                                        + ("one per step (C5: both replicas' roots + diff counts)" if c5 else
-                                          f"one per {bucket} builds") + ", overlapped with the next build")
+                                          f"one per {GATHER_BUCKET if fused else 1} builds") + ", overlapped with the next build")
                        if use_dist else None},
             "roofline": {"bound": "hbm",
                          "kernel": ("build_step_kernel" if fused else "bucket_digest_kernel")
@@ -594,17 +684,11 @@ def main():
                                     "second stream, overlapping the next build's digest kernel",
                          "off": None}[mode],
         }
+        if per_build is not None:
+            result["root_gather_per_build"] = per_build
         if world == 1 and not args.no_cpu_baseline and not args.profile:
-            result["cpu_baseline"], ref = cpu_baseline(cfg, args.cpu_baseline_seconds, w.partition_ids)
-            # the oracle is the checker of the timed kernel: the last timed build's digests,
-            # sizes and roots of the sampled partitions (local slots 0..n-1) equal the C restatement's
-            n = ref["items"].size
-            o = {k: v.cpu().numpy() for k, v in last_out[0].items() if k in ("digest", "size", "root")}
-            ok = (np.array_equal(o["digest"][:n * B].view(np.uint64), ref["digest"]) and
-                  np.array_equal(o["size"][:n * B], ref["size"]) and np.array_equal(o["root"][:n * 32], ref["root"]))
-            parity["oracle_sample_partitions"] = int(n)
-            parity["timed_build_equals_c_oracle_on_sample"] = bool(ok)
-            parity["all_ranks_ok"] = bool(parity["all_ranks_ok"] and ok)
+            result["cpu_baseline"] = cpu_baseline(co, s_vals, s_seg, s_n, cfg, args.cpu_baseline_seconds,
+                                                  threads, info)
         else:
             result["cpu_baseline"] = None
         if world == 1 and not args.no_e2e and not args.profile and not c5:

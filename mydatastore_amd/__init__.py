@@ -566,6 +566,7 @@ class Group:
     """mde_group: one process driving several GPUs (contiguous partition blocks per device)."""
 
     def __init__(self, devices):
+        self._mu = threading.Lock()
         self.lib = load_library()
         devs = (C.c_int * len(devices))(*devices)
         h = C.c_void_p()
@@ -612,12 +613,16 @@ class Group:
             "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
         }
         to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
-        if streamed:
-            rc = self.lib.mde_multi_build_streamed(self.g, C.byref(rec), C.byref(to), chunk_bytes)
-        else:
-            rc = self.lib.mde_multi_build(self.g, C.byref(rec), C.byref(to))
+        # the call and the copy of ITS message are one critical section (threads sharing a Group
+        # cannot swap messages; the group lock serialises the builds anyway)
+        with self._mu:
+            if streamed:
+                rc = self.lib.mde_multi_build_streamed(self.g, C.byref(rec), C.byref(to), chunk_bytes)
+            else:
+                rc = self.lib.mde_multi_build(self.g, C.byref(rec), C.byref(to))
+            if rc != MDE_OK:
+                buf = C.create_string_buffer(512)
+                self.lib.mde_group_last_error_copy(self.g, buf, len(buf))
         if rc != MDE_OK:
-            buf = C.create_string_buffer(512)
-            self.lib.mde_group_last_error_copy(self.g, buf, len(buf))
             raise MdeError(rc, buf.value.decode(errors="replace"))
         return out

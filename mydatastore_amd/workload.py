@@ -93,6 +93,29 @@ class Workload:
         return [int(c) if c < 0 else ids[p * cap:p * cap + c].tolist() for p, c in enumerate(cnt)]
 
 
+def perturb_replica(w: Workload):
+    """Replica B of BASELINE config 5: replica A's values with one record
+    per partition changed -- the first record of bucket (p * 37) % B (p = global partition id)
+    gets its first value byte + 1 mod 256, which always changes that bucket's digest (the sum moves
+    by +1 or -255, never a multiple of 999999). Returns (values B on device, {local partition:
+    bucket}) for the partitions whose bucket is non-empty."""
+    import torch
+    B, V = w.n_buckets, w.value_len
+    vb = w.values.clone()
+    seg = w.seg_rec.cpu().numpy()
+    touched, idx = {}, []
+    for lp, gp in enumerate(w.partition_ids):
+        b = int(gp * 37) % B
+        r0, r1 = int(seg[lp * B + b]), int(seg[lp * B + b + 1])
+        if r1 > r0:
+            touched[lp] = b
+            idx.append(r0 * V)
+    if idx:
+        ii = torch.tensor(idx, dtype=torch.int64, device=vb.device)
+        vb[ii] = ((vb[ii].to(torch.int32) + 1) % 256).to(torch.uint8)
+    return vb, touched
+
+
 def make_workload(engine: "mde.Engine", n_partitions: int, n_buckets: int, value_len: int,
                   part_mode: str = "block", keys_per_partition: int = 0, n_keys: int = 0,
                   rank: int = 0, world: int = 1, seed: int = SYNTH_SEED,

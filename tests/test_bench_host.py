@@ -1,0 +1,58 @@
+"""CPU tests of bench.py's host side: the oracle sample a rank regenerates for its partitions
+(tests/sample.py) equals the matching rows of the oracle's whole-workload build, the config-5
+perturbation changes exactly one bucket per partition, and the CPU-share rule."""
+import numpy as np
+import pytest
+
+from tests.sample import host_sample, perturb_first_record
+
+P, B, N_KEYS, V = 12, 16, 3000, 40
+
+
+def _full(co, mode):
+    kpp = -(-N_KEYS // P)
+    g = np.arange(N_KEYS, dtype=np.uint64)
+    part, bk = co.synth_tags(g, P, B, {"block": 0, "mod": 1}[mode], kpp)
+    order, seg = co.layout_a(part, bk, P, B)
+    vals = co.synth_values(g[order], V, 0x4D445354)
+    return co.build(vals, seg, P, B, V)
+
+
+@pytest.mark.parametrize("mode", ["mod", "block"])
+@pytest.mark.parametrize("sample", [[0, 1, 2], [3, 7, 11], [11], list(range(12))])
+def test_host_sample_equals_whole_build_rows(coracle, mode, sample):
+    full = _full(coracle, mode)
+    values, seg, n, _ = host_sample(coracle, N_KEYS, P, V, B, mode, sample)
+    ref = coracle.build(values, seg, n, B, V)
+    ni = full["nodes"].size // P
+    for i, p in enumerate(sample):
+        assert np.array_equal(ref["digest"][i * B:(i + 1) * B], full["digest"][p * B:(p + 1) * B])
+        assert np.array_equal(ref["size"][i * B:(i + 1) * B], full["size"][p * B:(p + 1) * B])
+        assert ref["items"][i] == full["items"][p]
+        assert np.array_equal(ref["root"][i * 32:(i + 1) * 32], full["root"][p * 32:(p + 1) * 32])
+        assert np.array_equal(ref["nodes"][i * ni:(i + 1) * ni], full["nodes"][p * ni:(p + 1) * ni])
+
+
+def test_perturbed_replica_differs_in_exactly_one_bucket(coracle):
+    sample = list(range(P))
+    values, seg, n, _ = host_sample(coracle, N_KEYS, P, V, B, "mod", sample)
+    vb, touched = perturb_first_record(values, seg, V, B, sample)
+    a = coracle.build(values, seg, n, B, V)
+    b = coracle.build(vb, seg, n, B, V)
+    for i in range(n):
+        want = [touched[i]] if i in touched else []
+        assert coracle.diff(a["digest"][i * B:(i + 1) * B], b["digest"][i * B:(i + 1) * B]) == want
+        assert want == [] or touched[i] == (sample[i] * 37) % B
+
+
+def test_cpu_share_rule():
+    import bench
+    info = {"nproc": 192, "affinity_cpus": 192, "cgroup_cpu_quota": None, "omp_num_threads": 16}
+    assert bench.cpu_share(info) == 16
+    assert bench.cpu_share(info, world=8) == 2
+    info = {"nproc": 8, "affinity_cpus": 8, "cgroup_cpu_quota": 4.0, "omp_num_threads": None}
+    assert bench.cpu_share(info) == 4
+    info = {"nproc": 8, "affinity_cpus": None, "cgroup_cpu_quota": None, "omp_num_threads": None}
+    assert bench.cpu_share(info) == 8
+    h = bench.host_cpu_info()
+    assert h["nproc"] and "cpu_model" in h
