@@ -263,6 +263,13 @@ int mde_decode_epoch_tree_objects(mde_ctx* ctx, uint32_t n, const uint8_t* bytes
  * mde_verify_peer_capacity(n_buckets) buckets builds a deeper tree, which the reference's diff
  * always rejects; it is reported as MDE_E_TREE without being rebuilt. */
 uint32_t mde_verify_peer_capacity(uint32_t n_buckets);
+/* Unknown groups nested deeper than 64 levels (a hostile peer object) spill their group numbers
+ * to a per-context device area, so decoding stays linear in the object bytes however the nesting
+ * oscillates. The host-buffer calls size it exactly; the *_async decode / verify calls use what
+ * the context holds (by default enough for 8 MiB of objects per call; past that a deep object
+ * falls back to rescanning its outer group). Reserve room for `n_objects` objects of
+ * `object_bytes` bytes in all before such a call to keep every object linear. */
+int mde_reserve_decode_scratch(mde_ctx* ctx, uint64_t n_objects, uint64_t object_bytes);
 int mde_verify_epochs_async(mde_ctx* ctx, uint32_t n_partitions, uint32_t n_buckets,
                             const int32_t* partition, int64_t epoch, const uint64_t* digest,
                             const int32_t* size, const uint8_t* nodes, uint32_t n_peers,
@@ -301,6 +308,46 @@ int mde_multi_build(mde_group* group, const mde_records* rec, const mde_tree_out
  * one PCIe link per device. Same contract and results as mde_multi_build. */
 int mde_multi_build_streamed(mde_group* group, const mde_records* rec, const mde_tree_out* out,
                              uint64_t chunk_bytes);
+
+/* Request coalescing for the production call shape (one partition per call). The reference runs
+ * RawPartitionMerkleTree and the VerifyEpoch decision for ONE (partition, epoch) per call, on any
+ * of workers_count = 100 goroutines with up to partition_concurrency = 10 in flight
+ * (config/default-config.yaml:7,9; main/manager.go:68,166-170,489-497,998-1118). A batcher owns
+ * its own contexts on `device` and merges concurrent calls by group commit: a caller's request
+ * joins the queue; the first caller to find no batch running takes every compatible queued
+ * request (same kind and n_buckets; verify: same epoch and replica_count, objects wanted or not;
+ * at most max_partitions partitions; after waiting up to max_wait_us for more, 0 = no wait) and
+ * runs them as ONE H2D copy + ONE build (or trees + verify) + ONE D2H copy; requests arriving
+ * meanwhile form the next batch. Every call is synchronous and thread-safe, returns exactly what
+ * the per-call entry point returns for its own inputs, and writes its own error message into
+ * err (err_cap bytes, NUL-terminated; may be NULL) -- no shared last-error state, so the Go shim
+ * needs no lock. Inputs are host pointers, read only during the call (cgo pointer rules).
+ * mde_batcher_destroy must not race with calls in flight. */
+typedef struct mde_batcher mde_batcher;
+int mde_batcher_create(int device, uint32_t max_partitions, uint32_t max_wait_us, mde_batcher** out);
+void mde_batcher_destroy(mde_batcher* b);
+/* A batcher keeps up to mde_batcher_contexts() batches in flight, each on its own context (own
+ * stream and scratch), so small batches run concurrently on the device; mde_batcher_ctx(b, i)
+ * gives context i (tuning, device info). */
+uint32_t mde_batcher_contexts(const mde_batcher* b);
+mde_ctx* mde_batcher_ctx(mde_batcher* b, uint32_t i);
+/* batches run, requests served and partitions built since creation */
+int mde_batcher_stats(mde_batcher* b, uint64_t* batches, uint64_t* requests, uint64_t* partitions);
+/* RawPartitionMerkleTree (main/merkle_tree.go:86-116) for the caller's partitions: mde_build's
+ * contract for layout A records (fixed or variable-length values); records outside
+ * [seg_rec[0], seg_rec[P*B]) are not read. */
+int mde_batch_build(mde_batcher* b, const mde_records* rec, const mde_tree_out* out, char* err,
+                    uint64_t err_cap);
+/* The VerifyEpoch decision step (main/manager.go:1072-1104) for ONE partition: mde_verify_epochs
+ * with n_partitions = 1, whose local tree is given by its bucket digests (and sizes, required for
+ * object_out) -- the tree itself (EpochTreeObjectToMerkleTree of the local object) is built on the
+ * device in the same batch. n_peers may differ between callers of one batch. */
+int mde_batch_verify(mde_batcher* b, uint32_t n_buckets, int32_t partition, int64_t epoch,
+                     const uint64_t* digest, const int32_t* size, uint32_t n_peers,
+                     const uint8_t* peer_bytes, const uint64_t* peer_off, uint32_t replica_count,
+                     uint8_t* valid, int32_t* valid_count, int32_t* diff_ids, int32_t* diff_count,
+                     int32_t* peer_status, uint8_t* object_out, uint64_t object_stride,
+                     uint32_t* object_len, char* err, uint64_t err_cap);
 
 /* Write-time tagging of raw keys (device): bucket = BE64(SHA256(key)[:8]) % n_buckets
  * (main/manager.go:773-778), partition = XXH64(key, 0) % n_partitions (hashring.go:108-110).

@@ -44,6 +44,8 @@ EXPORTED_SYMBOLS = (
     "mde_memcpy_h2d", "mde_memcpy_d2h", "mde_verify_peer_capacity", "mde_verify_epochs",
     "mde_verify_epochs_async", "mde_group_create", "mde_group_destroy", "mde_group_size",
     "mde_group_ctx", "mde_group_last_error", "mde_multi_build", "mde_multi_build_streamed",
+    "mde_batcher_create", "mde_batcher_destroy", "mde_batcher_ctx", "mde_batcher_contexts", "mde_batcher_stats",
+    "mde_batch_build", "mde_batch_verify", "mde_reserve_decode_scratch",
 )
 
 
@@ -131,6 +133,7 @@ def load_library() -> C.CDLL:
         "mde_decode_epoch_tree_objects": (C.c_int, [vp, u32, vp, vp, u32, vp, vp, vp, vp, vp, vp, vp, vp]),
         "mde_decode_epoch_tree_objects_async": (C.c_int, [vp, u32, vp, vp, u32, vp, vp, vp, vp, vp, vp, vp, vp]),
         "mde_verify_peer_capacity": (u32, [u32]),
+        "mde_reserve_decode_scratch": (C.c_int, [vp, u64, u64]),
         "mde_verify_epochs": (C.c_int, [vp, u32, u32, vp, C.c_int64, vp, vp, vp, u32, vp, vp, u32,
                                         vp, vp, vp, vp, vp, vp, u64, vp]),
         "mde_verify_epochs_async": (C.c_int, [vp, u32, u32, vp, C.c_int64, vp, vp, vp, u32, vp, vp,
@@ -143,6 +146,14 @@ def load_library() -> C.CDLL:
         "mde_group_last_error_copy": (C.c_uint64, [vp, C.c_char_p, C.c_uint64]),
         "mde_multi_build": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
         "mde_multi_build_streamed": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), C.c_uint64]),
+        "mde_batcher_create": (C.c_int, [C.c_int, u32, u32, C.POINTER(vp)]),
+        "mde_batcher_destroy": (None, [vp]),
+        "mde_batcher_ctx": (vp, [vp, u32]),
+        "mde_batcher_contexts": (u32, [vp]),
+        "mde_batcher_stats": (C.c_int, [vp, vp, vp, vp]),
+        "mde_batch_build": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), C.c_char_p, u64]),
+        "mde_batch_verify": (C.c_int, [vp, u32, i32, C.c_int64, vp, vp, u32, vp, vp, u32, vp, vp, vp, vp,
+                                       vp, vp, u64, vp, C.c_char_p, u64]),
         "mde_synth_tags_async": (C.c_int, [vp, vp, u64, u32, u32, C.c_int, u64, vp, vp]),
         "mde_synth_values_async": (C.c_int, [vp, vp, vp, u64, u32, u64]),
         "mde_dev_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
@@ -626,3 +637,82 @@ class Group:
         if rc != MDE_OK:
             raise MdeError(rc, buf.value.decode(errors="replace"))
         return out
+
+
+class Batcher:
+    """mde_batcher: concurrent one-partition calls coalesced into one device build / verify (group
+    commit). Thread-safe; ctypes releases the GIL, so Python threads really call concurrently."""
+
+    def __init__(self, device: int = 0, max_partitions: int = 256, max_wait_us: int = 0):
+        self.lib = load_library()
+        h = C.c_void_p()
+        rc = self.lib.mde_batcher_create(device, max_partitions, max_wait_us, C.byref(h))
+        if rc != MDE_OK:
+            raise MdeError(rc, f"mde_batcher_create(device={device}) failed: {self.lib.mde_strerror(rc).decode()}")
+        self.b = h
+
+    def close(self):
+        if getattr(self, "b", None):
+            self.lib.mde_batcher_destroy(self.b)
+            self.b = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stats(self):
+        v = [C.c_uint64() for _ in range(3)]
+        self.lib.mde_batcher_stats(self.b, *(C.byref(x) for x in v))
+        return {"batches": v[0].value, "requests": v[1].value, "partitions": v[2].value}
+
+    def build(self, values, seg_rec, n_partitions, n_buckets, value_stride=0, value_off=None, want_nodes=True):
+        """mde_batch_build: RawPartitionMerkleTree for this caller's partitions; same outputs as
+        Engine.build."""
+        P, B = n_partitions, n_buckets
+        seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
+        values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)
+        if value_off is not None:
+            value_off = np.ascontiguousarray(value_off, dtype=np.uint64)
+        n_rec = (value_off.size - 1) if value_off is not None else (values.size // value_stride if value_stride else 0)
+        rec = Records(_ptr(values), values.nbytes, value_stride, 0, _ptr(value_off), n_rec, P, B, _ptr(seg_rec))
+        out = {
+            "digest": np.zeros(P * B, np.uint64), "size": np.zeros(P * B, np.int32),
+            "items": np.zeros(P, np.int32), "root": np.zeros(P * 32, np.uint8),
+            "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
+        }
+        to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
+        err = C.create_string_buffer(512)
+        rc = self.lib.mde_batch_build(self.b, C.byref(rec), C.byref(to), err, len(err))
+        if rc != MDE_OK:
+            raise MdeError(rc, err.value.decode(errors="replace"))
+        return out
+
+    def verify(self, n_buckets, digest, size, peer_objects, replica_count, epoch, partition=0, want_object=True):
+        """mde_batch_verify for one partition: peer_objects = list of wire bytes (None = absent)."""
+        B = n_buckets
+        digest = np.ascontiguousarray(digest, dtype=np.uint64).reshape(-1)
+        size = np.ascontiguousarray(size, dtype=np.int32).reshape(-1)
+        R = len(peer_objects)
+        flat = [o or b"" for o in peer_objects]
+        off = np.zeros(R + 1, np.uint64)
+        off[1:] = np.cumsum([len(o) for o in flat])
+        blob = np.frombuffer(b"".join(flat) or b"\0", dtype=np.uint8).copy()
+        valid = np.zeros(1, np.uint8)
+        vc = np.zeros(1, np.int32)
+        ids = np.zeros(B, np.int32)
+        dc = np.zeros(1, np.int32)
+        st = np.zeros(max(R, 1), np.int32)
+        stride = int(self.lib.mde_epoch_tree_object_max_bytes(B)) if want_object else 0
+        obj = np.zeros(max(stride, 1), np.uint8) if want_object else None
+        olen = np.zeros(1, np.uint32) if want_object else None
+        err = C.create_string_buffer(512)
+        rc = self.lib.mde_batch_verify(self.b, B, int(partition), epoch, _ptr(digest), _ptr(size), R, _ptr(blob),
+                                       _ptr(off), replica_count, _ptr(valid), _ptr(vc), _ptr(ids), _ptr(dc),
+                                       _ptr(st), _ptr(obj), stride, _ptr(olen), err, len(err))
+        if rc != MDE_OK:
+            raise MdeError(rc, err.value.decode(errors="replace"))
+        return {"valid": bool(valid[0]), "valid_count": int(vc[0]), "diff": ids[:int(dc[0])].tolist(),
+                "peer_status": st[:R].tolist(),
+                "object": obj[:int(olen[0])].tobytes() if want_object else None}

@@ -7,6 +7,9 @@ Outputs (git-ignored, but shipped to the GPU box with the snapshot):
   mydatastore_amd/libmde_host.so    C++ mirror of main/merkle_tree.go over the C ABI
   tests/cpp/build/test_merkle_tree  C++ port of the reference's Merkle tests
   tests/cpp/build/cabi_bench        plain-C driver of the C ABI (C4 build, no PyTorch)
+  tests/cpp/build/batch_test        concurrent callers of the batcher vs mde_build / the C oracle
+  tests/cpp/build/batch_bench       production call shape: CPU oracle vs per-call vs batched, P callers
+  tests/cpp/build/shim_replay       the Go shim's call sequences replayed from C (checked by pytest)
   oracle/build/liboracle.so         CPU restatement (test infrastructure only)
 """
 from __future__ import annotations
@@ -31,6 +34,9 @@ HOST_LIB = PKG / "libmde_host.so"
 ORACLE_LIB = ROOT / "oracle" / "build" / "liboracle.so"
 CPP_TEST = ROOT / "tests" / "cpp" / "build" / "test_merkle_tree"
 C_BENCH = ROOT / "tests" / "cpp" / "build" / "cabi_bench"
+BATCH_TEST = ROOT / "tests" / "cpp" / "build" / "batch_test"
+BATCH_BENCH = ROOT / "tests" / "cpp" / "build" / "batch_bench"
+SHIM_REPLAY = ROOT / "tests" / "cpp" / "build" / "shim_replay"
 
 
 def _stale(target: Path, deps) -> bool:
@@ -49,7 +55,7 @@ def _run(cmd, verbose):
 def build_engine(verbose: bool = True) -> Path:
     OBJ.mkdir(exist_ok=True)
     headers = list(CSRC.glob("*.hpp")) + [ROOT / "include" / "mde.h"]
-    sources = sorted(CSRC.glob("*.hip")) + [CSRC / "mde_api.cpp"]
+    sources = sorted(CSRC.glob("*.hip")) + [CSRC / "mde_api.cpp", CSRC / "batch.cpp"]
     objs = []
     for src in sources:
         obj = OBJ / (src.stem + ".o")
@@ -81,6 +87,16 @@ def build_host(verbose: bool = True) -> Path:
         _run(["gcc", "-O2", "-std=c11", "-D_POSIX_C_SOURCE=199309L", "-Wall", f"-I{ROOT / 'include'}",
               c_src, "-o", C_BENCH, f"-L{PKG}", "-lmde", f"-Wl,-rpath,{PKG}",
               "-Wl,-rpath,$ORIGIN/../../../mydatastore_amd"], verbose)
+    # test programs that also link the C oracle (test infrastructure) as their checker
+    for name, out in (("batch_test.c", BATCH_TEST), ("batch_bench.c", BATCH_BENCH), ("shim_replay.c", SHIM_REPLAY)):
+        src = ROOT / "tests" / "cpp" / name
+        if src.exists() and _stale(out, [src, ROOT / "include" / "mde.h", LIB, ORACLE_LIB]):
+            out.parent.mkdir(parents=True, exist_ok=True)
+            _run(["gcc", "-O2", "-std=c11", "-D_GNU_SOURCE", "-Wall", f"-I{ROOT / 'include'}", src, "-o", out,
+                  f"-L{PKG}", "-lmde", f"-L{ORACLE_LIB.parent}", "-loracle", "-lpthread",
+                  f"-Wl,-rpath,{PKG}", f"-Wl,-rpath,{ORACLE_LIB.parent}",
+                  "-Wl,-rpath,$ORIGIN/../../../mydatastore_amd", "-Wl,-rpath,$ORIGIN/../../../oracle/build"],
+                 verbose)
     return HOST_LIB
 
 
@@ -94,8 +110,8 @@ def build_oracle(verbose: bool = True) -> Path:
 
 def build_all(verbose: bool = True) -> None:
     build_engine(verbose)
-    build_host(verbose)
     build_oracle(verbose)
+    build_host(verbose)
 
 
 if __name__ == "__main__":

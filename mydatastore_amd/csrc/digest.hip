@@ -690,22 +690,28 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
   digest_dispatch<U, NT, PIPE, PRIO, MODE, false>(a, db);
 }
 
-// One-launch build of a small arena (the synchronous one-partition calls of VerifyEpoch). Digest
-// phase bucket-parallel: thread i sums bucket i's bytes with 16-byte loads (a wave walking the
-// bucket boundaries of a small arena in order pays one dependent seg_rec load per bucket, which is
-// what bounds the streaming kernel there); then, after a device-scope fence and a barrier, the same
-// workgroup builds the <= 256/G partitions' trees with tree_body. It saves the second launch of
-// the digest + tree pair.
+// One-launch build of small arenas (the synchronous one-partition calls of VerifyEpoch, and the
+// batcher's many small partitions, mde_batch_build). Workgroup b owns partitions
+// [b * groups, (b + 1) * groups) (groups = 256 / G trees per workgroup, tree_body's shape): digest
+// phase bucket-parallel over ITS partitions' buckets -- thread i sums bucket i's bytes with 16-byte
+// loads (a wave walking the bucket boundaries of a small arena in order pays one dependent seg_rec
+// load per bucket, which is what bounds the streaming kernel there) -- then, after a device-scope
+// fence and a barrier, the same workgroup builds those partitions' trees with tree_body. Every
+// bucket is summed by exactly one workgroup, so no cross-workgroup synchronisation is needed; it
+// saves the second launch of the digest + tree pair.
 __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLaunch t, uint32_t G, uint32_t words) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const u32x4* base = reinterpret_cast<const u32x4*>(d.base);
   unsigned long long* sums = const_cast<unsigned long long*>(t.sums_in);  // zero on entry
-  // K threads per bucket (K = 256 / S rounded down to a power of two, >= 1), each taking every
+  const uint32_t groups = (uint32_t)kThreads / G;
+  const uint32_t s_beg = min(blockIdx.x * groups * t.B, d.S), s_end = min((blockIdx.x + 1) * groups * t.B, d.S);
+  const uint32_t nb = s_end - s_beg;
+  // K threads per bucket (K = 256 / nb rounded down to a power of two, >= 1), each taking every
   // K-th 16-byte vector of the bucket, four loads in flight
   uint32_t K = 1;
-  while (K * 2 * d.S <= (uint32_t)kThreads) K *= 2;
+  while (K * 2 * nb <= (uint32_t)kThreads) K *= 2;
   const uint32_t j = threadIdx.x % K;
-  for (uint32_t s = threadIdx.x / K; s < d.S; s += kThreads / K) {
+  for (uint32_t s = s_beg + threadIdx.x / K; s < s_end; s += kThreads / K) {
     const uint64_t lo = segpos(d, s), hi = segpos(d, s + 1);
     const int64_t l = (int64_t)lo, h = (int64_t)hi;
     uint32_t acc = 0;
@@ -726,7 +732,7 @@ __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLa
   }
   __threadfence();  // the sums are visible before any wave reads them
   __syncthreads();
-  tree_body<true>(t, G, words, 0, lds, kThreads);
+  tree_body<true>(t, G, words, blockIdx.x, lds, kThreads);
 }
 
 typedef void (*DigestKernel)(DigestLaunch);
@@ -762,17 +768,23 @@ const Variant& variant(int v) { return kVariants[(v >= 0 && v < kNumVariants) ? 
 
 int bucket_digest_variants() { return kNumVariants; }
 
+// The one-launch build serves arenas of at most kSmallBuildMaxBytes per workgroup on average:
+// one workgroup streams its partitions' bytes alone (~0.1 TB/s), so larger arenas go to the
+// full-chip digest kernel + tree kernel instead.
 bool small_build_fits(uint64_t bytes, uint32_t P, uint32_t B) {
   TreeGeometry g;
-  if (!tree_geometry(B, &g) || g.G > (uint32_t)kThreads) return false;
-  return bytes <= kSmallBuildMaxBytes && P >= 1 && P <= (uint32_t)kThreads / g.G;
+  if (!tree_geometry(B, &g) || g.G > (uint32_t)kThreads || P < 1) return false;
+  const uint64_t blocks = (P + (uint64_t)kThreads / g.G - 1) / ((uint64_t)kThreads / g.G);
+  return bytes <= kSmallBuildMaxBytes * blocks;
 }
 
 hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t st) {
   TreeGeometry g;
   tree_geometry(t.B, &g);
-  const size_t lds = (size_t)g.words * 4u * ((uint32_t)kThreads / g.G);
-  hipLaunchKernelGGL(small_build_kernel, dim3(1), dim3(kThreads), lds, st, d, t, g.G, g.words);
+  const uint32_t groups = (uint32_t)kThreads / g.G;
+  const size_t lds = (size_t)g.words * 4u * groups;
+  hipLaunchKernelGGL(small_build_kernel, dim3((t.P + groups - 1) / groups), dim3(kThreads), lds, st, d, t, g.G,
+                     g.words);
   return hipGetLastError();
 }
 

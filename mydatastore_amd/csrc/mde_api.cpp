@@ -66,6 +66,7 @@ struct mde_ctx {
   Buf packed_in, packed_out, pin_in, pin_out;
   Buf extract_scratch;
   Buf verify_scratch;
+  Buf deep_scratch;  // spill area of deeply nested unknown groups (WireDecodeLaunch::deep)
   bool verify_chain = false;  // mde_set_verify_mode(1): the five-launch chain even when fusable
   // Host-ingest ring (mde_build_streamed): two slots of values / value_off / seg_rec.
   Buf ring_vals[2], ring_voff[2], ring_seg[2];
@@ -684,11 +685,32 @@ int tree_digests_async(mde_ctx* c, uint32_t n_trees, uint32_t B, const uint64_t*
   return MDE_OK;
 }
 
+// Default spill area for async decodes (objects of up to this many bytes in all never rescan).
+constexpr uint64_t kDefaultDeepObjectBytes = 8ull << 20;
+
+// The decode's spill area: at least the entries `n` objects of `bytes` bytes need (exact for the
+// host-buffer calls), else whatever the context holds (async calls; mde_reserve_decode_scratch).
+int attach_deep(mde_ctx* c, mde::WireDecodeLaunch* d, uint64_t n, uint64_t bytes) {
+  const uint64_t want = mde::wire_deep_entries(n, bytes) * 4;
+  int rc = ensure_buf(c, c->deep_scratch, std::max(want, c->deep_scratch.cap));
+  if (rc) return rc;
+  d->deep = static_cast<uint32_t*>(c->deep_scratch.p);
+  d->deep_cap = c->deep_scratch.cap / 4;
+  return MDE_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int mde_abi_version(void) { return MDE_ABI_VERSION; }
+
+int mde_reserve_decode_scratch(mde_ctx* c, uint64_t n_objects, uint64_t object_bytes) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  return ensure_buf(c, c->deep_scratch, std::max(mde::wire_deep_entries(n_objects, object_bytes) * 4,
+                                                  c->deep_scratch.cap));
+}
 
 const char* mde_strerror(int code) {
   switch (code) {
@@ -749,6 +771,7 @@ void mde_destroy(mde_ctx* c) {
     if (c->pin_out.p) (void)hipHostFree(c->pin_out.p);
     if (c->extract_scratch.p) (void)hipFree(c->extract_scratch.p);
     if (c->verify_scratch.p) (void)hipFree(c->verify_scratch.p);
+    if (c->deep_scratch.p) (void)hipFree(c->deep_scratch.p);
     for (int i = 0; i < 2; i++) {
       for (auto* b : {&c->ring_vals[i], &c->ring_voff[i], &c->ring_seg[i]})
         if (b->p) (void)hipFree(b->p);
@@ -1279,6 +1302,8 @@ int mde_decode_epoch_tree_objects_async(mde_ctx* c, uint32_t n, const uint8_t* b
   if (!off || !digest || !size || !n_buckets || (n && !bytes))
     return set_err(c, MDE_E_INVAL, "bad decode arguments");
   mde::WireDecodeLaunch a{n, bytes, off, cap, partition, lower, upper, digest, size, valid, items, n_buckets};
+  int rc = attach_deep(c, &a, 0, kDefaultDeepObjectBytes);
+  if (rc) return rc;
   MDE_HIP(c, mde::launch_wire_decode(a, c->stream));
   return MDE_OK;
 }
@@ -1315,6 +1340,7 @@ int mde_decode_epoch_tree_objects(mde_ctx* c, uint32_t n, const uint8_t* bytes, 
                           static_cast<uint8_t*>(dp(7)),
                           static_cast<int32_t*>(dp(8)),
                           static_cast<int32_t*>(dp(9))};
+  if ((rc = attach_deep(c, &a, N, nbytes))) return rc;
   MDE_HIP(c, mde::launch_wire_decode(a, c->stream));
   auto down = [&](void* dst, int i) -> int {
     if (!dst) return MDE_OK;
@@ -1373,6 +1399,7 @@ int verify_async(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, i
     mde::VerifyFusedLaunch f{};
     f.dec = mde::WireDecodeLaunch{(uint32_t)T, peer_bytes, peer_off, cap, nullptr, nullptr, nullptr, pd,
                                   static_cast<int32_t*>(at(1)), pvalid, nullptr, nbk};
+    if ((rc = attach_deep(c, &f.dec, 0, kDefaultDeepObjectBytes))) return rc;
     f.tree.B = cap;
     f.tree.digest_in = pd;
     f.tree.root_out = static_cast<uint8_t*>(at(5));
@@ -1391,6 +1418,7 @@ int verify_async(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, i
     // EpochTreeObjectToMerkleTree: decode (>cap buckets can only diff with an error: deeper tree)
     mde::WireDecodeLaunch d{(uint32_t)T, peer_bytes, peer_off, cap, nullptr, nullptr, nullptr, pd,
                             static_cast<int32_t*>(at(1)), pvalid, nullptr, nbk};
+    if ((rc = attach_deep(c, &d, 0, kDefaultDeepObjectBytes))) return rc;
     MDE_HIP(c, mde::launch_wire_decode(d, c->stream));
     mde::TreeLaunch t{};
     t.P = (uint32_t)T;
@@ -1460,6 +1488,9 @@ int mde_verify_epochs(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partiti
   const int o_dc = io.out(diff_count, N * 4), o_ps = io.out(T ? peer_status : nullptr, T * 4);
   const int o_obj = io.out(object_out, N * ostride), o_olen = io.out(object_out ? object_len : nullptr, N * 4);
   int rc = io.upload();
+  if (rc) return rc;
+  // the spill area covers every object of this call (no rescans, whatever they nest)
+  rc = ensure_buf(c, c->deep_scratch, std::max(mde::wire_deep_entries(T, nbytes) * 4, c->deep_scratch.cap));
   if (rc) return rc;
   rc = verify_async(c, P, B, partition ? static_cast<const int32_t*>(io.dev(i_part)) : nullptr, epoch,
                     static_cast<const uint64_t*>(io.dev(i_dig)),

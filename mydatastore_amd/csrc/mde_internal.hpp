@@ -208,7 +208,13 @@ struct WireDecodeLaunch {
   uint8_t* valid;
   int32_t* items;
   int32_t* n_buckets;        // [n] bucket count, or MDE_E_DECODE / MDE_E_CAPACITY
+  // Spill area of deeply nested unknown groups (wire_body.hpp skip_group): object i uses entries
+  // [(off[i] - off[0]) / 2 + i, + len_i / 2 + 1); nullptr / too small = rescan fallback.
+  uint32_t* deep = nullptr;
+  uint64_t deep_cap = 0;     // entries
 };
+// Entries a decode of n objects of `bytes` bytes in all needs in WireDecodeLaunch::deep.
+inline uint64_t wire_deep_entries(uint64_t n, uint64_t bytes) { return bytes / 2 + 2 * n + 2; }
 inline uint64_t wire_max_bytes(uint32_t B) { return 57 + 20ull * (B + (B & 1u)); }
 hipError_t launch_wire_encode(const WireEncodeLaunch& a, hipStream_t st);
 hipError_t launch_wire_decode(const WireDecodeLaunch& a, hipStream_t st);

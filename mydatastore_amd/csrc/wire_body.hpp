@@ -262,9 +262,15 @@ struct Cursor {
 // nest and the 10,002nd fails.
 // The open groups' numbers live in gstack, a ring of the kWireGroupDepth deepest levels
 // (wave-uniform LDS): level k at gstack[(k - 1) % kWireGroupDepth], valid for levels
-// [lo, depth]. An end tag below lo (only after more than kWireGroupDepth levels) refills the ring
-// by rescanning the group from its first byte: the last start tag seen at level k before the end
-// tag is the open level-k group. Objects nested no deeper than the ring never rescan.
+// [lo, depth]. Every level's number is also written through to `deep` (level k at deep[k - 1]),
+// the object's spill area in global memory (wire_deep_slot: half an entry per object byte, as a
+// level takes at least a start and an end tag byte), so an end tag below lo reads its number
+// back in one load: the skip stays linear however the depth oscillates (a hostile peer object
+// nested past 64 levels that repeatedly dips below the ring and climbs again). Without a spill
+// area (an async call whose objects exceed the context's reserved scratch) an end tag below lo
+// refills the ring by rescanning the group from its first byte: the last start tag seen at level k
+// before the end tag is the open level-k group. Objects nested no deeper than the ring never
+// touch either.
 constexpr uint32_t kWireGroupDepth = 64;
 constexpr uint32_t kWireGroupMaxNest = 10001;
 __device__ __forceinline__ void group_refill(const Cursor& c, uint64_t start, uint64_t stop, uint32_t depth,
@@ -295,10 +301,27 @@ __device__ __forceinline__ void group_refill(const Cursor& c, uint64_t start, ui
   }
 }
 
-__device__ __forceinline__ void skip_group(Cursor& c, uint64_t num, uint32_t* gstack) {
+// The spill area's reads and writes are lane 0's vector memory operations (relaxed atomics:
+// read-your-writes within the lane), broadcast to the wave.
+// A level deeper than half the object's bytes can never be closed (each open level still needs
+// an end tag byte), so such an object fails whatever happens next: levels past the area's
+// n / 2 + 1 entries are not spilled, and an end tag for one of them fails the object at once.
+__device__ __forceinline__ void deep_put(uint32_t* deep, uint32_t levels, uint32_t level, uint32_t v, uint32_t lane) {
+  if (deep && level <= levels && lane == 0)
+    __hip_atomic_store(deep + (level - 1), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t deep_get(uint32_t* deep, uint32_t level, uint32_t lane) {
+  uint32_t v = 0;
+  if (lane == 0) v = __hip_atomic_load(deep + (level - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (uint32_t)__shfl((int)v, 0);
+}
+
+__device__ __forceinline__ void skip_group(Cursor& c, uint64_t num, uint32_t* gstack, uint32_t* deep, uint32_t lane) {
   const uint64_t start = c.pos;  // first byte inside the outermost group (level 1)
-  uint32_t depth = 1, lo = 1;
+  const uint32_t levels = (uint32_t)min<uint64_t>(c.n / 2 + 1, kWireGroupMaxNest);  // spilled levels
+  uint32_t depth = 1, lo = 1;    // invariant: lo <= depth + 1 (lo = depth + 1: no ring level valid)
   gstack[0] = (uint32_t)num;
+  deep_put(deep, levels, 1, (uint32_t)num, lane);
   while (c.ok) {
     const uint64_t key = c.varint();
     if (!c.ok) return;
@@ -306,17 +329,26 @@ __device__ __forceinline__ void skip_group(Cursor& c, uint64_t num, uint32_t* gs
     const uint32_t w = (uint32_t)(key & 7);
     if (n2 < 1 || n2 > 0x7FFFFFFFull) { c.ok = false; return; }
     if (w == 4) {
-      if (depth < lo) {  // this level's number left the ring: rescan up to this end tag
+      uint32_t open;
+      if (depth >= lo) {
+        open = gstack[(depth - 1) % kWireGroupDepth];
+      } else if (deep) {  // this level's number left the ring: read it back from the spill area
+        if (depth > levels) { c.ok = false; return; }  // unclosable (see deep_put)
+        open = deep_get(deep, depth, lane);
+        lo = depth;  // after the pop below, the ring holds no level
+      } else {  // no spill area: rescan up to this end tag
         group_refill(c, start, c.pos, depth, (uint32_t)num, gstack);
         lo = depth > kWireGroupDepth ? depth - kWireGroupDepth + 1 : 1u;
+        open = gstack[(depth - 1) % kWireGroupDepth];
       }
-      if ((uint32_t)n2 != gstack[(depth - 1) % kWireGroupDepth]) { c.ok = false; return; }
+      if ((uint32_t)n2 != open) { c.ok = false; return; }
       if (--depth == 0) return;
       continue;
     }
     if (w == 3) {
       if (depth == kWireGroupMaxNest) { c.ok = false; return; }  // errCodeRecursion
       gstack[depth++ % kWireGroupDepth] = (uint32_t)n2;
+      deep_put(deep, levels, depth, (uint32_t)n2, lane);
       if (depth - lo >= kWireGroupDepth) lo = depth - kWireGroupDepth + 1;
       continue;
     }
@@ -326,6 +358,14 @@ __device__ __forceinline__ void skip_group(Cursor& c, uint64_t num, uint32_t* gs
     if (w == 2) { const uint64_t len = c.varint(); if (c.ok) c.skip(len); continue; }
     c.ok = false;  // reserved wire types 6, 7
   }
+}
+
+// Object i's spill area in a.deep (entries [(off[i] - off[0]) / 2 + i, + n / 2 + 1): disjoint per
+// object, n / 2 + 1 entries >= its deepest level), or nullptr when a.deep does not cover it.
+__device__ __forceinline__ uint32_t* wire_deep_slot(const WireDecodeLaunch& a, uint32_t i, uint64_t n) {
+  if (!a.deep) return nullptr;
+  const uint64_t base = (a.off[i] - a.off[0]) / 2 + i;
+  return base + n / 2 + 1 <= a.deep_cap ? a.deep + base : nullptr;
 }
 
 // Object i by ALL 64 lanes of one wave (lane = 0..63), parsing the n bytes at p (the object in
@@ -485,7 +525,7 @@ __device__ __forceinline__ void decode_object(const WireDecodeLaunch& a, uint32_
     if (wt == 1) { c.skip(8); continue; }
     if (wt == 5) { c.skip(4); continue; }
     if (wt == 2) { const uint64_t len = c.varint(); if (c.ok) c.skip(len); continue; }
-    if (wt == 3) { skip_group(c, key >> 3, gstack); continue; }
+    if (wt == 3) { skip_group(c, key >> 3, gstack, wire_deep_slot(a, i, n), lane); continue; }
     c.ok = false;  // a stray end group, reserved wire types 6, 7
   }
   if (!c.ok && !err) err = -6;

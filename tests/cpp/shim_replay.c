@@ -1,0 +1,213 @@
+/*
+ * shim_replay.c -- the Go shim's exact call sequences (integration/go/merkle_gpu.go) replayed in
+ * plain C through include/mde.h, on scenarios read from a file; the results go to stdout and the
+ * pytest driver (tests/test_integration.py) compares them with the oracle's restatement of the
+ * reference (oracle/oracle.py: raw_partition_merkle_tree, different_merkle_tree_buckets,
+ * verify_epoch). The shim cannot be compiled here (no Go toolchain); this program makes the same
+ * ABI calls with the same argument shapes:
+ *
+ *   build B n           RawPartitionMerkleTree (main/merkle_tree.go:86-116): the shim walks the
+ *                       B bucket ranges and appends every value to ONE arena, record by record:
+ *                       value_off grows by each value's length, seg_rec by the record count per
+ *                       bucket, n_partitions = 1, value_stride = 0 (variable-length values); an
+ *                       empty arena gets one padding byte. -> mde_batch_build.
+ *   diff Ba Bb          DifferentMerkleTreeBuckets (main/merkle_tree.go:159-161): the two trees'
+ *                       leaf digests with merkletree's duplicate of an odd last leaf dropped -- so a
+ *                       tree rebuilt from an odd-B object keeps its B+1 leaves -> mde_diff_digests.
+ *   verify B p E rc R   VerifyEpoch's peer loop (main/manager.go:1072-1104): the local tree's
+ *                       digests and sizes, R peer objects as wire bytes (absent = empty range)
+ *                       -> mde_batch_verify.
+ *
+ * Input: whitespace-separated tokens; values and peer objects as hex strings ("-" = empty).
+ *   build B n  <bucket of each record, nondecreasing>  <hex value of each record>
+ *   diff Ba Bb <Ba digests> <Bb digests>
+ *   verify B p E rc R <B digests> <B sizes> <R hex objects>
+ * Output, one line per op:
+ *   build <digests> ; <sizes> ; <items> ; <root hex>
+ *   diff <count> <ids>            (count = MDE_E_TREE where the reference errors)
+ *   verify <valid> <validCount> ; <diffSet> ; <peer statuses> ; <object hex>
+ */
+#include <inttypes.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mde.h"
+
+static void* xmalloc(size_t n) {
+  void* p = calloc(1, n ? n : 1);
+  if (!p) {
+    fprintf(stderr, "allocation failed\n");
+    exit(1);
+  }
+  return p;
+}
+
+static char tok[1 << 22];
+
+static const char* next(FILE* f) {
+  if (fscanf(f, "%4194303s", tok) != 1) return NULL;
+  return tok;
+}
+
+static uint64_t num(FILE* f) {
+  const char* t = next(f);
+  if (!t) {
+    fprintf(stderr, "truncated input\n");
+    exit(2);
+  }
+  return strtoull(t, NULL, 10);
+}
+
+/* hex token -> bytes appended at *buf (capacity grown as needed); returns the length */
+static uint64_t hex(FILE* f, uint8_t** buf, uint64_t* len, uint64_t* cap) {
+  const char* t = next(f);
+  if (!t) exit(2);
+  if (!strcmp(t, "-")) return 0;
+  const uint64_t n = strlen(t) / 2;
+  if (*len + n > *cap) {
+    *cap = (*len + n) * 2 + 64;
+    *buf = realloc(*buf, *cap);
+    if (!*buf) exit(1);
+  }
+  for (uint64_t i = 0; i < n; i++) {
+    unsigned v;
+    sscanf(t + 2 * i, "%2x", &v);
+    (*buf)[*len + i] = (uint8_t)v;
+  }
+  *len += n;
+  return n;
+}
+
+static void print_hex(const uint8_t* p, uint64_t n) {
+  for (uint64_t i = 0; i < n; i++) printf("%02x", p[i]);
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) return 2;
+  FILE* f = fopen(argv[1], "r");
+  if (!f) return 2;
+  mde_batcher* batcher = NULL;
+  mde_ctx* ctx = NULL;
+  int rc = mde_batcher_create(0, 256, 0, &batcher);
+  if (rc || (rc = mde_create(0, &ctx))) {
+    fprintf(stderr, "create: %d (%s)\n", rc, mde_strerror(rc));
+    return 1;
+  }
+  char err[512];
+  const char* op;
+  while ((op = next(f))) {
+    if (!strcmp(op, "build")) {
+      const uint32_t B = (uint32_t)num(f);
+      const uint64_t n = num(f);
+      uint64_t* bucket = xmalloc(n * 8);
+      for (uint64_t i = 0; i < n; i++) bucket[i] = num(f);
+      /* the shim's loop: for each bucket, for each record of its range, append the value */
+      uint8_t* values = NULL;
+      uint64_t vlen = 0, vcap = 0;
+      uint64_t* value_off = xmalloc((n + 1) * 8);
+      uint64_t* seg_rec = xmalloc(((uint64_t)B + 1) * 8);
+      uint64_t r = 0;
+      seg_rec[0] = 0;
+      for (uint32_t b = 0; b < B; b++) {
+        while (r < n && bucket[r] == b) {
+          hex(f, &values, &vlen, &vcap);
+          value_off[++r] = vlen;
+        }
+        seg_rec[b + 1] = r;
+      }
+      if (vlen == 0) { /* values = append(values, 0): never a zero-length arena */
+        values = realloc(values, 1);
+        values[0] = 0;
+        vlen = 1;
+      }
+      mde_records rec;
+      memset(&rec, 0, sizeof rec);
+      rec.values = values;
+      rec.values_bytes = vlen;
+      rec.value_off = value_off;
+      rec.n_records = r;
+      rec.n_partitions = 1;
+      rec.n_buckets = B;
+      rec.seg_rec = seg_rec;
+      uint64_t* digest = xmalloc((uint64_t)B * 8);
+      int32_t* size = xmalloc((uint64_t)B * 4);
+      int32_t items = 0;
+      uint8_t root[32];
+      mde_tree_out out = {digest, size, &items, root, NULL};
+      if ((rc = mde_batch_build(batcher, &rec, &out, err, sizeof err))) {
+        fprintf(stderr, "mde_batch_build: %d %s\n", rc, err);
+        return 1;
+      }
+      printf("build");
+      for (uint32_t b = 0; b < B; b++) printf(" %" PRIu64, digest[b]);
+      printf(" ;");
+      for (uint32_t b = 0; b < B; b++) printf(" %d", size[b]);
+      printf(" ; %d ; ", items);
+      print_hex(root, 32);
+      printf("\n");
+      free(bucket), free(values), free(value_off), free(seg_rec), free(digest), free(size);
+    } else if (!strcmp(op, "diff")) {
+      const uint32_t Ba = (uint32_t)num(f), Bb = (uint32_t)num(f);
+      uint64_t* da = xmalloc((uint64_t)Ba * 8);
+      uint64_t* db = xmalloc((uint64_t)Bb * 8);
+      for (uint32_t i = 0; i < Ba; i++) da[i] = num(f);
+      for (uint32_t i = 0; i < Bb; i++) db[i] = num(f);
+      const uint64_t capids = mde_diff_capacity(Ba, Bb);
+      int32_t* ids = xmalloc(capids * 4);
+      int32_t count = 0;
+      if ((rc = mde_diff_digests(ctx, 1, Ba, da, Bb, db, ids, capids, &count))) {
+        fprintf(stderr, "mde_diff_digests: %d %s\n", rc, mde_last_error(ctx));
+        return 1;
+      }
+      printf("diff %d", count);
+      for (int32_t i = 0; i < count; i++) printf(" %d", ids[i]);
+      printf("\n");
+      free(da), free(db), free(ids);
+    } else if (!strcmp(op, "verify")) {
+      const uint32_t B = (uint32_t)num(f);
+      const int32_t part = (int32_t)num(f);
+      const int64_t epoch = (int64_t)num(f);
+      const uint32_t replicas = (uint32_t)num(f), R = (uint32_t)num(f);
+      uint64_t* digest = xmalloc((uint64_t)B * 8);
+      int32_t* size = xmalloc((uint64_t)B * 4);
+      for (uint32_t i = 0; i < B; i++) digest[i] = num(f);
+      for (uint32_t i = 0; i < B; i++) size[i] = (int32_t)num(f);
+      uint8_t* blob = NULL;
+      uint64_t blen = 0, bcap = 0;
+      uint64_t* off = xmalloc(((uint64_t)R + 1) * 8);
+      for (uint32_t i = 0; i < R; i++) { /* proto.Marshal of each peer object, concatenated */
+        hex(f, &blob, &blen, &bcap);
+        off[i + 1] = blen;
+      }
+      blob = realloc(blob, blen + 1); /* blob = append(blob, 0) */
+      const uint64_t stride = mde_epoch_tree_object_max_bytes(B);
+      uint8_t* obj = xmalloc(stride);
+      int32_t* ids = xmalloc((uint64_t)B * 4);
+      int32_t* status = xmalloc(((uint64_t)R + 1) * 4);
+      uint8_t valid = 0;
+      int32_t vc = 0, dc = 0;
+      uint32_t olen = 0;
+      if ((rc = mde_batch_verify(batcher, B, part, epoch, digest, size, R, blob, off, replicas, &valid, &vc, ids, &dc,
+                                 status, obj, stride, &olen, err, sizeof err))) {
+        fprintf(stderr, "mde_batch_verify: %d %s\n", rc, err);
+        return 1;
+      }
+      printf("verify %d %d ;", valid, vc);
+      for (int32_t i = 0; i < dc; i++) printf(" %d", ids[i]);
+      printf(" ;");
+      for (uint32_t i = 0; i < R; i++) printf(" %d", status[i]);
+      printf(" ; ");
+      print_hex(obj, olen);
+      printf("\n");
+      free(digest), free(size), free(blob), free(off), free(obj), free(ids), free(status);
+    } else {
+      fprintf(stderr, "unknown op %s\n", op);
+      return 2;
+    }
+  }
+  fclose(f);
+  mde_batcher_destroy(batcher);
+  mde_destroy(ctx);
+  return 0;
+}

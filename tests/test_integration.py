@@ -74,3 +74,131 @@ def test_shim_reimplements_the_reference_signatures():
             "(*merkletree.MerkleTree, error)") in src
     assert ("func DifferentMerkleTreeBuckets(tree1 *merkletree.MerkleTree, tree2 *merkletree.MerkleTree) "
             "([]int32, error)") in src
+
+
+# ---------------------------------------------------------------------------------------------
+# The shim's call sequences, replayed from C (tests/cpp/shim_replay.c) and checked against the
+# oracle's restatement of the reference functions the shim replaces.
+import pytest  # noqa: E402
+
+REPLAY = ROOT / "tests" / "cpp" / "build" / "shim_replay"
+
+
+def _replay_scenarios():
+    """(input tokens, expected output line) per op, from the oracle (oracle/oracle.py)."""
+    import numpy as np
+    from oracle import oracle as O
+    from oracle import wire_pb
+    rng = np.random.default_rng(2024)
+    lines, expect = [], []
+
+    # RawPartitionMerkleTree: one partition, the arena filled record by record
+    def build(B, n, lens):
+        bucket = np.sort(rng.integers(0, B, n)) if n else np.zeros(0, np.int64)
+        vals = [rng.integers(0, 256, int(ln), dtype=np.uint8).tobytes() for ln in lens]
+        toks = ["build", str(B), str(n)] + [str(int(b)) for b in bucket] + [v.hex() or "-" for v in vals]
+        lines.append(" ".join(toks))
+        voff = np.zeros(n + 1, np.uint64)
+        voff[1:] = np.cumsum([len(v) for v in vals])
+        seg = np.searchsorted(bucket, np.arange(B + 1)).astype(np.uint64)
+        arena = np.frombuffer(b"".join(vals) or b"\0", np.uint8)
+        d, z = O.bucket_digests(arena, voff, seg)
+        t = O.tree_from_digests(d, z)
+        items = O.merkle_tree_to_partition_epoch_object(t, 0, 0, 1).items
+        expect.append(f"build {' '.join(map(str, d))} ; {' '.join(map(str, z))} ; {items} ; "
+                      f"{t.merkle_root().hex()}")
+        return list(map(int, d)), list(map(int, z))
+
+    build(31, 300, rng.integers(0, 41, 300))                  # variable lengths, empty values, odd B
+    build(64, 1000, [8] * 1000)                                # 8-byte timestamps
+    d1000, z1000 = build(1000, 5000, [8] * 5000)               # the reference's default B
+    build(30, 0, [])                                           # no records: one padding byte
+    d31, z31 = build(31, 200, rng.integers(1, 17, 200))
+
+    # DifferentMerkleTreeBuckets: local B = 31 (merkletree duplicates the last leaf; the shim drops
+    # it) against a tree rebuilt from an odd-B object (B + 1 distinct leaves, kept by the shim)
+    def diff(local, peer_src):
+        t1 = O.tree_from_digests(local)
+        t2 = O.epoch_tree_object_to_merkle_tree(
+            O.merkle_tree_to_partition_epoch_object(O.tree_from_digests(peer_src), 0, 0, 1))
+        peer_leaves = [O.decode_bytes_to_int64(l.c.calculate_hash()) for l in t2.leafs]
+        lines.append(" ".join(["diff", str(len(local)), str(len(peer_leaves))] + list(map(str, local)) +
+                     list(map(str, peer_leaves))))
+        try:
+            ids = O.different_merkle_tree_buckets(t1, t2)
+            expect.append(" ".join(["diff", str(len(ids))] + list(map(str, ids))))
+        except O.MerkleError:
+            expect.append("diff -4")
+
+    diff(d31, d31)                                              # equal: the duplicate leaves agree
+    p = list(d31)
+    p[5] = (p[5] + 1) % 999999
+    diff(d31, p)                                                # one inner bucket differs
+    p = list(d31)
+    p[30] = (p[30] + 7) % 999999
+    diff(d31, p)                                                # the duplicated bucket differs
+    p = list(d1000)
+    p[999] = (p[999] + 1) % 999999
+    diff(d1000, p)                                              # even B: same leaf counts
+
+    # VerifyEpoch's decision: an agreeing odd-B object, an absent peer, a garbage peer, a differing
+    # object marked Valid (validDiff), and B = 1000 with another bucket count
+    def verify(d, z, peers, rc, part=7, epoch=4):
+        t = O.tree_from_digests(d, z)
+        lines.append(" ".join(["verify", str(len(d)), str(part), str(epoch), str(rc), str(len(peers))] +
+                              list(map(str, d)) + list(map(str, z)) + [(x.hex() if x else "-") for x in peers]))
+        w = O.verify_epoch(t, part, epoch, peers, rc)
+        st = [O_STATUS.get(s, s) for s in w["status"]]
+        expect.append(f"verify {int(w['valid'])} {w['valid_count']} ; {' '.join(map(str, w['diff']))} ; "
+                      f"{' '.join(map(str, st))} ; {w['object'].hex()}")
+
+    O_STATUS = {O.VERIFY_DECODE: -6, O.VERIFY_TREE: -4}
+
+    def obj(d, z, valid=False):
+        t = O.tree_from_digests(d, z)
+        o = O.merkle_tree_to_partition_epoch_object(t, 7, 4, 5)
+        return wire_pb.marshal(7, 4, 5, [O.decode_bytes_to_int64(h) for h in o.buckets], o.buckets_size,
+                               valid=valid, items=o.items)
+
+    p = list(d31)
+    p[3] = (p[3] + 1) % 999999
+    verify(d31, z31, [obj(d31, z31), None, b"\xff\xff\xff", obj(p, z31, valid=True)], 2)
+    verify(d31, z31, [obj(d31, z31), None, b"\x0a"], 1)
+    q = list(d1000)
+    q[10] = (q[10] + 1) % 999999
+    verify(d1000, z1000, [obj(q, z1000), obj(d1000[:998], z1000[:998]), None], 3)
+    return lines, expect
+
+
+@pytest.mark.gpu
+def test_shim_call_sequences_replayed_from_c_match_oracle(tmp_path):
+    """The Go shim's exact ABI call sequences (integration/go/merkle_gpu.go, which cannot be
+    compiled here), replayed in C: RawPartitionMerkleTree's one-partition arena with value_off
+    built record by record -> mde_batch_build; DifferentMerkleTreeBuckets with B local leaves
+    against B + 1 peer leaves (odd-B object quirk, SURVEY App. A.2) -> mde_diff_digests;
+    verifyEpochDecision with agreeing, absent, garbage, Valid-differing and other-B peers ->
+    mde_batch_verify. Every output equals the oracle's restatement of the reference
+    (main/merkle_tree.go:86-216, main/manager.go:1072-1104)."""
+    import subprocess
+    lines, expect = _replay_scenarios()
+    f = tmp_path / "scenarios.txt"
+    f.write_text("\n".join(lines) + "\n")
+    r = subprocess.run([str(REPLAY), str(f)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = r.stdout.strip().splitlines()
+    assert len(got) == len(expect)
+    for i, (g, e) in enumerate(zip(got, expect)):
+        assert " ".join(g.split()) == " ".join(e.split()), (i, lines[i][:80])
+
+
+def test_shim_replay_scenarios_exercise_every_branch():
+    """CPU: the replay's expectations cover the branches the verdict asked for -- an error diff
+    (the duplicated odd-B bucket), a non-empty diff, the padding byte of an empty arena, and absent
+    (-6), garbage (-6) and other-shape peers."""
+    lines, expect = _replay_scenarios()
+    assert any(e == "diff -4" for e in expect)
+    assert any(e.startswith("diff 1 5") for e in expect)
+    assert any(e.startswith("build") and e.split(" ; ")[2] == "0" for e in expect)
+    verifies = [e for e in expect if e.startswith("verify")]
+    assert all("-6" in v.split(" ; ")[2] for v in verifies)
+    assert verifies[0].startswith("verify 1 ")  # validDiff: a differing peer object marked Valid

@@ -362,3 +362,66 @@ def test_decode_deep_unknown_groups_follow_go(engine, cap):
     bad = [(i, len(objs[i]), g if not isinstance(g, dict) else "ok", e if not isinstance(e, dict) else "ok")
            for i, (g, e) in enumerate(zip(got, exp)) if g != e]
     assert not bad, bad
+
+
+@pytest.mark.gpu
+def test_decode_oscillating_deep_groups_stays_linear(engine):
+    """a hostile peer object that nests unknown groups past the 64-level ring and then
+    oscillates -- down below the ring's lowest level and back up, ~2,000 times -- made the rescan
+    decoder quadratic (each dip rescanned the outer group from its first byte: ~10^8 serial varint
+    steps for this 270 KB object). With the spill area the decode is linear: the host-buffer
+    decode, the async decode (the context's default spill area) and a VerifyEpoch call carrying the
+    object as a peer each finish within a wall-clock bound, and equal the protobuf-go restatement.
+    Also the same walk with a wrong end number near the end, and a truncation."""
+    import time
+    import torch
+    import mydatastore_amd as mde
+    rng = np.random.default_rng(77)
+    targets = [70]
+    for _ in range(2000):
+        targets += [2, 70]
+    targets += [0]
+    walk, _ = _group_walk(rng, targets, sib=0.0, big_numbers=False)
+    tail = b"\x08\x05\x10\x06\x22\x08" + (1234).to_bytes(8, "little")
+    good = walk + tail
+    bad_end = bytearray(good)
+    i = len(walk) - 3
+    while bad_end[i] & 7 != 4:
+        i -= 1
+    bad_end[i] ^= 0x08
+    objs = [good, bytes(bad_end), good[: len(walk) // 2]]
+    exp = [_expect_decode(o, 64) for o in objs]
+    assert isinstance(exp[0], dict) and exp[1] == mde.MDE_E_DECODE and exp[2] == mde.MDE_E_DECODE
+    t0 = time.perf_counter()
+    got = engine.decode_objects(objs, cap=64)
+    t_sync = time.perf_counter() - t0
+    assert got == exp
+    # async entry point with device buffers (the context's default spill area covers 8 MiB)
+    dev = torch.device("cuda:0")
+    engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    off = np.zeros(len(objs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(o) for o in objs])
+    blob = torch.from_numpy(np.frombuffer(b"".join(objs), np.uint8).copy()).to(dev)
+    doff = torch.from_numpy(off.view(np.int64)).to(dev)
+    n = len(objs)
+    outs = [torch.zeros(n, dtype=torch.int32, device=dev), torch.zeros(n, dtype=torch.int64, device=dev),
+            torch.zeros(n, dtype=torch.int64, device=dev), torch.zeros(n * 64, dtype=torch.int64, device=dev),
+            torch.zeros(n * 64, dtype=torch.int32, device=dev), torch.zeros(n, dtype=torch.uint8, device=dev),
+            torch.zeros(n, dtype=torch.int32, device=dev), torch.zeros(n, dtype=torch.int32, device=dev)]
+    t0 = time.perf_counter()
+    engine._call("mde_decode_epoch_tree_objects_async", n, mde._ptr(blob), mde._ptr(doff), 64,
+                 *(mde._ptr(o) for o in outs))
+    engine.synchronize()
+    t_async = time.perf_counter() - t0
+    nb = outs[7].cpu().tolist()
+    assert nb == [1, mde.MDE_E_DECODE, mde.MDE_E_DECODE]
+    assert outs[3].cpu().numpy()[0] == 1234 and outs[0].cpu().numpy()[0] == 5
+    # VerifyEpoch with the hostile object as a peer beside an agreeing one (B = 1)
+    d = np.array([1234], np.uint64)
+    z = np.zeros(1, np.int32)
+    root, nodes = engine.tree_from_digests(d, 1)
+    t0 = time.perf_counter()
+    res = engine.verify_epochs(1, d, z, nodes, [[good, bytes(bad_end)]], replica_count=1, epoch=6, partition=[5])
+    t_verify = time.perf_counter() - t0
+    assert res["valid_count"] == [1] and res["peer_status"][0] == [0, mde.MDE_E_DECODE]
+    assert max(t_sync, t_async, t_verify) < 10.0, (t_sync, t_async, t_verify)

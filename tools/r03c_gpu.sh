@@ -1,0 +1,8 @@
+#!/bin/bash
+# r03c: batcher parity (C program + Python threads) and the production-shape timing
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+  > gpurun_out/r03c_pytest.log 2>&1 &&
+timeout -k 10 300 tests/cpp/build/batch_bench 0.4 > gpurun_out/r03c_batch_bench.jsonl 2> gpurun_out/r03c_batch_bench.err
