@@ -29,16 +29,22 @@ import (
 
 var (
 	mdeOnce sync.Once
-	mdeCtx  *C.mde_ctx
-	mdeErr  error
-	// VerifyEpoch runs on a pool of worker goroutines (main/manager.go:166-170,491) that share
-	// mdeCtx. mdeMu pairs each call with its own error message; it costs no concurrency, since
-	// the context lock serialises calls on one context anyway.
-	mdeMu sync.Mutex
+	// mdeBatcher serves RawPartitionMerkleTree and verifyEpochDecision: VerifyEpoch runs one
+	// partition per call on a pool of worker goroutines (main/manager.go:166-170,491), up to
+	// PartitionConcurrency at once (config/default-config.yaml:9); the batcher coalesces the calls
+	// in flight into one device build / verify (group commit, mde_batch_build / mde_batch_verify).
+	// Each call gets its own error message back in its own buffer, so no lock is needed.
+	mdeBatcher *C.mde_batcher
+	// mdeCtx serves the unbatched calls (DifferentMerkleTreeBuckets). mdeMu pairs each call with
+	// its own error message; it costs no concurrency, since the context lock serialises calls on
+	// one context anyway.
+	mdeCtx *C.mde_ctx
+	mdeErr error
+	mdeMu  sync.Mutex
 )
 
-// mdeCall runs one engine call and, when it fails, returns ITS message (copied under the context
-// lock by mde_last_error_copy while mdeMu is still held).
+// mdeCall runs one engine call on mdeCtx and, when it fails, returns ITS message (copied under
+// the context lock by mde_last_error_copy while mdeMu is still held).
 func mdeCall(ctx *C.mde_ctx, name string, call func() C.int) error {
 	mdeMu.Lock()
 	defer mdeMu.Unlock()
@@ -50,25 +56,32 @@ func mdeCall(ctx *C.mde_ctx, name string, call func() C.int) error {
 	return nil
 }
 
-func mdeEngine() (*C.mde_ctx, error) {
+func mdeEngine() (*C.mde_batcher, *C.mde_ctx, error) {
 	mdeOnce.Do(func() {
+		var b *C.mde_batcher
+		// at most 256 partitions per batch, no wait window: a batch is whatever queued while the
+		// previous batches ran
+		if rc := C.mde_batcher_create(0, 256, 0, &b); rc != C.MDE_OK {
+			mdeErr = errors.Errorf("mde_batcher_create: %s", C.GoString(C.mde_strerror(rc)))
+			return
+		}
 		var ctx *C.mde_ctx
 		if rc := C.mde_create(0, &ctx); rc != C.MDE_OK {
 			mdeErr = errors.Errorf("mde_create: %s", C.GoString(C.mde_strerror(rc)))
 			return
 		}
-		mdeCtx = ctx
+		mdeBatcher, mdeCtx = b, ctx
 	})
-	return mdeCtx, mdeErr
+	return mdeBatcher, mdeCtx, mdeErr
 }
 
 func cU64(v []uint64) unsafe.Pointer { return C.CBytes(unsafe.Slice((*byte)(unsafe.Pointer(&v[0])), len(v)*8)) }
 
 // RawPartitionMerkleTree -- drop-in for main/merkle_tree.go:86-116. The per-bucket range scans are
 // unchanged; the values go into one arena that the MI355X engine reduces (bucket digests + SHA-256
-// tree on device).
+// tree on device), batched with the other partitions' calls in flight.
 func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, upperEpoch int64) (*merkletree.MerkleTree, error) {
-	ctx, err := mdeEngine()
+	batcher, _, err := mdeEngine()
 	if err != nil {
 		return nil, err
 	}
@@ -116,8 +129,9 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 	}
 	out := C.mde_tree_out{digest: (*C.uint64_t)(cDigest), size: (*C.int32_t)(cSize),
 		items: (*C.int32_t)(cItems), root: (*C.uint8_t)(cRoot)}
-	if err := mdeCall(ctx, "mde_build", func() C.int { return C.mde_build(ctx, &rec, &out) }); err != nil {
-		return nil, err
+	var errBuf [512]C.char
+	if rc := C.mde_batch_build(batcher, &rec, &out, &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
+		return nil, errors.Errorf("mde_batch_build: %s", C.GoString(&errBuf[0]))
 	}
 	digest := unsafe.Slice((*uint64)(cDigest), B)
 	size := unsafe.Slice((*int32)(cSize), B)
@@ -139,7 +153,7 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 
 // DifferentMerkleTreeBuckets -- drop-in for main/merkle_tree.go:159-161 (DFS order, duplicates).
 func DifferentMerkleTreeBuckets(tree1 *merkletree.MerkleTree, tree2 *merkletree.MerkleTree) ([]int32, error) {
-	ctx, err := mdeEngine()
+	_, ctx, err := mdeEngine()
 	if err != nil {
 		return nil, err
 	}
@@ -190,15 +204,16 @@ func DifferentMerkleTreeBuckets(tree1 *merkletree.MerkleTree, tree2 *merkletree.
 }
 
 // verifyEpochDecision -- the decision step of Manager.VerifyEpoch (main/manager.go:1072-1104) in
-// one mde_verify_epochs call: every peer object is decoded, rebuilt and diffed against myTree on
-// the device; failed peers are skipped (the reference logs and continues); validCount, validDiff
-// and diffSet fold as the reference does. Returns valid (validCount >= replicaCount || validDiff),
-// validCount, diffSet (ascending) and the EpochTreeObject to persist (Valid set) as wire bytes.
-// VerifyEpoch keeps its own flow: on valid it stores data, otherwise it calls
-// PoliteStreamRequest(partitionId, epoch, epoch+1, diffSet).
+// one mde_batch_verify call, batched with the other partitions' decisions in flight: every peer
+// object is decoded, rebuilt and diffed against myTree on the device (myTree's own nodes are built
+// there from its digests); failed peers are skipped (the reference logs and continues);
+// validCount, validDiff and diffSet fold as the reference does. Returns valid (validCount >=
+// replicaCount || validDiff), validCount, diffSet (ascending) and the EpochTreeObject to persist
+// (Valid set) as wire bytes. VerifyEpoch keeps its own flow: on valid it stores data, otherwise it
+// calls PoliteStreamRequest(partitionId, epoch, epoch+1, diffSet).
 func verifyEpochDecision(myTree *merkletree.MerkleTree, partitionId int, epoch int64,
 	epochTreeObjects []*rpc.RpcEpochTreeObject, replicaCount int) (bool, int, []int32, []byte, error) {
-	ctx, err := mdeEngine()
+	batcher, _, err := mdeEngine()
 	if err != nil {
 		return false, 0, nil, nil, err
 	}
@@ -222,17 +237,6 @@ func verifyEpochDecision(myTree *merkletree.MerkleTree, partitionId int, epoch i
 	defer C.free(cDigest)
 	cSize := C.CBytes(unsafe.Slice((*byte)(unsafe.Pointer(&size[0])), B*4))
 	defer C.free(cSize)
-	nodeBytes := C.size_t(C.mde_tree_internal_nodes(C.uint32_t(B)) * 32)
-	cNodes := C.malloc(nodeBytes)
-	cRoot := C.malloc(32)
-	defer C.free(cNodes)
-	defer C.free(cRoot)
-	if err := mdeCall(ctx, "mde_tree_from_digests", func() C.int {
-		return C.mde_tree_from_digests(ctx, 1, C.uint32_t(B), (*C.uint64_t)(cDigest), (*C.uint8_t)(cRoot),
-			(*C.uint8_t)(cNodes))
-	}); err != nil {
-		return false, 0, nil, nil, err
-	}
 	// peer objects back to wire bytes (gRPC already unmarshalled them); a nil object is absent
 	R := len(epochTreeObjects)
 	var blob []byte
@@ -261,16 +265,14 @@ func verifyEpochDecision(myTree *merkletree.MerkleTree, partitionId int, epoch i
 	defer C.free(cIds)
 	defer C.free(cStatus)
 	defer C.free(cOut)
-	part := C.int32_t(partitionId)
 	outs := unsafe.Slice((*int32)(cOut), 4)
-	if err := mdeCall(ctx, "mde_verify_epochs", func() C.int {
-		return C.mde_verify_epochs(ctx, 1, C.uint32_t(B), &part, C.int64_t(epoch), (*C.uint64_t)(cDigest),
-			(*C.int32_t)(cSize), (*C.uint8_t)(cNodes), C.uint32_t(R), (*C.uint8_t)(cBlob), (*C.uint64_t)(cOff),
-			C.uint32_t(replicaCount), (*C.uint8_t)(unsafe.Pointer(&outs[0])), (*C.int32_t)(unsafe.Pointer(&outs[1])),
-			(*C.int32_t)(cIds), (*C.int32_t)(unsafe.Pointer(&outs[2])), (*C.int32_t)(cStatus), (*C.uint8_t)(cObj),
-			stride, (*C.uint32_t)(unsafe.Pointer(&outs[3])))
-	}); err != nil {
-		return false, 0, nil, nil, err
+	var errBuf [512]C.char
+	if rc := C.mde_batch_verify(batcher, C.uint32_t(B), C.int32_t(partitionId), C.int64_t(epoch),
+		(*C.uint64_t)(cDigest), (*C.int32_t)(cSize), C.uint32_t(R), (*C.uint8_t)(cBlob), (*C.uint64_t)(cOff),
+		C.uint32_t(replicaCount), (*C.uint8_t)(unsafe.Pointer(&outs[0])), (*C.int32_t)(unsafe.Pointer(&outs[1])),
+		(*C.int32_t)(cIds), (*C.int32_t)(unsafe.Pointer(&outs[2])), (*C.int32_t)(cStatus), (*C.uint8_t)(cObj),
+		stride, (*C.uint32_t)(unsafe.Pointer(&outs[3])), &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
+		return false, 0, nil, nil, errors.Errorf("mde_batch_verify: %s", C.GoString(&errBuf[0]))
 	}
 	valid := *(*uint8)(unsafe.Pointer(&outs[0])) != 0
 	diffSet := make([]int32, outs[2])
