@@ -406,10 +406,159 @@ __device__ __forceinline__ uint32_t digest_range_win(const DigestLaunch& a, uint
   return s;
 }
 
+// digest_range for fixed 8-byte records (the production epoch-index value is the LE64 write
+// timestamp, main/manager.go:816) with short buckets (the reference's default B = 1,000 puts a
+// bucket start every ~100 records). Counters showed the register-window kernel's prefix-scan path
+// issue-bound there: ~300 VALU per 4 KiB step (four wave scans of the vector sums, a 64-bit window
+// walk, per-row shuffles to gather each start's prefix; profiles/r02ae_digest_sq_counters.json).
+// Here the scan runs in RECORD space, once per step:
+//   * each lane byte-sums its 8 records (two per 16-byte vector of each of the 4 coalesced 1 KiB
+//     rows) and writes the 8 sums to LDS at their record index; the wave reads them back
+//     transposed -- lane l gets records 8l .. 8l+7 of the step -- so ONE wave scan of the lane
+//     totals plus a 7-add local scan give every record's prefix (LDS XOR-swizzled so the row
+//     writes and the transposed ds_read_b128 are conflict-free);
+//   * each lane writes its 8 exclusive local prefixes back (and its lane prefix), so the window
+//     lane of every bucket starting in the step reads F(start) = bytes of the step before it with
+//     two ds_read_b32 -- bucket i's bytes in the step are F(y_{i+1}) - F(y_i), as in
+//     digest_range_win's scan path;
+//   * the buckets' step sums accumulate in a wave-uniform u64 (no per-bucket wave reduction); a
+//     step inside one bucket just byte-sums into the lane accumulators;
+//   * loads are buffer loads bounded by the wave range (no per-load address clamping; the last
+//     vector of the range may extend past its end, whose slots the prefix clamp at q excludes).
+// Needs value_stride == 8 and an 8-byte-aligned arena start (segpos multiples of 8), 4 KiB steps.
+__device__ __forceinline__ uint32_t rec8_swz(uint32_t w) { return w ^ (((w >> 6) & 1u) << 2); }
+constexpr uint32_t kRec8Sums = 528;                 // swizzled record words (512 + word 512 = 0)
+constexpr uint32_t kRec8WaveWords = kRec8Sums + 80;  // + 65 lane prefixes, padded
+constexpr uint32_t kRec8LdsBytes = kRec8WaveWords * 4u * (kThreads / 64);
+
+template <bool NT>
+__device__ __forceinline__ void load_rec8(u32x4 (&v)[4], __amdgpu_buffer_rsrc_t rs, uint32_t off, int lane) {
+#pragma unroll
+  for (int u = 0; u < 4; u++)
+    v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(u * 64 + lane) * 16u,
+                                                                          off, NT ? 2 : 0));
+}
+
+template <bool NT>
+__device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uint64_t beg, uint64_t end, uint32_t s_lo,
+                                                      int lane, uint32_t* lds) {
+  constexpr uint64_t kStep = 4096;
+  const SegDesc& d = a.seg;
+  uint32_t* R = lds;               // record sums, then exclusive local prefixes (swizzled)
+  uint32_t* E = lds + kRec8Sums;   // lane exclusive prefixes; E[64] = the step's total
+  const uint64_t span = ((end - beg) + 15) & ~15ull;  // <= kMaxWaveBytes
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(d.base + beg), (short)0, (int)span, 0x00020000);
+  u32x4 va[4], vb[4];
+  load_rec8<NT>(va, rs, 0, lane);  // the first step's loads before the bucket search
+  if (lane == 0) R[512] = 0;       // F(512) = E[64] + 0
+  uint32_t s = seg_search(d, s_lo, beg, lane);
+  SegWindow win;
+  win.load(d, s, lane);
+  uint64_t sb = readlane64(win.start, 0), se = readlane64(win.start, 1);
+  uint64_t wsum = 0;     // this lane's window bucket (win.base + lane): its finished sum
+  uint64_t bfrom = beg;  // where this wave entered bucket s
+  uint32_t acc = 0;      // lane accumulator of whole steps inside bucket s
+  uint64_t accs = 0;     // wave-uniform: bucket s's bytes from steps with bucket starts
+
+  auto retire = [&](uint64_t upto) {  // bucket s is left: its sum into its window lane
+    uint64_t v;
+    if (upto - bfrom <= (16ull << 20)) {
+      v = wave_sum_u32(acc);  // <= 255 x 16 MiB < 2^32
+    } else {
+      v = acc;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    }
+    if ((uint32_t)lane == s - win.base) wsum = v + accs;
+    acc = 0;
+    accs = 0;
+  };
+  auto window_out = [&]() {  // one coalesced atomic for the window's finished buckets
+    if (wsum) atomicAdd(a.sums + win.base + (uint32_t)lane, (unsigned long long)wsum);
+    wsum = 0;
+  };
+  auto process = [&](const u32x4 (&v)[4], uint64_t p) {
+    const uint64_t q = min(p + kStep, end);
+    if (q == p + kStep && sb <= p && q <= se) {  // the whole step inside bucket s
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
+      }
+      return;
+    }
+    // record sums -> LDS at their record index (row u, lane l: records 128u + 2l, 128u + 2l + 1)
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t r0 = __builtin_amdgcn_sad_u8(v[u].y, 0u, __builtin_amdgcn_sad_u8(v[u].x, 0u, 0u));
+      const uint32_t r1 = __builtin_amdgcn_sad_u8(v[u].w, 0u, __builtin_amdgcn_sad_u8(v[u].z, 0u, 0u));
+      *reinterpret_cast<uint2*>(R + rec8_swz(128u * u + 2u * (uint32_t)lane)) = make_uint2(r0, r1);
+    }
+    // transposed: this lane's records 8l .. 8l+7, their local prefix, one wave scan of the totals
+    const uint4 x = *reinterpret_cast<const uint4*>(R + rec8_swz(8u * (uint32_t)lane));
+    const uint4 y = *reinterpret_cast<const uint4*>(R + rec8_swz(8u * (uint32_t)lane + 4u));
+    const uint32_t c1 = x.x, c2 = c1 + x.y, c3 = c2 + x.z, c4 = c3 + x.w;
+    const uint32_t c5 = c4 + y.x, c6 = c5 + y.y, c7 = c6 + y.z, tot = c7 + y.w;
+    const uint32_t incl = wave_incl_scan_u32(tot);
+    *reinterpret_cast<uint4*>(R + rec8_swz(8u * (uint32_t)lane)) = make_uint4(0u, c1, c2, c3);
+    *reinterpret_cast<uint4*>(R + rec8_swz(8u * (uint32_t)lane + 4u)) = make_uint4(c4, c5, c6, c7);
+    E[lane] = incl - tot;
+    if (lane == 63) E[64] = incl;
+    // F(y) for this lane's bucket start y, clamped to [p, q]: record slot k = (y - p) / 8
+    const uint32_t kq = (uint32_t)((q - p) >> 3);
+    for (;;) {
+      const uint64_t st = win.start;
+      const uint32_t k = st <= p ? 0u : (st >= q ? kq : (uint32_t)((st - p) >> 3));
+      const uint32_t F = R[rec8_swz(k)] + E[k >> 3];
+      const uint32_t c = (uint32_t)__shfl_down((int)F, 1) - F;  // bucket base + lane, lanes 0..62
+      const uint32_t k0 = s - win.base;
+      const uint32_t cnt = (uint32_t)__popcll(__ballot(st < q));
+      accs += (uint32_t)__builtin_amdgcn_readlane((int)c, (int)k0);
+      if (cnt == 64u) {  // the step runs past the window: buckets k0..62 all end inside it
+        retire(readlane64(st, k0 + 1u));
+        if ((uint32_t)lane > k0 && lane < 63) wsum = c;
+        window_out();
+        win.load(d, win.base + 63u, lane);
+        s = win.base;
+        sb = readlane64(win.start, 0);
+        se = readlane64(win.start, 1);
+        bfrom = sb;
+        continue;
+      }
+      const uint32_t m = cnt - 1u;  // the last bucket starting before q: it runs on past q
+      if (m > k0) {
+        retire(readlane64(st, k0 + 1u));
+        if ((uint32_t)lane > k0 && (uint32_t)lane < m) wsum = c;
+        s = win.base + m;
+        sb = readlane64(st, m);
+        se = readlane64(st, m + 1u);
+        bfrom = sb;
+        accs = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)m);
+      }
+      return;
+    }
+  };
+
+  for (uint64_t p = beg;; p += 2 * kStep) {
+    load_rec8<NT>(vb, rs, (uint32_t)(p + kStep - beg), lane);  // always issued (bounded by the range)
+    process(va, p);
+    if (p + kStep >= end) break;
+    load_rec8<NT>(va, rs, (uint32_t)(p + 2 * kStep - beg), lane);
+    process(vb, p + kStep);
+    if (p + 2 * kStep >= end) break;
+  }
+  retire(min(se, end));
+  window_out();
+  return s;
+}
+
 // One contiguous range of wave_bytes per wave. `block` = this workgroup's index among the digest
 // workgroups of the launch.
-template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false>
-__device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t block) {
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, bool REC8 = false>
+__device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t block, uint32_t* lds = nullptr) {
   // Streaming waves issue little VALU; when tree waves (back-to-back SHA-256 VALU) share the CU,
   // a raised priority keeps the loads flowing and the SHA waves take the slack.
   if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
@@ -421,7 +570,9 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
   const uint64_t last = segpos(d, d.S);
   const uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
   if (beg >= last) return;
-  if (WIN)
+  if (REC8)
+    digest_range_rec8<NT>(a, beg, min(beg + a.wave_bytes, last), 0u, lane, lds + (threadIdx.x >> 6) * kRec8WaveWords);
+  else if (WIN)
     digest_range_win<U, NT, PIPE, A8>(a, beg, min(beg + a.wave_bytes, last), 0u, lane);
   else
     digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), 0u, lane);
@@ -430,8 +581,8 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
 // Interleaved pieces (DigestLaunch::pieces): the wave streams `pieces` ranges of wave_bytes,
 // piece_stride apart, so the whole grid sweeps the arena front to back together. Each piece is a
 // digest_range (its own bucket search, from the previous piece's last bucket on, and flush).
-template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false>
-__device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32_t block) {
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, bool REC8 = false>
+__device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32_t block, uint32_t* lds = nullptr) {
   if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const int lane = threadIdx.x & 63;
   const uint32_t wave = block * (kThreads / 64) + (threadIdx.x >> 6);
@@ -442,8 +593,10 @@ __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32
   uint32_t s = 0;
   uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
   for (uint32_t j = 0; j < a.pieces && beg < last; j++, beg += a.piece_stride)
-    s = WIN ? digest_range_win<U, NT, PIPE, A8>(a, beg, min(beg + a.wave_bytes, last), s, lane)
-            : digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), s, lane);
+    s = REC8  ? digest_range_rec8<NT>(a, beg, min(beg + a.wave_bytes, last), s, lane,
+                                      lds + (threadIdx.x >> 6) * kRec8WaveWords)
+        : WIN ? digest_range_win<U, NT, PIPE, A8>(a, beg, min(beg + a.wave_bytes, last), s, lane)
+              : digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), s, lane);
 }
 
 
@@ -640,20 +793,22 @@ __device__ __forceinline__ void digest_body_steal(const DigestLaunch& a, uint32_
 }
 
 // MODE: 0 = one static range per wave, 1 = tail stealing, 2 = interleaved pieces; 3 and 4 = 0 and
-// 2 with the bucket bounds in a register window (SegWindow).
+// 2 with the bucket bounds in a register window (SegWindow); 5 and 6 = 0 and 2 for fixed 8-byte
+// records with the prefix scan in record space (digest_range_rec8; LDS: kRec8LdsBytes).
 template <int U, bool NT, int PIPE, int PRIO, int MODE, bool A8>
-__device__ __forceinline__ void digest_dispatch(const DigestLaunch& a, uint32_t block) {
+__device__ __forceinline__ void digest_dispatch(const DigestLaunch& a, uint32_t block, uint32_t* lds) {
   if (MODE == 1)
     digest_body_steal<U, NT, PRIO>(a, block);
-  else if (MODE == 2 || MODE == 4)
-    digest_body_pieces<U, NT, PIPE, PRIO, MODE == 4, A8>(a, block);
+  else if (MODE == 2 || MODE == 4 || MODE == 6)
+    digest_body_pieces<U, NT, PIPE, PRIO, MODE == 4, A8, MODE == 6>(a, block, lds);
   else
-    digest_body<U, NT, PIPE, PRIO, MODE == 3, A8>(a, block);
+    digest_body<U, NT, PIPE, PRIO, MODE == 3, A8, MODE == 5>(a, block, lds);
 }
 
 template <int U, bool NT, int PIPE, int PRIO = 0, int MODE = 0>
 __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a) {
-  digest_dispatch<U, NT, PIPE, PRIO, MODE, true>(a, blockIdx.x);
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  digest_dispatch<U, NT, PIPE, PRIO, MODE, true>(a, blockIdx.x, lds);
 }
 
 
@@ -687,7 +842,7 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
   }
   const uint32_t db = blockIdx.x - tree_blocks;
 #endif
-  digest_dispatch<U, NT, PIPE, PRIO, MODE, false>(a, db);
+  digest_dispatch<U, NT, PIPE, PRIO, MODE, false>(a, db, lds);
 }
 
 // One-launch build of small arenas (the synchronous one-partition calls of VerifyEpoch, and the
@@ -756,7 +911,8 @@ const Variant kVariants[] = {
     MDE_VARIANT(4, true, true, 3, 0),   MDE_VARIANT(4, true, true, 2, 1),
     MDE_VARIANT(8, true, true, 2, 1),    MDE_VARIANT(4, true, 2, 2, 0),
     MDE_VARIANT(4, true, 2, 2, 2),      MDE_VARIANT(4, true, 2, 2, 3),
-    MDE_VARIANT(4, true, 2, 2, 4),
+    MDE_VARIANT(4, true, 2, 2, 4),      MDE_VARIANT(4, true, 2, 2, 5),
+    MDE_VARIANT(4, true, 2, 2, 6),
 };
 #undef MDE_VARIANT
 
@@ -789,11 +945,14 @@ hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t
 }
 
 bool bucket_digest_steals(int v) { return variant(v).mode == 1; }
-bool bucket_digest_pieces(int v) { return variant(v).mode == 2 || variant(v).mode == 4; }
+bool bucket_digest_pieces(int v) { return variant(v).mode == 2 || variant(v).mode == 4 || variant(v).mode == 6; }
+bool bucket_digest_rec8(int v) { return variant(v).mode == 5 || variant(v).mode == 6; }
+uint32_t bucket_digest_rec8_lds_bytes() { return kRec8LdsBytes; }
 int bucket_digest_pieces_sibling(int v) {  // the same kernel with interleaved pieces
   switch (v) {
     case 11: return 12;
     case 13: return 14;
+    case 15: return 16;
     default: return v;
   }
 }
@@ -814,7 +973,8 @@ void plan_steal(uint64_t wave_bytes, uint64_t* head_bytes, uint64_t* chunk_bytes
 
 int bucket_digest_blocks_per_cu(int v, int cap) {
   int blocks = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, variant(v).fn, kThreads, 0) != hipSuccess ||
+  const size_t lds = bucket_digest_rec8(v) ? kRec8LdsBytes : 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, variant(v).fn, kThreads, lds) != hipSuccess ||
       blocks <= 0)
     blocks = 4;
   if (cap > 0 && cap < blocks) blocks = cap;

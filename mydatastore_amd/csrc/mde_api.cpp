@@ -36,12 +36,14 @@ constexpr uint64_t kAutoPieceBytes = UINT64_MAX;  // digest_piece_bytes value: t
 constexpr uint64_t kAutoPieceMinShare = 4ull << 20;
 constexpr uint64_t kAutoPieces = 5;
 constexpr int kWindowDigestVariant = 13;                 // SegWindow + true double buffer (plan_digest)
+constexpr int kRec8DigestVariant = 15;  // fixed 8-byte records: record-space prefix scan (plan_digest)
 constexpr uint64_t kWindowMaxAvgBucketBytes = 64ull << 10;  // average bucket bytes below which it runs
 
 struct mde_ctx {
   int device = 0;
   int cus = 256;
   int digest_blocks_per_cu = 0;  // resident workgroups per CU for the digest kernel (queried)
+  int variant_blocks[32] = {0};  // the same per digest variant (plan_digest queries the one it runs)
   int digest_variant = kDefaultDigestVariant;
   bool digest_auto = true;  // no explicit variant: plan_digest picks the window / pieces forms
   int digest_cap = kDefaultDigestCap;
@@ -343,8 +345,12 @@ int plan_digest(mde_ctx* c, uint64_t bytes, mde::DigestLaunch* a) {
   // register-window kernel (variant 13). Same-box A/B (profiles/r02u_window.jsonl): C4 at
   // B = 1000 (10 KiB buckets) 2,685 -> 1,493 us, its N=8 shard 376 -> 192 us; at B = 64 (156 KiB
   // buckets) it costs 0.3-0.8 %, so longer buckets keep variant 11.
-  if (c->digest_auto && a->seg.S && bytes / a->seg.S < kWindowMaxAvgBucketBytes)
+  if (c->digest_auto && a->seg.S && bytes / a->seg.S < kWindowMaxAvgBucketBytes) {
     a->variant = kWindowDigestVariant;
+    // the production epoch-index value: 8-byte LE timestamps (main/manager.go:816), a bucket start
+    // every ~100 records at B = 1,000; the record-space scan (digest.hip digest_range_rec8)
+    if (a->seg.stride == 8 && (a->seg.shift & 7) == 0) a->variant = kRec8DigestVariant;
+  }
   uint64_t piece_bytes = 0;
   if (c->digest_piece_bytes == kAutoPieceBytes) {
     // automatic pieces: the default's (or an explicitly chosen pieces variant's) pieces form
@@ -363,10 +369,22 @@ int plan_digest(mde_ctx* c, uint64_t bytes, mde::DigestLaunch* a) {
     piece_bytes = c->digest_piece_bytes;
   }
   const bool steals = mde::bucket_digest_steals(a->variant);
-  mde::plan_bucket_digest(bytes, c->cus, c->digest_blocks_per_cu, c->digest_oversub, piece_bytes,
+  // grid from the resident workgroups of the variant that actually runs (the window and rec8
+  // kernels may fit fewer per CU than the default under a raised cap: then every wave of the
+  // equal-range grid is still co-resident, no tail)
+  int& vb = c->variant_blocks[a->variant & 31];
+  if (!vb) vb = mde::bucket_digest_blocks_per_cu(a->variant, c->digest_cap);
+  const int blocks_per_cu = std::min(vb, c->digest_blocks_per_cu > 0 ? c->digest_blocks_per_cu : vb);
+  mde::plan_bucket_digest(bytes, c->cus, blocks_per_cu, c->digest_oversub, piece_bytes,
                           &a->wave_bytes, &a->n_waves, &a->pieces);
   a->piece_stride = (uint64_t)a->n_waves * a->wave_bytes;
   a->lds_bytes = c->digest_oversub > 1 ? (uint32_t)((160u * 1024u) / (uint32_t)c->digest_blocks_per_cu) & ~255u : 0u;
+  if (mde::bucket_digest_rec8(a->variant)) {
+    if (a->seg.stride != 8 || (a->seg.shift & 7))  // needs 8-byte records: the window kernel instead
+      a->variant = mde::bucket_digest_pieces(a->variant) ? mde::bucket_digest_pieces_sibling(kWindowDigestVariant)
+                                                         : kWindowDigestVariant;
+    else a->lds_bytes = std::max(a->lds_bytes, mde::bucket_digest_rec8_lds_bytes());
+  }
   // Tail stealing needs fixed-length values and a split range; otherwise the static sibling.
   if (steals) {
     mde::plan_steal(a->wave_bytes, &a->head_bytes, &a->chunk_bytes, &a->tail_chunks);
@@ -813,6 +831,7 @@ int mde_set_tuning(mde_ctx* c, int digest_variant, int digest_blocks_per_cu, int
   c->digest_cap = digest_blocks_per_cu < 0 ? kDefaultDigestCap : digest_blocks_per_cu;
   c->digest_oversub = digest_oversub < 0 ? kDefaultDigestOversub : (digest_oversub ? digest_oversub : 1);
   c->digest_blocks_per_cu = 0;  // re-query
+  for (int& x : c->variant_blocks) x = 0;
   return MDE_OK;
 }
 

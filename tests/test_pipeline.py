@@ -245,11 +245,13 @@ PIECES_VARIANT = 12  # digest.hip kVariants: U = 4, nontemporal, prefetched, int
 WINDOW_VARIANTS = (13, 14)  # the same with the bucket bounds in a register window (14: + pieces)
 
 
-def _skewed_arena(dev, variable, seed=11, P=37, B=100, max_count=8_000, big=(3_000_000, 1_500_000, 2_000_000)):
+def _skewed_arena(dev, variable, seed=11, P=37, B=100, max_count=8_000, big=(3_000_000, 1_500_000, 2_000_000),
+                  stride=13, start=5):
     """Ragged layout-A arena of ~100-300 MB for the digest work split: empty buckets and an empty
-    partition, a few buckets of tens of MB, the arena start 5 bytes past an allocation. Fixed
-    13-byte records (never 16-byte aligned) or variable lengths 0..40 (value_off). Returns the
-    Records, the per-bucket record counts and the expected digests (torch byte sums mod 999999)."""
+    partition, a few buckets of tens of MB, the arena start `start` bytes past an allocation. Fixed
+    `stride`-byte records (13: never 16-byte aligned) or variable lengths 0..40 (value_off). Returns
+    the Records, the per-bucket record counts and the expected digests (torch byte sums mod
+    999999)."""
     import torch
     import mydatastore_amd as mde
     g = torch.Generator(device="cpu").manual_seed(seed)
@@ -268,9 +270,9 @@ def _skewed_arena(dev, variable, seed=11, P=37, B=100, max_count=8_000, big=(3_0
         nbytes = int(voff[-1])
         stride = 0
     else:
-        nbytes, stride = n * 13, 13
+        nbytes = n * stride
     buf = torch.randint(0, 256, (nbytes + 32,), dtype=torch.uint8, device=dev)
-    vals = buf[5:5 + nbytes]
+    vals = buf[start:start + nbytes]
     cb = torch.zeros(nbytes + 1, dtype=torch.int64, device=dev)
     cb[1:] = torch.cumsum(vals.to(torch.int64), 0)
     if variable:
@@ -278,11 +280,11 @@ def _skewed_arena(dev, variable, seed=11, P=37, B=100, max_count=8_000, big=(3_0
         bpos = dvoff[seg.to(dev)]
         keep.append(dvoff)
     else:
-        bpos = seg.to(dev) * 13
+        bpos = seg.to(dev) * stride
     want = ((cb[bpos[1:]] - cb[bpos[:-1]]) % 999999).cpu()
     dseg = seg.to(dev)
     keep += [buf, dseg]
-    rec = mde.Records(vals.data_ptr(), nbytes, stride, mde.LAYOUT_SORTED,
+    rec = mde.Records(vals.data_ptr(), nbytes, 0 if variable else stride, mde.LAYOUT_SORTED,
                       keep[0].data_ptr() if variable else 0, n, P, B, dseg.data_ptr())
     return rec, counts, want, keep, (P, B)
 
@@ -499,3 +501,46 @@ def test_default_variant_choice_b1000_full_size(engine, value_len, n_keys, n_buc
     finally:
         engine.set_tuning(-1, -1)
         engine.set_digest_piece_bytes(-1)
+
+
+REC8_VARIANTS = (15, 16)  # digest.hip: fixed 8-byte records, record-space prefix scan (+ pieces)
+
+
+@pytest.mark.parametrize("start", [0, 8])
+@pytest.mark.parametrize("P,B,max_count", [(37, 1000, 300), (64, 64, 3000)])
+def test_rec8_ragged_arena_matches_torch_sums(engine, start, P, B, max_count):
+    """The 8-byte-record digest (production timestamps, main/manager.go:816): 37 or 64 partitions, a
+    quarter of the buckets empty, an empty partition, three buckets of 12-24 MB (past the 16 MiB
+    exact-u32 reduction), the arena 16-byte aligned or 8 bytes past it (record slots on 8-byte
+    boundaries), both variants and piece sizes from 1 KiB (piece and range ends inside buckets and
+    in the middle of 16-byte vectors), standalone and fused: digests equal torch byte sums, sizes
+    the record counts, and the automatic choice picks it."""
+    import torch
+    import mydatastore_amd as mde
+    dev = torch.device("cuda:0")
+    engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    rec, counts, want, keep, (P, B) = _skewed_arena(dev, False, seed=3 + start, P=P, B=B, max_count=max_count,
+                                                    big=(3_000_000, 1_500_000, 2_000_000), stride=8, start=start)
+    try:
+        for v, pbs in [(-1, (-1,)), (REC8_VARIANTS[0], (-1,)), (REC8_VARIANTS[1], (1024, 8192, 1 << 20))]:
+            engine.set_tuning(v, -1)
+            for pb in pbs:
+                engine.set_digest_piece_bytes(pb)
+                for fused in (False, True):
+                    o = {"digest": torch.zeros(P * B, dtype=torch.int64, device=dev),
+                         "size": torch.zeros(P * B, dtype=torch.int32, device=dev),
+                         "items": torch.zeros(P, dtype=torch.int32, device=dev),
+                         "root": torch.zeros(P * 32, dtype=torch.uint8, device=dev)}
+                    to = mde.TreeOut(o["digest"].data_ptr(), o["size"].data_ptr(), o["items"].data_ptr(),
+                                     o["root"].data_ptr(), 0)
+                    if fused:
+                        engine.build_pipelined_async(rec, to)
+                        engine.build_pipeline_drain_async()
+                    else:
+                        engine.build_async(rec, to)
+                    engine.synchronize()
+                    assert torch.equal(o["digest"].cpu(), want), (v, pb, fused)
+                    assert torch.equal(o["size"].cpu().to(torch.int64), counts), (v, pb, fused)
+    finally:
+        engine.set_digest_piece_bytes(-1)
+        engine.set_tuning(-1, -1)

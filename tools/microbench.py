@@ -203,6 +203,25 @@ def bench_digest_only(eng, shape, reps=5):
     return r
 
 
+def bench_fused_only(eng, shape, reps=5):
+    """`reps` fused pipelined builds (build_step_kernel / tagged_step_kernel) of one workload shape
+    and the drain, nothing else after the workload build (for rocprofv3 PMC passes)."""
+    from mydatastore_amd.workload import make_workload
+    w = make_workload(eng, **{"n_buckets": 64, "value_len": 1024, "rank": 0, **SHAPES[shape]})
+    sets = [w._outs() for _ in range(2)]
+
+    def run():
+        for i in range(reps):
+            eng.build_pipelined_async(w.rec, sets[i % 2][1])
+        eng.build_pipeline_drain_async()
+
+    us = timeit(run, reps=1, warm=1) / reps
+    r = {"shape": shape, "bytes": w.value_bytes, "fused_us_per_build": round(us, 2),
+         "fused_GBps": round(w.value_bytes / us / 1e3, 1)}
+    print(json.dumps(r), flush=True)
+    return r
+
+
 def bench_verify(eng, P=1024, B=64, R=2, mode=0):
     """VerifyEpoch decision step (mde_verify_epochs) for P partitions x R peer objects: peer 0
     agrees, peer 1 differs in one bucket. Device-resident call timed with HIP events; the
@@ -314,6 +333,9 @@ def main():
         if w.startswith("digestonly:"):  # digestonly:ts8k[:reps] -- the digest kernel alone (PMC runs)
             parts = w.split(":")
             out["digestonly"] = bench_digest_only(eng, parts[1], int(parts[2]) if len(parts) > 2 else 5)
+        if w.startswith("fusedonly:"):  # fusedonly:c4bk[:reps] -- fused pipelined builds alone (PMC runs)
+            parts = w.split(":")
+            out["fusedonly"] = bench_fused_only(eng, parts[1], int(parts[2]) if len(parts) > 2 else 5)
         if w.startswith("digest:"):
             out["digest"] = bench_digest(eng, [int(x) for x in w.split(":")[1].split(",")])
     Path("gpurun_out").mkdir(exist_ok=True)
