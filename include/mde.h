@@ -243,7 +243,9 @@ int mde_decode_epoch_tree_objects(mde_ctx* ctx, uint32_t n, const uint8_t* bytes
                                   int32_t* size, uint8_t* valid, int32_t* items, int32_t* n_buckets);
 
 /* Manager.VerifyEpoch (main/manager.go:1036-1118) for n_partitions partitions of epoch E, given
- * this node's trees (digest/size/nodes from mde_build with the nodes output, n_buckets each) and
+ * this node's trees (digest/size/nodes from mde_build with the nodes output, n_buckets each; nodes
+ * may be NULL: a partition then builds its own tree on the device, only if one of its peers has
+ * another shape -- the one diff that reads inner nodes) and
  * n_peers peer EpochTreeObject wire objects per partition (what EpochTreeObjectRequest returned):
  * object (p, r) = peer_bytes[peer_off[p*n_peers+r] .. peer_off[p*n_peers+r+1]); an empty range is
  * an absent peer. Each peer object is decoded and rebuilt (EpochTreeObjectToMerkleTree) and diffed

@@ -508,7 +508,8 @@ class Engine:
         B = n_buckets
         digest = np.ascontiguousarray(digest, dtype=np.uint64).reshape(-1)
         size = np.ascontiguousarray(size, dtype=np.int32).reshape(-1)
-        nodes = np.ascontiguousarray(nodes, dtype=np.uint8).reshape(-1)
+        if nodes is not None:  # None: each partition builds its tree on the device if a peer needs it
+            nodes = np.ascontiguousarray(nodes, dtype=np.uint8).reshape(-1)
         P = digest.size // B
         R = len(peer_objects[0]) if P else 0
         if any(len(x) != R for x in peer_objects):

@@ -360,8 +360,8 @@ int check_verify(Req* q, uint64_t object_stride) {
   return MDE_OK;
 }
 
-// Stage + launch one verify batch: the local trees from their digests, then mde_verify_epochs over
-// all of them; peers padded to the batch's largest peer count with absent (empty) objects, which
+// Stage + launch one verify batch: mde_verify_epochs over all of them, the local trees given by
+// their digests; peers padded to the batch's largest peer count with absent (empty) objects, which
 // the reference skips like a failed EpochTreeObjectRequest (main/manager.go:1064-1070).
 void launch_verify(mde_batcher* b, Batch* bt) {
   const std::vector<Req*>& v = bt->v;
@@ -369,7 +369,7 @@ void launch_verify(mde_batcher* b, Batch* bt) {
   const int64_t epoch = v[0]->epoch;
   const uint32_t rcount = v[0]->replica_count;
   const bool want_obj = v[0]->object_out != nullptr;
-  const uint64_t P = v.size(), NI = mde_tree_internal_nodes(B);
+  const uint64_t P = v.size();
   uint32_t R = 0;
   uint64_t nbytes = 0;
   for (Req* x : v) {
@@ -380,7 +380,7 @@ void launch_verify(mde_batcher* b, Batch* bt) {
   const uint64_t i_dig = 0, i_size = align256(P * B * 8), i_part = i_size + align256(P * B * 4),
                  i_off = i_part + align256(P * 4), i_peer = i_off + align256((P * R + 1) * 8);
   const uint64_t in_bytes = i_peer + nbytes + 16;
-  uint64_t* o = bt->o;  // valid, valid_count, ids, diff_count, status, object_len, objects | roots, nodes
+  uint64_t* o = bt->o;  // valid, valid_count, ids, diff_count, status, object_len, objects
   o[0] = 0;
   o[1] = align256(P);
   o[2] = o[1] + align256(P * 4);
@@ -388,9 +388,8 @@ void launch_verify(mde_batcher* b, Batch* bt) {
   o[4] = o[3] + align256(P * 4);
   o[5] = o[4] + align256(P * R * 4 + 4);
   o[6] = o[5] + align256(P * 4);
-  o[7] = o[6] + align256(P * stride);  // results end here: roots and nodes stay on the device
-  o[8] = o[7] + align256(P * 32);
-  const uint64_t out_bytes = o[8] + P * NI * 32;
+  o[7] = o[6] + align256(P * stride);
+  const uint64_t out_bytes = o[7];
   bt->B = B;
   bt->stride = stride;
   bt->R = R;
@@ -427,13 +426,10 @@ void launch_verify(mde_batcher* b, Batch* bt) {
     ctx_error(bt->slot->ctx, v, rc);
     return;
   }
-  rc = mde_tree_from_digests_async(bt->slot->ctx, (uint32_t)P, B, d_dig, dout + o[7], dout + o[8]);
-  if (rc) {
-    ctx_error(bt->slot->ctx, v, rc);
-    return;
-  }
+  // local trees as digests only (nodes NULL): a partition builds its own tree on the device only
+  // when a peer of another shape needs its inner nodes
   rc = mde_verify_epochs_async(bt->slot->ctx, (uint32_t)P, B, reinterpret_cast<const int32_t*>(din + i_part), epoch, d_dig,
-                               reinterpret_cast<const int32_t*>(din + i_size), dout + o[8], R, din + i_peer,
+                               reinterpret_cast<const int32_t*>(din + i_size), nullptr, R, din + i_peer,
                                reinterpret_cast<const uint64_t*>(din + i_off), rcount, dout + o[0],
                                reinterpret_cast<int32_t*>(dout + o[1]), reinterpret_cast<int32_t*>(dout + o[2]),
                                reinterpret_cast<int32_t*>(dout + o[3]), reinterpret_cast<int32_t*>(dout + o[4]),

@@ -1389,7 +1389,7 @@ int verify_async(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, i
                  const uint8_t* peer_bytes, const uint64_t* peer_off, uint32_t replica_count,
                  uint8_t* valid, int32_t* valid_count, int32_t* diff_ids, int32_t* diff_count,
                  int32_t* peer_status, uint8_t* object_out, uint64_t object_stride, uint32_t* object_len) {
-  if (!B || B > mde::kVerifyMaxBuckets || !digest || !nodes || !valid || !valid_count || !diff_ids ||
+  if (!B || B > mde::kVerifyMaxBuckets || !digest || !valid || !valid_count || !diff_ids ||
       !diff_count || (R && (!peer_off || !peer_bytes)) || (object_out && (!size || !object_len)))
     return set_err(c, MDE_E_INVAL, "bad verify arguments");
   if (object_out && object_stride < mde::wire_max_bytes(B))
@@ -1399,11 +1399,14 @@ int verify_async(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, i
   const uint32_t cap = mde_verify_peer_capacity(B);
   if (!cap) return set_err(c, MDE_E_INVAL, "n_buckets too large");
   const uint64_t NI = mde::tree_internal(cap), idcap = mde_diff_capacity(B, cap);
-  // scratch: digests, sizes, bucket counts, valid flags, nodes, roots, diff ids, statuses
-  const uint64_t part[8] = {T * cap * 8, T * cap * 4, T * 4, T, T * NI * 32, T * 32, T * idcap * 4, T * 4};
-  uint64_t off[9] = {0};
-  for (int i = 0; i < 8; i++) off[i + 1] = off[i] + ((part[i] + 255) & ~255ull);
-  int rc = ensure_buf(c, c->verify_scratch, off[8]);
+  // scratch: digests, sizes, bucket counts, valid flags, nodes, roots, diff ids, statuses; without
+  // local nodes (nodes == NULL) also the local trees' nodes and roots, built where needed
+  const uint64_t NL = mde::tree_internal(B);
+  const uint64_t part[10] = {T * cap * 8, T * cap * 4, T * 4, T, T * NI * 32, T * 32, T * idcap * 4, T * 4,
+                             nodes ? 0 : (uint64_t)P * NL * 32, nodes ? 0 : (uint64_t)P * 32};
+  uint64_t off[11] = {0};
+  for (int i = 0; i < 10; i++) off[i + 1] = off[i] + ((part[i] + 255) & ~255ull);
+  int rc = ensure_buf(c, c->verify_scratch, off[10]);
   if (rc) return rc;
   uint8_t* base = static_cast<uint8_t*>(c->verify_scratch.p);
   auto at = [&](int i) { return static_cast<void*>(base + off[i]); };
@@ -1413,6 +1416,15 @@ int verify_async(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, i
   uint8_t* pnodes = static_cast<uint8_t*>(at(4));
   int32_t* pids = static_cast<int32_t*>(at(6));
   int32_t* pst = peer_status ? peer_status : static_cast<int32_t*>(at(7));
+  const bool build_local = !nodes;
+  if (build_local) nodes = static_cast<const uint8_t*>(at(8));
+  mde::TreeLaunch lt{};
+  lt.P = build_local ? P : 0;
+  lt.B = B;
+  lt.digest_in = digest;
+  lt.root_out = static_cast<uint8_t*>(at(9));
+  lt.nodes_out = static_cast<uint8_t*>(at(8));
+  lt.n_int = NL;
   if (mde::verify_fused_fits(R, cap) && !c->verify_chain) {
     // one launch: decode (LDS-staged) -> trees of other-shape peers -> diffs -> fold -> encode
     mde::VerifyFusedLaunch f{};
@@ -1430,9 +1442,11 @@ int verify_async(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, i
     if (object_out)
       f.enc = mde::WireEncodeLaunch{P, B, partition, epoch, epoch + 1, digest, size, valid, nullptr,
                                     object_out, object_stride, object_len};
+    f.local = lt;
     MDE_HIP(c, mde::launch_verify_fused(f, c->stream));
     return MDE_OK;
   }
+  if (T && build_local) MDE_HIP(c, mde::launch_tree(lt, c->stream));  // the chain diffs read every node
   if (T) {
     // EpochTreeObjectToMerkleTree: decode (>cap buckets can only diff with an error: deeper tree)
     mde::WireDecodeLaunch d{(uint32_t)T, peer_bytes, peer_off, cap, nullptr, nullptr, nullptr, pd,
@@ -1485,7 +1499,7 @@ int mde_verify_epochs(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partiti
                       int32_t* peer_status, uint8_t* object_out, uint64_t object_stride, uint32_t* object_len) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
-  if (!B || !digest || !nodes || !valid || !valid_count || !diff_ids || !diff_count ||
+  if (!B || !digest || !valid || !valid_count || !diff_ids || !diff_count ||
       (R && P && !peer_off) || (object_out && (!size || !object_len)))
     return set_err(c, MDE_E_INVAL, "bad verify arguments");
   const uint64_t N = P, T = N * R, NI = mde::tree_internal(B);
@@ -1500,7 +1514,7 @@ int mde_verify_epochs(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partiti
   const int i_part = io.in(partition, partition ? N * 4 : 0, N * 4);
   const int i_dig = io.in(digest, N * B * 8, N * B * 8);
   const int i_size = io.in(size, size ? N * B * 4 : 0, N * B * 4);
-  const int i_nodes = io.in(nodes, N * NI * 32, N * NI * 32);
+  const int i_nodes = io.in(nodes, nodes ? N * NI * 32 : 0, nodes ? N * NI * 32 : 0);
   const int i_peer = io.in(nbytes ? peer_bytes + peer_off[0] : nullptr, nbytes, nbytes + 1);
   const int i_rel = io.in(rel.data(), (T + 1) * 8, (T + 1) * 8);
   const int o_valid = io.out(valid, N), o_vc = io.out(valid_count, N * 4), o_ids = io.out(diff_ids, N * B * 4);
@@ -1514,7 +1528,8 @@ int mde_verify_epochs(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partiti
   rc = verify_async(c, P, B, partition ? static_cast<const int32_t*>(io.dev(i_part)) : nullptr, epoch,
                     static_cast<const uint64_t*>(io.dev(i_dig)),
                     size ? static_cast<const int32_t*>(io.dev(i_size)) : nullptr,
-                    static_cast<const uint8_t*>(io.dev(i_nodes)), R, static_cast<const uint8_t*>(io.dev(i_peer)),
+                    nodes ? static_cast<const uint8_t*>(io.dev(i_nodes)) : nullptr, R,
+                    static_cast<const uint8_t*>(io.dev(i_peer)),
                     static_cast<const uint64_t*>(io.dev(i_rel)), replica_count,
                     static_cast<uint8_t*>(io.dev(o_valid)), static_cast<int32_t*>(io.dev(o_vc)),
                     static_cast<int32_t*>(io.dev(o_ids)), static_cast<int32_t*>(io.dev(o_dc)),

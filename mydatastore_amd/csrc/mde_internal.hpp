@@ -251,6 +251,10 @@ struct VerifyFusedLaunch {
   DiffLaunch diff;       // n_pairs = P*R, a_div = R
   VerifyLaunch fold;
   WireEncodeLaunch enc;  // enc.n = 0: no object
+  // local.P != 0: the local trees were given as digests only; partition p builds its own tree
+  // (local.digest_in + p*B -> local.nodes_out + p*n_int*32) when one of its peers has another
+  // shape (the only diff that reads local nodes). local.nodes_out == diff.na.
+  TreeLaunch local;
 };
 bool verify_fused_fits(uint32_t R, uint32_t cap);
 hipError_t launch_verify_fused(const VerifyFusedLaunch& a, hipStream_t st);

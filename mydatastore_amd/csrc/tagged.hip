@@ -165,6 +165,8 @@ __device__ __forceinline__ void tagged_body(const TaggedLaunch& a, uint32_t bloc
   const uint32_t vsh = V >= kStep / 64 && (V & (V - 1)) == 0 ? (uint32_t)__builtin_ctzll(V) : 0u;
   const uint32_t vmask = (uint32_t)V - 1u;
   const bool fast_ok = vsh != 0 && !straddles && w.sum != nullptr && start == beg;
+  // one record per 1 KiB row (records of 2^k >= 1 KiB starting on the wave's row grid), shared slots
+  const bool rows_ok = fast_ok && vsh >= 10 && L < 64 && ((beg - pos0) & 1023u) == 0;
   // Small records (8 or 16 bytes: production values are 8-byte timestamps,
   // main/manager.go:816), each vector holding 16 / V whole records: every lane bins its own
   // records, whose tags it prefetches with the step (16 / V u16 loads per vector).
@@ -227,6 +229,41 @@ __device__ __forceinline__ void tagged_body(const TaggedLaunch& a, uint32_t bloc
           atomicAdd(w.cnt + b, 1u);
         }
       }
+    } else if (rows_ok && pn <= end && r0 + ((pn - 1 - pos0) >> vsh) < q_end) {
+      // Records of >= 1 KiB with fewer than 64 bin slots per bucket (B > 64; 4 at the reference's
+      // default B = 1,000): one 1 KiB row of the step lies in ONE record, so the 64 lanes' ds_adds
+      // of a row all hit that bucket's L slots -- 64/L-way on one address (SQ_LDS_BANK_CONFLICT
+      // 142.6 M vs 0.05 M at B = 64, profiles/r03f_sq_counters.json). Instead the 8 rows are
+      // reduced together: exchanges across lane bits 5, 4 and 3 leave lane l holding 1/8 of row
+      // l >> 3 (8 partials per row, one per lane bit 0-2 class); DPP folds those to L partials;
+      // then ONE ds_add puts every row's partials in its bucket's distinct slots, and one adds
+      // the record counts.
+      uint32_t f[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) f[u] = full_sum16(cur[u]);
+      const bool b5 = (lane & 32) != 0, b4 = (lane & 16) != 0, b3 = (lane & 8) != 0;
+      uint32_t g[4], h[2];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {  // bit 5: keep rows 4*b5 + j, give the partner the other half
+        const uint32_t send = b5 ? f[j] : f[j + 4], keep = b5 ? f[j + 4] : f[j];
+        g[j] = keep + (uint32_t)__shfl_xor((int)send, 32);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; j++) {  // bit 4
+        const uint32_t send = b4 ? g[j] : g[j + 2], keep = b4 ? g[j + 2] : g[j];
+        h[j] = keep + (uint32_t)__shfl_xor((int)send, 16);
+      }
+      const uint32_t send = b3 ? h[0] : h[1];  // bit 3: within a 16-lane row, row_ror:8 = lane ^ 8
+      uint32_t x = (b3 ? h[1] : h[0]) + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0x128, 0xf, 0xf, true);
+      if (L < 8) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xf, 0xf, true);  // j ~ 7 - j
+      if (L < 4) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4e, 0xf, 0xf, true);   // j ~ j ^ 2
+      if (L < 2) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xb1, 0xf, 0xf, true);   // j ~ j ^ 1
+      const uint32_t r = (uint32_t)lane >> 3, j = (uint32_t)lane & 7u;
+      const uint32_t xr = (uint32_t)(p - pos0) + r * 1024u;
+      const uint32_t k = (xr >> vsh) - (uint32_t)(cur_r0 - r0);  // < 64
+      const uint32_t b = min((uint32_t)__shfl((int)cur_tags, (int)k), a.B - 1);
+      if (j < L) atomicAdd(w.sum + b * L + j, x);
+      if (j == 0 && (xr & vmask) == 0) atomicAdd(w.cnt + b, 1u);
     } else if (fast_ok && pn <= end && r0 + ((pn - 1 - pos0) >> vsh) < q_end) {
       // Fast step (wave-uniform): power-of-two records of >= kStep/64 B on 16-byte boundaries, the
       // whole step inside [start, end) and inside partition q. Every vector then lies in one

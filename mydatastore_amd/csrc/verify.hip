@@ -166,6 +166,16 @@ __global__ __launch_bounds__(kThreads) void verify_fused_kernel(VerifyFusedLaunc
     if (other) need_tree = 1;
   }
   __syncthreads();
+  if (need_tree && f.local.P) {  // the local tree, only now that an other-shape peer needs its nodes
+    TreeLaunch t = f.local;
+    t.P = 1;
+    t.digest_in += (uint64_t)p * B;
+    t.nodes_out += (uint64_t)p * t.n_int * 32;
+    t.root_out += (uint64_t)p * 32;
+    tree_body<true>(t, G, words, 0, dyn, kThreads);  // G, words: the geometry of cap >= B
+    __threadfence();
+    __syncthreads();
+  }
   if (need_tree) {
     TreeLaunch t = f.tree;
     t.P = R;

@@ -352,14 +352,16 @@ def test_digest_pieces_full_size(engine):
 @pytest.mark.parametrize("value_len,n_keys,world,n_buckets", [
     (1024, 10_000_000, 1, 64), (1024, 10_000_000, 8, 64), (100, 4_000_000, 1, 64),
     (8, 20_000_000, 1, 1000), (8, 20_000_000, 8, 64), (16, 10_000_000, 1, 64),
-    (1024, 2_000_000, 1, 1000), (2048, 1_000_000, 1, 128)])
+    (1024, 2_000_000, 1, 1000), (2048, 1_000_000, 1, 128), (1024, 10_000_000, 1, 1000),
+    (4096, 500_000, 1, 300), (1024, 4_000_000, 8, 1000), (1024, 3_000_000, 1, 4000)])
 def test_tagged_equals_layout_a_full_size(engine, value_len, n_keys, world, n_buckets):
     """Layout B (arrival order + bucket tags, binned on device), standalone and fused: digests,
     sizes, items and roots equal the layout-A build of the same records, at C4 (N=1 and the N=8
     shard). 100-byte values put record boundaries inside the 16-byte vectors (the general
     binning path); 8- and 16-byte values take the small-record path (the production timestamp
-    size), at B = 64 and the reference's default B = 1000. 1 and 2 KiB values at B = 1,000 / 128
-    take the fast step with fewer than 64 lane slots per bucket (slots shared by 16 / 2 lanes)."""
+    size), at B = 64 and the reference's default B = 1000. 1, 2 and 4 KiB values at B = 128 to
+    4,000 take the row-reduced fast step (fewer than 64 lane slots per bucket: 32 down to 1; C4 at
+    B = 1,000 whole, and its N = 8 shard)."""
     import torch
     from mydatastore_amd.workload import make_workload
     kw = dict(n_partitions=1024, n_buckets=n_buckets, value_len=value_len, part_mode="mod", n_keys=n_keys,

@@ -91,11 +91,14 @@ def test_oracle_verify_testmerkletreeraw_relations(golden):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("local_nodes", [True, False], ids=["nodes", "digests_only"])
 @pytest.mark.parametrize("mode", [0, 1], ids=["fused", "chain"])
 @pytest.mark.parametrize("B", [64, 30, 7, 1, 65, 129, 513, 1000, 1024, 2000])
-def test_verify_epochs_matches_oracle(engine, B, mode):
+def test_verify_epochs_matches_oracle(engine, B, mode, local_nodes):
     """Both launch shapes (one fused launch; the decode/tree/diff/fold/encode chain) against the
-    oracle. B = 2000 exceeds the fused kernel's peer capacity and runs the chain in both modes."""
+    oracle. B = 2000 exceeds the fused kernel's peer capacity and runs the chain in both modes.
+    digests_only: the local trees' nodes are not given (nodes = NULL, the batcher's form); a
+    partition builds its tree on the device when a peer of another shape needs it."""
     rng = np.random.default_rng(1000 + B)
     P, E, replica = 16, 41, 2
     digests = rng.integers(0, 999999, size=P * B, dtype=np.uint64)
@@ -106,7 +109,8 @@ def test_verify_epochs_matches_oracle(engine, B, mode):
              for p in range(P)]
     engine.set_verify_mode(mode)
     try:
-        got = engine.verify_epochs(B, digests, sizes, nodes, peers, replica, E, partition=parts)
+        got = engine.verify_epochs(B, digests, sizes, nodes if local_nodes else None, peers, replica, E,
+                                   partition=parts)
     finally:
         engine.set_verify_mode(0)
     want = _oracle_verify(B, digests, sizes, peers, replica, E, parts)
