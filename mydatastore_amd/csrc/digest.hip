@@ -443,6 +443,7 @@ template <bool NT>
 __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uint64_t beg, uint64_t end, uint32_t s_lo,
                                                       int lane, uint32_t* lds) {
   constexpr uint64_t kStep = 4096;
+  constexpr uint32_t kFoldSteps = 4096;  // fast steps per lane fold: 255 x 16 MiB < 2^32 exact
   const SegDesc& d = a.seg;
   uint32_t* R = lds;               // record sums, then exclusive local prefixes (swizzled)
   uint32_t* E = lds + kRec8Sums;   // lane exclusive prefixes; E[64] = the step's total
@@ -456,22 +457,24 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
   SegWindow win;
   win.load(d, s, lane);
   uint64_t sb = readlane64(win.start, 0), se = readlane64(win.start, 1);
-  uint64_t wsum = 0;     // this lane's window bucket (win.base + lane): its finished sum
-  uint64_t bfrom = beg;  // where this wave entered bucket s
-  uint32_t acc = 0;      // lane accumulator of whole steps inside bucket s
-  uint64_t accs = 0;     // wave-uniform: bucket s's bytes from steps with bucket starts
+  uint64_t wsum = 0;       // this lane's window bucket (win.base + lane): its finished sum
+  uint32_t acc = 0;        // lane accumulator of whole steps inside bucket s
+  uint32_t acc_steps = 0;  // wave-uniform: fast steps in acc (0: acc is all zero)
+  uint64_t accs = 0;       // wave-uniform: bucket s's bytes folded out of acc and from scan steps
+  // lane-invariant LDS addresses
+  uint32_t* const wrow = R + rec8_swz(2u * (uint32_t)lane);
+  uint32_t* const rd0 = R + rec8_swz(8u * (uint32_t)lane);
+  uint32_t* const rd1 = R + rec8_swz(8u * (uint32_t)lane + 4u);
 
-  auto retire = [&](uint64_t upto) {  // bucket s is left: its sum into its window lane
-    uint64_t v;
-    if (upto - bfrom <= (16ull << 20)) {
-      v = wave_sum_u32(acc);  // <= 255 x 16 MiB < 2^32
-    } else {
-      v = acc;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    }
-    if ((uint32_t)lane == s - win.base) wsum = v + accs;
+  auto fold = [&]() {  // acc -> accs (exact: acc_steps <= kFoldSteps)
+    if (acc_steps) accs += wave_sum_u32(acc);
     acc = 0;
+    acc_steps = 0;
+  };
+  auto retire = [&]() {  // bucket s is left: its sum into its window lane
+    fold();
+    const uint32_t k = __builtin_amdgcn_readfirstlane(s - win.base);
+    if ((uint32_t)lane == k) wsum = accs;
     accs = 0;
   };
   auto window_out = [&]() {  // one coalesced atomic for the window's finished buckets
@@ -488,23 +491,25 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
         acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
         acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
       }
+      if (++acc_steps == kFoldSteps) fold();
       return;
     }
-    // record sums -> LDS at their record index (row u, lane l: records 128u + 2l, 128u + 2l + 1)
+    // record sums -> LDS at their record index (row u, lane l: records 128u + 2l, 128u + 2l + 1;
+    // rec8_swz only flips bit 2 from bit 6, so row u's words sit at wrow + 128u)
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const uint32_t r0 = __builtin_amdgcn_sad_u8(v[u].y, 0u, __builtin_amdgcn_sad_u8(v[u].x, 0u, 0u));
       const uint32_t r1 = __builtin_amdgcn_sad_u8(v[u].w, 0u, __builtin_amdgcn_sad_u8(v[u].z, 0u, 0u));
-      *reinterpret_cast<uint2*>(R + rec8_swz(128u * u + 2u * (uint32_t)lane)) = make_uint2(r0, r1);
+      *reinterpret_cast<uint2*>(wrow + 128u * u) = make_uint2(r0, r1);
     }
     // transposed: this lane's records 8l .. 8l+7, their local prefix, one wave scan of the totals
-    const uint4 x = *reinterpret_cast<const uint4*>(R + rec8_swz(8u * (uint32_t)lane));
-    const uint4 y = *reinterpret_cast<const uint4*>(R + rec8_swz(8u * (uint32_t)lane + 4u));
+    const uint4 x = *reinterpret_cast<const uint4*>(rd0);
+    const uint4 y = *reinterpret_cast<const uint4*>(rd1);
     const uint32_t c1 = x.x, c2 = c1 + x.y, c3 = c2 + x.z, c4 = c3 + x.w;
     const uint32_t c5 = c4 + y.x, c6 = c5 + y.y, c7 = c6 + y.z, tot = c7 + y.w;
     const uint32_t incl = wave_incl_scan_u32(tot);
-    *reinterpret_cast<uint4*>(R + rec8_swz(8u * (uint32_t)lane)) = make_uint4(0u, c1, c2, c3);
-    *reinterpret_cast<uint4*>(R + rec8_swz(8u * (uint32_t)lane + 4u)) = make_uint4(c4, c5, c6, c7);
+    *reinterpret_cast<uint4*>(rd0) = make_uint4(0u, c1, c2, c3);
+    *reinterpret_cast<uint4*>(rd1) = make_uint4(c4, c5, c6, c7);
     E[lane] = incl - tot;
     if (lane == 63) E[64] = incl;
     // F(y) for this lane's bucket start y, clamped to [p, q]: record slot k = (y - p) / 8
@@ -513,29 +518,28 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
       const uint64_t st = win.start;
       const uint32_t k = st <= p ? 0u : (st >= q ? kq : (uint32_t)((st - p) >> 3));
       const uint32_t F = R[rec8_swz(k)] + E[k >> 3];
-      const uint32_t c = (uint32_t)__shfl_down((int)F, 1) - F;  // bucket base + lane, lanes 0..62
-      const uint32_t k0 = s - win.base;
+      // bucket base + lane's bytes in the step, lanes 0..62: F of the next lane (DPP wave_shl:1)
+      const uint32_t c = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)F, 0x130, 0xf, 0xf, true) - F;
+      const uint32_t k0 = __builtin_amdgcn_readfirstlane(s - win.base);
       const uint32_t cnt = (uint32_t)__popcll(__ballot(st < q));
       accs += (uint32_t)__builtin_amdgcn_readlane((int)c, (int)k0);
       if (cnt == 64u) {  // the step runs past the window: buckets k0..62 all end inside it
-        retire(readlane64(st, k0 + 1u));
+        retire();
         if ((uint32_t)lane > k0 && lane < 63) wsum = c;
         window_out();
         win.load(d, win.base + 63u, lane);
         s = win.base;
         sb = readlane64(win.start, 0);
         se = readlane64(win.start, 1);
-        bfrom = sb;
         continue;
       }
       const uint32_t m = cnt - 1u;  // the last bucket starting before q: it runs on past q
       if (m > k0) {
-        retire(readlane64(st, k0 + 1u));
+        retire();
         if ((uint32_t)lane > k0 && (uint32_t)lane < m) wsum = c;
         s = win.base + m;
         sb = readlane64(st, m);
         se = readlane64(st, m + 1u);
-        bfrom = sb;
         accs = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)m);
       }
       return;
@@ -550,7 +554,7 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
     process(vb, p + kStep);
     if (p + 2 * kStep >= end) break;
   }
-  retire(min(se, end));
+  retire();
   window_out();
   return s;
 }

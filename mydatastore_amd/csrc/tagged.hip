@@ -359,6 +359,12 @@ size_t prepare_tagged(TaggedLaunch& a) {  // launcher-set fields; returns the bi
   // bins of one workgroup <= 64 KiB: (kThreads/64) * B * (L + 1) * 4 bytes
   uint32_t L = 64;
   while (L > 1 && (uint64_t)a.B * (L + 1) * (kThreads / 64) * 4 > 65536) L >>= 1;
+  // Records of 2^k >= 1 KiB on 16-byte boundaries take the row-reduced fast step (tagged_body
+  // rows_ok), which folds each row to L partials itself: one slot per bucket is enough there, and
+  // the bins shrink so that the fused step's tree workgroups still fit beside four binning
+  // workgroups (at B = 1,000: 16 instead of 40 KiB per workgroup; with 40 KiB the CU's LDS was
+  // full and the trees ran only after the binning, +139 vs +68 us over the digest in layout A).
+  if (L < 64 && a.stride >= 1024 && (a.stride & (a.stride - 1)) == 0 && ((a.stride | a.shift) & 15) == 0) L = 1;
   a.lrep = L;
   a.inv_stride_f = 1.0f / (float)a.stride;
   return a.use_lds ? (size_t)(kThreads / 64) * ((size_t)a.B * L + a.B) * 4 : 0;
