@@ -353,8 +353,12 @@ __host__ __device__ inline uint32_t tree_lds_words(uint32_t B) {
 __device__ __forceinline__ void step_trees(const TreeLaunch& t, uint32_t Q, uint32_t block, uint32_t* lds) {
   if (Q)
     tree_body_packed(t, Q, block, lds);
-  else
+  else {
+#ifdef MDE_STEP_WIDE_PRIO  // probe only: wide-tree waves at this priority beside the stream
+    __builtin_amdgcn_s_setprio(MDE_STEP_WIDE_PRIO);
+#endif
     tree_body<true>(t, kStepTreeWideThreads, tree_lds_words(t.B), block, lds, kStepTreeWideThreads);
+  }
 }
 
 }  // namespace mde

@@ -4,7 +4,7 @@
 # repo root on the GPU box:  bash tools/r03f_pmc.sh fusedonly:c4bk fusedonly:c4b digestonly:ts8k ...
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out/r03f
+mkdir -p gpurun_out/r03f; rm -rf gpurun_out/r03f/*
 for what in "$@"; do
   tag=${what//:/_}
   out=gpurun_out/r03f/$tag
