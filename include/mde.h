@@ -319,8 +319,9 @@ int mde_multi_build_streamed(mde_group* group, const mde_records* rec, const mde
  * joins the queue; the first caller to find no batch running takes every compatible queued
  * request (same kind and n_buckets; verify: same epoch and replica_count, objects wanted or not;
  * at most max_partitions partitions; after waiting up to max_wait_us for more, 0 = no wait) and
- * runs them as ONE H2D copy + ONE build (or trees + verify) + ONE D2H copy; requests arriving
- * meanwhile form the next batch. Every call is synchronous and thread-safe, returns exactly what
+ * runs them as ONE H2D copy + ONE build (or verify) launch + ONE D2H copy; requests arriving
+ * meanwhile form the next batch (up to mde_batcher_contexts() batches in flight). A build batch
+ * holds at most 2^32 buckets in all. Every call is synchronous and thread-safe, returns exactly what
  * the per-call entry point returns for its own inputs, and writes its own error message into
  * err (err_cap bytes, NUL-terminated; may be NULL) -- no shared last-error state, so the Go shim
  * needs no lock. Inputs are host pointers, read only during the call (cgo pointer rules).
@@ -342,8 +343,9 @@ int mde_batch_build(mde_batcher* b, const mde_records* rec, const mde_tree_out* 
                     uint64_t err_cap);
 /* The VerifyEpoch decision step (main/manager.go:1072-1104) for ONE partition: mde_verify_epochs
  * with n_partitions = 1, whose local tree is given by its bucket digests (and sizes, required for
- * object_out) -- the tree itself (EpochTreeObjectToMerkleTree of the local object) is built on the
- * device in the same batch. n_peers may differ between callers of one batch. */
+ * object_out); its inner nodes (EpochTreeObjectToMerkleTree of the local object) are built on the
+ * device inside the verify launch, and only when a peer of another shape needs them. n_peers may
+ * differ between callers of one batch. */
 int mde_batch_verify(mde_batcher* b, uint32_t n_buckets, int32_t partition, int64_t epoch,
                      const uint64_t* digest, const int32_t* size, uint32_t n_peers,
                      const uint8_t* peer_bytes, const uint64_t* peer_off, uint32_t replica_count,

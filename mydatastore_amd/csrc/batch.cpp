@@ -11,12 +11,17 @@
 //   * if no batch is running it becomes the leader: it takes every compatible queued request (up
 //     to max_partitions partitions; optionally waiting up to max_wait_us for more to arrive),
 //     packs their records into ONE pinned arena, runs ONE H2D copy, mde_build_async (or
-//     mde_tree_from_digests_async + mde_verify_epochs_async) and ONE D2H copy on the batcher's own
-//     context, scatters the results into each caller's buffers and wakes the callers;
+//     mde_verify_epochs_async with the local trees given by their digests) and ONE D2H copy on a
+//     free slot's context, scatters the results into each caller's buffers and wakes the callers;
 //   * requests that arrive while a batch runs form the next batch, whose leader is one of them:
-//     two batches are in flight at once (two staging slots), so the next batch's staging, copies
-//     and launches overlap the previous batch's device work, and a finished batch wakes only its
-//     own callers (one condition variable per request: no thundering herd at 100 callers).
+//     up to kSlots batches are in flight at once (one context, stream and staging area per slot),
+//     so the next batch's staging, copies and launches overlap the earlier batches' device work,
+//     and a finished batch wakes only its own callers (one condition variable per request: no
+//     thundering herd at 100 callers).
+// Liveness: every lead() ends with a handoff() after its slot is freed, and a leader hands off
+// again right after launching, so a queued request is picked up by the next free slot even when
+// the request it was handed the role to has meanwhile finished inside another batch.
+// mde_batcher_destroy must not race with calls in flight (like mde_destroy).
 // Each caller gets exactly what the per-call entry point returns for its own inputs (bit-exact:
 // a partition's digests, sizes and tree depend only on its own records; tests/cpp/batch_test.c
 // checks it against mde_build / mde_verify_epochs and the C oracle under concurrent callers).
@@ -183,14 +188,17 @@ int check_build(Req* q) {
 
 bool same_key(const Req* a, const Req* b) { return std::memcmp(a->key, b->key, sizeof a->key) == 0; }
 
-// The leader's batch: the front request and every later compatible one, up to max_parts.
+// The leader's batch: the front request and every later compatible one, up to max_parts (and,
+// for builds, up to 2^32 buckets in all: mde_build's limit on n_partitions * n_buckets).
 std::vector<Req*> take(mde_batcher* b) {
   std::vector<Req*> out;
   Req* first = b->q.front();
+  const uint64_t per_part = first->kind == Kind::Build ? first->rec.n_buckets : 1;
   uint64_t parts = 0;
   for (auto it = b->q.begin(); it != b->q.end();) {
     Req* x = *it;
-    if (x == first || (same_key(x, first) && parts + x->parts <= b->max_parts)) {
+    if (x == first || (same_key(x, first) && parts + x->parts <= b->max_parts &&
+                       (parts + x->parts) * per_part <= 0xffffffffull)) {
       out.push_back(x);
       parts += x->parts;
       it = b->q.erase(it);

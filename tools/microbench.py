@@ -148,14 +148,15 @@ def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
         sets = [w._outs() for _ in range(2)]
         n_steps = 10
 
-        def fused():
-            for i in range(n_steps):
+        def fused(n=n_steps):
+            for i in range(n):
                 eng.build_pipelined_async(w.rec, sets[i % 2][1])
             eng.build_pipeline_drain_async()
 
         ref = None
         td = {p: [] for p in pieces}
         tf = {p: [] for p in pieces}
+        ts = {p: [] for p in pieces}  # steady state: (2n builds - n builds) / n, the drain cancels
         tt = {p: [] for p in pieces}
         for _ in range(reps):
             for p in pieces:
@@ -171,7 +172,9 @@ def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
                 eng.set_tuning(v, -1)
                 eng.set_digest_piece_bytes({"d": -1, "x": 0}[rest] if rest in ("d", "x") else int(rest))
                 td[p].append(timeit(w.digest_async, reps=10, warm=2))
-                tf[p].append(timeit(fused, reps=1, warm=1) / n_steps)
+                t1 = timeit(fused, reps=1, warm=1)
+                tf[p].append(t1 / n_steps)
+                ts[p].append((timeit(lambda: fused(2 * n_steps), reps=1, warm=0) - t1) / n_steps)
                 tt[p].append(timeit(w.tree_async, reps=5, warm=1))
                 o = w.build()
                 if ref is None:
@@ -184,6 +187,7 @@ def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
             res.append({"shape": shape, "piece_bytes": p, "bytes": w.value_bytes, "digest_us": round(md, 2),
                         "digest_GBps": round(w.value_bytes / md / 1e3, 1), "fused_us_per_build": round(mf, 2),
                         "fused_GBps": round(w.value_bytes / mf / 1e3, 1),
+                        "fused_steady_us": round(float(np.median(ts[p])), 2),
                         "tree_us": round(float(np.median(tt[p])), 2)})
             print(json.dumps(res[-1]), flush=True)
         del w, sets
