@@ -134,6 +134,18 @@ SHAPES = {"c4": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", worl
                            n_buckets=1000)}
 
 
+def apply_setting(eng, p):
+    """Digest variant / piece setting by name (see bench_pieces)."""
+    v, rest = (11 if p == "x" else -1), p
+    if p.startswith("v"):
+        num = "".join(ch for ch in p[1:] if ch.isdigit())
+        v, rest = int(num), p[1 + len(num):].lstrip("_")
+    elif p not in ("d", "x"):
+        v = 12
+    eng.set_tuning(v, -1)
+    eng.set_digest_piece_bytes({"d": -1, "x": 0}[rest] if rest in ("d", "x") else int(rest))
+
+
 def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
     """Interleaved A/B of the layout-A digest work split: the defaults ("d", automatic pieces),
     the default variant with one contiguous range per wave ("x") and the interleaved-pieces
@@ -163,14 +175,7 @@ def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
                 # "d": the defaults (automatic variant and pieces); "x": variant 11 (round 1's
                 # default) with one range per wave; a number: the interleaved-pieces variant at that piece size; "v13d",
                 # "v13x", "v14_1048576": variant 13 / 14 with the same piece settings
-                v, rest = (11 if p == "x" else -1), p
-                if p.startswith("v"):
-                    num = "".join(ch for ch in p[1:] if ch.isdigit())
-                    v, rest = int(num), p[1 + len(num):].lstrip("_")
-                elif p not in ("d", "x"):
-                    v = 12
-                eng.set_tuning(v, -1)
-                eng.set_digest_piece_bytes({"d": -1, "x": 0}[rest] if rest in ("d", "x") else int(rest))
+                apply_setting(eng, p)
                 td[p].append(timeit(w.digest_async, reps=10, warm=2))
                 t1 = timeit(fused, reps=1, warm=1)
                 tf[p].append(t1 / n_steps)
@@ -195,13 +200,15 @@ def bench_pieces(eng, pieces, shapes=("c4", "c4/8", "c3"), reps=5):
     return res
 
 
-def bench_digest_only(eng, shape, reps=5):
-    """The default digest kernel alone on one workload shape, `reps` launches (for rocprofv3 PMC
-    passes: no other kernels between the workload build and the launches but its own)."""
+def bench_digest_only(eng, shape, reps=5, setting="d"):
+    """The digest kernel alone on one workload shape, `reps` launches (for rocprofv3 PMC passes: no
+    other kernels between the workload build and the launches but its own); `setting` as in
+    bench_pieces (default: the automatic choice)."""
     from mydatastore_amd.workload import make_workload
     w = make_workload(eng, **{"n_buckets": 64, "value_len": 1024, "rank": 0, **SHAPES[shape]})
+    apply_setting(eng, setting)
     us = timeit(w.digest_async, reps=reps, warm=1)
-    r = {"shape": shape, "bytes": w.value_bytes, "digest_us": round(us, 2),
+    r = {"shape": shape, "setting": setting, "bytes": w.value_bytes, "digest_us": round(us, 2),
          "digest_GBps": round(w.value_bytes / us / 1e3, 1)}
     print(json.dumps(r), flush=True)
     return r
@@ -336,7 +343,8 @@ def main():
             out["pieces"] = bench_pieces(eng, parts[1].split(","), shapes)
         if w.startswith("digestonly:"):  # digestonly:ts8k[:reps] -- the digest kernel alone (PMC runs)
             parts = w.split(":")
-            out["digestonly"] = bench_digest_only(eng, parts[1], int(parts[2]) if len(parts) > 2 else 5)
+            out["digestonly"] = bench_digest_only(eng, parts[1], int(parts[2]) if len(parts) > 2 else 5,
+                                                  parts[3] if len(parts) > 3 else "d")
         if w.startswith("fusedonly:"):  # fusedonly:c4bk[:reps] -- fused pipelined builds alone (PMC runs)
             parts = w.split(":")
             out["fusedonly"] = bench_fused_only(eng, parts[1], int(parts[2]) if len(parts) > 2 else 5)
