@@ -351,6 +351,11 @@ int plan_digest(mde_ctx* c, uint64_t bytes, mde::DigestLaunch* a) {
     // every ~100 records at B = 1,000; the record-space scan (digest.hip digest_range_rec8)
     if (a->seg.stride == 8 && (a->seg.shift & 7) == 0) a->variant = kRec8DigestVariant;
   }
+  // an explicitly chosen rec8 variant needs 8-byte records: the window kernel instead (decided
+  // before the grid is planned, so the occupancy below is the one of the kernel that runs)
+  if (mde::bucket_digest_rec8(a->variant) && (a->seg.stride != 8 || (a->seg.shift & 7)))
+    a->variant = mde::bucket_digest_pieces(a->variant) ? mde::bucket_digest_pieces_sibling(kWindowDigestVariant)
+                                                       : kWindowDigestVariant;
   uint64_t piece_bytes = 0;
   if (c->digest_piece_bytes == kAutoPieceBytes) {
     // automatic pieces: the default's (or an explicitly chosen pieces variant's) pieces form
@@ -379,12 +384,7 @@ int plan_digest(mde_ctx* c, uint64_t bytes, mde::DigestLaunch* a) {
                           &a->wave_bytes, &a->n_waves, &a->pieces);
   a->piece_stride = (uint64_t)a->n_waves * a->wave_bytes;
   a->lds_bytes = c->digest_oversub > 1 ? (uint32_t)((160u * 1024u) / (uint32_t)c->digest_blocks_per_cu) & ~255u : 0u;
-  if (mde::bucket_digest_rec8(a->variant)) {
-    if (a->seg.stride != 8 || (a->seg.shift & 7))  // needs 8-byte records: the window kernel instead
-      a->variant = mde::bucket_digest_pieces(a->variant) ? mde::bucket_digest_pieces_sibling(kWindowDigestVariant)
-                                                         : kWindowDigestVariant;
-    else a->lds_bytes = std::max(a->lds_bytes, mde::bucket_digest_rec8_lds_bytes());
-  }
+  if (mde::bucket_digest_rec8(a->variant)) a->lds_bytes = std::max(a->lds_bytes, mde::bucket_digest_rec8_lds_bytes());
   // Tail stealing needs fixed-length values and a split range; otherwise the static sibling.
   if (steals) {
     mde::plan_steal(a->wave_bytes, &a->head_bytes, &a->chunk_bytes, &a->tail_chunks);

@@ -135,14 +135,19 @@ SHAPES = {"c4": dict(n_partitions=1024, n_keys=10_000_000, part_mode="mod", worl
 
 
 def apply_setting(eng, p):
-    """Digest variant / piece setting by name (see bench_pieces)."""
+    """Digest variant / piece setting by name (see bench_pieces); a suffix "@N" caps the resident
+    digest workgroups per CU at N."""
+    cap = -1
+    if "@" in p:
+        p, c = p.split("@")
+        cap = int(c)
     v, rest = (11 if p == "x" else -1), p
     if p.startswith("v"):
         num = "".join(ch for ch in p[1:] if ch.isdigit())
         v, rest = int(num), p[1 + len(num):].lstrip("_")
     elif p not in ("d", "x"):
         v = 12
-    eng.set_tuning(v, -1)
+    eng.set_tuning(v, cap)
     eng.set_digest_piece_bytes({"d": -1, "x": 0}[rest] if rest in ("d", "x") else int(rest))
 
 
