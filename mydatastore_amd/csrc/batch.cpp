@@ -36,6 +36,7 @@
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -125,6 +126,10 @@ struct mde_batcher {
     bool busy = false;
   } slots[kSlots];
   uint64_t n_batches = 0, n_requests = 0, n_partitions = 0;
+  // write-once outputs stored by the kernels straight into the slot's pinned out buffer (no D2H
+  // copy; above ~16 KB such a copy starts ~11 us after the kernel, profiles/r03q_call_trace.txt);
+  // MDE_DIRECT_OUT=0 turns it off (A/B)
+  bool direct_out = true;
 };
 
 namespace {
@@ -251,6 +256,16 @@ int grow_slot(mde_batcher::Slot* sl, uint64_t in_bytes, uint64_t d2h_bytes, uint
   return MDE_OK;
 }
 
+// Device address of the slot's pinned out buffer (NULL: not mapped, copy instead).
+uint8_t* mapped_out(mde_batcher* b, mde_batcher::Slot* sl) {
+  void* p = nullptr;
+  if (!b->direct_out || hipHostGetDevicePointer(&p, sl->pin_out.p, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return static_cast<uint8_t*>(p);
+}
+
 // Stage + launch one build batch (records rebased into one arena): ONE H2D copy, mde_build_async,
 // ONE D2H copy and an event, all enqueued on the batcher context's stream.
 void launch_build(mde_batcher* b, Batch* bt) {
@@ -306,8 +321,11 @@ void launch_build(mde_batcher* b, Batch* bt) {
   hseg[S] = N;
   hipStream_t st = static_cast<hipStream_t>(mde_get_stream(bt->slot->ctx));
   uint8_t* din = static_cast<uint8_t*>(bt->slot->dev_in.p);
-  uint8_t* dout = static_cast<uint8_t*>(bt->slot->dev_out.p);
   BHIP(hipSetDevice(b->device));
+  // every build output is stored once by the tree pass (trees wider than the LDS levels re-read
+  // their nodes: device memory and a copy for those)
+  uint8_t* mapped = B <= 4096u ? mapped_out(b, bt->slot) : nullptr;
+  uint8_t* dout = mapped ? mapped : static_cast<uint8_t*>(bt->slot->dev_out.p);
   BHIP(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, st));
   mde_records dr{};
   dr.values = din + o_vals;
@@ -326,7 +344,7 @@ void launch_build(mde_batcher* b, Batch* bt) {
     ctx_error(bt->slot->ctx, v, brc);
     return;
   }
-  BHIP(hipMemcpyAsync(bt->slot->pin_out.p, dout, out_bytes, hipMemcpyDeviceToHost, st));
+  if (!mapped) BHIP(hipMemcpyAsync(bt->slot->pin_out.p, dout, out_bytes, hipMemcpyDeviceToHost, st));
   BHIP(hipEventRecord(bt->slot->done, st));
   bt->launched = true;
 }
@@ -427,6 +445,10 @@ void launch_verify(mde_batcher* b, Batch* bt) {
   uint8_t* din = static_cast<uint8_t*>(bt->slot->dev_in.p);
   uint8_t* dout = static_cast<uint8_t*>(bt->slot->dev_out.p);
   BHIP(hipSetDevice(b->device));
+  // valid and the peer statuses are read back inside the launch (the fold, the encode): device
+  // memory, copied; the counts, ids and objects are stored once, straight into pinned memory
+  uint8_t* mapped = mapped_out(b, bt->slot);
+  uint8_t* wout = mapped ? mapped : dout;
   BHIP(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, st));
   const uint64_t* d_dig = reinterpret_cast<const uint64_t*>(din + i_dig);
   int rc = mde_reserve_decode_scratch(bt->slot->ctx, P * R, nbytes);  // linear decode of any peer object
@@ -439,15 +461,21 @@ void launch_verify(mde_batcher* b, Batch* bt) {
   rc = mde_verify_epochs_async(bt->slot->ctx, (uint32_t)P, B, reinterpret_cast<const int32_t*>(din + i_part), epoch, d_dig,
                                reinterpret_cast<const int32_t*>(din + i_size), nullptr, R, din + i_peer,
                                reinterpret_cast<const uint64_t*>(din + i_off), rcount, dout + o[0],
-                               reinterpret_cast<int32_t*>(dout + o[1]), reinterpret_cast<int32_t*>(dout + o[2]),
-                               reinterpret_cast<int32_t*>(dout + o[3]), reinterpret_cast<int32_t*>(dout + o[4]),
-                               want_obj ? dout + o[6] : nullptr, stride,
-                               want_obj ? reinterpret_cast<uint32_t*>(dout + o[5]) : nullptr);
+                               reinterpret_cast<int32_t*>(wout + o[1]), reinterpret_cast<int32_t*>(wout + o[2]),
+                               reinterpret_cast<int32_t*>(wout + o[3]), reinterpret_cast<int32_t*>(dout + o[4]),
+                               want_obj ? wout + o[6] : nullptr, stride,
+                               want_obj ? reinterpret_cast<uint32_t*>(wout + o[5]) : nullptr);
   if (rc) {
     ctx_error(bt->slot->ctx, v, rc);
     return;
   }
-  BHIP(hipMemcpyAsync(bt->slot->pin_out.p, dout, o[7], hipMemcpyDeviceToHost, st));
+  uint8_t* hout = static_cast<uint8_t*>(bt->slot->pin_out.p);
+  if (mapped) {
+    BHIP(hipMemcpyAsync(hout + o[0], dout + o[0], P, hipMemcpyDeviceToHost, st));
+    if (R) BHIP(hipMemcpyAsync(hout + o[4], dout + o[4], P * R * 4, hipMemcpyDeviceToHost, st));
+  } else {
+    BHIP(hipMemcpyAsync(hout, dout, o[7], hipMemcpyDeviceToHost, st));
+  }
   BHIP(hipEventRecord(bt->slot->done, st));
   bt->launched = true;
 }
@@ -584,6 +612,7 @@ int mde_batcher_create(int device, uint32_t max_partitions, uint32_t max_wait_us
     }
   }
   b->device = device;
+  if (const char* e = std::getenv("MDE_DIRECT_OUT")) b->direct_out = std::atoi(e) != 0;
   b->max_parts = max_partitions ? max_partitions : 256;
   b->max_wait_us = max_wait_us;
   *out = b;

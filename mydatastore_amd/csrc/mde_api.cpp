@@ -12,6 +12,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -49,6 +50,7 @@ struct mde_ctx {
   int digest_cap = kDefaultDigestCap;
   int digest_oversub = kDefaultDigestOversub;
   uint64_t digest_piece_bytes = kAutoPieceBytes;
+  bool direct_out = true;  // packed host calls: kernels store write-once outputs into pinned memory
   char arch[64] = {0};
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
@@ -171,29 +173,43 @@ constexpr uint64_t kPackedCallMax = 8ull << 20;
 // outputs (host destination, bytes), then upload() -> launch on dev_in/dev_out -> download().
 // Packed calls use the context's packed_* / pin_* regions; larger ones one stage[] buffer per
 // piece (inputs first, then outputs) with direct copies. A NULL host pointer skips its copy.
+// An output declared write_once (the launch stores each of its bytes at most once and never reads
+// it back, no atomics) is, in a packed call, stored by the kernels straight into the pinned
+// staging area: no D2H copy for it, and none at all when every output is write-once -- a D2H copy
+// above ~16 KB otherwise starts ~11 us after the kernel ends (profiles/r03q_call_trace.txt).
 class HostIo {
  public:
   explicit HostIo(mde_ctx* c) : c_(c) {}
   int in(const void* src, uint64_t copy_bytes, uint64_t dev_bytes) {
-    pieces_[n_] = {const_cast<void*>(src), copy_bytes, dev_bytes, pin_.add(dev_bytes), true};
+    pieces_[n_] = {const_cast<void*>(src), copy_bytes, dev_bytes, pin_.add(dev_bytes), true, false};
     return n_++;
   }
-  int out(void* dst, uint64_t bytes) {
-    pieces_[n_] = {dst, bytes, bytes, pout_.add(bytes), false};
+  int out(void* dst, uint64_t bytes, bool write_once = false) {
+    const bool direct = write_once && c_->direct_out;
+    pieces_[n_] = {dst, bytes, bytes, (direct ? pdir_ : pcopy_).add(bytes), false, direct};
     return n_++;
   }
   void* dev(int i) const { return dev_[i]; }
   int upload() {
-    packed_ = pin_.total <= kPackedCallMax && pout_.total <= kPackedCallMax;
+    const uint64_t out_total = pcopy_.total + pdir_.total;
+    packed_ = pin_.total <= kPackedCallMax && out_total <= kPackedCallMax;
     int rc;
     if (packed_) {
-      if ((rc = ensure_buf(c_, c_->packed_in, pin_.total)) || (rc = ensure_buf(c_, c_->packed_out, pout_.total)) ||
-          (rc = ensure_pinned(c_, c_->pin_in, pin_.total)) || (rc = ensure_pinned(c_, c_->pin_out, pout_.total)))
+      if ((rc = ensure_buf(c_, c_->packed_in, pin_.total)) || (rc = ensure_buf(c_, c_->packed_out, out_total)) ||
+          (rc = ensure_pinned(c_, c_->pin_in, pin_.total)) || (rc = ensure_pinned(c_, c_->pin_out, out_total)))
         return rc;
+      void* out_dev = nullptr;
+      if (pdir_.total && hipHostGetDevicePointer(&out_dev, c_->pin_out.p, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        out_dev = nullptr;
+      }
+      copy_bytes_ = out_dev ? pcopy_.total : out_total;  // no mapping: every output is copied
       uint8_t* hi = static_cast<uint8_t*>(c_->pin_in.p);
       for (int i = 0; i < n_; i++) {
         const Piece& q = pieces_[i];
-        dev_[i] = static_cast<uint8_t*>(q.input ? c_->packed_in.p : c_->packed_out.p) + q.off;
+        if (q.input) dev_[i] = static_cast<uint8_t*>(c_->packed_in.p) + q.off;
+        else if (q.direct) dev_[i] = static_cast<uint8_t*>(out_dev ? out_dev : c_->packed_out.p) + pcopy_.total + q.off;
+        else dev_[i] = static_cast<uint8_t*>(c_->packed_out.p) + q.off;
         if (q.input && q.host && q.copy) std::memcpy(hi + q.off, q.host, q.copy);
       }
       MDE_HIP(c_, hipMemcpyAsync(c_->packed_in.p, hi, pin_.total, hipMemcpyHostToDevice, c_->stream));
@@ -211,11 +227,11 @@ class HostIo {
   int download() {
     if (packed_) {
       uint8_t* ho = static_cast<uint8_t*>(c_->pin_out.p);
-      MDE_HIP(c_, hipMemcpyAsync(ho, c_->packed_out.p, pout_.total, hipMemcpyDeviceToHost, c_->stream));
+      if (copy_bytes_) MDE_HIP(c_, hipMemcpyAsync(ho, c_->packed_out.p, copy_bytes_, hipMemcpyDeviceToHost, c_->stream));
       MDE_HIP(c_, hipStreamSynchronize(c_->stream));
       for (int i = 0; i < n_; i++) {
         const Piece& q = pieces_[i];
-        if (!q.input && q.host && q.copy) std::memcpy(q.host, ho + q.off, q.copy);
+        if (!q.input && q.host && q.copy) std::memcpy(q.host, ho + (q.direct ? pcopy_.total : 0) + q.off, q.copy);
       }
       return MDE_OK;
     }
@@ -232,13 +248,14 @@ class HostIo {
   struct Piece {
     void* host;
     uint64_t copy, dev, off;
-    bool input;
+    bool input, direct;
   };
   mde_ctx* c_;
+  uint64_t copy_bytes_ = 0;
   Piece pieces_[16];
   void* dev_[16] = {};
   int n_ = 0;
-  Pack pin_, pout_;
+  Pack pin_, pcopy_, pdir_;
   bool packed_ = false;
 };
 
@@ -763,6 +780,7 @@ int mde_create(int device, mde_ctx** out) {
     return MDE_E_DEVICE;
   }
   c->stream = c->own_stream;
+  if (const char* e = std::getenv("MDE_DIRECT_OUT")) c->direct_out = std::atoi(e) != 0;  // A/B switch
   *out = c;
   return MDE_OK;
 }
@@ -942,8 +960,11 @@ int mde_build(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   const int i_voff = io.in(r->value_off, nvo * 8, nvo * 8);
   const int i_seg = io.in(tagged ? r->part_rec : r->seg_rec, nseg, nseg);
   const int i_tag = io.in(r->bucket_tag, ntag, ntag);
-  const int o_dig = io.out(o->digest, S * 8), o_size = io.out(o->size, S * 4), o_items = io.out(o->items, P * 4);
-  const int o_root = io.out(o->root, P * 32), o_nodes = io.out(o->nodes, o->nodes ? P * NI * 32 : 0);
+  // every output is stored once by the tree pass (wider trees re-read their node levels)
+  const bool wo = r->n_buckets <= mde::kTreeLdsMaxBuckets;
+  const int o_dig = io.out(o->digest, S * 8, wo), o_size = io.out(o->size, S * 4, wo),
+            o_items = io.out(o->items, P * 4, wo);
+  const int o_root = io.out(o->root, P * 32, wo), o_nodes = io.out(o->nodes, o->nodes ? P * NI * 32 : 0, wo);
   if ((rc = io.upload())) return rc;
   mde_records dr = *r;
   dr.values = static_cast<const uint8_t*>(io.dev(i_val));
@@ -1517,9 +1538,13 @@ int mde_verify_epochs(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partiti
   const int i_nodes = io.in(nodes, nodes ? N * NI * 32 : 0, nodes ? N * NI * 32 : 0);
   const int i_peer = io.in(nbytes ? peer_bytes + peer_off[0] : nullptr, nbytes, nbytes + 1);
   const int i_rel = io.in(rel.data(), (T + 1) * 8, (T + 1) * 8);
-  const int o_valid = io.out(valid, N), o_vc = io.out(valid_count, N * 4), o_ids = io.out(diff_ids, N * B * 4);
-  const int o_dc = io.out(diff_count, N * 4), o_ps = io.out(T ? peer_status : nullptr, T * 4);
-  const int o_obj = io.out(object_out, N * ostride), o_olen = io.out(object_out ? object_len : nullptr, N * 4);
+  // valid and the peer statuses are read back inside the launch (the fold, the encode): device
+  // memory; the rest is stored once
+  const int o_valid = io.out(valid, N), o_vc = io.out(valid_count, N * 4, true),
+            o_ids = io.out(diff_ids, N * B * 4, true);
+  const int o_dc = io.out(diff_count, N * 4, true), o_ps = io.out(T ? peer_status : nullptr, T * 4);
+  const int o_obj = io.out(object_out, N * ostride, true),
+            o_olen = io.out(object_out ? object_len : nullptr, N * 4, true);
   int rc = io.upload();
   if (rc) return rc;
   // the spill area covers every object of this call (no rescans, whatever they nest)
