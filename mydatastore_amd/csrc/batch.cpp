@@ -130,6 +130,7 @@ struct mde_batcher {
   // copy; above ~16 KB such a copy starts ~11 us after the kernel, profiles/r03q_call_trace.txt);
   // MDE_DIRECT_OUT=0 turns it off (A/B)
   bool direct_out = true;
+  bool blocking_sync = false;  // MDE_BATCH_BLOCKING_SYNC=1: leaders sleep on their batch's event (A/B)
 };
 
 namespace {
@@ -243,12 +244,14 @@ void ctx_error(mde_ctx* c, const std::vector<Req*>& v, int rc) {
   fail_all(v, rc, m);
 }
 
-int grow_slot(mde_batcher::Slot* sl, uint64_t in_bytes, uint64_t d2h_bytes, uint64_t dev_out_bytes, std::string* msg) {
+int grow_slot(mde_batcher::Slot* sl, uint64_t in_bytes, uint64_t d2h_bytes, uint64_t dev_out_bytes, std::string* msg,
+              bool blocking) {
   int rc;
   if ((rc = grow(sl->pin_in, in_bytes, true, msg)) || (rc = grow(sl->dev_in, in_bytes, false, msg)) ||
       (rc = grow(sl->pin_out, d2h_bytes, true, msg)) || (rc = grow(sl->dev_out, dev_out_bytes, false, msg)))
     return rc;
-  if (!sl->done && hipEventCreateWithFlags(&sl->done, hipEventDisableTiming) != hipSuccess) {
+  if (!sl->done && hipEventCreateWithFlags(&sl->done, hipEventDisableTiming | (blocking ? hipEventBlockingSync : 0u)) !=
+                       hipSuccess) {
     sl->done = nullptr;
     *msg = "hipEventCreate failed";
     return MDE_E_DEVICE;
@@ -295,7 +298,7 @@ void launch_build(mde_batcher* b, Batch* bt) {
   bt->B = B;
   bt->NI = NI;
   std::string msg;
-  const int rc = grow_slot(bt->slot, in_bytes, out_bytes, out_bytes, &msg);
+  const int rc = grow_slot(bt->slot, in_bytes, out_bytes, out_bytes, &msg, b->blocking_sync);
   if (rc) {
     fail_all(v, rc, msg);
     return;
@@ -420,7 +423,7 @@ void launch_verify(mde_batcher* b, Batch* bt) {
   bt->stride = stride;
   bt->R = R;
   std::string msg;
-  const int grc = grow_slot(bt->slot, in_bytes, o[7], out_bytes, &msg);
+  const int grc = grow_slot(bt->slot, in_bytes, o[7], out_bytes, &msg, b->blocking_sync);
   if (grc) {
     fail_all(v, grc, msg);
     return;
@@ -613,6 +616,7 @@ int mde_batcher_create(int device, uint32_t max_partitions, uint32_t max_wait_us
   }
   b->device = device;
   if (const char* e = std::getenv("MDE_DIRECT_OUT")) b->direct_out = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MDE_BATCH_BLOCKING_SYNC")) b->blocking_sync = std::atoi(e) != 0;
   b->max_parts = max_partitions ? max_partitions : 256;
   b->max_wait_us = max_wait_us;
   *out = b;
