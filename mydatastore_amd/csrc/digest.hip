@@ -826,10 +826,32 @@ __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a)
 // wave per workgroup up to B = 128, the rest exit at once), so the SHA waves spread over many
 // CUs instead of crowding a few; tree workgroups come first so the dispatcher places them before
 // the streaming grid (sized to be fully resident) fills the remaining slots.
+#ifdef MDE_STEP_STAMPS  // probe only: first start / last end (s_memrealtime) of the tree and stream waves
+__device__ unsigned long long g_step_stamps[4];
+__device__ __forceinline__ void step_stamp(int role, unsigned long long t0) {
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&g_step_stamps[2 * role], t0);
+    atomicMax(&g_step_stamps[2 * role + 1], t1);
+  }
+}
+#endif
+
 template <int U, bool NT, int PIPE, int PRIO = 0, int MODE = 0>
 __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, TreeLaunch t, uint32_t tree_blocks,
                                                               uint32_t Q) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+#ifdef MDE_STEP_STAMPS
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  if (blockIdx.x < tree_blocks) {
+    step_trees(t, Q, blockIdx.x, lds);
+    step_stamp(0, t0);
+    return;
+  }
+  digest_dispatch<U, NT, PIPE, PRIO, MODE, false>(a, blockIdx.x - tree_blocks, lds);
+  step_stamp(1, t0);
+  return;
+#endif
 #ifdef MDE_STEP_TREES_LAST
   const uint32_t digest_blocks = gridDim.x - tree_blocks;
   if (blockIdx.x >= digest_blocks) {
@@ -1104,3 +1126,14 @@ hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStre
 }
 
 }  // namespace mde
+
+#ifdef MDE_STEP_STAMPS
+extern "C" int mde_probe_step_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mde::g_step_stamps), sizeof(unsigned long long) * 4) != hipSuccess) return -1;
+  if (reset) {
+    const unsigned long long init[4] = {~0ull, 0ull, ~0ull, 0ull};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(mde::g_step_stamps), init, sizeof init) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif

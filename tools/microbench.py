@@ -238,6 +238,38 @@ def bench_fused_only(eng, shape, reps=5):
     return r
 
 
+def bench_step_stamps(eng, shape, reps=8):
+    """Probe library only (-DMDE_STEP_STAMPS): per fused build step, when the first / last tree
+    wave and the first / last streaming wave started and ended (s_memrealtime, 100 MHz), relative
+    to the first streaming wave's start, in us."""
+    import ctypes as C
+    import torch
+    from mydatastore_amd.workload import make_workload
+    fn = eng.lib.mde_probe_step_stamps
+    fn.argtypes = [C.c_void_p, C.c_int]
+    buf = (C.c_ulonglong * 4)()
+    w = make_workload(eng, **{"n_buckets": 64, "value_len": 1024, "rank": 0, **SHAPES[shape]})
+    sets = [w._outs() for _ in range(2)]
+    rows = []
+    for i in range(reps + 2):
+        torch.cuda.synchronize()
+        fn(buf, 1)
+        eng.build_pipelined_async(w.rec, sets[i % 2][1])
+        torch.cuda.synchronize()
+        fn(buf, 0)
+        t = list(buf)
+        if i < 2:
+            continue
+        z = t[2]
+        r = {"shape": shape, "tree_start_us": round((t[0] - z) / 100, 2), "tree_end_us": round((t[1] - z) / 100, 2),
+             "stream_end_us": round((t[3] - z) / 100, 2)}
+        rows.append(r)
+        print(json.dumps(r), flush=True)
+    eng.build_pipeline_drain_async()
+    torch.cuda.synchronize()
+    return rows
+
+
 def bench_verify(eng, P=1024, B=64, R=2, mode=0):
     """VerifyEpoch decision step (mde_verify_epochs) for P partitions x R peer objects: peer 0
     agrees, peer 1 differs in one bucket. Device-resident call timed with HIP events; the
@@ -346,6 +378,8 @@ def main():
             parts = w.split(":")
             shapes = tuple(parts[2].split(",")) if len(parts) > 2 else ("c4", "c4/8", "c3")
             out["pieces"] = bench_pieces(eng, parts[1].split(","), shapes)
+        if w.startswith("stamps:"):  # stamps:ts8k -- probe library only
+            out["stamps"] = bench_step_stamps(eng, w.split(":")[1])
         if w.startswith("digestonly:"):  # digestonly:ts8k[:reps] -- the digest kernel alone (PMC runs)
             parts = w.split(":")
             out["digestonly"] = bench_digest_only(eng, parts[1], int(parts[2]) if len(parts) > 2 else 5,
