@@ -447,6 +447,13 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
   const SegDesc& d = a.seg;
   uint32_t* R = lds;               // record sums, then exclusive local prefixes (swizzled)
   uint32_t* E = lds + kRec8Sums;   // lane exclusive prefixes; E[64] = the step's total
+  // beg / end stay where the compiler puts them (VGPRs: they derive from threadIdx.x >> 6), so the
+  // resource below is a VGPR quadruple and every buffer load runs as a one-iteration readfirstlane
+  // loop. Moving them to SGPRs was measured (r03): the digest alone unchanged (134-139 us at 8-byte
+  // values, B = 1,000), the fused build step SLOWER, 174-176 -> 187-191 us per build -- the slower
+  // issue of the stream leaves SIMD cycles to the co-resident tree waves, whose dependent SHA-256
+  // chain bounds that step; a deliberate s_sleep per scan step or priority 0 did not do as well
+  // (profiles/r03y_rec8_scalar_ab.txt, r03z_rec8_throttle_ab.txt).
   const uint64_t span = ((end - beg) + 15) & ~15ull;  // <= kMaxWaveBytes
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)(d.base + beg), (short)0, (int)span, 0x00020000);
