@@ -878,6 +878,11 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
   digest_dispatch<U, NT, PIPE, PRIO, MODE, false>(a, db, lds);
 }
 
+// First LDS word of the small build's bucket sums (after `groups` tree regions, 16-byte aligned).
+__host__ __device__ __forceinline__ uint32_t small_build_sums_word(uint32_t groups, uint32_t words) {
+  return (groups * words + 3u) & ~3u;
+}
+
 // One-launch build of small arenas (the synchronous one-partition calls of VerifyEpoch, and the
 // batcher's many small partitions, mde_batch_build). Workgroup b owns partitions
 // [b * groups, (b + 1) * groups) (groups = 256 / G trees per workgroup, tree_body's shape): digest
@@ -890,10 +895,13 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
 __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLaunch t, uint32_t G, uint32_t words) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const u32x4* base = reinterpret_cast<const u32x4*>(d.base);
-  unsigned long long* sums = const_cast<unsigned long long*>(t.sums_in);  // zero on entry
   const uint32_t groups = (uint32_t)kThreads / G;
   const uint32_t s_beg = min(blockIdx.x * groups * t.B, d.S), s_end = min((blockIdx.x + 1) * groups * t.B, d.S);
   const uint32_t nb = s_end - s_beg;
+  // this workgroup's bucket sums live in LDS after the tree levels (no global atomics, no fence)
+  unsigned long long* sums = reinterpret_cast<unsigned long long*>(lds + small_build_sums_word(groups, words));
+  for (uint32_t i = threadIdx.x; i < nb; i += kThreads) sums[i] = 0ull;
+  __syncthreads();
   // K threads per bucket (K = 256 / nb rounded down to a power of two, >= 1), each taking every
   // K-th 16-byte vector of the bucket, four loads in flight
   uint32_t K = 1;
@@ -916,11 +924,14 @@ __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLa
     }
     for (; x < hi; x += 16ull * K)
       acc = masked_sum16(__builtin_nontemporal_load(base + (x >> 4)), l - (int64_t)x, h - (int64_t)x, acc);
-    if (acc) atomicAdd(sums + s, (unsigned long long)acc);
+    if (acc) atomicAdd(sums + (s - s_beg), (unsigned long long)acc);
   }
-  __threadfence();  // the sums are visible before any wave reads them
   __syncthreads();
-  tree_body<true>(t, G, words, blockIdx.x, lds, kThreads);
+  TreeLaunch tl = t;
+  tl.sums_in = sums;
+  tl.sums_clear = nullptr;
+  tl.sums_base = s_beg;
+  tree_body<true>(tl, G, words, blockIdx.x, lds, kThreads);
 }
 
 typedef void (*DigestKernel)(DigestLaunch);
@@ -971,7 +982,7 @@ hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t
   TreeGeometry g;
   tree_geometry(t.B, &g);
   const uint32_t groups = (uint32_t)kThreads / g.G;
-  const size_t lds = (size_t)g.words * 4u * groups;
+  const size_t lds = (size_t)small_build_sums_word(groups, g.words) * 4u + (size_t)groups * t.B * 8u;
   hipLaunchKernelGGL(small_build_kernel, dim3((t.P + groups - 1) / groups), dim3(kThreads), lds, st, d, t, g.G,
                      g.words);
   return hipGetLastError();

@@ -110,6 +110,9 @@ struct TreeLaunch {
   // n_in[p] <= B buckets at digest_in + p*B (n_in[p] <= 0: no tree, nothing written); its nodes
   // use its own shape at stride n_int (= tree_internal(B)). Null: every tree has B buckets.
   const int32_t* n_in;
+  // sums_in / sums_clear hold buckets [sums_base, ...) (the one-launch small build keeps each
+  // workgroup's bucket sums in LDS)
+  uint64_t sums_base = 0;
 };
 constexpr uint32_t kTreeLdsMaxBuckets = 4096;
 constexpr uint32_t kTreePairLdsMax = 64u * 1024u;  // standalone pair-shape trees (B <= 2,728)
@@ -137,8 +140,8 @@ constexpr uint32_t kStepTreeWideThreads = 128;
 constexpr uint32_t kStepTreeWideMinPartitions = 512;
 void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint32_t* lds_bytes);
 hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st);
-// One-launch build of a small layout-A arena (digest.hip small_build_kernel); t.sums_in is the
-// (zeroed) scratch the digest phase writes and the tree phase reads and clears.
+// One-launch build of a small layout-A arena (digest.hip small_build_kernel): each workgroup sums
+// its partitions' buckets into LDS and builds their trees from there (t.sums_in is not used).
 constexpr uint64_t kSmallBuildMaxBytes = 96u * 1024u;
 bool small_build_fits(uint64_t bytes, uint32_t P, uint32_t B);
 hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t st);

@@ -35,8 +35,8 @@ __device__ __forceinline__ void store_node(uint32_t* dst, const uint32_t st[8]) 
 __device__ __forceinline__ uint64_t tree_leaf(const TreeLaunch& a, uint64_t s, uint32_t& items, uint32_t& sz_out) {
   uint64_t v;
   if (a.sums_in) {
-    v = (uint64_t)(a.sums_in[s] % kHashMod);
-    if (a.sums_clear) a.sums_clear[s] = 0ull;
+    v = (uint64_t)(a.sums_in[s - a.sums_base] % kHashMod);
+    if (a.sums_clear) a.sums_clear[s - a.sums_base] = 0ull;
   } else {
     v = a.digest_in[s];
   }
