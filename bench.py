@@ -85,6 +85,8 @@ def parse():
                          "config 4 as stated: 10M keys over 1024 partitions in all, partition p on "
                          "rank p %% N); weak: every rank holds the config's full workload (N x the "
                          "partitions and keys in all)")
+    ap.add_argument("--no-production-shape", action="store_true",
+                    help="N = 1: skip the 8-byte-timestamp, B = 1000 line (production_shape)")
     ap.add_argument("--no-gather-per-build", action="store_true",
                     help="N > 1: skip the second timed run with one root-gather collective per build")
     return ap.parse_args()
@@ -191,6 +193,58 @@ def pmc_traffic(config_name: str, local_bytes: int):
     except Exception:
         return None
     return None
+
+
+# The reference's production value shape (not a BASELINE config): every epoch-index record's value
+# is the 8-byte LE write timestamp (main/manager.go:816), at partition_buckets = 1000
+# (config/default-config.yaml:10); 100M of them over 1,024 partitions = 800 MB.
+PROD_SHAPE = (100_000_000, 1024, 8, 1000, "mod", "8-byte LE timestamps x 100M, 1024 partitions, B=1000")
+
+
+def production_shape(torch, eng, dev, threads, reps=10):
+    """Steady-state fused pipelined builds of PROD_SHAPE on this device (HIP events; a run of 2n
+    builds minus a run of n, so the drain's tree launch cancels), the standalone digest kernel, and
+    the C-oracle check of a sample of the last build. Reported beside `value`, never as it."""
+    from mydatastore_amd.workload import make_workload
+    n_keys, P, V, B, mode, desc = PROD_SHAPE
+    w = make_workload(eng, n_partitions=P, n_buckets=B, value_len=V, part_mode=mode, n_keys=n_keys, rank=0, world=1)
+    sets = [w._outs() for _ in range(2)]
+    st = torch.cuda.current_stream(dev)
+
+    def run(n):
+        for i in range(n):
+            eng.build_pipelined_async(w.rec, sets[i % 2][1])
+        eng.build_pipeline_drain_async()
+
+    def timed(fn):
+        fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        fn()
+        b.record(st)
+        torch.cuda.synchronize(dev)
+        return a.elapsed_time(b) * 1e3  # us
+
+    t1, t2 = timed(lambda: run(reps)), timed(lambda: run(2 * reps))
+    fused_us = (t2 - t1) / reps
+    digest_us = timed(lambda: [w.digest_async() for _ in range(reps)]) / reps
+    run(1)  # the last build's outputs in set 0
+    torch.cuda.synchronize(dev)
+    co, _, _, s_n, ref = oracle_sample(PROD_SHAPE, list(range(P)), threads)
+    got = {k: sets[0][0][k].cpu().numpy() for k in ("digest", "size", "root")}
+    ok = (np.array_equal(got["digest"][:s_n * B].view(np.uint64), ref["digest"]) and
+          np.array_equal(got["size"][:s_n * B], ref["size"]) and np.array_equal(got["root"][:s_n * 32], ref["root"]))
+    res = {"workload": desc, "bytes": w.value_bytes,
+           "fused_us_per_build": round(fused_us, 2), "fused_frac": round(w.value_bytes / fused_us / 1e3 / HBM_PEAK_GBS, 4),
+           "digest_kernel_us": round(digest_us, 2),
+           "digest_frac": round(w.value_bytes / digest_us / 1e3 / HBM_PEAK_GBS, 4),
+           "oracle_sample_partitions": int(s_n), "equals_c_oracle_on_sample": bool(ok),
+           "note": "steady state of mde_build_pipelined_async (this build's digest + the previous build's "
+                   "1,024 trees of 1,000 leaves per launch); bound by the trees' dependent SHA-256 chain "
+                   "(DESIGN.md section 4.1)"}
+    del w, sets
+    torch.cuda.empty_cache()
+    return res
 
 
 def end_to_end(torch, eng, w, B, reps=3):
@@ -693,6 +747,8 @@ def main():
             result["cpu_baseline"] = None
         if world == 1 and not args.no_e2e and not args.profile and not c5:
             result["end_to_end"] = end_to_end(torch, eng, w, B)
+        if world == 1 and not args.no_production_shape and not args.profile and not c5 and args.layout == "a":
+            result["production_shape"] = production_shape(torch, eng, dev, threads)
         print(json.dumps(result), flush=True)
     if use_dist:
         dist.barrier()
