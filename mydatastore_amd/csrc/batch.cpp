@@ -75,6 +75,7 @@ struct Req {
   uint64_t err_cap = 0;
   bool done = false;
   bool lead = false;  // handed the leader role for the next batch
+  std::chrono::steady_clock::time_point lead_t;  // when it was handed the role (MDE_BATCH_PROFILE)
   std::condition_variable cv;
 };
 
@@ -131,6 +132,10 @@ struct mde_batcher {
   // MDE_DIRECT_OUT=0 turns it off (A/B)
   bool direct_out = true;
   bool blocking_sync = false;  // MDE_BATCH_BLOCKING_SYNC=1: leaders sleep on their batch's event (A/B)
+  // MDE_BATCH_PROFILE=1: host-side phase times summed over batches, printed by mde_batcher_destroy
+  bool profile = false;
+  double t_handoff = 0, t_stage = 0, t_device = 0, t_scatter = 0;
+  uint64_t n_handoff = 0;
 };
 
 namespace {
@@ -514,6 +519,7 @@ void handoff(mde_batcher* b) {
     if (!sl.busy) {
       Req* x = b->q.front();
       x->lead = true;
+      if (b->profile) x->lead_t = std::chrono::steady_clock::now();
       x->cv.notify_one();
       return;
     }
@@ -547,19 +553,30 @@ void lead(mde_batcher* b, std::unique_lock<std::mutex>& lk) {
   b->n_requests += bt.v.size();
   b->n_partitions += parts;
   lk.unlock();
+  using clk = std::chrono::steady_clock;
+  const clk::time_point t0 = b->profile ? clk::now() : clk::time_point{};
   if (bt.v[0]->kind == Kind::Build) launch_build(b, &bt);
   else launch_verify(b, &bt);
   lk.lock();
   b->leading = false;
   handoff(b);  // the next batch stages and launches while this one runs on the device
   lk.unlock();
+  const clk::time_point t1 = b->profile ? clk::now() : clk::time_point{};
+  clk::time_point t2 = t1;
   if (bt.launched) {
     const hipError_t e = hipEventSynchronize(bt.slot->done);
+    if (b->profile) t2 = clk::now();
     if (e != hipSuccess) fail_all(bt.v, MDE_E_DEVICE, std::string("batch: ") + hipGetErrorString(e));
     else if (bt.v[0]->kind == Kind::Build) scatter_build(&bt);
     else scatter_verify(&bt);
   }
   lk.lock();
+  if (b->profile) {
+    const clk::time_point t3 = clk::now();
+    b->t_stage += std::chrono::duration<double>(t1 - t0).count();
+    b->t_device += std::chrono::duration<double>(t2 - t1).count();
+    b->t_scatter += std::chrono::duration<double>(t3 - t2).count();
+  }
   bt.slot->busy = false;
   for (Req* x : bt.v) {
     x->done = true;
@@ -588,7 +605,13 @@ int submit(mde_batcher* b, Req* r) {
       for (auto& sl : b->slots) free_slot |= !sl.busy;
       // the role may have gone stale (another caller took it, the queue drained, no free slot):
       // then wait for a handoff or for this request to finish in someone else's batch
-      if (!b->leading && free_slot && !b->q.empty()) lead(b, lk);
+      if (!b->leading && free_slot && !b->q.empty()) {
+        if (b->profile && r->lead_t != std::chrono::steady_clock::time_point{}) {
+          b->t_handoff += std::chrono::duration<double>(std::chrono::steady_clock::now() - r->lead_t).count();
+          b->n_handoff++;
+        }
+        lead(b, lk);
+      }
       continue;
     }
     r->cv.wait(lk);
@@ -617,6 +640,7 @@ int mde_batcher_create(int device, uint32_t max_partitions, uint32_t max_wait_us
   b->device = device;
   if (const char* e = std::getenv("MDE_DIRECT_OUT")) b->direct_out = std::atoi(e) != 0;
   if (const char* e = std::getenv("MDE_BATCH_BLOCKING_SYNC")) b->blocking_sync = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MDE_BATCH_PROFILE")) b->profile = std::atoi(e) != 0;
   b->max_parts = max_partitions ? max_partitions : 256;
   b->max_wait_us = max_wait_us;
   *out = b;
@@ -625,6 +649,13 @@ int mde_batcher_create(int device, uint32_t max_partitions, uint32_t max_wait_us
 
 void mde_batcher_destroy(mde_batcher* b) {
   if (!b) return;
+  if (b->profile && b->n_batches)
+    std::fprintf(stderr,
+                 "{\"batcher_profile\": {\"batches\": %llu, \"requests\": %llu, \"stage_launch_us\": %.2f, "
+                 "\"device_wait_us\": %.2f, \"scatter_wake_us\": %.2f, \"handoffs\": %llu, \"handoff_us\": %.2f}}\n",
+                 (unsigned long long)b->n_batches, (unsigned long long)b->n_requests, 1e6 * b->t_stage / b->n_batches,
+                 1e6 * b->t_device / b->n_batches, 1e6 * b->t_scatter / b->n_batches, (unsigned long long)b->n_handoff,
+                 b->n_handoff ? 1e6 * b->t_handoff / b->n_handoff : 0.0);
   (void)hipSetDevice(b->device);
   for (auto& sl : b->slots) {
     (void)mde_synchronize(sl.ctx);

@@ -882,6 +882,16 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
 __host__ __device__ __forceinline__ uint32_t small_build_sums_word(uint32_t groups, uint32_t words) {
   return (groups * words + 3u) & ~3u;
 }
+// Partitions per small-build workgroup: 256 / G, or in the split-schedule form 128 / G (a wide
+// tree, G = 256: one).
+__host__ __device__ __forceinline__ uint32_t small_build_groups(uint32_t G, bool duo) {
+  const uint32_t half = (uint32_t)kThreads / 2;
+  return duo ? (G > half ? 1u : half / G) : (uint32_t)kThreads / G;
+}
+// First LDS word of the split-schedule K+W slots (after the bucket sums, 16-byte aligned).
+__host__ __device__ __forceinline__ uint32_t small_build_kw_word(uint32_t groups, uint32_t words, uint32_t B) {
+  return (small_build_sums_word(groups, words) + groups * B * 2u + 3u) & ~3u;
+}
 
 // One-launch build of small arenas (the synchronous one-partition calls of VerifyEpoch, and the
 // batcher's many small partitions, mde_batch_build). Workgroup b owns partitions
@@ -892,10 +902,13 @@ __host__ __device__ __forceinline__ uint32_t small_build_sums_word(uint32_t grou
 // fence and a barrier, the same workgroup builds those partitions' trees with tree_body. Every
 // bucket is summed by exactly one workgroup, so no cross-workgroup synchronisation is needed; it
 // saves the second launch of the digest + tree pair.
+// kDuo: the trees run split-schedule (tree_body_duo, the latency form) with the workgroup's upper
+// half as schedule helpers, so a workgroup holds half as many partitions of B <= 128 buckets.
+template <bool kDuo>
 __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLaunch t, uint32_t G, uint32_t words) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const u32x4* base = reinterpret_cast<const u32x4*>(d.base);
-  const uint32_t groups = (uint32_t)kThreads / G;
+  const uint32_t groups = small_build_groups(G, kDuo);
   const uint32_t s_beg = min(blockIdx.x * groups * t.B, d.S), s_end = min((blockIdx.x + 1) * groups * t.B, d.S);
   const uint32_t nb = s_end - s_beg;
   // this workgroup's bucket sums live in LDS after the tree levels (no global atomics, no fence)
@@ -906,12 +919,33 @@ __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLa
   // K-th 16-byte vector of the bucket, four loads in flight
   uint32_t K = 1;
   while (K * 2 * nb <= (uint32_t)kThreads) K *= 2;
-  const uint32_t j = threadIdx.x % K;
-  for (uint32_t s = s_beg + threadIdx.x / K; s < s_end; s += kThreads / K) {
-    const uint64_t lo = segpos(d, s), hi = segpos(d, s + 1);
+  // kSmallRounds buckets per thread at a time: their boundaries, then the first vector of each, are
+  // loaded together (one dependent load pair per bucket in turn cost ~7 us of a B = 1,000 call)
+  constexpr int kSmallRounds = 4;
+  const uint32_t j = threadIdx.x % K, step = (uint32_t)kThreads / K;
+  for (uint32_t s0 = s_beg + threadIdx.x / K; s0 < s_end; s0 += kSmallRounds * step) {
+    uint64_t los[kSmallRounds], his[kSmallRounds];
+#pragma unroll
+    for (int i = 0; i < kSmallRounds; i++) {
+      const uint32_t s = s0 + i * step;
+      const bool in = s < s_end;
+      los[i] = in ? segpos(d, s) : 0ull;
+      his[i] = in ? segpos(d, s + 1) : 0ull;
+    }
+    u32x4 firsts[kSmallRounds];
+#pragma unroll
+    for (int i = 0; i < kSmallRounds; i++) {
+      const uint64_t x = (los[i] & ~15ull) + 16ull * j;
+      firsts[i] = x < his[i] ? __builtin_nontemporal_load(base + (x >> 4)) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int i = 0; i < kSmallRounds; i++) {
+    const uint32_t s = s0 + i * step;
+    const uint64_t lo = los[i], hi = his[i];
     const int64_t l = (int64_t)lo, h = (int64_t)hi;
-    uint32_t acc = 0;
     uint64_t x = (lo & ~15ull) + 16ull * j;
+    uint32_t acc = x < hi ? masked_sum16(firsts[i], l - (int64_t)x, h - (int64_t)x, 0u) : 0u;
+    x += 16ull * K;
     for (; x + 48ull * K < hi; x += 64ull * K) {
       const u32x4 v0 = __builtin_nontemporal_load(base + (x >> 4));
       const u32x4 v1 = __builtin_nontemporal_load(base + ((x + 16ull * K) >> 4));
@@ -925,13 +959,19 @@ __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLa
     for (; x < hi; x += 16ull * K)
       acc = masked_sum16(__builtin_nontemporal_load(base + (x >> 4)), l - (int64_t)x, h - (int64_t)x, acc);
     if (acc) atomicAdd(sums + (s - s_beg), (unsigned long long)acc);
+    }
   }
   __syncthreads();
   TreeLaunch tl = t;
   tl.sums_in = sums;
   tl.sums_clear = nullptr;
   tl.sums_base = s_beg;
-  tree_body<true>(tl, G, words, blockIdx.x, lds, kThreads);
+  if (kDuo) {
+    u32x4* kw = reinterpret_cast<u32x4*>(lds + small_build_kw_word(groups, words, t.B));
+    tree_body_duo(tl, G, words, blockIdx.x, lds, (uint32_t)kThreads / 2, kw);
+  } else {
+    tree_body<true>(tl, G, words, blockIdx.x, lds, kThreads);
+  }
 }
 
 typedef void (*DigestKernel)(DigestLaunch);
@@ -981,10 +1021,21 @@ bool small_build_fits(uint64_t bytes, uint32_t P, uint32_t B) {
 hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t st) {
   TreeGeometry g;
   tree_geometry(t.B, &g);
-  const uint32_t groups = (uint32_t)kThreads / g.G;
-  const size_t lds = (size_t)small_build_sums_word(groups, g.words) * 4u + (size_t)groups * t.B * 8u;
-  hipLaunchKernelGGL(small_build_kernel, dim3((t.P + groups - 1) / groups), dim3(kThreads), lds, st, d, t, g.G,
-                     g.words);
+  // Split-schedule trees (latency form) unless that would take more than kDuoMaxBlocks
+  // workgroups: a wide tree has one workgroup per partition either way; narrower trees pack half
+  // as many partitions per workgroup.
+  const uint32_t groups_duo = small_build_groups(g.G, true);
+  const uint32_t blocks_duo = (t.P + groups_duo - 1) / groups_duo;
+  const bool duo = tree_duo_enabled() && (g.G > (uint32_t)kThreads / 2 || blocks_duo <= kDuoMaxBlocks);
+  const uint32_t groups = small_build_groups(g.G, duo);
+  const uint32_t blocks = (t.P + groups - 1) / groups;
+  if (duo) {
+    const size_t lds = (size_t)small_build_kw_word(groups, g.words, t.B) * 4u + duo_kw_bytes((uint32_t)kThreads / 2);
+    hipLaunchKernelGGL(small_build_kernel<true>, dim3(blocks), dim3(kThreads), lds, st, d, t, g.G, g.words);
+  } else {
+    const size_t lds = (size_t)small_build_sums_word(groups, g.words) * 4u + (size_t)groups * t.B * 8u;
+    hipLaunchKernelGGL(small_build_kernel<false>, dim3(blocks), dim3(kThreads), lds, st, d, t, g.G, g.words);
+  }
   return hipGetLastError();
 }
 

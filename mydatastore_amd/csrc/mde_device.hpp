@@ -145,6 +145,93 @@ __device__ __forceinline__ void sha256_compress_pad64(uint32_t st[8]) {
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
+// ---- Split-schedule node hash (latency form, tree_body_duo) ----
+// One wave issues at most one VALU instruction per ~4.6 cycles, so a lone dependent chain costs its
+// instruction count: the data block of SHA256(hl || hr) is 64 rounds of ~15 instructions plus 48
+// schedule words of ~10. Here a compute thread runs only the rounds; its mirror thread, in another
+// wave of the workgroup, computes W16..63 (pre-added to K) and hands them over through LDS in three
+// 16-word chunks, each published behind a workgroup barrier four rounds before the compute thread
+// needs it (the LDS read latency hides under those four rounds). Both sides execute exactly three
+// barriers per node, so every wave of the workgroup must call one side or the other (or
+// duo_idle()) the same number of times. kw: this thread's slot of a [12][stride] u32x4 array
+// (chunk c of 16 words = slots 4c .. 4c+3).
+#define MDE_SHA_4A(KW)                                     \
+  MDE_SHA_ROUND(a, b, c, d, e, f, g, h, KW(0));            \
+  MDE_SHA_ROUND(h, a, b, c, d, e, f, g, KW(1));            \
+  MDE_SHA_ROUND(g, h, a, b, c, d, e, f, KW(2));            \
+  MDE_SHA_ROUND(f, g, h, a, b, c, d, e, KW(3))
+#define MDE_SHA_4B(KW)                                     \
+  MDE_SHA_ROUND(e, f, g, h, a, b, c, d, KW(0));            \
+  MDE_SHA_ROUND(d, e, f, g, h, a, b, c, KW(1));            \
+  MDE_SHA_ROUND(c, d, e, f, g, h, a, b, KW(2));            \
+  MDE_SHA_ROUND(b, c, d, e, f, g, h, a, KW(3))
+
+__device__ __forceinline__ void sha256_node_duo_main(const uint32_t hl[8], const uint32_t hr[8], uint32_t st[8],
+                                                     const u32x4* kw, uint32_t stride) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) { w[i] = hl[i]; w[8 + i] = hr[i]; }
+  sha256_init(st);
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#define MDE_KWM0(j) (kK[0 + (j)] + w[0 + (j)])
+#define MDE_KWM4(j) (kK[4 + (j)] + w[4 + (j)])
+#define MDE_KWM8(j) (kK[8 + (j)] + w[8 + (j)])
+#define MDE_KWM12(j) (kK[12 + (j)] + w[12 + (j)])
+#define MDE_KWV0(j) (v0[(j)])
+#define MDE_KWV1(j) (v1[(j)])
+#define MDE_KWV2(j) (v2[(j)])
+#define MDE_KWP3(j) (p3[(j)])
+  MDE_SHA_4A(MDE_KWM0);
+  MDE_SHA_4B(MDE_KWM4);
+  MDE_SHA_4A(MDE_KWM8);
+  u32x4 p3 = {0u, 0u, 0u, 0u};  // K+W of the previous chunk's last four rounds
+#pragma unroll
+  for (int cn = 0; cn < 3; cn++) {
+    __syncthreads();  // chunk cn = K+W of rounds 16(cn+1) .. 16(cn+1)+15 is in LDS
+    const u32x4 v0 = kw[(4 * cn + 0) * stride], v1 = kw[(4 * cn + 1) * stride];
+    const u32x4 v2 = kw[(4 * cn + 2) * stride], v3 = kw[(4 * cn + 3) * stride];
+    if (cn == 0) {
+      MDE_SHA_4B(MDE_KWM12);
+    } else {
+      MDE_SHA_4B(MDE_KWP3);
+    }
+    MDE_SHA_4A(MDE_KWV0);
+    MDE_SHA_4B(MDE_KWV1);
+    MDE_SHA_4A(MDE_KWV2);
+    p3 = v3;
+  }
+  MDE_SHA_4B(MDE_KWP3);
+#undef MDE_KWM0
+#undef MDE_KWM4
+#undef MDE_KWM8
+#undef MDE_KWM12
+#undef MDE_KWV0
+#undef MDE_KWV1
+#undef MDE_KWV2
+#undef MDE_KWP3
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+  sha256_compress_pad64(st);
+}
+
+// The mirror side: the message schedule of the same node, published chunk by chunk.
+__device__ __forceinline__ void sha256_node_duo_sched(const uint32_t hl[8], const uint32_t hr[8], u32x4* kw,
+                                                      uint32_t stride) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) { w[i] = hl[i]; w[8 + i] = hr[i]; }
+#pragma unroll
+  for (int cn = 0; cn < 3; cn++) {
+    sha_sched16(w);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int r = 16 * (cn + 1) + 4 * q;
+      kw[(4 * cn + q) * stride] = u32x4{kK[r] + w[4 * q], kK[r + 1] + w[4 * q + 1], kK[r + 2] + w[4 * q + 2],
+                                        kK[r + 3] + w[4 * q + 3]};
+    }
+    __syncthreads();
+  }
+}
+
 // Level-1 node: SHA256(LE64(dl) || LE64(dr)) -> state words (big-endian digest words).
 __device__ __forceinline__ void sha256_leaf_pair(uint64_t dl, uint64_t dr, uint32_t st[8]) {
   uint32_t w[16];

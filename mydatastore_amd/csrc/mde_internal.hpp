@@ -118,6 +118,10 @@ constexpr uint32_t kTreeLdsMaxBuckets = 4096;
 constexpr uint32_t kTreePairLdsMax = 64u * 1024u;  // standalone pair-shape trees (B <= 2,728)
 constexpr uint32_t kTreePairMinPartitions = 512;
 hipError_t launch_tree(const TreeLaunch& a, hipStream_t st);
+// Split-schedule trees (tree_body_duo) for launches of at most kDuoMaxBlocks workgroups (wide
+// trees: always); MDE_TREE_DUO=0 in the environment turns them off (A/B switch).
+constexpr uint32_t kDuoMaxBlocks = 256;
+bool tree_duo_enabled();
 struct TreeGeometry {
   uint32_t G, threads, groups, words, lds_bytes;
   bool lds;  // levels in LDS (B <= kTreeLdsMaxBuckets)

@@ -2,6 +2,8 @@
 //
 // The per-workgroup tree builder (reference semantics, node layout) is tree_body() in
 // tree_body.hpp, shared with the fused build-step kernel in digest.hip.
+#include <stdlib.h>
+
 #include "tree_body.hpp"
 
 
@@ -12,6 +14,14 @@ template <bool kLds>
 __global__ __launch_bounds__(256) void tree_kernel(TreeLaunch a, uint32_t G, uint32_t lds_words) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   tree_body<kLds>(a, G, lds_words, blockIdx.x, lds, blockDim.x);
+}
+
+// Latency form (tree_body_duo): the upper half of the workgroup computes the lower half's message
+// schedules. `half` = 128 for wide trees (G = 256), else 64 (one wave of groups + its mirror).
+__global__ __launch_bounds__(256) void tree_duo_kernel(TreeLaunch a, uint32_t G, uint32_t lds_words, uint32_t half,
+                                                       uint32_t kw_word) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  tree_body_duo(a, G, lds_words, blockIdx.x, lds, half, reinterpret_cast<u32x4*>(lds + kw_word));
 }
 
 // Two wide trees per workgroup (tree_body_pair): used for many partitions, where the trees are
@@ -65,6 +75,14 @@ bool tree_geometry(uint32_t B, TreeGeometry* g) {
   return g->lds;
 }
 
+bool tree_duo_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("MDE_TREE_DUO");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_tree(const TreeLaunch& a, hipStream_t st) {
   if (a.P == 0) return hipSuccess;
   // Wide trees of many partitions: two per workgroup. 1,024 partitions at B = 1,000: 142 -> 119.5 us
@@ -77,6 +95,15 @@ hipError_t launch_tree(const TreeLaunch& a, hipStream_t st) {
   TreeGeometry g;
   const bool lds = tree_geometry(a.B, &g);
   const uint32_t blocks = (a.P + g.groups - 1) / g.groups;
+  // Split-schedule form: the same partitions per workgroup (a wide tree: one; else one wave of
+  // groups) with a mirror half of schedule helpers, for launches of few workgroups.
+  if (lds && !a.n_in && tree_duo_enabled() && ((g.G == g.threads && g.threads == 256) || blocks <= kDuoMaxBlocks)) {
+    const uint32_t half = g.threads == 256 ? 128u : 64u;
+    const uint32_t kw_word = (g.groups * g.words + 3u) & ~3u;
+    hipLaunchKernelGGL(tree_duo_kernel, dim3(blocks), dim3(2 * half), kw_word * 4u + duo_kw_bytes(half), st, a, g.G,
+                       g.words, half, kw_word);
+    return hipGetLastError();
+  }
   if (lds) {
     hipLaunchKernelGGL(tree_kernel<true>, dim3(blocks), dim3(g.threads), g.lds_bytes, st, a, g.G, g.words);
   } else {

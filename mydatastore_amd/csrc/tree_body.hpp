@@ -341,6 +341,99 @@ __device__ __forceinline__ void tree_body_pair(const TreeLaunch& a, uint32_t blo
     for (uint32_t i = lane; i < nq; i += 64) a.items_out[p0 + i] = (int32_t)lds[i * rw];
 }
 
+// Latency form of tree_body for launches with few partitions (the one-partition calls of
+// VerifyEpoch, small batches), same outputs. The workgroup is 2 x `half` threads and its upper half
+// mirrors the lower half: on every level whose nodes fit the lower half, lower thread x hashes its
+// node's rounds while upper thread x + half computes that node's message schedule
+// (sha256_node_duo_main / _sched: 64 + 14 x 64 instead of ~2,340 instructions on the critical
+// path of each level). Partitions: G <= half -> half / G per workgroup, held by the lower half;
+// G = 2 x half (a wide tree, level 1 > 64 nodes) -> one per workgroup, whose levels wider than
+// `half` nodes (and level 1) run over all threads as in tree_body. Uniform B (no n_in), levels in
+// LDS. kw: duo_kw_bytes(half) of LDS.
+__host__ __device__ inline uint32_t duo_kw_bytes(uint32_t half) { return 12u * 16u * half; }
+
+__device__ __forceinline__ void tree_body_duo(const TreeLaunch& a, uint32_t G, uint32_t lds_words, uint32_t block,
+                                              uint32_t* lds, uint32_t half, u32x4* kw) {
+  const uint32_t x = threadIdx.x;
+  const bool wide = G > half;
+  const bool upper = x >= half;
+  const uint32_t xm = upper ? x - half : x;  // the lower thread this one is (or mirrors)
+  const uint32_t groups = wide ? 1u : half / G;
+  const uint32_t gi = wide ? 0u : xm / G;
+  const uint32_t tid = wide ? xm : xm % G;    // node slot within the group on split levels
+  const uint32_t p = block * groups + gi;
+  const bool live = p < a.P;
+  const uint32_t B = a.B;
+  const uint32_t n1 = (B + 1) / 2;
+  const uint64_t s0 = (uint64_t)p * B;
+  uint32_t* node_base = (a.nodes_out && live)
+                            ? reinterpret_cast<uint32_t*>(a.nodes_out + (uint64_t)p * a.n_int * 32)
+                            : nullptr;
+  uint32_t* region = lds + (uint64_t)gi * lds_words;
+  uint32_t* counter = region;
+  uint32_t* cur = region + 4;
+  uint32_t* nxt = region + 4 + (uint64_t)n1 * 8;
+  if (!upper && tid == 0) counter[0] = 0;
+  __syncthreads();
+
+  // Leaves + level 1: the lower half (a wide tree: every thread).
+  uint32_t items = 0;
+  if (live && (wide || !upper)) {
+    const uint32_t j0 = wide ? x : tid, step = wide ? 2u * half : G;
+    for (uint32_t j = j0; j < n1; j += step) {
+      uint32_t st[8];
+      tree_level1(a, s0, B, j, items, st);
+      store_node(cur + (uint64_t)j * 8, st);
+      if (node_base) store_node(node_base + (uint64_t)j * 8, st);
+    }
+  }
+  if (items) atomicAdd(counter, items);
+
+  uint32_t n = n1;
+  uint64_t level_off = 0;
+  while (n > 1) {
+    __syncthreads();
+    const uint32_t m = (n + 1) / 2;
+    if (wide && m > half) {  // a wide level: every thread hashes whole nodes
+      if (live) {
+        for (uint32_t j = x; j < m; j += 2u * half) {
+          const uint32_t l = 2 * j, r = (2 * j + 1 < n) ? 2 * j + 1 : 2 * j;
+          uint32_t hl[8], hr[8], st[8];
+          load_node(cur + (uint64_t)l * 8, hl);
+          load_node(cur + (uint64_t)r * 8, hr);
+          sha256_node_pair(hl, hr, st);
+          store_node(nxt + (uint64_t)j * 8, st);
+          if (node_base) store_node(node_base + (level_off + n + j) * 8, st);
+        }
+      }
+    } else {  // split level: no lane skips the three barriers inside the duo functions
+      const uint32_t j = tid < m ? tid : 0u;
+      const uint32_t l = 2 * j, r = (2 * j + 1 < n) ? 2 * j + 1 : 2 * j;
+      uint32_t hl[8], hr[8];
+      load_node(cur + (uint64_t)l * 8, hl);
+      load_node(cur + (uint64_t)r * 8, hr);
+      if (!upper) {
+        uint32_t st[8];
+        sha256_node_duo_main(hl, hr, st, kw + xm, half);
+        if (live && tid < m) {
+          store_node(nxt + (uint64_t)j * 8, st);
+          if (node_base) store_node(node_base + (level_off + n + j) * 8, st);
+        }
+      } else {
+        sha256_node_duo_sched(hl, hr, kw + xm, half);
+      }
+    }
+    level_off += n;
+    n = m;
+    uint32_t* t = cur; cur = nxt; nxt = t;
+  }
+  __syncthreads();
+  if (live && !upper) {
+    if (tid < 8) reinterpret_cast<uint32_t*>(a.root_out + (uint64_t)p * 32)[tid] = cur[tid];
+    if (tid == 0 && a.items_out) a.items_out[p] = (int32_t)counter[0];
+  }
+}
+
 // LDS words of one tree_body group for B buckets (counter slot + the two level buffers).
 __host__ __device__ inline uint32_t tree_lds_words(uint32_t B) {
   const uint32_t n1 = (B + 1) / 2;

@@ -253,6 +253,23 @@ int main(int argc, char** argv) {
     return 1;
   }
   if ((rc = mde_batcher_create(0, 256, 0, &batcher))) return 1;
+  /* batch_bench SECONDS B CALLERS [MODE]: only the concurrent cases of that shape (for kernel traces) */
+  if (argc > 3) {
+    const uint32_t B = (uint32_t)atoi(argv[2]);
+    const int P = atoi(argv[3]);
+    part_t* parts = xmalloc(sizeof(part_t) * (size_t)P * 4);
+    for (int i = 0; i < P * 4; i++) {
+      make_part(&parts[i], 1000, B, 100 + (uint64_t)i);
+      make_peers(&parts[i]);
+    }
+    /* optional 4th argument: one mode by name */
+    for (int mode = CPU; mode <= V_BATCHED; mode++)
+      if (argc <= 4 || !strcmp(argv[4], kModes[mode])) run_case(mode, P, 1000, B, parts, 4);
+    printf("{\"batched_outputs_equal_oracle\": %s}\n", g_bad ? "false" : "true");
+    mde_batcher_destroy(batcher);
+    mde_destroy(ctx);
+    return g_bad ? 3 : 0;
+  }
   /* single-call shapes: CPU oracle (1 thread) beside the synchronous device call */
   const uint64_t ns[3] = {1000, 10000, 100000};
   const uint32_t Bs[2] = {64, 1000};

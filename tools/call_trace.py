@@ -31,6 +31,9 @@ def main():
         d2[B // 3] = (d2[B // 3] + 1) % 999999
         peers = eng.encode_objects(B, np.concatenate([d, d2]), np.concatenate([z, z]), lower=3, upper=4)
         call = lambda: eng.verify_epochs(B, d, z, None, [peers], 2, 3, partition=np.array([7], np.int32))
+    elif what == "tree":  # the tree alone (tree_kernel from digests): the build minus its digest phase
+        dig = eng.build(vals, seg, 1, B, value_stride=8)["digest"]
+        call = lambda: eng.tree_from_digests(dig, B, want_nodes=nodes)
     else:
         call = lambda: eng.build(vals, seg, 1, B, value_stride=8, want_nodes=nodes)
     for _ in range(20):
