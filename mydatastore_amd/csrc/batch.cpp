@@ -8,19 +8,22 @@
 // SHA-256 chain -- for a few KB of 8-byte timestamps. The batcher turns concurrent calls into one
 // device build by group commit:
 //   * a caller validates its request on its own thread and enqueues it;
-//   * if no batch is running it becomes the leader: it takes every compatible queued request (up
-//     to max_partitions partitions; optionally waiting up to max_wait_us for more to arrive),
-//     packs their records into ONE pinned arena, runs ONE H2D copy, mde_build_async (or
-//     mde_verify_epochs_async with the local trees given by their digests) and ONE D2H copy on a
-//     free slot's context, scatters the results into each caller's buffers and wakes the callers;
-//   * requests that arrive while a batch runs form the next batch, whose leader is one of them:
-//     up to kSlots batches are in flight at once (one context, stream and staging area per slot),
-//     so the next batch's staging, copies and launches overlap the earlier batches' device work,
+//   * if no batch is being taken it becomes the leader: it takes every compatible queued request
+//     (up to max_partitions partitions; optionally waiting up to max_wait_us for more to arrive)
+//     into a free slot, passes the leader role on at once (the next leader takes the next batch
+//     while this one stages), packs their records into ONE pinned arena, runs ONE H2D copy and
+//     mde_build_async (or mde_verify_epochs_async with the local trees given by their digests) on
+//     the slot's context, waits for the batch's event and marks its callers ready;
+//   * each ready caller copies its own outputs out of the slot's pinned buffer on its own thread
+//     (100 callers' nodes are ~0.7 MB of copies: spread over their threads, not the leader's), and
+//     the last one frees the slot;
+//   * up to mde_batcher_contexts() batches are in flight at once (one context, stream and staging
+//     area per slot), so staging, copies and launches overlap the earlier batches' device work,
 //     and a finished batch wakes only its own callers (one condition variable per request: no
 //     thundering herd at 100 callers).
-// Liveness: every lead() ends with a handoff() after its slot is freed, and a leader hands off
-// again right after launching, so a queued request is picked up by the next free slot even when
-// the request it was handed the role to has meanwhile finished inside another batch.
+// Liveness: a leader hands the role on right after taking its batch, and the caller that frees a
+// slot hands it on again, so a queued request is picked up by the next free slot even when the
+// request it was handed the role to has meanwhile finished inside another batch.
 // mde_batcher_destroy must not race with calls in flight (like mde_destroy).
 // Each caller gets exactly what the per-call entry point returns for its own inputs (bit-exact:
 // a partition's digests, sizes and tree depend only on its own records; tests/cpp/batch_test.c
@@ -74,7 +77,10 @@ struct Req {
   char* err = nullptr;
   uint64_t err_cap = 0;
   bool done = false;
-  bool lead = false;  // handed the leader role for the next batch
+  bool lead = false;   // handed the leader role for the next batch
+  bool ready = false;  // its batch finished on the device: copy its own outputs out, then done
+  void* slot = nullptr;  // the mde_batcher::Slot its batch ran in
+  uint64_t pos = 0;      // build: its first partition in the batch; verify: its index
   std::chrono::steady_clock::time_point lead_t;  // when it was handed the role (MDE_BATCH_PROFILE)
   std::condition_variable cv;
 };
@@ -104,13 +110,26 @@ struct Buf {
 
 uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 
+// A batch between its launch and the last of its callers' copies: the output layout in the slot's
+// pinned out buffer, which stays the batch's until every caller has copied its part out.
+struct Batch {
+  std::vector<Req*> v;
+  bool launched = false;  // device work enqueued (else every request already failed)
+  uint32_t B = 0;
+  uint64_t NI = 0, stride = 0, R = 0;
+  uint64_t o[9] = {0};   // output offsets in the slot's pinned out buffer
+  size_t pending = 0;    // callers still copying their outputs out
+};
+
 }  // namespace
 
 // Batches in flight at once. Each slot owns a context -- its own stream and scratch -- so the
-// device runs up to kSlots batches concurrently (a batch of small partitions is a few workgroups
-// whose time is the tree's dependent SHA-256 chain, so batches overlap instead of queueing on one
-// stream); kSlots matches GPU_MAX_HW_QUEUES = 4, the HIP runtime's hardware queues per process.
-constexpr int kSlots = 4;
+// device runs several batches concurrently (a batch of small partitions is a few workgroups whose
+// time is the tree's dependent SHA-256 chain, so batches overlap instead of queueing on one
+// stream). Default 4 = GPU_MAX_HW_QUEUES, the HIP runtime's hardware queues per process;
+// MDE_BATCH_SLOTS=1..8 overrides it (A/B).
+constexpr int kMaxSlots = 8;
+constexpr int kDefaultSlots = 4;
 
 struct mde_batcher {
   int device = 0;
@@ -125,7 +144,9 @@ struct mde_batcher {
     Buf pin_in, pin_out, dev_in, dev_out;
     hipEvent_t done = nullptr;
     bool busy = false;
-  } slots[kSlots];
+    Batch bt;
+  } slots[kMaxSlots];
+  int n_slots = kDefaultSlots;
   uint64_t n_batches = 0, n_requests = 0, n_partitions = 0;
   // write-once outputs stored by the kernels straight into the slot's pinned out buffer (no D2H
   // copy; above ~16 KB such a copy starts ~11 us after the kernel, profiles/r03q_call_trace.txt);
@@ -134,6 +155,7 @@ struct mde_batcher {
   bool blocking_sync = false;  // MDE_BATCH_BLOCKING_SYNC=1: leaders sleep on their batch's event (A/B)
   // MDE_BATCH_PROFILE=1: host-side phase times summed over batches, printed by mde_batcher_destroy
   bool profile = false;
+  bool early_handoff = true;  // MDE_BATCH_EARLY=0: pass the leader role on only after the launch (A/B)
   double t_handoff = 0, t_stage = 0, t_device = 0, t_scatter = 0;
   uint64_t n_handoff = 0;
 };
@@ -224,16 +246,6 @@ void fail_all(const std::vector<Req*>& v, int code, const std::string& msg) {
   for (Req* x : v) fail(x, code, "%s", msg.c_str());
 }
 
-// A batch between its launch and its scatter: the staging slot and the output layout.
-struct Batch {
-  std::vector<Req*> v;
-  mde_batcher::Slot* slot = nullptr;
-  bool launched = false;  // device work enqueued (else every request already failed)
-  uint32_t B = 0;
-  uint64_t NI = 0, stride = 0, R = 0;
-  uint64_t o[9] = {0};  // output offsets in the slot's pinned out buffer
-};
-
 #define BHIP(expr)                                                                               \
   do {                                                                                           \
     hipError_t e_ = (expr);                                                                      \
@@ -276,7 +288,8 @@ uint8_t* mapped_out(mde_batcher* b, mde_batcher::Slot* sl) {
 
 // Stage + launch one build batch (records rebased into one arena): ONE H2D copy, mde_build_async,
 // ONE D2H copy and an event, all enqueued on the batcher context's stream.
-void launch_build(mde_batcher* b, Batch* bt) {
+void launch_build(mde_batcher* b, mde_batcher::Slot* sl) {
+  Batch* bt = &sl->bt;
   const std::vector<Req*>& v = bt->v;
   const uint32_t B = v[0]->rec.n_buckets;
   uint32_t stride = v[0]->rec.value_stride;
@@ -303,17 +316,18 @@ void launch_build(mde_batcher* b, Batch* bt) {
   bt->B = B;
   bt->NI = NI;
   std::string msg;
-  const int rc = grow_slot(bt->slot, in_bytes, out_bytes, out_bytes, &msg, b->blocking_sync);
+  const int rc = grow_slot(sl, in_bytes, out_bytes, out_bytes, &msg, b->blocking_sync);
   if (rc) {
     fail_all(v, rc, msg);
     return;
   }
-  uint8_t* hin = static_cast<uint8_t*>(bt->slot->pin_in.p);
+  uint8_t* hin = static_cast<uint8_t*>(sl->pin_in.p);
   uint64_t* hvoff = reinterpret_cast<uint64_t*>(hin + o_voff);
   uint64_t* hseg = reinterpret_cast<uint64_t*>(hin + o_seg);
   uint64_t rbase = 0, bbase = 0, sbase = 0;
   for (Req* x : v) {
     const mde_records& r = x->rec;
+    x->pos = sbase / B;
     if (x->b1 > x->b0) std::memcpy(hin + o_vals + bbase, r.values + x->b0, x->b1 - x->b0);
     if (!stride) {
       for (uint64_t k = x->r0; k < x->r1; k++)
@@ -327,13 +341,13 @@ void launch_build(mde_batcher* b, Batch* bt) {
   }
   if (!stride) hvoff[N] = V;
   hseg[S] = N;
-  hipStream_t st = static_cast<hipStream_t>(mde_get_stream(bt->slot->ctx));
-  uint8_t* din = static_cast<uint8_t*>(bt->slot->dev_in.p);
+  hipStream_t st = static_cast<hipStream_t>(mde_get_stream(sl->ctx));
+  uint8_t* din = static_cast<uint8_t*>(sl->dev_in.p);
   BHIP(hipSetDevice(b->device));
   // every build output is stored once by the tree pass (trees wider than the LDS levels re-read
   // their nodes: device memory and a copy for those)
-  uint8_t* mapped = B <= 4096u ? mapped_out(b, bt->slot) : nullptr;
-  uint8_t* dout = mapped ? mapped : static_cast<uint8_t*>(bt->slot->dev_out.p);
+  uint8_t* mapped = B <= 4096u ? mapped_out(b, sl) : nullptr;
+  uint8_t* dout = mapped ? mapped : static_cast<uint8_t*>(sl->dev_out.p);
   BHIP(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, st));
   mde_records dr{};
   dr.values = din + o_vals;
@@ -347,31 +361,27 @@ void launch_build(mde_batcher* b, Batch* bt) {
   dr.seg_rec = reinterpret_cast<const uint64_t*>(din + o_seg);
   mde_tree_out to{reinterpret_cast<uint64_t*>(dout + o[0]), reinterpret_cast<int32_t*>(dout + o[1]),
                   reinterpret_cast<int32_t*>(dout + o[2]), dout + o[3], want_nodes ? dout + o[4] : nullptr};
-  int brc = mde_build_async(bt->slot->ctx, &dr, &to);
+  int brc = mde_build_async(sl->ctx, &dr, &to);
   if (brc) {
-    ctx_error(bt->slot->ctx, v, brc);
+    ctx_error(sl->ctx, v, brc);
     return;
   }
-  if (!mapped) BHIP(hipMemcpyAsync(bt->slot->pin_out.p, dout, out_bytes, hipMemcpyDeviceToHost, st));
-  BHIP(hipEventRecord(bt->slot->done, st));
+  if (!mapped) BHIP(hipMemcpyAsync(sl->pin_out.p, dout, out_bytes, hipMemcpyDeviceToHost, st));
+  BHIP(hipEventRecord(sl->done, st));
   bt->launched = true;
 }
 
-void scatter_build(Batch* bt) {
-  const uint8_t* hout = static_cast<const uint8_t*>(bt->slot->pin_out.p);
-  const uint64_t B = bt->B, NI = bt->NI;
-  const uint64_t* o = bt->o;
-  uint64_t pbase = 0;
-  for (Req* x : bt->v) {
-    const uint64_t Pi = x->parts;
-    if (x->out.digest) std::memcpy(x->out.digest, hout + o[0] + pbase * B * 8, Pi * B * 8);
-    if (x->out.size) std::memcpy(x->out.size, hout + o[1] + pbase * B * 4, Pi * B * 4);
-    if (x->out.items) std::memcpy(x->out.items, hout + o[2] + pbase * 4, Pi * 4);
-    std::memcpy(x->out.root, hout + o[3] + pbase * 32, Pi * 32);
-    if (x->out.nodes) std::memcpy(x->out.nodes, hout + o[4] + pbase * NI * 32, Pi * NI * 32);
-    pbase += Pi;
-    x->rc = MDE_OK;
-  }
+// One caller's part of a finished build batch, copied out on the caller's own thread.
+void scatter_build(const mde_batcher::Slot* sl, Req* x) {
+  const Batch& bt = sl->bt;
+  const uint8_t* hout = static_cast<const uint8_t*>(sl->pin_out.p);
+  const uint64_t B = bt.B, NI = bt.NI, Pi = x->parts, pbase = x->pos;
+  const uint64_t* o = bt.o;
+  if (x->out.digest) std::memcpy(x->out.digest, hout + o[0] + pbase * B * 8, Pi * B * 8);
+  if (x->out.size) std::memcpy(x->out.size, hout + o[1] + pbase * B * 4, Pi * B * 4);
+  if (x->out.items) std::memcpy(x->out.items, hout + o[2] + pbase * 4, Pi * 4);
+  std::memcpy(x->out.root, hout + o[3] + pbase * 32, Pi * 32);
+  if (x->out.nodes) std::memcpy(x->out.nodes, hout + o[4] + pbase * NI * 32, Pi * NI * 32);
 }
 
 int check_verify(Req* q, uint64_t object_stride) {
@@ -397,7 +407,8 @@ int check_verify(Req* q, uint64_t object_stride) {
 // Stage + launch one verify batch: mde_verify_epochs over all of them, the local trees given by
 // their digests; peers padded to the batch's largest peer count with absent (empty) objects, which
 // the reference skips like a failed EpochTreeObjectRequest (main/manager.go:1064-1070).
-void launch_verify(mde_batcher* b, Batch* bt) {
+void launch_verify(mde_batcher* b, mde_batcher::Slot* sl) {
+  Batch* bt = &sl->bt;
   const std::vector<Req*>& v = bt->v;
   const uint32_t B = v[0]->B;
   const int64_t epoch = v[0]->epoch;
@@ -428,17 +439,18 @@ void launch_verify(mde_batcher* b, Batch* bt) {
   bt->stride = stride;
   bt->R = R;
   std::string msg;
-  const int grc = grow_slot(bt->slot, in_bytes, o[7], out_bytes, &msg, b->blocking_sync);
+  const int grc = grow_slot(sl, in_bytes, o[7], out_bytes, &msg, b->blocking_sync);
   if (grc) {
     fail_all(v, grc, msg);
     return;
   }
-  uint8_t* hin = static_cast<uint8_t*>(bt->slot->pin_in.p);
+  uint8_t* hin = static_cast<uint8_t*>(sl->pin_in.p);
   uint64_t* hoff = reinterpret_cast<uint64_t*>(hin + i_off);
   int32_t* hpart = reinterpret_cast<int32_t*>(hin + i_part);
   uint64_t base = 0;
   for (uint64_t p = 0; p < P; p++) {
     Req* x = v[p];
+    x->pos = p;
     std::memcpy(hin + i_dig + p * B * 8, x->digest, (uint64_t)B * 8);
     if (x->size) std::memcpy(hin + i_size + p * B * 4, x->size, (uint64_t)B * 4);
     else std::memset(hin + i_size + p * B * 4, 0, (uint64_t)B * 4);
@@ -449,24 +461,24 @@ void launch_verify(mde_batcher* b, Batch* bt) {
     base += hi - lo;
   }
   hoff[P * R] = base;
-  hipStream_t st = static_cast<hipStream_t>(mde_get_stream(bt->slot->ctx));
-  uint8_t* din = static_cast<uint8_t*>(bt->slot->dev_in.p);
-  uint8_t* dout = static_cast<uint8_t*>(bt->slot->dev_out.p);
+  hipStream_t st = static_cast<hipStream_t>(mde_get_stream(sl->ctx));
+  uint8_t* din = static_cast<uint8_t*>(sl->dev_in.p);
+  uint8_t* dout = static_cast<uint8_t*>(sl->dev_out.p);
   BHIP(hipSetDevice(b->device));
   // valid and the peer statuses are read back inside the launch (the fold, the encode): device
   // memory, copied; the counts, ids and objects are stored once, straight into pinned memory
-  uint8_t* mapped = mapped_out(b, bt->slot);
+  uint8_t* mapped = mapped_out(b, sl);
   uint8_t* wout = mapped ? mapped : dout;
   BHIP(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, st));
   const uint64_t* d_dig = reinterpret_cast<const uint64_t*>(din + i_dig);
-  int rc = mde_reserve_decode_scratch(bt->slot->ctx, P * R, nbytes);  // linear decode of any peer object
+  int rc = mde_reserve_decode_scratch(sl->ctx, P * R, nbytes);  // linear decode of any peer object
   if (rc) {
-    ctx_error(bt->slot->ctx, v, rc);
+    ctx_error(sl->ctx, v, rc);
     return;
   }
   // local trees as digests only (nodes NULL): a partition builds its own tree on the device only
   // when a peer of another shape needs its inner nodes
-  rc = mde_verify_epochs_async(bt->slot->ctx, (uint32_t)P, B, reinterpret_cast<const int32_t*>(din + i_part), epoch, d_dig,
+  rc = mde_verify_epochs_async(sl->ctx, (uint32_t)P, B, reinterpret_cast<const int32_t*>(din + i_part), epoch, d_dig,
                                reinterpret_cast<const int32_t*>(din + i_size), nullptr, R, din + i_peer,
                                reinterpret_cast<const uint64_t*>(din + i_off), rcount, dout + o[0],
                                reinterpret_cast<int32_t*>(wout + o[1]), reinterpret_cast<int32_t*>(wout + o[2]),
@@ -474,40 +486,38 @@ void launch_verify(mde_batcher* b, Batch* bt) {
                                want_obj ? wout + o[6] : nullptr, stride,
                                want_obj ? reinterpret_cast<uint32_t*>(wout + o[5]) : nullptr);
   if (rc) {
-    ctx_error(bt->slot->ctx, v, rc);
+    ctx_error(sl->ctx, v, rc);
     return;
   }
-  uint8_t* hout = static_cast<uint8_t*>(bt->slot->pin_out.p);
+  uint8_t* hout = static_cast<uint8_t*>(sl->pin_out.p);
   if (mapped) {
     BHIP(hipMemcpyAsync(hout + o[0], dout + o[0], P, hipMemcpyDeviceToHost, st));
     if (R) BHIP(hipMemcpyAsync(hout + o[4], dout + o[4], P * R * 4, hipMemcpyDeviceToHost, st));
   } else {
     BHIP(hipMemcpyAsync(hout, dout, o[7], hipMemcpyDeviceToHost, st));
   }
-  BHIP(hipEventRecord(bt->slot->done, st));
+  BHIP(hipEventRecord(sl->done, st));
   bt->launched = true;
 }
 
-void scatter_verify(Batch* bt) {
-  const uint8_t* hout = static_cast<const uint8_t*>(bt->slot->pin_out.p);
-  const uint64_t B = bt->B, R = bt->R, stride = bt->stride;
-  const uint64_t* o = bt->o;
-  for (uint64_t p = 0; p < bt->v.size(); p++) {
-    Req* x = bt->v[p];
-    *x->valid = hout[o[0] + p];
-    std::memcpy(x->valid_count, hout + o[1] + p * 4, 4);
-    int32_t dc;
-    std::memcpy(&dc, hout + o[3] + p * 4, 4);
-    *x->diff_count = dc;
-    if (dc > 0) std::memcpy(x->diff_ids, hout + o[2] + p * B * 4, (uint64_t)dc * 4);
-    if (x->peer_status && x->R) std::memcpy(x->peer_status, hout + o[4] + p * R * 4, (uint64_t)x->R * 4);
-    if (x->object_out) {
-      uint32_t len;
-      std::memcpy(&len, hout + o[5] + p * 4, 4);
-      *x->object_len = len;
-      std::memcpy(x->object_out, hout + o[6] + p * stride, len);
-    }
-    x->rc = MDE_OK;
+// One caller's part of a finished verify batch, copied out on the caller's own thread.
+void scatter_verify(const mde_batcher::Slot* sl, Req* x) {
+  const Batch& bt = sl->bt;
+  const uint8_t* hout = static_cast<const uint8_t*>(sl->pin_out.p);
+  const uint64_t B = bt.B, R = bt.R, stride = bt.stride, p = x->pos;
+  const uint64_t* o = bt.o;
+  *x->valid = hout[o[0] + p];
+  std::memcpy(x->valid_count, hout + o[1] + p * 4, 4);
+  int32_t dc;
+  std::memcpy(&dc, hout + o[3] + p * 4, 4);
+  *x->diff_count = dc;
+  if (dc > 0) std::memcpy(x->diff_ids, hout + o[2] + p * B * 4, (uint64_t)dc * 4);
+  if (x->peer_status && x->R) std::memcpy(x->peer_status, hout + o[4] + p * R * 4, (uint64_t)x->R * 4);
+  if (x->object_out) {
+    uint32_t len;
+    std::memcpy(&len, hout + o[5] + p * 4, 4);
+    *x->object_len = len;
+    std::memcpy(x->object_out, hout + o[6] + p * stride, len);
   }
 }
 
@@ -515,8 +525,8 @@ void scatter_verify(Batch* bt) {
 // is free (called with the lock held). That request's thread wakes alone.
 void handoff(mde_batcher* b) {
   if (b->leading || b->q.empty()) return;
-  for (auto& sl : b->slots)
-    if (!sl.busy) {
+  for (int i = 0; i < b->n_slots; i++)
+    if (!b->slots[i].busy) {
       Req* x = b->q.front();
       x->lead = true;
       if (b->profile) x->lead_t = std::chrono::steady_clock::now();
@@ -525,9 +535,16 @@ void handoff(mde_batcher* b) {
     }
 }
 
-// The leader's turn (lock held on entry and exit): take a batch into a free slot, stage and launch
-// it with the lock released, pass the leader role on, wait for the batch's event, scatter, wake
-// its callers, free the slot.
+bool free_slot(const mde_batcher* b) {
+  for (int i = 0; i < b->n_slots; i++)
+    if (!b->slots[i].busy) return true;
+  return false;
+}
+
+// The leader's turn (lock held on entry and exit): take a batch into a free slot, pass the leader
+// role on (the next leader stages its batch while this one stages and runs), stage and launch with
+// the lock released, wait for the batch's event, then mark its callers ready: each copies its own
+// outputs out of the slot on its own thread, and the last one frees the slot.
 void lead(mde_batcher* b, std::unique_lock<std::mutex>& lk) {
   b->leading = true;
   if (b->max_wait_us) {  // let concurrent callers join, until the batch is full or the window ends
@@ -539,73 +556,100 @@ void lead(mde_batcher* b, std::unique_lock<std::mutex>& lk) {
       if (parts >= b->max_parts || b->collect.wait_until(lk, until) == std::cv_status::timeout) break;
     }
   }
-  Batch bt;
-  for (auto& sl : b->slots)
-    if (!sl.busy) {
-      bt.slot = &sl;
-      break;
-    }
-  bt.slot->busy = true;
+  mde_batcher::Slot* sl = nullptr;
+  for (int i = 0; i < b->n_slots && !sl; i++)
+    if (!b->slots[i].busy) sl = &b->slots[i];
+  sl->busy = true;
+  Batch& bt = sl->bt;
+  bt = Batch{};
   bt.v = take(b);
   uint64_t parts = 0;
-  for (Req* x : bt.v) parts += x->parts;
+  for (Req* x : bt.v) {
+    parts += x->parts;
+    x->slot = sl;
+  }
   b->n_batches++;
   b->n_requests += bt.v.size();
   b->n_partitions += parts;
+  if (b->early_handoff) {
+    b->leading = false;
+    handoff(b);
+  }
   lk.unlock();
   using clk = std::chrono::steady_clock;
   const clk::time_point t0 = b->profile ? clk::now() : clk::time_point{};
-  if (bt.v[0]->kind == Kind::Build) launch_build(b, &bt);
-  else launch_verify(b, &bt);
-  lk.lock();
-  b->leading = false;
-  handoff(b);  // the next batch stages and launches while this one runs on the device
-  lk.unlock();
+  const Kind kind = bt.v[0]->kind;
+  if (kind == Kind::Build) launch_build(b, sl);
+  else launch_verify(b, sl);
+  if (!b->early_handoff) {
+    lk.lock();
+    b->leading = false;
+    handoff(b);  // the next batch stages and launches while this one runs on the device
+    lk.unlock();
+  }
   const clk::time_point t1 = b->profile ? clk::now() : clk::time_point{};
   clk::time_point t2 = t1;
   if (bt.launched) {
-    const hipError_t e = hipEventSynchronize(bt.slot->done);
+    const hipError_t e = hipEventSynchronize(sl->done);
     if (b->profile) t2 = clk::now();
-    if (e != hipSuccess) fail_all(bt.v, MDE_E_DEVICE, std::string("batch: ") + hipGetErrorString(e));
-    else if (bt.v[0]->kind == Kind::Build) scatter_build(&bt);
-    else scatter_verify(&bt);
+    if (e != hipSuccess) {
+      fail_all(bt.v, MDE_E_DEVICE, std::string("batch: ") + hipGetErrorString(e));
+      bt.launched = false;
+    }
   }
   lk.lock();
   if (b->profile) {
-    const clk::time_point t3 = clk::now();
     b->t_stage += std::chrono::duration<double>(t1 - t0).count();
     b->t_device += std::chrono::duration<double>(t2 - t1).count();
-    b->t_scatter += std::chrono::duration<double>(t3 - t2).count();
   }
-  bt.slot->busy = false;
+  bt.pending = bt.v.size();
   for (Req* x : bt.v) {
-    x->done = true;
+    x->ready = true;
     x->cv.notify_one();
   }
-  handoff(b);
 }
 
-// Enqueue, then either lead a batch or wait (on this request's own condition variable) until a
-// leader finished it or handed this request the leader role.
+// A ready request copies its outputs out (lock released), then frees its batch's slot if it was
+// the last one (lock held on entry and exit).
+void finish(mde_batcher* b, Req* r, std::unique_lock<std::mutex>& lk) {
+  r->ready = false;
+  mde_batcher::Slot* sl = static_cast<mde_batcher::Slot*>(r->slot);
+  const bool copy = sl->bt.launched && r->rc == MDE_OK;
+  lk.unlock();
+  using clk = std::chrono::steady_clock;
+  const clk::time_point t0 = b->profile ? clk::now() : clk::time_point{};
+  if (copy) {
+    if (r->kind == Kind::Build) scatter_build(sl, r);
+    else scatter_verify(sl, r);
+  }
+  const clk::time_point t1 = b->profile ? clk::now() : clk::time_point{};
+  lk.lock();
+  if (b->profile) b->t_scatter += std::chrono::duration<double>(t1 - t0).count();
+  r->done = true;
+  if (--sl->bt.pending == 0) {
+    sl->bt.v.clear();
+    sl->busy = false;
+    handoff(b);
+  }
+}
+
+// Enqueue, then either lead a batch or wait (on this request's own condition variable) until its
+// batch is ready or it is handed the leader role.
 int submit(mde_batcher* b, Req* r) {
   std::unique_lock<std::mutex> lk(b->m);
   b->q.push_back(r);
   b->collect.notify_one();
-  if (!b->leading) {
-    for (auto& sl : b->slots)
-      if (!sl.busy) {
-        r->lead = true;
-        break;
-      }
-  }
+  if (!b->leading && free_slot(b)) r->lead = true;
   while (!r->done) {
+    if (r->ready) {
+      finish(b, r, lk);
+      continue;
+    }
     if (r->lead) {
       r->lead = false;
-      bool free_slot = false;
-      for (auto& sl : b->slots) free_slot |= !sl.busy;
       // the role may have gone stale (another caller took it, the queue drained, no free slot):
-      // then wait for a handoff or for this request to finish in someone else's batch
-      if (!b->leading && free_slot && !b->q.empty()) {
+      // then wait for a handoff or for this request's batch
+      if (!b->leading && free_slot(b) && !b->q.empty()) {
         if (b->profile && r->lead_t != std::chrono::steady_clock::time_point{}) {
           b->t_handoff += std::chrono::duration<double>(std::chrono::steady_clock::now() - r->lead_t).count();
           b->n_handoff++;
@@ -628,8 +672,9 @@ int mde_batcher_create(int device, uint32_t max_partitions, uint32_t max_wait_us
   *out = nullptr;
   mde_batcher* b = new (std::nothrow) mde_batcher();
   if (!b) return MDE_E_NOMEM;
-  for (auto& sl : b->slots) {
-    const int rc = mde_create(device, &sl.ctx);
+  if (const char* e = std::getenv("MDE_BATCH_SLOTS")) b->n_slots = std::min(kMaxSlots, std::max(1, std::atoi(e)));
+  for (int i = 0; i < b->n_slots; i++) {
+    const int rc = mde_create(device, &b->slots[i].ctx);
     if (rc != MDE_OK) {
       for (auto& x : b->slots)
         if (x.ctx) mde_destroy(x.ctx);
@@ -641,6 +686,7 @@ int mde_batcher_create(int device, uint32_t max_partitions, uint32_t max_wait_us
   if (const char* e = std::getenv("MDE_DIRECT_OUT")) b->direct_out = std::atoi(e) != 0;
   if (const char* e = std::getenv("MDE_BATCH_BLOCKING_SYNC")) b->blocking_sync = std::atoi(e) != 0;
   if (const char* e = std::getenv("MDE_BATCH_PROFILE")) b->profile = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MDE_BATCH_EARLY")) b->early_handoff = std::atoi(e) != 0;
   b->max_parts = max_partitions ? max_partitions : 256;
   b->max_wait_us = max_wait_us;
   *out = b;
@@ -652,12 +698,13 @@ void mde_batcher_destroy(mde_batcher* b) {
   if (b->profile && b->n_batches)
     std::fprintf(stderr,
                  "{\"batcher_profile\": {\"batches\": %llu, \"requests\": %llu, \"stage_launch_us\": %.2f, "
-                 "\"device_wait_us\": %.2f, \"scatter_wake_us\": %.2f, \"handoffs\": %llu, \"handoff_us\": %.2f}}\n",
+                 "\"device_wait_us\": %.2f, \"copy_out_us_per_batch\": %.2f, \"handoffs\": %llu, \"handoff_us\": %.2f}}\n",
                  (unsigned long long)b->n_batches, (unsigned long long)b->n_requests, 1e6 * b->t_stage / b->n_batches,
                  1e6 * b->t_device / b->n_batches, 1e6 * b->t_scatter / b->n_batches, (unsigned long long)b->n_handoff,
                  b->n_handoff ? 1e6 * b->t_handoff / b->n_handoff : 0.0);
   (void)hipSetDevice(b->device);
   for (auto& sl : b->slots) {
+    if (!sl.ctx) continue;
     (void)mde_synchronize(sl.ctx);
     if (sl.pin_in.p) (void)hipHostFree(sl.pin_in.p);
     if (sl.pin_out.p) (void)hipHostFree(sl.pin_out.p);
@@ -670,10 +717,10 @@ void mde_batcher_destroy(mde_batcher* b) {
 }
 
 mde_ctx* mde_batcher_ctx(mde_batcher* b, uint32_t i) {
-  return b && i < (uint32_t)kSlots ? b->slots[i].ctx : nullptr;
+  return b && i < (uint32_t)b->n_slots ? b->slots[i].ctx : nullptr;
 }
 
-uint32_t mde_batcher_contexts(const mde_batcher* b) { return b ? (uint32_t)kSlots : 0u; }
+uint32_t mde_batcher_contexts(const mde_batcher* b) { return b ? (uint32_t)b->n_slots : 0u; }
 
 int mde_batcher_stats(mde_batcher* b, uint64_t* batches, uint64_t* requests, uint64_t* partitions) {
   if (!b) return MDE_E_INVAL;

@@ -919,33 +919,12 @@ __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLa
   // K-th 16-byte vector of the bucket, four loads in flight
   uint32_t K = 1;
   while (K * 2 * nb <= (uint32_t)kThreads) K *= 2;
-  // kSmallRounds buckets per thread at a time: their boundaries, then the first vector of each, are
-  // loaded together (one dependent load pair per bucket in turn cost ~7 us of a B = 1,000 call)
-  constexpr int kSmallRounds = 4;
-  const uint32_t j = threadIdx.x % K, step = (uint32_t)kThreads / K;
-  for (uint32_t s0 = s_beg + threadIdx.x / K; s0 < s_end; s0 += kSmallRounds * step) {
-    uint64_t los[kSmallRounds], his[kSmallRounds];
-#pragma unroll
-    for (int i = 0; i < kSmallRounds; i++) {
-      const uint32_t s = s0 + i * step;
-      const bool in = s < s_end;
-      los[i] = in ? segpos(d, s) : 0ull;
-      his[i] = in ? segpos(d, s + 1) : 0ull;
-    }
-    u32x4 firsts[kSmallRounds];
-#pragma unroll
-    for (int i = 0; i < kSmallRounds; i++) {
-      const uint64_t x = (los[i] & ~15ull) + 16ull * j;
-      firsts[i] = x < his[i] ? __builtin_nontemporal_load(base + (x >> 4)) : u32x4{0u, 0u, 0u, 0u};
-    }
-#pragma unroll
-    for (int i = 0; i < kSmallRounds; i++) {
-    const uint32_t s = s0 + i * step;
-    const uint64_t lo = los[i], hi = his[i];
+  const uint32_t j = threadIdx.x % K;
+  for (uint32_t s = s_beg + threadIdx.x / K; s < s_end; s += kThreads / K) {
+    const uint64_t lo = segpos(d, s), hi = segpos(d, s + 1);
     const int64_t l = (int64_t)lo, h = (int64_t)hi;
+    uint32_t acc = 0;
     uint64_t x = (lo & ~15ull) + 16ull * j;
-    uint32_t acc = x < hi ? masked_sum16(firsts[i], l - (int64_t)x, h - (int64_t)x, 0u) : 0u;
-    x += 16ull * K;
     for (; x + 48ull * K < hi; x += 64ull * K) {
       const u32x4 v0 = __builtin_nontemporal_load(base + (x >> 4));
       const u32x4 v1 = __builtin_nontemporal_load(base + ((x + 16ull * K) >> 4));
@@ -959,7 +938,6 @@ __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLa
     for (; x < hi; x += 16ull * K)
       acc = masked_sum16(__builtin_nontemporal_load(base + (x >> 4)), l - (int64_t)x, h - (int64_t)x, acc);
     if (acc) atomicAdd(sums + (s - s_beg), (unsigned long long)acc);
-    }
   }
   __syncthreads();
   TreeLaunch tl = t;
@@ -1147,7 +1125,23 @@ uint32_t build_step_tree_q(uint32_t B) {
 
 bool build_step_fusable(uint32_t B) { return B >= 1 && build_step_tree_q(B) >= 1; }
 
-void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint32_t* lds_bytes) {
+// Where the split-schedule trees of a fused step keep their K+W ring: after the level buffers when
+// that fits kStepTreeLdsMax, else over level-1 buffer space that levels of <= 64 nodes never touch
+// (they read at most 128 nodes of either level buffer); 0 = no room (plain tree_body).
+uint32_t duo_step_kw_word(uint32_t B, uint32_t* lds_bytes) {
+  if (!tree_duo_enabled()) return 0;
+  const uint32_t words = tree_lds_words(B), kw_words = duo_kw_bytes(kStepTreeWideThreads / 2) / 4u;
+  const uint32_t app = (words + 3u) & ~3u;
+  if ((app + kw_words) * 4u <= kStepTreeLdsMax) {
+    *lds_bytes = std::max<uint32_t>(*lds_bytes, (app + kw_words) * 4u);
+    return app;
+  }
+  const uint32_t n1 = (B + 1) / 2;
+  return n1 * 8u >= 128u * 8u + kw_words ? 4u + 128u * 8u : 0u;
+}
+
+void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint32_t* lds_bytes, uint32_t* duo_kw_word) {
+  *duo_kw_word = 0;
   // One packed tree wave per partition (Q = 1, B > 128) has a critical path of 34 dependent
   // compressions at B = 1,000; two waves per partition (tree_body over 128 threads) cut it to 24.
   // With many partitions the trees, not the stream, bound a small arena: 800 MB of 8-byte values
@@ -1168,6 +1162,7 @@ void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint
     *Q = 0;
     *blocks = P;
     *lds_bytes = tree_lds_words(B) * 4u;
+    *duo_kw_word = duo_step_kw_word(B, lds_bytes);
     return;
   }
   *Q = q;
@@ -1176,19 +1171,20 @@ void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint
 }
 
 hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st) {
-  uint32_t tree_blocks = 0, Q = 0, lds = a.lds_bytes;
+  uint32_t tree_blocks = 0, Q = 0, lds = a.lds_bytes, kw_word = 0;
   if (t && t->P) {
     // every partition of a fused step has t->B buckets (no per-tree n_in)
     if (!build_step_fusable(t->B) || !t->sums_in || t->n_in) return hipErrorInvalidValue;
     uint32_t tree_lds = 0;
-    plan_step_trees(t->B, t->P, &Q, &tree_blocks, &tree_lds);
+    plan_step_trees(t->B, t->P, &Q, &tree_blocks, &tree_lds, &kw_word);
     // every workgroup of the dispatch reserves the tree waves' LDS; kStepTreeLdsMax keeps the
     // streaming grid fully resident
     lds = std::max<uint32_t>(lds, tree_lds);
   }
   const uint32_t digest_blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);
   if (tree_blocks + digest_blocks == 0) return hipSuccess;
-  const TreeLaunch tl = t ? *t : TreeLaunch{};
+  TreeLaunch tl = t ? *t : TreeLaunch{};
+  tl.duo_kw_word = kw_word;
   hipLaunchKernelGGL(variant(a.variant).step, dim3(tree_blocks + digest_blocks), dim3(kThreads), lds, st, a, tl,
                      tree_blocks, Q);
   return hipGetLastError();

@@ -152,9 +152,10 @@ __device__ __forceinline__ void sha256_compress_pad64(uint32_t st[8]) {
 // wave of the workgroup, computes W16..63 (pre-added to K) and hands them over through LDS in three
 // 16-word chunks, each published behind a workgroup barrier four rounds before the compute thread
 // needs it (the LDS read latency hides under those four rounds). Both sides execute exactly three
-// barriers per node, so every wave of the workgroup must call one side or the other (or
-// duo_idle()) the same number of times. kw: this thread's slot of a [12][stride] u32x4 array
-// (chunk c of 16 words = slots 4c .. 4c+3).
+// barriers per node, so every wave of the workgroup must call one side or the other the same
+// number of times. kw: this thread's slot of a [8][stride] u32x4 ring of two chunks (chunk c of 16
+// words = slots 4 (c % 2) .. +3): the helper writes chunk c + 2 only after the barrier that
+// follows the compute side's reads of chunk c (a barrier waits for the wave's LDS reads).
 #define MDE_SHA_4A(KW)                                     \
   MDE_SHA_ROUND(a, b, c, d, e, f, g, h, KW(0));            \
   MDE_SHA_ROUND(h, a, b, c, d, e, f, g, KW(1));            \
@@ -188,8 +189,9 @@ __device__ __forceinline__ void sha256_node_duo_main(const uint32_t hl[8], const
 #pragma unroll
   for (int cn = 0; cn < 3; cn++) {
     __syncthreads();  // chunk cn = K+W of rounds 16(cn+1) .. 16(cn+1)+15 is in LDS
-    const u32x4 v0 = kw[(4 * cn + 0) * stride], v1 = kw[(4 * cn + 1) * stride];
-    const u32x4 v2 = kw[(4 * cn + 2) * stride], v3 = kw[(4 * cn + 3) * stride];
+    const int r = 4 * (cn & 1);
+    const u32x4 v0 = kw[(r + 0) * stride], v1 = kw[(r + 1) * stride];
+    const u32x4 v2 = kw[(r + 2) * stride], v3 = kw[(r + 3) * stride];
     if (cn == 0) {
       MDE_SHA_4B(MDE_KWM12);
     } else {
@@ -225,7 +227,7 @@ __device__ __forceinline__ void sha256_node_duo_sched(const uint32_t hl[8], cons
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int r = 16 * (cn + 1) + 4 * q;
-      kw[(4 * cn + q) * stride] = u32x4{kK[r] + w[4 * q], kK[r + 1] + w[4 * q + 1], kK[r + 2] + w[4 * q + 2],
+      kw[(4 * (cn & 1) + q) * stride] = u32x4{kK[r] + w[4 * q], kK[r + 1] + w[4 * q + 1], kK[r + 2] + w[4 * q + 2],
                                         kK[r + 3] + w[4 * q + 3]};
     }
     __syncthreads();

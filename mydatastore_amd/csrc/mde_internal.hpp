@@ -113,6 +113,9 @@ struct TreeLaunch {
   // sums_in / sums_clear hold buckets [sums_base, ...) (the one-launch small build keeps each
   // workgroup's bucket sums in LDS)
   uint64_t sums_base = 0;
+  // Fused build step, one partition per tree workgroup (Q = 0): LDS word of the split-schedule
+  // K+W ring (tree_body_duo), 0 = plain tree_body. Set by the step launchers (plan_step_trees).
+  uint32_t duo_kw_word = 0;
 };
 constexpr uint32_t kTreeLdsMaxBuckets = 4096;
 constexpr uint32_t kTreePairLdsMax = 64u * 1024u;  // standalone pair-shape trees (B <= 2,728)
@@ -142,7 +145,8 @@ uint32_t build_step_tree_q(uint32_t B);  // partitions per packed tree wave
 // tree_body); blocks = tree workgroups, lds_bytes = their LDS.
 constexpr uint32_t kStepTreeWideThreads = 128;
 constexpr uint32_t kStepTreeWideMinPartitions = 512;
-void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint32_t* lds_bytes);
+// duo_kw_word: see TreeLaunch::duo_kw_word (may raise lds_bytes within kStepTreeLdsMax).
+void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint32_t* lds_bytes, uint32_t* duo_kw_word);
 hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st);
 // One-launch build of a small layout-A arena (digest.hip small_build_kernel): each workgroup sums
 // its partitions' buckets into LDS and builds their trees from there (t.sums_in is not used).

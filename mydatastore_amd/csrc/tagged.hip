@@ -392,17 +392,18 @@ hipError_t launch_tagged_digest(TaggedLaunch& a, hipStream_t st) {
 
 hipError_t launch_tagged_step(TaggedLaunch& a, const TreeLaunch* t, hipStream_t st) {
   const size_t bins = a.n_waves ? prepare_tagged(a) : 0;
-  uint32_t tree_blocks = 0, Q = 0;
+  uint32_t tree_blocks = 0, Q = 0, kw_word = 0;
   size_t lds = bins;
   if (t && t->P) {
     if (!build_step_fusable(t->B) || !t->sums_in || t->n_in) return hipErrorInvalidValue;
     uint32_t tree_lds = 0;
-    plan_step_trees(t->B, t->P, &Q, &tree_blocks, &tree_lds);
+    plan_step_trees(t->B, t->P, &Q, &tree_blocks, &tree_lds, &kw_word);
     lds = std::max<size_t>(lds, (size_t)tree_lds);
   }
   const uint32_t blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);
   if (tree_blocks + blocks == 0) return hipSuccess;
-  const TreeLaunch tl = t ? *t : TreeLaunch{};
+  TreeLaunch tl = t ? *t : TreeLaunch{};
+  tl.duo_kw_word = kw_word;
   hipLaunchKernelGGL(tagged_step_kernel, dim3(tree_blocks + blocks), dim3(kThreads), lds, st, a, tl, tree_blocks, Q);
   return hipGetLastError();
 }

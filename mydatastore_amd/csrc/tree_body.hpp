@@ -348,12 +348,14 @@ __device__ __forceinline__ void tree_body_pair(const TreeLaunch& a, uint32_t blo
 // (sha256_node_duo_main / _sched: 64 + 14 x 64 instead of ~2,340 instructions on the critical
 // path of each level). Partitions: G <= half -> half / G per workgroup, held by the lower half;
 // G = 2 x half (a wide tree, level 1 > 64 nodes) -> one per workgroup, whose levels wider than
-// `half` nodes (and level 1) run over all threads as in tree_body. Uniform B (no n_in), levels in
-// LDS. kw: duo_kw_bytes(half) of LDS.
-__host__ __device__ inline uint32_t duo_kw_bytes(uint32_t half) { return 12u * 16u * half; }
+// `half` nodes (and level 1) run over all threads as in tree_body. Threads from 2 x half on leave
+// at once. Uniform B (no n_in), levels in LDS. kw: duo_kw_bytes(half) of LDS, touched only on
+// split levels (it may overlay level-buffer space those levels do not use, duo_step_kw_word).
+__host__ __device__ inline uint32_t duo_kw_bytes(uint32_t half) { return 8u * 16u * half; }
 
 __device__ __forceinline__ void tree_body_duo(const TreeLaunch& a, uint32_t G, uint32_t lds_words, uint32_t block,
                                               uint32_t* lds, uint32_t half, u32x4* kw) {
+  if (threadIdx.x >= 2 * half) return;
   const uint32_t x = threadIdx.x;
   const bool wide = G > half;
   const bool upper = x >= half;
@@ -450,7 +452,11 @@ __device__ __forceinline__ void step_trees(const TreeLaunch& t, uint32_t Q, uint
 #ifdef MDE_STEP_WIDE_PRIO  // probe only: wide-tree waves at this priority beside the stream
     __builtin_amdgcn_s_setprio(MDE_STEP_WIDE_PRIO);
 #endif
-    tree_body<true>(t, kStepTreeWideThreads, tree_lds_words(t.B), block, lds, kStepTreeWideThreads);
+    if (t.duo_kw_word)  // the second wave computes the first's message schedules on its <= 64-node levels
+      tree_body_duo(t, kStepTreeWideThreads, tree_lds_words(t.B), block, lds, kStepTreeWideThreads / 2,
+                    reinterpret_cast<u32x4*>(lds + t.duo_kw_word));
+    else
+      tree_body<true>(t, kStepTreeWideThreads, tree_lds_words(t.B), block, lds, kStepTreeWideThreads);
   }
 }
 
