@@ -263,7 +263,9 @@ int mde_decode_epoch_tree_objects(mde_ctx* ctx, uint32_t n, const uint8_t* bytes
  *                    Valid = valid[p], at object_out + p*object_stride (length object_len[p]).
  * partition may be NULL (0). n_buckets <= 65536. A peer object with more than
  * mde_verify_peer_capacity(n_buckets) buckets builds a deeper tree, which the reference's diff
- * always rejects; it is reported as MDE_E_TREE without being rebuilt. */
+ * always rejects; it is reported as MDE_E_TREE without being rebuilt. Every output is stored
+ * exactly once and never read back by the call (the _async form may point them at pinned host
+ * memory mapped into the device address space). */
 uint32_t mde_verify_peer_capacity(uint32_t n_buckets);
 /* Unknown groups nested deeper than 64 levels (a hostile peer object) spill their group numbers
  * to a per-context device area, so decoding stays linear in the object bytes however the nesting

@@ -465,8 +465,7 @@ void launch_verify(mde_batcher* b, mde_batcher::Slot* sl) {
   uint8_t* din = static_cast<uint8_t*>(sl->dev_in.p);
   uint8_t* dout = static_cast<uint8_t*>(sl->dev_out.p);
   BHIP(hipSetDevice(b->device));
-  // valid and the peer statuses are read back inside the launch (the fold, the encode): device
-  // memory, copied; the counts, ids and objects are stored once, straight into pinned memory
+  // every verify output is stored once by the launch: straight into pinned memory
   uint8_t* mapped = mapped_out(b, sl);
   uint8_t* wout = mapped ? mapped : dout;
   BHIP(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, st));
@@ -480,9 +479,9 @@ void launch_verify(mde_batcher* b, mde_batcher::Slot* sl) {
   // when a peer of another shape needs its inner nodes
   rc = mde_verify_epochs_async(sl->ctx, (uint32_t)P, B, reinterpret_cast<const int32_t*>(din + i_part), epoch, d_dig,
                                reinterpret_cast<const int32_t*>(din + i_size), nullptr, R, din + i_peer,
-                               reinterpret_cast<const uint64_t*>(din + i_off), rcount, dout + o[0],
+                               reinterpret_cast<const uint64_t*>(din + i_off), rcount, wout + o[0],
                                reinterpret_cast<int32_t*>(wout + o[1]), reinterpret_cast<int32_t*>(wout + o[2]),
-                               reinterpret_cast<int32_t*>(wout + o[3]), reinterpret_cast<int32_t*>(dout + o[4]),
+                               reinterpret_cast<int32_t*>(wout + o[3]), reinterpret_cast<int32_t*>(wout + o[4]),
                                want_obj ? wout + o[6] : nullptr, stride,
                                want_obj ? reinterpret_cast<uint32_t*>(wout + o[5]) : nullptr);
   if (rc) {
@@ -490,12 +489,7 @@ void launch_verify(mde_batcher* b, mde_batcher::Slot* sl) {
     return;
   }
   uint8_t* hout = static_cast<uint8_t*>(sl->pin_out.p);
-  if (mapped) {
-    BHIP(hipMemcpyAsync(hout + o[0], dout + o[0], P, hipMemcpyDeviceToHost, st));
-    if (R) BHIP(hipMemcpyAsync(hout + o[4], dout + o[4], P * R * 4, hipMemcpyDeviceToHost, st));
-  } else {
-    BHIP(hipMemcpyAsync(hout, dout, o[7], hipMemcpyDeviceToHost, st));
-  }
+  if (!mapped) BHIP(hipMemcpyAsync(hout, dout, o[7], hipMemcpyDeviceToHost, st));
   BHIP(hipEventRecord(sl->done, st));
   bt->launched = true;
 }

@@ -1420,14 +1420,16 @@ int verify_async(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, i
   const uint32_t cap = mde_verify_peer_capacity(B);
   if (!cap) return set_err(c, MDE_E_INVAL, "n_buckets too large");
   const uint64_t NI = mde::tree_internal(cap), idcap = mde_diff_capacity(B, cap);
-  // scratch: digests, sizes, bucket counts, valid flags, nodes, roots, diff ids, statuses; without
-  // local nodes (nodes == NULL) also the local trees' nodes and roots, built where needed
+  // scratch: digests, sizes, bucket counts, valid flags, nodes, roots, diff ids, statuses, the
+  // partitions' valid flags (the encoder reads them; the caller's `valid` and `peer_status` are
+  // stored once by the fold, so they may be pinned host memory); without local nodes
+  // (nodes == NULL) also the local trees' nodes and roots, built where needed
   const uint64_t NL = mde::tree_internal(B);
-  const uint64_t part[10] = {T * cap * 8, T * cap * 4, T * 4, T, T * NI * 32, T * 32, T * idcap * 4, T * 4,
-                             nodes ? 0 : (uint64_t)P * NL * 32, nodes ? 0 : (uint64_t)P * 32};
-  uint64_t off[11] = {0};
-  for (int i = 0; i < 10; i++) off[i + 1] = off[i] + ((part[i] + 255) & ~255ull);
-  int rc = ensure_buf(c, c->verify_scratch, off[10]);
+  const uint64_t part[11] = {T * cap * 8, T * cap * 4, T * 4, T, T * NI * 32, T * 32, T * idcap * 4, T * 4,
+                             nodes ? 0 : (uint64_t)P * NL * 32, nodes ? 0 : (uint64_t)P * 32, P};
+  uint64_t off[12] = {0};
+  for (int i = 0; i < 11; i++) off[i + 1] = off[i] + ((part[i] + 255) & ~255ull);
+  int rc = ensure_buf(c, c->verify_scratch, off[11]);
   if (rc) return rc;
   uint8_t* base = static_cast<uint8_t*>(c->verify_scratch.p);
   auto at = [&](int i) { return static_cast<void*>(base + off[i]); };
@@ -1436,7 +1438,9 @@ int verify_async(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, i
   uint8_t* pvalid = static_cast<uint8_t*>(at(3));
   uint8_t* pnodes = static_cast<uint8_t*>(at(4));
   int32_t* pids = static_cast<int32_t*>(at(6));
-  int32_t* pst = peer_status ? peer_status : static_cast<int32_t*>(at(7));
+  int32_t* pst = static_cast<int32_t*>(at(7));
+  uint8_t* const valid_user = valid;
+  valid = static_cast<uint8_t*>(at(10));
   const bool build_local = !nodes;
   if (build_local) nodes = static_cast<const uint8_t*>(at(8));
   mde::TreeLaunch lt{};
@@ -1459,7 +1463,7 @@ int verify_async(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, i
     f.tree.n_int = NI;
     f.diff = mde::DiffLaunch{(uint32_t)T, B, cap, digest, nodes, pd, pnodes, pids, idcap, pst, R, nbk};
     f.fold = mde::VerifyLaunch{P, R, B, pst, pids, idcap, pvalid, replica_count, valid, valid_count, diff_ids,
-                               diff_count};
+                               diff_count, valid_user, peer_status};
     if (object_out)
       f.enc = mde::WireEncodeLaunch{P, B, partition, epoch, epoch + 1, digest, size, valid, nullptr,
                                     object_out, object_stride, object_len};
@@ -1487,7 +1491,8 @@ int verify_async(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partition, i
     mde::DiffLaunch df{(uint32_t)T, B, cap, digest, nodes, pd, pnodes, pids, idcap, pst, R, nbk};
     MDE_HIP(c, mde::launch_diff(df, c->stream));
   }
-  mde::VerifyLaunch v{P, R, B, pst, pids, idcap, pvalid, replica_count, valid, valid_count, diff_ids, diff_count};
+  mde::VerifyLaunch v{P, R, B, pst, pids, idcap, pvalid, replica_count, valid, valid_count, diff_ids, diff_count,
+                      valid_user, peer_status};
   MDE_HIP(c, mde::launch_verify(v, c->stream));
   if (object_out) {
     // the object VerifyEpoch persists: MerkleTreeToPartitionEpochObject(myTree, p, E, E+1) with Valid
@@ -1538,11 +1543,11 @@ int mde_verify_epochs(mde_ctx* c, uint32_t P, uint32_t B, const int32_t* partiti
   const int i_nodes = io.in(nodes, nodes ? N * NI * 32 : 0, nodes ? N * NI * 32 : 0);
   const int i_peer = io.in(nbytes ? peer_bytes + peer_off[0] : nullptr, nbytes, nbytes + 1);
   const int i_rel = io.in(rel.data(), (T + 1) * 8, (T + 1) * 8);
-  // valid and the peer statuses are read back inside the launch (the fold, the encode): device
-  // memory; the rest is stored once
-  const int o_valid = io.out(valid, N), o_vc = io.out(valid_count, N * 4, true),
+  // every output is stored once (valid and the peer statuses are also kept in device scratch for
+  // the fold and the encode to read back)
+  const int o_valid = io.out(valid, N, true), o_vc = io.out(valid_count, N * 4, true),
             o_ids = io.out(diff_ids, N * B * 4, true);
-  const int o_dc = io.out(diff_count, N * 4, true), o_ps = io.out(T ? peer_status : nullptr, T * 4);
+  const int o_dc = io.out(diff_count, N * 4, true), o_ps = io.out(T ? peer_status : nullptr, T * 4, true);
   const int o_obj = io.out(object_out, N * ostride, true),
             o_olen = io.out(object_out ? object_len : nullptr, N * 4, true);
   int rc = io.upload();

@@ -240,10 +240,14 @@ struct VerifyLaunch {
   uint64_t ids_stride;
   const uint8_t* peer_valid;   // [P*R] decoded EpochTreeObject.valid
   uint32_t replica_count;
-  uint8_t* valid;              // [P]
+  uint8_t* valid;              // [P] (read again by the encoder: device memory)
   int32_t* valid_count;        // [P]
   int32_t* diff_ids;           // [P*B] ascending, de-duplicated (utils.Int32Set)
   int32_t* diff_count;         // [P]
+  // the caller's copies, stored once at the end of the fold (so they may live in pinned host
+  // memory, no D2H copy): valid, and peer_status (may be null)
+  uint8_t* valid_out = nullptr;
+  int32_t* status_out = nullptr;
 };
 constexpr uint32_t kVerifyMaxBuckets = 1u << 16;
 hipError_t launch_verify(const VerifyLaunch& a, hipStream_t st);

@@ -95,10 +95,14 @@ __device__ __forceinline__ void verify_body(const VerifyLaunch& a, uint32_t p, u
     }
   }
   if (t == 0) {
+    const uint8_t v = (valid_count >= (int32_t)a.replica_count || valid_diff) ? 1 : 0;
     a.diff_count[p] = (int32_t)total;
     a.valid_count[p] = valid_count;
-    a.valid[p] = (valid_count >= (int32_t)a.replica_count || valid_diff) ? 1 : 0;
+    a.valid[p] = v;
+    if (a.valid_out) a.valid_out[p] = v;
   }
+  if (a.status_out)
+    for (uint32_t r = t; r < a.R; r += kThreads) a.status_out[(uint64_t)p * a.R + r] = a.peer_status[(uint64_t)p * a.R + r];
 }
 
 __global__ __launch_bounds__(kThreads) void verify_kernel(VerifyLaunch a) {
