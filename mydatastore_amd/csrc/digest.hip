@@ -907,6 +907,9 @@ __host__ __device__ __forceinline__ uint32_t small_build_kw_word(uint32_t groups
 template <bool kDuo>
 __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLaunch t, uint32_t G, uint32_t words) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+#ifdef MDE_SMALL_PROF  // probe only: digest-phase / tree-phase split of a one-workgroup launch
+  const uint64_t prof0 = wall_clock64();
+#endif
   const u32x4* base = reinterpret_cast<const u32x4*>(d.base);
   const uint32_t groups = small_build_groups(G, kDuo);
   const uint32_t s_beg = min(blockIdx.x * groups * t.B, d.S), s_end = min((blockIdx.x + 1) * groups * t.B, d.S);
@@ -944,12 +947,20 @@ __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLa
   tl.sums_in = sums;
   tl.sums_clear = nullptr;
   tl.sums_base = s_beg;
+#ifdef MDE_SMALL_PROF
+  const uint64_t prof1 = wall_clock64();
+#endif
   if (kDuo) {
     u32x4* kw = reinterpret_cast<u32x4*>(lds + small_build_kw_word(groups, words, t.B));
     tree_body_duo(tl, G, words, blockIdx.x, lds, (uint32_t)kThreads / 2, kw);
   } else {
     tree_body<true>(tl, G, words, blockIdx.x, lds, kThreads);
   }
+#ifdef MDE_SMALL_PROF
+  __syncthreads();
+  if (gridDim.x == 1 && threadIdx.x == 0)
+    printf("small_prof digest %lu tree %lu (x10ns)\n", prof1 - prof0, wall_clock64() - prof1);
+#endif
 }
 
 typedef void (*DigestKernel)(DigestLaunch);
@@ -986,34 +997,49 @@ const Variant& variant(int v) { return kVariants[(v >= 0 && v < kNumVariants) ? 
 
 int bucket_digest_variants() { return kNumVariants; }
 
+// LDS of one small-build workgroup: tree regions, bucket sums and counts, and in the split-schedule
+// form the K+W ring.
+size_t small_build_lds(const TreeGeometry& g, uint32_t B, bool duo) {
+  const uint32_t groups = small_build_groups(g.G, duo);
+  return duo ? (size_t)small_build_kw_word(groups, g.words, B) * 4u + duo_kw_bytes((uint32_t)kThreads / 2)
+             : (size_t)small_build_sums_word(groups, g.words) * 4u + (size_t)groups * B * 8u;
+}
+constexpr size_t kSmallBuildLdsMax = 160u * 1024u;  // one gfx950 CU
+
+// Split-schedule trees (latency form) unless that would take more than kDuoMaxBlocks
+// workgroups (a wide tree has one workgroup per partition either way; narrower trees pack half as
+// many partitions per workgroup) or more LDS than a CU has (B = 4,096: the plain form).
+bool small_build_duo(const TreeGeometry& g, uint32_t P, uint32_t B) {
+  const uint32_t groups_duo = small_build_groups(g.G, true);
+  const uint32_t blocks_duo = (P + groups_duo - 1) / groups_duo;
+  return tree_duo_enabled() && (g.G > (uint32_t)kThreads / 2 || blocks_duo <= kDuoMaxBlocks) &&
+         small_build_lds(g, B, true) <= kSmallBuildLdsMax;
+}
+
 // The one-launch build serves arenas of at most kSmallBuildMaxBytes per workgroup on average:
 // one workgroup streams its partitions' bytes alone (~0.1 TB/s), so larger arenas go to the
 // full-chip digest kernel + tree kernel instead.
 bool small_build_fits(uint64_t bytes, uint32_t P, uint32_t B) {
   TreeGeometry g;
   if (!tree_geometry(B, &g) || g.G > (uint32_t)kThreads || P < 1) return false;
-  const uint64_t blocks = (P + (uint64_t)kThreads / g.G - 1) / ((uint64_t)kThreads / g.G);
+  const bool duo = small_build_duo(g, P, B);
+  if (small_build_lds(g, B, duo) > kSmallBuildLdsMax) return false;
+  const uint32_t groups = small_build_groups(g.G, duo);
+  const uint64_t blocks = (P + (uint64_t)groups - 1) / groups;
   return bytes <= kSmallBuildMaxBytes * blocks;
 }
 
 hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t st) {
   TreeGeometry g;
   tree_geometry(t.B, &g);
-  // Split-schedule trees (latency form) unless that would take more than kDuoMaxBlocks
-  // workgroups: a wide tree has one workgroup per partition either way; narrower trees pack half
-  // as many partitions per workgroup.
-  const uint32_t groups_duo = small_build_groups(g.G, true);
-  const uint32_t blocks_duo = (t.P + groups_duo - 1) / groups_duo;
-  const bool duo = tree_duo_enabled() && (g.G > (uint32_t)kThreads / 2 || blocks_duo <= kDuoMaxBlocks);
+  const bool duo = small_build_duo(g, t.P, t.B);
   const uint32_t groups = small_build_groups(g.G, duo);
   const uint32_t blocks = (t.P + groups - 1) / groups;
-  if (duo) {
-    const size_t lds = (size_t)small_build_kw_word(groups, g.words, t.B) * 4u + duo_kw_bytes((uint32_t)kThreads / 2);
+  const size_t lds = small_build_lds(g, t.B, duo);
+  if (duo)
     hipLaunchKernelGGL(small_build_kernel<true>, dim3(blocks), dim3(kThreads), lds, st, d, t, g.G, g.words);
-  } else {
-    const size_t lds = (size_t)small_build_sums_word(groups, g.words) * 4u + (size_t)groups * t.B * 8u;
+  else
     hipLaunchKernelGGL(small_build_kernel<false>, dim3(blocks), dim3(kThreads), lds, st, d, t, g.G, g.words);
-  }
   return hipGetLastError();
 }
 

@@ -46,8 +46,8 @@ __device__ __forceinline__ uint64_t tree_leaf(const TreeLaunch& a, uint64_t s, u
     if (a.seg_rec) {
       sz = (uint32_t)(a.seg_rec[s + 1] - a.seg_rec[s]);
     } else {
-      sz = a.counts_in[s];
-      a.counts_in[s] = 0u;
+      sz = a.counts_in[s - a.sums_base];
+      a.counts_in[s - a.sums_base] = 0u;
     }
     if (a.size_out) a.size_out[s] = (int32_t)sz;
     items += sz;
