@@ -240,8 +240,8 @@ def production_shape(torch, eng, dev, threads, reps=10):
            "digest_frac": round(w.value_bytes / digest_us / 1e3 / HBM_PEAK_GBS, 4),
            "oracle_sample_partitions": int(s_n), "equals_c_oracle_on_sample": bool(ok),
            "note": "steady state of mde_build_pipelined_async (this build's digest + the previous build's "
-                   "1,024 trees of 1,000 leaves per launch); bound by the trees' dependent SHA-256 chain "
-                   "(DESIGN.md section 4.1)"}
+                   "1,024 trees of 1,000 leaves per launch); the rec8 stream sharing its CUs with the "
+                   "trees' SHA-256 waves (DESIGN.md sections 4.1, 4.2, 9)"}
     del w, sets
     torch.cuda.empty_cache()
     return res
