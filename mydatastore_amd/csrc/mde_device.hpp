@@ -145,6 +145,47 @@ __device__ __forceinline__ void sha256_compress_pad64(uint32_t st[8]) {
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
+// ---- Two-lane padding block (latency form) ----
+// A lane pair (even lane "E" = the e..h chain, odd lane "A" = the a..d chain) runs one padding-
+// block compression with 11 instructions per round instead of 14: both chains' big sigma and
+// Ch / Maj come from the same instructions (per-lane rotate amounts; Maj(a,b,c) = Ch(~(a^b), b, c)),
+// and two DPP quad permutes exchange T1 and d. Per round, with P = Sigma + Ch|Maj + KW (A: KW = 0):
+//   E: Q = P + h = T1;  A: P = T2;  new e = T1 + d (d: the A lane's x3),  new a = T1 + T2.
+// v: this lane's four state words (E: st[4..7], A: st[0..3]) in, its four hash words out.
+#define MDE_SHA2_ROUND(a, b, c, d, kw)                                                            \
+  do {                                                                                            \
+    const uint32_t dd_ = (uint32_t)__builtin_amdgcn_mov_dpp((int)(d), 0xF5, 0xF, 0xF, true);      \
+    const uint32_t s_ = xor3(__builtin_amdgcn_alignbit((a), (a), r1), __builtin_amdgcn_alignbit((a), (a), r2), \
+                             __builtin_amdgcn_alignbit((a), (a), r3));                             \
+    const uint32_t f_ = ch(__builtin_amdgcn_bitop3_b32((a), (b), m, 0xD2), (b), (c));             \
+    const uint32_t p_ = s_ + f_ + (kw);                                                           \
+    const uint32_t q_ = p_ + (d);                                                                 \
+    const uint32_t r_ = is_a ? p_ : dd_;                                                          \
+    (d) = (uint32_t)__builtin_amdgcn_mov_dpp((int)q_, 0xA0, 0xF, 0xF, true) + r_;                 \
+  } while (0)
+#define MDE_SHA2_4ROUNDS(KW)                 \
+  MDE_SHA2_ROUND(x0, x1, x2, x3, KW(0));     \
+  MDE_SHA2_ROUND(x3, x0, x1, x2, KW(1));     \
+  MDE_SHA2_ROUND(x2, x3, x0, x1, KW(2));     \
+  MDE_SHA2_ROUND(x1, x2, x3, x0, KW(3))
+
+__device__ __forceinline__ void sha256_pad64_pair(uint32_t v[4], bool is_a) {
+  const uint32_t r1 = is_a ? 2u : 6u, r2 = is_a ? 13u : 11u, r3 = is_a ? 22u : 25u, m = is_a ? ~0u : 0u;
+  uint32_t me = ~m;  // E lanes add the round constant, A lanes add 0 (one v_and per round)
+  asm volatile("" : "+v"(me));  // keep the AND: a known select costs a v_mov + v_cndmask
+  uint32_t x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3];
+#pragma unroll 1
+  for (int i = 0; i < 64; i += 8) {
+#define MDE_KW_PAD2(j) (kPad.kw[i + (j)] & me)
+#define MDE_KW_PAD2B(j) (kPad.kw[i + 4 + (j)] & me)
+    MDE_SHA2_4ROUNDS(MDE_KW_PAD2);
+    MDE_SHA2_4ROUNDS(MDE_KW_PAD2B);
+#undef MDE_KW_PAD2
+#undef MDE_KW_PAD2B
+  }
+  v[0] += x0; v[1] += x1; v[2] += x2; v[3] += x3;
+}
+
 // ---- Split-schedule node hash (latency form, tree_body_duo) ----
 // One wave issues at most one VALU instruction per ~4.6 cycles, so a lone dependent chain costs its
 // instruction count: the data block of SHA256(hl || hr) is 64 rounds of ~15 instructions plus 48
@@ -167,8 +208,11 @@ __device__ __forceinline__ void sha256_compress_pad64(uint32_t st[8]) {
   MDE_SHA_ROUND(c, d, e, f, g, h, a, b, KW(2));            \
   MDE_SHA_ROUND(b, c, d, e, f, g, h, a, KW(3))
 
+// kPair: the node's lane pair runs the data block redundantly, then the padding block in the
+// two-lane form; st[0..3] then holds this lane's four hash words (A: words 0..3, E: 4..7).
+template <bool kPair = false>
 __device__ __forceinline__ void sha256_node_duo_main(const uint32_t hl[8], const uint32_t hr[8], uint32_t st[8],
-                                                     const u32x4* kw, uint32_t stride) {
+                                                     const u32x4* kw, uint32_t stride, bool is_a = false) {
   uint32_t w[16];
 #pragma unroll
   for (int i = 0; i < 8; i++) { w[i] = hl[i]; w[8 + i] = hr[i]; }
@@ -212,7 +256,16 @@ __device__ __forceinline__ void sha256_node_duo_main(const uint32_t hl[8], const
 #undef MDE_KWV2
 #undef MDE_KWP3
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
-  sha256_compress_pad64(st);
+  if (kPair) {  // this lane's half of the state through the two-lane padding block (st[0..3] out)
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = is_a ? st[k] : st[4 + k];
+    sha256_pad64_pair(v, is_a);
+#pragma unroll
+    for (int k = 0; k < 4; k++) st[k] = v[k];
+  } else {
+    sha256_compress_pad64(st);
+  }
 }
 
 // The mirror side: the message schedule of the same node, published chunk by chunk.

@@ -31,6 +31,11 @@ __device__ __forceinline__ void store_node(uint32_t* dst, const uint32_t st[8]) 
   d[1] = u32x4{bswap(st[4]), bswap(st[5]), bswap(st[6]), bswap(st[7])};
 }
 
+// One lane's half of a node from the two-lane padding block: A lanes words 0..3, E lanes 4..7.
+__device__ __forceinline__ void store_half_node(uint32_t* dst, const uint32_t v[4], bool is_a) {
+  reinterpret_cast<u32x4*>(dst)[is_a ? 0 : 1] = u32x4{bswap(v[0]), bswap(v[1]), bswap(v[2]), bswap(v[3])};
+}
+
 // Leaf b of partition p: digest, and (when building from byte sums) its size/digest outputs.
 __device__ __forceinline__ uint64_t tree_leaf(const TreeLaunch& a, uint64_t s, uint32_t& items, uint32_t& sz_out) {
   uint64_t v;
@@ -409,17 +414,29 @@ __device__ __forceinline__ void tree_body_duo(const TreeLaunch& a, uint32_t G, u
         }
       }
     } else {  // split level: no lane skips the three barriers inside the duo functions
-      const uint32_t j = tid < m ? tid : 0u;
+      // two lanes per node when they fit (the padding block then runs in the two-lane form)
+      const bool pair = 2u * m <= (wide ? half : G);
+      const uint32_t slot = pair ? tid >> 1 : tid;
+      const bool is_a = pair && (tid & 1u);
+      const uint32_t j = slot < m ? slot : 0u;
       const uint32_t l = 2 * j, r = (2 * j + 1 < n) ? 2 * j + 1 : 2 * j;
       uint32_t hl[8], hr[8];
       load_node(cur + (uint64_t)l * 8, hl);
       load_node(cur + (uint64_t)r * 8, hr);
       if (!upper) {
         uint32_t st[8];
-        sha256_node_duo_main(hl, hr, st, kw + xm, half);
-        if (live && tid < m) {
-          store_node(nxt + (uint64_t)j * 8, st);
-          if (node_base) store_node(node_base + (level_off + n + j) * 8, st);
+        if (pair) {
+          sha256_node_duo_main<true>(hl, hr, st, kw + xm, half, is_a);
+          if (live && slot < m) {
+            store_half_node(nxt + (uint64_t)j * 8, st, is_a);
+            if (node_base) store_half_node(node_base + (level_off + n + j) * 8, st, is_a);
+          }
+        } else {
+          sha256_node_duo_main(hl, hr, st, kw + xm, half);
+          if (live && slot < m) {
+            store_node(nxt + (uint64_t)j * 8, st);
+            if (node_base) store_node(node_base + (level_off + n + j) * 8, st);
+          }
         }
       } else {
         sha256_node_duo_sched(hl, hr, kw + xm, half);
