@@ -1,8 +1,10 @@
 // merkle_gpu.go -- cgo shim: drop-in for the hot path of main/merkle_tree.go (MyDataStore).
 //
-// Copy into the reference's main/ package and delete RawPartitionMerkleTree and
-// DifferentMerkleTreeBuckets from merkle_tree.go (INTEGRATION.md section 2); VerifyEpoch may then
-// replace its peer loop (main/manager.go:1072-1104) with verifyEpochDecision. It binds only what
+// Copy into the reference's main/ package and delete RawPartitionMerkleTree from merkle_tree.go
+// (INTEGRATION.md section 2); VerifyEpoch may then replace its peer loop (main/manager.go:1072-1104)
+// with verifyEpochDecision. DifferentMerkleTreeBuckets stays the reference's own DFS: it compares
+// node hashes the trees already hold (<= 2B-1 byte compares, no hashing), which no device round
+// trip beats for one pair (tests/cpp/batch_bench.c diff_host / diff_device). It binds only what
 // include/mde.h declares (tests/test_integration.py checks every C.* name against the header).
 // Not compiled in this repository: the image has no Go toolchain (DESIGN.md section 1).
 package main
@@ -35,28 +37,17 @@ var (
 	// in flight into one device build / verify (group commit, mde_batch_build / mde_batch_verify).
 	// Each call gets its own error message back in its own buffer, so no lock is needed.
 	mdeBatcher *C.mde_batcher
-	// mdeCtx serves the unbatched calls (DifferentMerkleTreeBuckets). mdeMu pairs each call with
-	// its own error message; it costs no concurrency, since the context lock serialises calls on
-	// one context anyway.
-	mdeCtx *C.mde_ctx
-	mdeErr error
-	mdeMu  sync.Mutex
+	mdeErr     error
+	// mdeHostTree: build the returned trees with merkletree.NewTree over the device digests (B-1
+	// host SHA-256s per call, and the device root as a cross-check) instead of assembling them from
+	// the device's node hashes. Only callers of merkletree's own methods need it -- MerkleRoot(),
+	// VerifyTree(), RebuildTree() read unexported fields a tree literal cannot set; the reference
+	// calls MerkleRoot() in main/merkle_tree_test.go:90-92,150-152 only. Production reads the
+	// exported Root / Leafs / Left / Right / Hash / C (main/merkle_tree.go:122,160-216).
+	mdeHostTree = false
 )
 
-// mdeCall runs one engine call on mdeCtx and, when it fails, returns ITS message (copied under
-// the context lock by mde_last_error_copy while mdeMu is still held).
-func mdeCall(ctx *C.mde_ctx, name string, call func() C.int) error {
-	mdeMu.Lock()
-	defer mdeMu.Unlock()
-	if rc := call(); rc != C.MDE_OK {
-		var buf [512]C.char
-		C.mde_last_error_copy(ctx, &buf[0], C.uint64_t(len(buf)))
-		return errors.Errorf("%s: %s", name, C.GoString(&buf[0]))
-	}
-	return nil
-}
-
-func mdeEngine() (*C.mde_batcher, *C.mde_ctx, error) {
+func mdeEngine() (*C.mde_batcher, error) {
 	mdeOnce.Do(func() {
 		var b *C.mde_batcher
 		// at most 256 partitions per batch, no wait window: a batch is whatever queued while the
@@ -65,23 +56,57 @@ func mdeEngine() (*C.mde_batcher, *C.mde_ctx, error) {
 			mdeErr = errors.Errorf("mde_batcher_create: %s", C.GoString(C.mde_strerror(rc)))
 			return
 		}
-		var ctx *C.mde_ctx
-		if rc := C.mde_create(0, &ctx); rc != C.MDE_OK {
-			mdeErr = errors.Errorf("mde_create: %s", C.GoString(C.mde_strerror(rc)))
-			return
-		}
-		mdeBatcher, mdeCtx = b, ctx
+		mdeBatcher = b
 	})
-	return mdeBatcher, mdeCtx, mdeErr
+	return mdeBatcher, mdeErr
+}
+
+// mdeTree -- the *merkletree.MerkleTree NewTree would build over these buckets (cbergoon/merkletree
+// v0.2.0: a duplicate of the last leaf when B is odd, level nodes pairing (2j, 2j+1) and the last
+// node of an odd level paired with itself), assembled from the device's outputs without hashing:
+// nodes holds the internal node hashes level 1 .. root, 32 bytes each (mde_tree_out.nodes).
+func mdeTree(digest []uint64, size []int32, nodes []byte) *merkletree.MerkleTree {
+	B := len(digest)
+	t := &merkletree.MerkleTree{}
+	level := make([]*merkletree.Node, B, B+1)
+	for i := 0; i < B; i++ {
+		c := &MerkleBucket{bucketId: int32(i), hasher: &CustomHash{value: int64(digest[i])}, size: size[i]}
+		h, _ := c.CalculateHash()
+		level[i] = &merkletree.Node{Hash: h, C: c}
+	}
+	if B%2 == 1 {
+		last := level[B-1]
+		level = append(level, &merkletree.Node{Hash: last.Hash, C: last.C})
+	}
+	t.Leafs = level
+	off := 0
+	for len(level) > 1 {
+		next := make([]*merkletree.Node, (len(level)+1)/2)
+		for j := range next {
+			l, r := level[2*j], level[2*j]
+			if 2*j+1 < len(level) {
+				r = level[2*j+1]
+			}
+			h := nodes[(off+j)*32 : (off+j+1)*32 : (off+j+1)*32]
+			n := &merkletree.Node{Left: l, Right: r, Hash: h}
+			l.Parent, r.Parent = n, n
+			next[j] = n
+		}
+		off += len(next)
+		level = next
+	}
+	t.Root = level[0]
+	return t
 }
 
 func cU64(v []uint64) unsafe.Pointer { return C.CBytes(unsafe.Slice((*byte)(unsafe.Pointer(&v[0])), len(v)*8)) }
 
 // RawPartitionMerkleTree -- drop-in for main/merkle_tree.go:86-116. The per-bucket range scans are
 // unchanged; the values go into one arena that the MI355X engine reduces (bucket digests + SHA-256
-// tree on device), batched with the other partitions' calls in flight.
+// tree on device), batched with the other partitions' calls in flight; the tree comes back as its
+// node hashes and is assembled without hashing (mdeTree).
 func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, upperEpoch int64) (*merkletree.MerkleTree, error) {
-	batcher, _, err := mdeEngine()
+	batcher, err := mdeEngine()
 	if err != nil {
 		return nil, err
 	}
@@ -114,14 +139,17 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 	defer C.free(cValues)
 	defer C.free(cOff)
 	defer C.free(cSeg)
+	nodeBytes := 32 * int(C.mde_tree_internal_nodes(C.uint32_t(B)))
 	cDigest := C.malloc(C.size_t(8 * B))
 	cSize := C.malloc(C.size_t(4 * B))
 	cItems := C.malloc(4)
 	cRoot := C.malloc(32)
+	cNodes := C.malloc(C.size_t(nodeBytes))
 	defer C.free(cDigest)
 	defer C.free(cSize)
 	defer C.free(cItems)
 	defer C.free(cRoot)
+	defer C.free(cNodes)
 	rec := C.mde_records{
 		values: (*C.uint8_t)(cValues), values_bytes: C.uint64_t(len(values)),
 		value_off: (*C.uint64_t)(cOff), n_records: C.uint64_t(len(valueOff) - 1),
@@ -129,14 +157,19 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 	}
 	out := C.mde_tree_out{digest: (*C.uint64_t)(cDigest), size: (*C.int32_t)(cSize),
 		items: (*C.int32_t)(cItems), root: (*C.uint8_t)(cRoot)}
+	if !mdeHostTree {
+		out.nodes = (*C.uint8_t)(cNodes)
+	}
 	var errBuf [512]C.char
 	if rc := C.mde_batch_build(batcher, &rec, &out, &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
 		return nil, errors.Errorf("mde_batch_build: %s", C.GoString(&errBuf[0]))
 	}
-	digest := unsafe.Slice((*uint64)(cDigest), B)
-	size := unsafe.Slice((*int32)(cSize), B)
-	// Rebuild the reference's tree type from the device digests so every caller keeps its types;
-	// merkletree.NewTree costs B-1 host SHA-256s, and the device root cross-checks it.
+	digest := append([]uint64(nil), unsafe.Slice((*uint64)(cDigest), B)...)
+	size := append([]int32(nil), unsafe.Slice((*int32)(cSize), B)...)
+	if !mdeHostTree {
+		return mdeTree(digest, size, C.GoBytes(cNodes, C.int(nodeBytes))), nil
+	}
+	// merkletree.NewTree over the device digests (B-1 host SHA-256s); the device root cross-checks it.
 	bucketList := make([]merkletree.Content, B)
 	for i := 0; i < B; i++ {
 		bucketList[i] = &MerkleBucket{bucketId: int32(i), hasher: &CustomHash{value: int64(digest[i])}, size: size[i]}
@@ -151,58 +184,6 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 	return tree, nil
 }
 
-// DifferentMerkleTreeBuckets -- drop-in for main/merkle_tree.go:159-161 (DFS order, duplicates).
-func DifferentMerkleTreeBuckets(tree1 *merkletree.MerkleTree, tree2 *merkletree.MerkleTree) ([]int32, error) {
-	_, ctx, err := mdeEngine()
-	if err != nil {
-		return nil, err
-	}
-	digests := func(t *merkletree.MerkleTree) ([]uint64, error) {
-		n := len(t.Leafs)
-		if n > 1 && t.Leafs[n-1].C == t.Leafs[n-2].C { // merkletree's duplicate of the last leaf
-			n--
-		}
-		d := make([]uint64, n)
-		for i := 0; i < n; i++ {
-			b, ok := t.Leafs[i].C.(*MerkleBucket)
-			if !ok {
-				return nil, errors.New("failed to decode MerkleBucket")
-			}
-			d[i] = uint64(b.hasher.Hash())
-		}
-		return d, nil
-	}
-	d1, err := digests(tree1)
-	if err != nil {
-		return nil, err
-	}
-	d2, err := digests(tree2)
-	if err != nil {
-		return nil, err
-	}
-	capIds := C.mde_diff_capacity(C.uint32_t(len(d1)), C.uint32_t(len(d2)))
-	cA, cB := cU64(d1), cU64(d2)
-	defer C.free(cA)
-	defer C.free(cB)
-	cIds := C.malloc(C.size_t(4 * capIds))
-	cCount := C.malloc(4)
-	defer C.free(cIds)
-	defer C.free(cCount)
-	if err := mdeCall(ctx, "mde_diff", func() C.int {
-		return C.mde_diff_digests(ctx, 1, C.uint32_t(len(d1)), (*C.uint64_t)(cA), C.uint32_t(len(d2)),
-			(*C.uint64_t)(cB), (*C.int32_t)(cIds), capIds, (*C.int32_t)(cCount))
-	}); err != nil {
-		return nil, err
-	}
-	n := *(*int32)(cCount)
-	if n == C.MDE_E_TREE {
-		return nil, errors.New("bucketIds dont match (or a merkletree.Node is nil)")
-	}
-	out := make([]int32, n)
-	copy(out, unsafe.Slice((*int32)(cIds), n))
-	return out, nil
-}
-
 // verifyEpochDecision -- the decision step of Manager.VerifyEpoch (main/manager.go:1072-1104) in
 // one mde_batch_verify call, batched with the other partitions' decisions in flight: every peer
 // object is decoded, rebuilt and diffed against myTree on the device (myTree's own nodes are built
@@ -213,7 +194,7 @@ func DifferentMerkleTreeBuckets(tree1 *merkletree.MerkleTree, tree2 *merkletree.
 // calls PoliteStreamRequest(partitionId, epoch, epoch+1, diffSet).
 func verifyEpochDecision(myTree *merkletree.MerkleTree, partitionId int, epoch int64,
 	epochTreeObjects []*rpc.RpcEpochTreeObject, replicaCount int) (bool, int, []int32, []byte, error) {
-	batcher, _, err := mdeEngine()
+	batcher, err := mdeEngine()
 	if err != nil {
 		return false, 0, nil, nil, err
 	}

@@ -181,6 +181,15 @@ def diff_capacity(b1: int, b2: int) -> int:
     return int(load_library().mde_diff_capacity(b1, b2))
 
 
+def _build_outputs(P: int, B: int, want_nodes: bool, want_tree: bool) -> dict:
+    """Host output arrays of a build; a digest-only build (want_tree False) has no root / nodes."""
+    return {
+        "digest": np.zeros(P * B, np.uint64), "size": np.zeros(P * B, np.int32),
+        "items": np.zeros(P, np.int32), "root": np.zeros(P * 32, np.uint8) if want_tree else None,
+        "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes and want_tree else None,
+    }
+
+
 def _ptr(a) -> int:
     """Address of a numpy array or a torch tensor (None -> NULL)."""
     if a is None:
@@ -281,8 +290,9 @@ class Engine:
                        _ptr(value_off), n_records, n_partitions, n_buckets, _ptr(seg_rec))
 
     def build(self, values: np.ndarray, seg_rec: np.ndarray, n_partitions: int, n_buckets: int,
-              value_stride: int = 0, value_off: np.ndarray | None = None, want_nodes=True):
-        """RawPartitionMerkleTree for P partitions from host arrays (H2D, build, D2H)."""
+              value_stride: int = 0, value_off: np.ndarray | None = None, want_nodes=True, want_tree=True):
+        """RawPartitionMerkleTree for P partitions from host arrays (H2D, build, D2H).
+        want_tree=False: a digest-only build (root and nodes None: digests, sizes, items)."""
         P, B = n_partitions, n_buckets
         seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
         values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)
@@ -292,17 +302,14 @@ class Engine:
             values.size // value_stride if value_stride else 0)
         rec = Records(_ptr(values), values.nbytes, value_stride, 0, _ptr(value_off), n_rec, P, B,
                       _ptr(seg_rec))
-        out = {
-            "digest": np.zeros(P * B, np.uint64), "size": np.zeros(P * B, np.int32),
-            "items": np.zeros(P, np.int32), "root": np.zeros(P * 32, np.uint8),
-            "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
-        }
+        out = _build_outputs(P, B, want_nodes, want_tree)
         to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
         self._call("mde_build", C.byref(rec), C.byref(to))
         return out
 
     def build_streamed(self, values, seg_rec, n_partitions, n_buckets, value_stride=0,
-                       value_off=None, chunk_bytes=0, want_nodes=True, part_rec=None, bucket_tag=None):
+                       value_off=None, chunk_bytes=0, want_nodes=True, part_rec=None, bucket_tag=None,
+                       want_tree=True):
         """mde_build_streamed: host arena streamed through a two-slot device ring. `values` may
         be a numpy array or a (pinned) CPU torch tensor. Layout B: pass part_rec + bucket_tag
         (seg_rec None)."""
@@ -319,17 +326,13 @@ class Engine:
         else:
             seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
             rec = Records(_ptr(values), nbytes, value_stride, 0, _ptr(value_off), n_rec, P, B, _ptr(seg_rec))
-        out = {
-            "digest": np.zeros(P * B, np.uint64), "size": np.zeros(P * B, np.int32),
-            "items": np.zeros(P, np.int32), "root": np.zeros(P * 32, np.uint8),
-            "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
-        }
+        out = _build_outputs(P, B, want_nodes, want_tree)
         to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
         self._call("mde_build_streamed", C.byref(rec), C.byref(to), chunk_bytes)
         return out
 
     def build_tagged(self, values: np.ndarray, part_rec: np.ndarray, bucket_tag: np.ndarray,
-                     n_partitions: int, n_buckets: int, value_stride: int, want_nodes=True):
+                     n_partitions: int, n_buckets: int, value_stride: int, want_nodes=True, want_tree=True):
         """Layout B build: records grouped by partition in arrival order + bucket tags."""
         P, B = n_partitions, n_buckets
         values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)
@@ -337,11 +340,7 @@ class Engine:
         tags = np.ascontiguousarray(bucket_tag, dtype=np.uint16)
         rec = Records(_ptr(values), values.nbytes, value_stride, LAYOUT_TAGGED, 0,
                       values.size // value_stride, P, B, 0, _ptr(tags), _ptr(part_rec))
-        out = {
-            "digest": np.zeros(P * B, np.uint64), "size": np.zeros(P * B, np.int32),
-            "items": np.zeros(P, np.int32), "root": np.zeros(P * 32, np.uint8),
-            "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
-        }
+        out = _build_outputs(P, B, want_nodes, want_tree)
         to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
         self._call("mde_build", C.byref(rec), C.byref(to))
         return out
@@ -602,7 +601,7 @@ class Group:
         return int(self.lib.mde_group_size(self.g))
 
     def build(self, values, n_partitions, n_buckets, value_stride=0, value_off=None, seg_rec=None,
-              part_rec=None, bucket_tag=None, want_nodes=True, streamed=False, chunk_bytes=0):
+              part_rec=None, bucket_tag=None, want_nodes=True, streamed=False, chunk_bytes=0, want_tree=True):
         """mde_multi_build (or mde_multi_build_streamed) from host arrays (layout A with seg_rec,
         or layout B with part_rec + bucket_tag); same outputs as Engine.build."""
         P, B = n_partitions, n_buckets
@@ -619,11 +618,7 @@ class Group:
             seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
             rec = Records(_ptr(values), values.nbytes, value_stride, LAYOUT_SORTED, _ptr(value_off), n_rec, P, B,
                           _ptr(seg_rec))
-        out = {
-            "digest": np.zeros(P * B, np.uint64), "size": np.zeros(P * B, np.int32),
-            "items": np.zeros(P, np.int32), "root": np.zeros(P * 32, np.uint8),
-            "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
-        }
+        out = _build_outputs(P, B, want_nodes, want_tree)
         to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
         # the call and the copy of ITS message are one critical section (threads sharing a Group
         # cannot swap messages; the group lock serialises the builds anyway)
@@ -668,9 +663,10 @@ class Batcher:
         self.lib.mde_batcher_stats(self.b, *(C.byref(x) for x in v))
         return {"batches": v[0].value, "requests": v[1].value, "partitions": v[2].value}
 
-    def build(self, values, seg_rec, n_partitions, n_buckets, value_stride=0, value_off=None, want_nodes=True):
+    def build(self, values, seg_rec, n_partitions, n_buckets, value_stride=0, value_off=None, want_nodes=True,
+              want_tree=True):
         """mde_batch_build: RawPartitionMerkleTree for this caller's partitions; same outputs as
-        Engine.build."""
+        Engine.build (want_tree=False: digest-only)."""
         P, B = n_partitions, n_buckets
         seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
         values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)
@@ -678,11 +674,7 @@ class Batcher:
             value_off = np.ascontiguousarray(value_off, dtype=np.uint64)
         n_rec = (value_off.size - 1) if value_off is not None else (values.size // value_stride if value_stride else 0)
         rec = Records(_ptr(values), values.nbytes, value_stride, 0, _ptr(value_off), n_rec, P, B, _ptr(seg_rec))
-        out = {
-            "digest": np.zeros(P * B, np.uint64), "size": np.zeros(P * B, np.int32),
-            "items": np.zeros(P, np.int32), "root": np.zeros(P * 32, np.uint8),
-            "nodes": np.zeros(P * tree_internal_nodes(B) * 32, np.uint8) if want_nodes else None,
-        }
+        out = _build_outputs(P, B, want_nodes, want_tree)
         to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
         err = C.create_string_buffer(512)
         rc = self.lib.mde_batch_build(self.b, C.byref(rec), C.byref(to), err, len(err))

@@ -189,7 +189,7 @@ int check_build(Req* q) {
   if (r->layout != MDE_LAYOUT_SORTED) return fail(q, MDE_E_INVAL, "mde_batch_build takes layout A records");
   if (!r->seg_rec || !r->n_buckets || !r->n_partitions)
     return fail(q, MDE_E_INVAL, "seg_rec, n_buckets and n_partitions are required");
-  if (!q->out.root) return fail(q, MDE_E_INVAL, "out/root is NULL");
+  if (!q->out.root && q->out.nodes) return fail(q, MDE_E_INVAL, "out/nodes needs out/root");
   if ((uint64_t)r->n_partitions * r->n_buckets > 0xffffffffull)
     return fail(q, MDE_E_INVAL, "n_partitions * n_buckets exceeds 2^32");
   if (r->value_stride == 0 && !r->value_off && r->n_records)
@@ -216,16 +216,18 @@ int check_build(Req* q) {
   q->parts = r->n_partitions;
   q->key[0] = 1;
   q->key[1] = r->n_buckets;
+  q->key[2] = q->out.root ? 1 : 0;  // digest-only builds (root NULL) batch apart: no tree latency
   return MDE_OK;
 }
 
 bool same_key(const Req* a, const Req* b) { return std::memcmp(a->key, b->key, sizeof a->key) == 0; }
 
-// The leader's batch: the front request and every later compatible one, up to max_parts (and,
-// for builds, up to 2^32 buckets in all: mde_build's limit on n_partitions * n_buckets).
-std::vector<Req*> take(mde_batcher* b) {
+// The leader's batch: its own request (still queued: a leader only leads for its own request, so
+// the batch it then waits for is the one its outputs come from) and every other compatible queued
+// request in arrival order, up to max_parts (and, for builds, up to 2^32 buckets in all:
+// mde_build's limit on n_partitions * n_buckets).
+std::vector<Req*> take(mde_batcher* b, Req* first) {
   std::vector<Req*> out;
-  Req* first = b->q.front();
   const uint64_t per_part = first->kind == Kind::Build ? first->rec.n_buckets : 1;
   uint64_t parts = 0;
   for (auto it = b->q.begin(); it != b->q.end();) {
@@ -291,7 +293,11 @@ uint8_t* mapped_out(mde_batcher* b, mde_batcher::Slot* sl) {
 void launch_build(mde_batcher* b, mde_batcher::Slot* sl) {
   Batch* bt = &sl->bt;
   const std::vector<Req*>& v = bt->v;
+  // the batcher's device before any allocation (grow_slot) or event creation: the leader is
+  // whichever caller thread leads, whatever device it has current
+  BHIP(hipSetDevice(b->device));
   const uint32_t B = v[0]->rec.n_buckets;
+  const bool want_tree = v[0]->out.root != nullptr;  // same for the whole batch (request key)
   uint32_t stride = v[0]->rec.value_stride;
   for (Req* x : v)
     if (x->rec.value_stride != stride) stride = 0;  // mixed: variable-length offsets for all
@@ -311,7 +317,7 @@ void launch_build(mde_batcher* b, mde_batcher::Slot* sl) {
   o[1] = align256(S * 8);
   o[2] = o[1] + align256(S * 4);
   o[3] = o[2] + align256(P * 4);
-  o[4] = o[3] + align256(P * 32);
+  o[4] = o[3] + (want_tree ? align256(P * 32) : 0);
   const uint64_t out_bytes = o[4] + (want_nodes ? P * NI * 32 : 0);
   bt->B = B;
   bt->NI = NI;
@@ -343,7 +349,6 @@ void launch_build(mde_batcher* b, mde_batcher::Slot* sl) {
   hseg[S] = N;
   hipStream_t st = static_cast<hipStream_t>(mde_get_stream(sl->ctx));
   uint8_t* din = static_cast<uint8_t*>(sl->dev_in.p);
-  BHIP(hipSetDevice(b->device));
   // every build output is stored once by the tree pass (trees wider than the LDS levels re-read
   // their nodes: device memory and a copy for those)
   uint8_t* mapped = B <= 4096u ? mapped_out(b, sl) : nullptr;
@@ -360,7 +365,8 @@ void launch_build(mde_batcher* b, mde_batcher::Slot* sl) {
   dr.n_buckets = B;
   dr.seg_rec = reinterpret_cast<const uint64_t*>(din + o_seg);
   mde_tree_out to{reinterpret_cast<uint64_t*>(dout + o[0]), reinterpret_cast<int32_t*>(dout + o[1]),
-                  reinterpret_cast<int32_t*>(dout + o[2]), dout + o[3], want_nodes ? dout + o[4] : nullptr};
+                  reinterpret_cast<int32_t*>(dout + o[2]), want_tree ? dout + o[3] : nullptr,
+                  want_nodes ? dout + o[4] : nullptr};
   int brc = mde_build_async(sl->ctx, &dr, &to);
   if (brc) {
     ctx_error(sl->ctx, v, brc);
@@ -380,7 +386,7 @@ void scatter_build(const mde_batcher::Slot* sl, Req* x) {
   if (x->out.digest) std::memcpy(x->out.digest, hout + o[0] + pbase * B * 8, Pi * B * 8);
   if (x->out.size) std::memcpy(x->out.size, hout + o[1] + pbase * B * 4, Pi * B * 4);
   if (x->out.items) std::memcpy(x->out.items, hout + o[2] + pbase * 4, Pi * 4);
-  std::memcpy(x->out.root, hout + o[3] + pbase * 32, Pi * 32);
+  if (x->out.root) std::memcpy(x->out.root, hout + o[3] + pbase * 32, Pi * 32);
   if (x->out.nodes) std::memcpy(x->out.nodes, hout + o[4] + pbase * NI * 32, Pi * NI * 32);
 }
 
@@ -410,6 +416,7 @@ int check_verify(Req* q, uint64_t object_stride) {
 void launch_verify(mde_batcher* b, mde_batcher::Slot* sl) {
   Batch* bt = &sl->bt;
   const std::vector<Req*>& v = bt->v;
+  BHIP(hipSetDevice(b->device));  // before grow_slot (see launch_build)
   const uint32_t B = v[0]->B;
   const int64_t epoch = v[0]->epoch;
   const uint32_t rcount = v[0]->replica_count;
@@ -464,7 +471,6 @@ void launch_verify(mde_batcher* b, mde_batcher::Slot* sl) {
   hipStream_t st = static_cast<hipStream_t>(mde_get_stream(sl->ctx));
   uint8_t* din = static_cast<uint8_t*>(sl->dev_in.p);
   uint8_t* dout = static_cast<uint8_t*>(sl->dev_out.p);
-  BHIP(hipSetDevice(b->device));
   // every verify output is stored once by the launch: straight into pinned memory
   uint8_t* mapped = mapped_out(b, sl);
   uint8_t* wout = mapped ? mapped : dout;
@@ -535,18 +541,19 @@ bool free_slot(const mde_batcher* b) {
   return false;
 }
 
-// The leader's turn (lock held on entry and exit): take a batch into a free slot, pass the leader
-// role on (the next leader stages its batch while this one stages and runs), stage and launch with
-// the lock released, wait for the batch's event, then mark its callers ready: each copies its own
-// outputs out of the slot on its own thread, and the last one frees the slot.
-void lead(mde_batcher* b, std::unique_lock<std::mutex>& lk) {
+// The leader's turn (lock held on entry and exit; `r` = the leader's own request, still queued):
+// take a batch into a free slot, pass the leader role on (the next leader stages its batch while
+// this one stages and runs), stage and launch with the lock released, wait for the batch's event,
+// then mark its callers ready: each copies its own outputs out of the slot on its own thread, and
+// the last one frees the slot.
+void lead(mde_batcher* b, Req* r, std::unique_lock<std::mutex>& lk) {
   b->leading = true;
   if (b->max_wait_us) {  // let concurrent callers join, until the batch is full or the window ends
     const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(b->max_wait_us);
     for (;;) {
       uint64_t parts = 0;
       for (Req* x : b->q)
-        if (same_key(x, b->q.front())) parts += x->parts;
+        if (same_key(x, r)) parts += x->parts;
       if (parts >= b->max_parts || b->collect.wait_until(lk, until) == std::cv_status::timeout) break;
     }
   }
@@ -556,7 +563,7 @@ void lead(mde_batcher* b, std::unique_lock<std::mutex>& lk) {
   sl->busy = true;
   Batch& bt = sl->bt;
   bt = Batch{};
-  bt.v = take(b);
+  bt.v = take(b, r);
   uint64_t parts = 0;
   for (Req* x : bt.v) {
     parts += x->parts;
@@ -641,14 +648,17 @@ int submit(mde_batcher* b, Req* r) {
     }
     if (r->lead) {
       r->lead = false;
-      // the role may have gone stale (another caller took it, the queue drained, no free slot):
-      // then wait for a handoff or for this request's batch
-      if (!b->leading && free_slot(b) && !b->q.empty()) {
+      // Lead only while this request is still queued, so the leader waits for its own batch. A
+      // stale role (another leader took this request meanwhile, or is active, or no slot is free)
+      // is passed on to the oldest queued request instead of being dropped.
+      if (!r->slot && !b->leading && free_slot(b)) {
         if (b->profile && r->lead_t != std::chrono::steady_clock::time_point{}) {
           b->t_handoff += std::chrono::duration<double>(std::chrono::steady_clock::now() - r->lead_t).count();
           b->n_handoff++;
         }
-        lead(b, lk);
+        lead(b, r, lk);
+      } else {
+        handoff(b);
       }
       continue;
     }

@@ -947,6 +947,11 @@ __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLa
   tl.sums_in = sums;
   tl.sums_clear = nullptr;
   tl.sums_base = s_beg;
+  if (!t.root_out) {  // digest-only build: the leaf outputs of this workgroup's partitions, no tree
+    const uint32_t p0 = blockIdx.x * groups;
+    leaves_waves(tl, p0 + threadIdx.x / 64u, (uint32_t)kThreads / 64u, p0 + groups);
+    return;
+  }
 #ifdef MDE_SMALL_PROF
   const uint64_t prof1 = wall_clock64();
 #endif

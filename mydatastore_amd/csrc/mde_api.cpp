@@ -543,7 +543,7 @@ int tree_launch_for(mde_ctx* c, const mde_records* r, const mde_tree_out* o, uns
   t->root_out = o->root;
   t->nodes_out = o->nodes;
   t->n_int = mde::tree_internal(r->n_buckets);
-  if (!t->nodes_out && r->n_buckets > mde::kTreeLdsMaxBuckets) {
+  if (!t->nodes_out && o->root && r->n_buckets > mde::kTreeLdsMaxBuckets) {
     int rc = ensure_buf(c, c->nodes_scratch, (uint64_t)t->P * t->n_int * 32);
     if (rc) return rc;
     t->nodes_out = static_cast<uint8_t*>(c->nodes_scratch.p);
@@ -551,8 +551,17 @@ int tree_launch_for(mde_ctx* c, const mde_records* r, const mde_tree_out* o, uns
   return MDE_OK;
 }
 
+// Outputs of a build: any pointer may be NULL; root == NULL (nodes then NULL too) is a digest-only
+// build -- digests, sizes and items without the SHA-256 tree.
+int check_out(mde_ctx* c, const mde_tree_out* o) {
+  if (!o) return set_err(c, MDE_E_INVAL, "out is NULL");
+  if (!o->root && o->nodes) return set_err(c, MDE_E_INVAL, "out/nodes needs out/root");
+  return MDE_OK;
+}
+
 int tree_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
-  if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
+  int rc0 = check_out(c, o);
+  if (rc0) return rc0;
   const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
   int rc = ensure_sums(c, S);
   if (rc) return rc;
@@ -925,7 +934,7 @@ int mde_build_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   Guard g(c);
   int rc = check_records(c, r);
   if (rc) return rc;
-  if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
+  if ((rc = check_out(c, o))) return rc;
   return build_async_impl(c, r, o);
 }
 
@@ -950,7 +959,7 @@ int mde_build(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   int rc = check_records(c, r);
   if (rc) return rc;
   if ((rc = check_host_records(c, r))) return rc;
-  if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
+  if ((rc = check_out(c, o))) return rc;
   const uint64_t P = r->n_partitions, S = P * r->n_buckets, NI = mde::tree_internal(r->n_buckets);
   const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
   const uint64_t nvo = r->value_stride ? 0 : (r->n_records + 1);
@@ -964,7 +973,7 @@ int mde_build(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   const bool wo = r->n_buckets <= mde::kTreeLdsMaxBuckets;
   const int o_dig = io.out(o->digest, S * 8, wo), o_size = io.out(o->size, S * 4, wo),
             o_items = io.out(o->items, P * 4, wo);
-  const int o_root = io.out(o->root, P * 32, wo), o_nodes = io.out(o->nodes, o->nodes ? P * NI * 32 : 0, wo);
+  const int o_root = io.out(o->root, o->root ? P * 32 : 0, wo), o_nodes = io.out(o->nodes, o->nodes ? P * NI * 32 : 0, wo);
   if ((rc = io.upload())) return rc;
   mde_records dr = *r;
   dr.values = static_cast<const uint8_t*>(io.dev(i_val));
@@ -973,7 +982,7 @@ int mde_build(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   dr.part_rec = tagged ? static_cast<const uint64_t*>(io.dev(i_seg)) : nullptr;
   dr.bucket_tag = tagged ? static_cast<const uint16_t*>(io.dev(i_tag)) : nullptr;
   mde_tree_out dout{static_cast<uint64_t*>(io.dev(o_dig)), static_cast<int32_t*>(io.dev(o_size)),
-                    static_cast<int32_t*>(io.dev(o_items)), static_cast<uint8_t*>(io.dev(o_root)),
+                    static_cast<int32_t*>(io.dev(o_items)), o->root ? static_cast<uint8_t*>(io.dev(o_root)) : nullptr,
                     o->nodes ? static_cast<uint8_t*>(io.dev(o_nodes)) : nullptr};
   if ((rc = build_async_impl(c, &dr, &dout))) return rc;
   return io.download();

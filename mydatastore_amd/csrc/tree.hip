@@ -31,6 +31,13 @@ __global__ __launch_bounds__(256) void tree_pair_kernel(TreeLaunch a) {
   tree_body_pair(a, blockIdx.x, lds);
 }
 
+// Digest-only build (root_out == NULL): digest, size and items of each partition, no tree; one
+// wave per partition.
+__global__ __launch_bounds__(256) void leaves_kernel(TreeLaunch a) {
+  const uint32_t p = blockIdx.x * 4u + threadIdx.x / 64u;
+  leaves_waves(a, p, 1u << 30, p + 1);
+}
+
 }  // namespace
 
 uint32_t tree_levels(uint32_t B, uint32_t* sizes) {
@@ -85,6 +92,10 @@ bool tree_duo_enabled() {
 
 hipError_t launch_tree(const TreeLaunch& a, hipStream_t st) {
   if (a.P == 0) return hipSuccess;
+  if (!a.root_out) {  // digest-only build
+    hipLaunchKernelGGL(leaves_kernel, dim3((a.P + 3) / 4), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
   // Wide trees of many partitions: two per workgroup. 1,024 partitions at B = 1,000: 142 -> 119.5 us
   // (-16 %); at 128 partitions the 4-wave tree_body's shorter critical path wins, 61.5 vs 73 us
   // (profiles/r02an_pair_trees.jsonl, `tree_us`).

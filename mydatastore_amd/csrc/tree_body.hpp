@@ -61,6 +61,35 @@ __device__ __forceinline__ uint64_t tree_leaf(const TreeLaunch& a, uint64_t s, u
   return v;
 }
 
+// Digest-only build (mde_tree_out.root == NULL): the leaf outputs of partition p -- digest, size
+// and its share of items -- over `width` lanes (this thread is `lane`), with no SHA-256 tree. The
+// caller reduces the returned items over the lanes. The duplicate leaf of an odd B counts its
+// size twice, as the tree.Leafs walk does (main/merkle_tree.go:121-134).
+__device__ __forceinline__ uint32_t leaves_items(const TreeLaunch& a, uint32_t p, uint32_t lane, uint32_t width) {
+  uint32_t items = 0;
+  const uint64_t s0 = (uint64_t)p * a.B;
+  for (uint32_t b = lane; b < a.B; b += width) {
+    uint32_t sz = 0;
+    tree_leaf(a, s0 + b, items, sz);
+    if (b == a.B - 1 && (a.B & 1u)) items += sz;
+  }
+  return items;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// One wave per partition: partitions wave0, wave0 + waves, ... below a.P (leaves_items + items).
+__device__ __forceinline__ void leaves_waves(const TreeLaunch& a, uint32_t wave0, uint32_t waves, uint32_t p_end) {
+  const uint32_t lane = threadIdx.x % 64;
+  for (uint32_t p = wave0; p < p_end && p < a.P; p += waves) {
+    const uint32_t items = wave_sum_u32(leaves_items(a, p, lane, 64));
+    if (lane == 0 && a.items_out) a.items_out[p] = (int32_t)items;
+  }
+}
+
 // One workgroup (`block` = its index among the tree workgroups) builds threads / G trees with its
 // first `threads` threads (a multiple of 64): a "group" of G threads per partition. Waves past
 // `threads` leave at once, before any barrier (s_barrier waits only for waves still running).

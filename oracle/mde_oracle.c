@@ -56,11 +56,78 @@ static void sha256_block(uint32_t st[8], const uint8_t blk[64]) {
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
+/* The same compression with the x86 SHA extensions, as Go's crypto/sha256 uses them on amd64
+ * when the CPU has them (the reference is Go 1.20, main/go.mod:3): the CPU baseline then hashes
+ * at the rate the reference's own SHA-256 calls would. Chosen at run time (CPUID leaf 7, EBX bit
+ * 29); MDE_ORACLE_SHA=portable forces the portable path above (the two are compared in
+ * tests/test_oracle.py). */
+#if defined(__x86_64__)
+#include <cpuid.h>
+#include <immintrin.h>
+__attribute__((target("sha,sse4.1,ssse3"))) static void sha256_block_ni(uint32_t st[8], const uint8_t blk[64]) {
+  const __m128i mask = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+  __m128i tmp = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)&st[0]), 0xB1); /* CDAB */
+  __m128i s1 = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)&st[4]), 0x1B);  /* EFGH */
+  __m128i s0 = _mm_alignr_epi8(tmp, s1, 8);                                        /* ABEF */
+  s1 = _mm_blend_epi16(s1, tmp, 0xF0);                                             /* CDGH */
+  const __m128i abef = s0, cdgh = s1;
+  __m128i w[4];
+  for (int g = 0; g < 16; g++) { /* four rounds per group */
+    __m128i m;
+    if (g < 4) {
+      m = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(blk + 16 * g)), mask);
+    } else {
+      const __m128i a = w[g & 3], b = w[(g + 1) & 3], c = w[(g + 2) & 3], d = w[(g + 3) & 3];
+      m = _mm_sha256msg2_epu32(_mm_add_epi32(_mm_sha256msg1_epu32(a, b), _mm_alignr_epi8(d, c, 4)), d);
+    }
+    w[g & 3] = m;
+    __m128i k = _mm_add_epi32(m, _mm_loadu_si128((const __m128i*)&K256[4 * g]));
+    s1 = _mm_sha256rnds2_epu32(s1, s0, k);
+    s0 = _mm_sha256rnds2_epu32(s0, s1, _mm_shuffle_epi32(k, 0x0E));
+  }
+  s0 = _mm_add_epi32(s0, abef);
+  s1 = _mm_add_epi32(s1, cdgh);
+  tmp = _mm_shuffle_epi32(s0, 0x1B);                   /* FEBA */
+  s1 = _mm_shuffle_epi32(s1, 0xB1);                    /* DCHG */
+  _mm_storeu_si128((__m128i*)&st[0], _mm_blend_epi16(tmp, s1, 0xF0)); /* DCBA */
+  _mm_storeu_si128((__m128i*)&st[4], _mm_alignr_epi8(s1, tmp, 8));    /* HGFE */
+}
+
+static int sha_ni_usable(void) {
+  static int v = -1;
+  if (v < 0) {
+    unsigned a, b, c, d;
+    const char* e = getenv("MDE_ORACLE_SHA");
+    v = !(e && !strcmp(e, "portable")) && __get_cpuid_count(7, 0, &a, &b, &c, &d) && ((b >> 29) & 1u);
+  }
+  return v;
+}
+#endif
+
+static void sha256_compress(uint32_t st[8], const uint8_t blk[64]) {
+#if defined(__x86_64__)
+  if (sha_ni_usable()) {
+    sha256_block_ni(st, blk);
+    return;
+  }
+#endif
+  sha256_block(st, blk);
+}
+
+/* 1 when oracle_sha256 runs on the SHA extensions (reported with the CPU baseline). */
+int oracle_sha_ni(void) {
+#if defined(__x86_64__)
+  return sha_ni_usable();
+#else
+  return 0;
+#endif
+}
+
 void oracle_sha256(const uint8_t* msg, uint64_t len, uint8_t out[32]) {
   uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                     0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
   uint64_t i = 0;
-  for (; i + 64 <= len; i += 64) sha256_block(st, msg + i);
+  for (; i + 64 <= len; i += 64) sha256_compress(st, msg + i);
   uint8_t tail[128];
   uint64_t rem = len - i;
   memset(tail, 0, sizeof tail);
@@ -69,8 +136,8 @@ void oracle_sha256(const uint8_t* msg, uint64_t len, uint8_t out[32]) {
   uint64_t tl = (rem + 9 <= 64) ? 64 : 128;
   uint64_t bits = len * 8;
   for (int k = 0; k < 8; k++) tail[tl - 1 - k] = (uint8_t)(bits >> (8 * k));
-  sha256_block(st, tail);
-  if (tl == 128) sha256_block(st, tail + 64);
+  sha256_compress(st, tail);
+  if (tl == 128) sha256_compress(st, tail + 64);
   for (int k = 0; k < 8; k++) {
     out[4 * k] = (uint8_t)(st[k] >> 24); out[4 * k + 1] = (uint8_t)(st[k] >> 16);
     out[4 * k + 2] = (uint8_t)(st[k] >> 8); out[4 * k + 3] = (uint8_t)st[k];
@@ -379,4 +446,74 @@ int32_t oracle_diff(const uint64_t* d1, uint32_t b1, const uint64_t* d2, uint32_
   int rc = (r1 && r2) ? dfs(r1, r2, out, cap, &n) : -2;
   free(p1); free(p2);
   return rc ? rc : n;
+}
+
+/* ------------------------------------------------------------------ trees as node graphs */
+/* A merkletree.MerkleTree-shaped node graph (what a Go caller holds after NewTree), for timing the
+ * host-side steps of the production call shape (tests/cpp/batch_bench.c):
+ *   oracle_graph_build      -- merkletree.NewTree from digests (SHA-256 of every internal node);
+ *   oracle_graph_from_nodes -- the same graph assembled from node hashes computed elsewhere (the
+ *                              Go shim's tree from the device's nodes: no hashing);
+ *   oracle_graph_diff       -- DifferentMerkleTreeBucketsDFS over two graphs (main/merkle_tree.go:163-216),
+ *                              the reference's own diff of two trees it already holds. */
+typedef struct oracle_graph {
+  onode* pool;
+  onode* root;
+} oracle_graph;
+
+oracle_graph* oracle_graph_build(const uint64_t* digest, uint32_t n_buckets) {
+  oracle_graph* g = (oracle_graph*)calloc(1, sizeof *g);
+  if (!g || !n_buckets) { free(g); return NULL; }
+  g->root = build_nodes(digest, n_buckets, &g->pool);
+  if (!g->root) { free(g); return NULL; }
+  return g;
+}
+
+oracle_graph* oracle_graph_from_nodes(const uint64_t* digest, uint32_t n_buckets, const uint8_t* nodes) {
+  if (!n_buckets || !nodes) return NULL;
+  uint32_t sz[64];
+  uint32_t L = oracle_level_count(n_buckets, sz);
+  uint64_t total = 0;
+  for (uint32_t k = 0; k < L; k++) total += sz[k];
+  oracle_graph* g = (oracle_graph*)calloc(1, sizeof *g);
+  onode* all = (onode*)calloc(total, sizeof(onode));
+  if (!g || !all) { free(g); free(all); return NULL; }
+  onode* lvl = all;
+  for (uint32_t i = 0; i < sz[0]; i++) {
+    uint32_t src = i < n_buckets ? i : n_buckets - 1;
+    for (int k = 0; k < 8; k++) lvl[i].hash[k] = (uint8_t)(digest[src] >> (8 * k));
+    lvl[i].hlen = 8;
+    lvl[i].bucket_id = (int32_t)src;
+  }
+  uint64_t off = 0;
+  for (uint32_t k = 1; k < L; k++) {
+    onode* up = lvl + sz[k - 1];
+    for (uint32_t j = 0; j < sz[k]; j++) {
+      memcpy(up[j].hash, nodes + (off + j) * 32, 32);
+      up[j].hlen = 32;
+      up[j].left = &lvl[2 * j];
+      up[j].right = (2 * j + 1 < sz[k - 1]) ? &lvl[2 * j + 1] : &lvl[2 * j];
+      up[j].bucket_id = -1;
+    }
+    off += sz[k];
+    lvl = up;
+  }
+  g->pool = all;
+  g->root = lvl;
+  return g;
+}
+
+/* root hash (32 bytes) of a graph */
+const uint8_t* oracle_graph_root(const oracle_graph* g) { return g->root->hash; }
+
+int32_t oracle_graph_diff(const oracle_graph* a, const oracle_graph* b, int32_t* out, int32_t cap) {
+  int32_t n = 0;
+  int rc = dfs(a->root, b->root, out, cap, &n);
+  return rc ? rc : n;
+}
+
+void oracle_graph_free(oracle_graph* g) {
+  if (!g) return;
+  free(g->pool);
+  free(g);
 }

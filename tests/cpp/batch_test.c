@@ -129,6 +129,20 @@ static void* worker(void* arg) {
     if (i1 != i2 || i1 != i3) bad("items", t, k);
     if (memcmp(r1, r2, 32) || memcmp(r1, r3, 32)) bad("root", t, k);
     if (memcmp(n1, n2, NI * 32) || memcmp(n1, n3, NI * 32)) bad("nodes", t, k);
+    /* digest-only builds (root = NULL: no device tree), batched and per call */
+    {
+      uint64_t* d4 = xmalloc(B * 8ull);
+      int32_t* z4 = xmalloc(B * 4ull);
+      int32_t i4 = 0;
+      mde_tree_out o4 = {d4, z4, &i4, NULL, NULL};
+      rc = (k & 1) ? mde_batch_build(batcher, &rec, &o4, err, sizeof err) : mde_build(ctx, &rec, &o4);
+      if (rc) {
+        fprintf(stderr, "digest-only build: %d %s\n", rc, err);
+        exit(1);
+      }
+      if (memcmp(d4, d3, B * 8ull) || memcmp(z4, z3, B * 4ull) || i4 != i3) bad("digest-only", t, k);
+      free(d4), free(z4);
+    }
 
     /* VerifyEpoch decision: peers = agreeing, one bucket differing, absent, garbage, and (every
      * third call) another bucket count -- a different tree shape */
@@ -237,7 +251,15 @@ int main(int argc, char** argv) {
   uint8_t rr[32];
   mde_tree_out ob = {NULL, NULL, NULL, rr, NULL};
   const int rc_bad = mde_batch_build(batcher, &badr, &ob, err, sizeof err);
-  const int ok_bad = rc_bad == MDE_E_INVAL && strstr(err, "nondecreasing") != NULL;
+  const int bad_msg = strstr(err, "nondecreasing") != NULL;
+  /* nodes without root is not a digest-only build */
+  uint64_t segok[3] = {0, 4, 8};
+  uint8_t nn[64 * 32];
+  mde_tree_out on = {NULL, NULL, NULL, NULL, nn};
+  badr.seg_rec = segok;
+  const int rc_nodes = mde_batch_build(batcher, &badr, &on, err, sizeof err);
+  badr.seg_rec = segbad;
+  const int ok_bad = rc_bad == MDE_E_INVAL && bad_msg && rc_nodes == MDE_E_INVAL;
   printf("{\"test\": \"batch_test\", \"threads\": %d, \"calls_per_thread\": %d, \"builds_checked\": %ld, "
          "\"verifies_checked\": %ld, \"mismatches\": %ld, \"batches\": %" PRIu64 ", \"requests\": %" PRIu64
          ", \"partitions\": %" PRIu64 ", \"mean_requests_per_batch\": %.2f, \"bad_request_rejected\": %s}\n",

@@ -10,10 +10,13 @@
  *                       B bucket ranges and appends every value to ONE arena, record by record:
  *                       value_off grows by each value's length, seg_rec by the record count per
  *                       bucket, n_partitions = 1, value_stride = 0 (variable-length values); an
- *                       empty arena gets one padding byte. -> mde_batch_build.
- *   diff Ba Bb          DifferentMerkleTreeBuckets (main/merkle_tree.go:159-161): the two trees'
- *                       leaf digests with merkletree's duplicate of an odd last leaf dropped -- so a
- *                       tree rebuilt from an odd-B object keeps its B+1 leaves -> mde_diff_digests.
+ *                       empty arena gets one padding byte. -> mde_batch_build with the nodes
+ *                       output, then the shim's mdeTree: the *merkletree.MerkleTree assembled from
+ *                       the device's digests and node hashes (no host hashing; mirrored below).
+ *   diff Ba Bb          DifferentMerkleTreeBuckets (main/merkle_tree.go:159-216), which the shim no
+ *                       longer replaces: the reference's DFS over two trees of the shim's shape --
+ *                       mdeTree over mde_tree_from_digests' nodes (a tree rebuilt from an odd-B
+ *                       object has B+1 leaves, no duplicate) -- mirrored below.
  *   verify B p E rc R   VerifyEpoch's peer loop (main/manager.go:1072-1104): the local tree's
  *                       digests and sizes, R peer objects as wire bytes (absent = empty range)
  *                       -> mde_batch_verify.
@@ -23,7 +26,8 @@
  *   diff Ba Bb <Ba digests> <Bb digests>
  *   verify B p E rc R <B digests> <B sizes> <R hex objects>
  * Output, one line per op:
- *   build <digests> ; <sizes> ; <items> ; <root hex>
+ *   build <digests> ; <sizes> ; <items> ; <Root.Hash hex> ; <leaf count> <SHA-256 of the pre-order
+ *         walk: every node's Hash, and each leaf's bucketId as LE32>
  *   diff <count> <ids>            (count = MDE_E_TREE where the reference errors)
  *   verify <valid> <validCount> ; <diffSet> ; <peer statuses> ; <object hex>
  */
@@ -33,6 +37,90 @@
 #include <string.h>
 
 #include "mde.h"
+
+void oracle_sha256(const uint8_t* msg, uint64_t len, uint8_t out[32]); /* checker's SHA-256 */
+
+/* ---- the shim's mdeTree (integration/go/merkle_gpu.go), in C: merkletree v0.2.0's node graph
+ * (leaf Hash = LE64(digest), a duplicate of the last leaf when B is odd -- same Hash, same
+ * content --, level nodes pairing (2j, 2j+1) with the last of an odd level paired with itself)
+ * whose internal Hash fields are the device's node hashes, level 1 .. root. */
+typedef struct snode {
+  struct snode *left, *right;
+  const uint8_t* hash;
+  uint32_t hlen;
+  int32_t bucket; /* leaf content's bucketId; -1 for internal nodes (C == nil) */
+} snode;
+
+typedef struct {
+  snode* pool;
+  snode* root;
+  uint32_t n_leafs;
+  uint8_t* leaf_hash;
+} stree;
+
+static void* xmalloc(size_t n);
+
+static stree mde_tree(const uint64_t* digest, uint32_t B, const uint8_t* nodes) {
+  stree t;
+  const uint32_t n0 = B + (B & 1u);
+  t.pool = xmalloc(sizeof(snode) * (2 * (size_t)n0 + 64)); /* every level rounds up: < 2 n0 + depth */
+  t.leaf_hash = xmalloc((size_t)B * 8);
+  t.n_leafs = n0;
+  snode* level = t.pool;
+  for (uint32_t i = 0; i < B; i++) {
+    for (int k = 0; k < 8; k++) t.leaf_hash[(size_t)i * 8 + k] = (uint8_t)(digest[i] >> (8 * k));
+    level[i] = (snode){NULL, NULL, t.leaf_hash + (size_t)i * 8, 8, (int32_t)i};
+  }
+  if (B & 1u) level[B] = level[B - 1]; /* merkletree's duplicate leaf */
+  uint32_t n = n0;
+  snode* next = level + n0;
+  uint64_t off = 0;
+  while (n > 1) {
+    const uint32_t m = (n + 1) / 2;
+    for (uint32_t j = 0; j < m; j++) {
+      snode* l = &level[2 * j];
+      snode* r = 2 * j + 1 < n ? &level[2 * j + 1] : l;
+      next[j] = (snode){l, r, nodes + (off + j) * 32, 32, -1};
+    }
+    off += m;
+    level = next;
+    next += m;
+    n = m;
+  }
+  t.root = level;
+  return t;
+}
+
+/* DifferentMerkleTreeBucketsDFS (main/merkle_tree.go:163-216): 0, or -1 where it errors. */
+static int ref_dfs(const snode* a, const snode* b, int32_t* out, int32_t* n) {
+  if (!a && !b) return 0;
+  if (!a || !b) return -1;
+  if (a->hlen == b->hlen && !memcmp(a->hash, b->hash, a->hlen)) return 0;
+  if (!a->left && !a->right) {
+    if (a->bucket < 0 || b->bucket < 0 || a->bucket != b->bucket) return -1;
+    out[(*n)++] = a->bucket;
+    return 0;
+  }
+  if (ref_dfs(a->left, b->left, out, n)) return -1;
+  return ref_dfs(a->right, b->right, out, n);
+}
+
+static void walk(const snode* x, uint8_t** buf, uint64_t* len, uint64_t* cap) {
+  if (*len + 40 > *cap) {
+    *cap = *cap * 2 + 4096;
+    *buf = realloc(*buf, *cap);
+    if (!*buf) exit(1);
+  }
+  memcpy(*buf + *len, x->hash, x->hlen);
+  *len += x->hlen;
+  if (!x->left && !x->right) {
+    memcpy(*buf + *len, &x->bucket, 4);
+    *len += 4;
+    return;
+  }
+  walk(x->left, buf, len, cap);
+  walk(x->right, buf, len, cap);
+}
 
 static void* xmalloc(size_t n) {
   void* p = calloc(1, n ? n : 1);
@@ -134,18 +222,32 @@ int main(int argc, char** argv) {
       int32_t* size = xmalloc((uint64_t)B * 4);
       int32_t items = 0;
       uint8_t root[32];
-      mde_tree_out out = {digest, size, &items, root, NULL};
+      uint8_t* nodes = xmalloc(mde_tree_internal_nodes(B) * 32);
+      mde_tree_out out = {digest, size, &items, root, nodes};
       if ((rc = mde_batch_build(batcher, &rec, &out, err, sizeof err))) {
         fprintf(stderr, "mde_batch_build: %d %s\n", rc, err);
         return 1;
       }
+      stree t = mde_tree(digest, B, nodes);
+      uint8_t* wb = NULL;
+      uint64_t wl = 0, wc = 0;
+      walk(t.root, &wb, &wl, &wc);
+      uint8_t wsig[32];
+      oracle_sha256(wb, wl, wsig);
       printf("build");
       for (uint32_t b = 0; b < B; b++) printf(" %" PRIu64, digest[b]);
       printf(" ;");
       for (uint32_t b = 0; b < B; b++) printf(" %d", size[b]);
       printf(" ; %d ; ", items);
-      print_hex(root, 32);
+      print_hex(t.root->hash, 32);
+      printf(" ; %u ", t.n_leafs);
+      print_hex(wsig, 32);
       printf("\n");
+      if (memcmp(root, t.root->hash, 32)) {
+        fprintf(stderr, "device root differs from the assembled tree's root\n");
+        return 1;
+      }
+      free(wb), free(t.pool), free(t.leaf_hash), free(nodes);
       free(bucket), free(values), free(value_off), free(seg_rec), free(digest), free(size);
     } else if (!strcmp(op, "diff")) {
       const uint32_t Ba = (uint32_t)num(f), Bb = (uint32_t)num(f);
@@ -153,16 +255,21 @@ int main(int argc, char** argv) {
       uint64_t* db = xmalloc((uint64_t)Bb * 8);
       for (uint32_t i = 0; i < Ba; i++) da[i] = num(f);
       for (uint32_t i = 0; i < Bb; i++) db[i] = num(f);
-      const uint64_t capids = mde_diff_capacity(Ba, Bb);
-      int32_t* ids = xmalloc(capids * 4);
-      int32_t count = 0;
-      if ((rc = mde_diff_digests(ctx, 1, Ba, da, Bb, db, ids, capids, &count))) {
-        fprintf(stderr, "mde_diff_digests: %d %s\n", rc, mde_last_error(ctx));
+      uint8_t ra[32], rb[32];
+      uint8_t* na = xmalloc(mde_tree_internal_nodes(Ba) * 32);
+      uint8_t* nb = xmalloc(mde_tree_internal_nodes(Bb) * 32);
+      if ((rc = mde_tree_from_digests(ctx, 1, Ba, da, ra, na)) || (rc = mde_tree_from_digests(ctx, 1, Bb, db, rb, nb))) {
+        fprintf(stderr, "mde_tree_from_digests: %d %s\n", rc, mde_last_error(ctx));
         return 1;
       }
+      stree ta = mde_tree(da, Ba, na), tb = mde_tree(db, Bb, nb);
+      int32_t* ids = xmalloc(((uint64_t)Ba + Bb + 2) * 8);
+      int32_t count = 0;
+      if (ref_dfs(ta.root, tb.root, ids, &count)) count = MDE_E_TREE;
       printf("diff %d", count);
       for (int32_t i = 0; i < count; i++) printf(" %d", ids[i]);
       printf("\n");
+      free(ta.pool), free(ta.leaf_hash), free(tb.pool), free(tb.leaf_hash), free(na), free(nb);
       free(da), free(db), free(ids);
     } else if (!strcmp(op, "verify")) {
       const uint32_t B = (uint32_t)num(f);

@@ -68,12 +68,17 @@ def test_shim_names_exist_in_header():
 
 
 def test_shim_reimplements_the_reference_signatures():
-    """The two replaced functions keep the reference's Go signatures (main/merkle_tree.go:86,159)."""
+    """The replaced function keeps the reference's Go signature (main/merkle_tree.go:86); the
+    reference's own DifferentMerkleTreeBuckets (:159-216) stays, so the shim must not redefine it
+    (two definitions in package main would not compile), and the trees the shim returns carry the
+    exported fields that DFS reads (Root, Left, Right, Hash, C) plus Leafs (:122)."""
     src = GO.read_text()
+    code = re.sub(r"//.*", "", src)
     assert ("func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, upperEpoch int64) "
             "(*merkletree.MerkleTree, error)") in src
-    assert ("func DifferentMerkleTreeBuckets(tree1 *merkletree.MerkleTree, tree2 *merkletree.MerkleTree) "
-            "([]int32, error)") in src
+    assert "func DifferentMerkleTreeBuckets(" not in code
+    for field in ("t.Leafs", "t.Root", "Left: l, Right: r, Hash: h", "Hash: h, C: c"):
+        assert field in code, field
 
 
 # ---------------------------------------------------------------------------------------------
@@ -82,6 +87,24 @@ def test_shim_reimplements_the_reference_signatures():
 import pytest  # noqa: E402
 
 REPLAY = ROOT / "tests" / "cpp" / "build" / "shim_replay"
+
+
+def _walk_sig(root):
+    """SHA-256 of the tree's pre-order walk (shim_replay.c `walk`): every node's Hash, and each
+    leaf's bucketId as LE32 -- a self-paired node's subtree is walked twice, as the DFS does."""
+    import hashlib
+    import struct
+    out = bytearray()
+
+    def go(n):
+        out.extend(n.hash)
+        if n.left is None and n.right is None:
+            out.extend(struct.pack("<i", n.c.bucket_id))
+            return
+        go(n.left)
+        go(n.right)
+    go(root)
+    return hashlib.sha256(bytes(out)).hexdigest()
 
 
 def _replay_scenarios():
@@ -106,7 +129,7 @@ def _replay_scenarios():
         t = O.tree_from_digests(d, z)
         items = O.merkle_tree_to_partition_epoch_object(t, 0, 0, 1).items
         expect.append(f"build {' '.join(map(str, d))} ; {' '.join(map(str, z))} ; {items} ; "
-                      f"{t.merkle_root().hex()}")
+                      f"{t.merkle_root().hex()} ; {len(t.leafs)} {_walk_sig(t.root)}")
         return list(map(int, d)), list(map(int, z))
 
     build(31, 300, rng.integers(0, 41, 300))                  # variable lengths, empty values, odd B
@@ -115,8 +138,9 @@ def _replay_scenarios():
     build(30, 0, [])                                           # no records: one padding byte
     d31, z31 = build(31, 200, rng.integers(1, 17, 200))
 
-    # DifferentMerkleTreeBuckets: local B = 31 (merkletree duplicates the last leaf; the shim drops
-    # it) against a tree rebuilt from an odd-B object (B + 1 distinct leaves, kept by the shim)
+    # DifferentMerkleTreeBuckets (the reference's DFS over two trees of the shim's shape): local
+    # B = 31 (merkletree duplicates the last leaf) against a tree rebuilt from an odd-B object
+    # (B + 1 distinct leaves)
     def diff(local, peer_src):
         t1 = O.tree_from_digests(local)
         t2 = O.epoch_tree_object_to_merkle_tree(
@@ -174,8 +198,10 @@ def _replay_scenarios():
 def test_shim_call_sequences_replayed_from_c_match_oracle(tmp_path):
     """The Go shim's exact ABI call sequences (integration/go/merkle_gpu.go, which cannot be
     compiled here), replayed in C: RawPartitionMerkleTree's one-partition arena with value_off
-    built record by record -> mde_batch_build; DifferentMerkleTreeBuckets with B local leaves
-    against B + 1 peer leaves (odd-B object quirk, SURVEY App. A.2) -> mde_diff_digests;
+    built record by record -> mde_batch_build with nodes -> the tree assembled from the device's
+    node hashes (mdeTree: Root.Hash, leaf count and the whole pre-order walk equal NewTree's);
+    the reference's DFS over trees of that shape, B local leaves against B + 1 peer leaves
+    (odd-B object quirk, SURVEY App. A.2);
     verifyEpochDecision with agreeing, absent, garbage, Valid-differing and other-B peers ->
     mde_batch_verify. Every output equals the oracle's restatement of the reference
     (main/merkle_tree.go:86-216, main/manager.go:1072-1104)."""

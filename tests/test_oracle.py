@@ -179,3 +179,35 @@ def test_testmerkletreeraw_fixture(golden, coracle):
             assert out["size"].tolist() == tr["sizes"]
             assert out["root"].tobytes().hex() == tr["root"]
             assert out["nodes"].tobytes().hex() == tr["nodes"]
+
+
+def test_c_oracle_sha_paths_agree_with_hashlib():
+    """oracle/mde_oracle.c hashes on the x86 SHA extensions when the CPU has them (as Go's
+    crypto/sha256 does on amd64) and on the portable FIPS 180-4 code otherwise; both equal hashlib
+    on every message length around the padding boundaries, and the trees built on them agree."""
+    import subprocess
+    import sys
+    code = r'''
+import ctypes, hashlib, json, random, sys
+sys.path.insert(0, sys.argv[1])
+from tests.oracle_c import COracle
+co = COracle()
+r = random.Random(7)
+for n in list(range(0, 200)) + [4096, 100003]:
+    m = bytes(r.getrandbits(8) for _ in range(n))
+    assert co.sha256(m) == hashlib.sha256(m).digest(), n
+import numpy as np
+d = np.array([r.randrange(999999) for _ in range(1000)], np.uint64)
+print(json.dumps({"ni": int(co.L.oracle_sha_ni()), "root": co.tree(d, 1000)[0].hex()}))
+'''
+    import json
+    import os
+    from tests.conftest import ROOT
+    outs = []
+    for env in ({}, {"MDE_ORACLE_SHA": "portable"}):
+        r = subprocess.run([sys.executable, "-c", code, str(ROOT)], capture_output=True, text=True,
+                           env={**os.environ, **env}, timeout=120)
+        assert r.returncode == 0, r.stderr
+        outs.append(json.loads(r.stdout))
+    assert outs[1]["ni"] == 0
+    assert outs[0]["root"] == outs[1]["root"]

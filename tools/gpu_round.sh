@@ -1,10 +1,53 @@
-# One GPU session: full parity suite, smoke, default bench line, rocprofv3 profile of the default
-# bench workload (trace + FETCH_SIZE + WRITE_SIZE passes). Run on the GPU box from the repo root:
-#   TAG=r01d bash tools/gpu_round.sh
+# The GPU session launcher (run on the GPU box from the repo root). One tag, any of these steps,
+# in order; each step runs under its own time limit and the script stops at the first failure.
+#   TAG=r04a bash tools/gpu_round.sh tests smoke bench batch prof
+# Steps:
+#   tests   -m gpu parity suite            -> gpurun_out/$TAG/pytest_gpu.log
+#   smoke   __graft_entry__.smoke()        -> smoke.log
+#   bench   default bench line (N=1)       -> bench_default.json
+#   batch   tests/cpp/batch_bench (all)    -> batch_bench.jsonl
+#   prod    bench.py --config prod line    -> bench_prod.json
+#   prof    rocprofv3 trace + FETCH/WRITE PMC of the default bench (tools/profile.sh)
+#   sq      SQ counters of the default bench workload (one --pmc pass)
+# Extra bench flags: BENCH_ARGS="...".
 set -o pipefail
-mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${TAG:-r01d}
-bash tools/gpu_tests_bench.sh || exit 1
-bash tools/profile.sh $TAG c4 c4 || exit 1
-python tools/timeline.py gpurun_out/prof_${TAG}_c4/trace 8
+TAG=${TAG:-r04}
+O=gpurun_out/$TAG
+mkdir -p $O
+step() { echo "== $1 $(date +%T)"; }
+for s in "$@"; do
+  case $s in
+    tests)
+      step tests
+      timeout -k 10 1000 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread \
+        > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+      tail -3 $O/pytest_gpu.log ;;
+    smoke)
+      step smoke
+      timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+      cat $O/smoke.log ;;
+    bench)
+      step bench
+      timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
+      cat $O/bench_default.json ;;
+    prod)
+      step prod
+      timeout -k 10 300 python bench.py --config prod ${BENCH_ARGS:-} > $O/bench_prod.json 2> $O/bench_prod.err || { tail -20 $O/bench_prod.err; exit 1; }
+      cat $O/bench_prod.json ;;
+    batch)
+      step batch
+      timeout -k 10 300 tests/cpp/build/batch_bench 0.4 > $O/batch_bench.jsonl 2> $O/batch_bench.err || { tail -20 $O/batch_bench.err; exit 1; }
+      tail -1 $O/batch_bench.jsonl ;;
+    prof)
+      step prof
+      bash tools/profile.sh $TAG c4 c4 || exit 1 ;;
+    sq)
+      step sq
+      timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES \
+        --output-format csv -d $O/sq -o run -- python3 bench.py --profile ${BENCH_ARGS:-} --steps 3 --warmup 1 \
+        > $O/sq.json 2> $O/sq.err || { tail -20 $O/sq.err; exit 1; } ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
