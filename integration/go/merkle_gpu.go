@@ -18,7 +18,6 @@ package main
 import "C"
 
 import (
-	"bytes"
 	"sync"
 	"unsafe"
 
@@ -38,14 +37,21 @@ var (
 	// Each call gets its own error message back in its own buffer, so no lock is needed.
 	mdeBatcher *C.mde_batcher
 	mdeErr     error
-	// mdeHostTree: build the returned trees with merkletree.NewTree over the device digests (B-1
-	// host SHA-256s per call, and the device root as a cross-check) instead of assembling them from
-	// the device's node hashes. Only callers of merkletree's own methods need it -- MerkleRoot(),
+	// mdeHostTree: build every returned tree with merkletree.NewTree over the device digests (a
+	// digest-only device build; B-1 host SHA-256s per call) instead of assembling it from the
+	// device's node hashes. Callers of merkletree's own methods need it -- MerkleRoot(),
 	// VerifyTree(), RebuildTree() read unexported fields a tree literal cannot set; the reference
 	// calls MerkleRoot() in main/merkle_tree_test.go:90-92,150-152 only. Production reads the
 	// exported Root / Leafs / Left / Right / Hash / C (main/merkle_tree.go:122,160-216).
 	mdeHostTree = false
 )
+
+// mdeHostTreeMaxBuckets: at most this many buckets, the tree is NewTree's on the host over a
+// digest-only device build. A tree is a chain of dependent SHA-256 compressions: the CPU's SHA
+// extensions (which crypto/sha256 uses on amd64) run it in ~5 us at B = 64, the device in ~25 us
+// of one workgroup; at B = 1,000 the device's wide levels win, 45 vs ~80 us
+// (profiles/r04/*batch_bench*: shim_hosttree vs shim, INTEGRATION.md section 3).
+const mdeHostTreeMaxBuckets = 256
 
 func mdeEngine() (*C.mde_batcher, error) {
 	mdeOnce.Do(func() {
@@ -102,9 +108,9 @@ func mdeTree(digest []uint64, size []int32, nodes []byte) *merkletree.MerkleTree
 func cU64(v []uint64) unsafe.Pointer { return C.CBytes(unsafe.Slice((*byte)(unsafe.Pointer(&v[0])), len(v)*8)) }
 
 // RawPartitionMerkleTree -- drop-in for main/merkle_tree.go:86-116. The per-bucket range scans are
-// unchanged; the values go into one arena that the MI355X engine reduces (bucket digests + SHA-256
-// tree on device), batched with the other partitions' calls in flight; the tree comes back as its
-// node hashes and is assembled without hashing (mdeTree).
+// unchanged; the values go into one arena that the MI355X engine reduces, batched with the other
+// partitions' calls in flight: bucket digests always on the device; for B > mdeHostTreeMaxBuckets
+// the SHA-256 tree too, returned as its node hashes and assembled without hashing (mdeTree).
 func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, upperEpoch int64) (*merkletree.MerkleTree, error) {
 	batcher, err := mdeEngine()
 	if err != nil {
@@ -155,10 +161,11 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 		value_off: (*C.uint64_t)(cOff), n_records: C.uint64_t(len(valueOff) - 1),
 		n_partitions: 1, n_buckets: C.uint32_t(B), seg_rec: (*C.uint64_t)(cSeg),
 	}
+	hostTree := mdeHostTree || B <= mdeHostTreeMaxBuckets
 	out := C.mde_tree_out{digest: (*C.uint64_t)(cDigest), size: (*C.int32_t)(cSize),
-		items: (*C.int32_t)(cItems), root: (*C.uint8_t)(cRoot)}
-	if !mdeHostTree {
-		out.nodes = (*C.uint8_t)(cNodes)
+		items: (*C.int32_t)(cItems)}
+	if !hostTree { // else a digest-only build: root and nodes stay NULL
+		out.root, out.nodes = (*C.uint8_t)(cRoot), (*C.uint8_t)(cNodes)
 	}
 	var errBuf [512]C.char
 	if rc := C.mde_batch_build(batcher, &rec, &out, &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
@@ -166,22 +173,15 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 	}
 	digest := append([]uint64(nil), unsafe.Slice((*uint64)(cDigest), B)...)
 	size := append([]int32(nil), unsafe.Slice((*int32)(cSize), B)...)
-	if !mdeHostTree {
+	if !hostTree {
 		return mdeTree(digest, size, C.GoBytes(cNodes, C.int(nodeBytes))), nil
 	}
-	// merkletree.NewTree over the device digests (B-1 host SHA-256s); the device root cross-checks it.
+	// merkletree.NewTree over the device digests (B-1 host SHA-256s)
 	bucketList := make([]merkletree.Content, B)
 	for i := 0; i < B; i++ {
 		bucketList[i] = &MerkleBucket{bucketId: int32(i), hasher: &CustomHash{value: int64(digest[i])}, size: size[i]}
 	}
-	tree, err := merkletree.NewTree(bucketList)
-	if err != nil {
-		return nil, err
-	}
-	if !bytes.Equal(tree.MerkleRoot(), C.GoBytes(cRoot, 32)) {
-		return nil, errors.New("device root differs from merkletree root")
-	}
-	return tree, nil
+	return merkletree.NewTree(bucketList)
 }
 
 // verifyEpochDecision -- the decision step of Manager.VerifyEpoch (main/manager.go:1072-1104) in

@@ -72,6 +72,44 @@ struct SegWindow {
   }
 };
 
+// The bucket holding position x (segpos(lo) <= x < segpos(S)), with a register window loaded over
+// it (win.base <= s <= win.base + 31), for a wave's first step. The 64-ary search costs log64(S)
+// dependent seg_rec round trips -- 4 at the reference's default B = 1,000 over 1,024 partitions --
+// plus the window's, each 1-2 us on a loaded HBM, while every wave of the launch waits: the fixed
+// cost of a short launch (13.5 us of a 139 us production-shape digest, tools/size_probe.py). Layout
+// A positions grow with the bucket index and buckets hold similar byte counts, so an interpolated
+// guess from the arena bounds [first, last), one 64-lane sample every 32 buckets around it, and the
+// window at the sampled bracket take two round trips; a guess off by more than ~1,000 buckets
+// falls back to the search.
+__device__ __forceinline__ uint32_t seg_start(const SegDesc& d, uint32_t lo, uint64_t x, uint64_t first, uint64_t last,
+                                              int lane, SegWindow& win) {
+  const uint32_t S = d.S;
+  if (S - lo > 64u && last > first && x >= first) {
+    const double f = (double)(x - first) / (double)(last - first);
+    const int64_t i0 = (int64_t)(f * (double)S) - 32 * 32;
+    const int64_t idx = i0 + 32 * (int64_t)lane;
+    // monotone in the lane: samples below lo lie at or before x, samples past S after it
+    const bool pred = idx < (int64_t)lo ? true : (idx >= (int64_t)S ? false : segpos(d, (uint32_t)idx) <= x);
+    const int c = __popcll(__ballot(pred));
+    if (c > 0 && c < 64) {
+      const int64_t b = i0 + 32 * (int64_t)(c - 1);
+      const uint32_t base = b < (int64_t)lo ? lo : (uint32_t)b;
+      win.load(d, base, lane);
+      // n = 0 only at lo (x before the first record, e.g. the 16-byte-rounded first wave):
+      // bucket lo, as seg_search answers
+      const int n = __popcll(__ballot(win.start <= x));
+      if (n < 64) return base + (uint32_t)(n > 0 ? n - 1 : 0);
+      // 64 bucket starts at or before x (a run of empty buckets): search on from the window's end
+      const uint32_t s = seg_search(d, base + 63u, x, lane);
+      win.load(d, s, lane);
+      return s;
+    }
+  }
+  const uint32_t s = seg_search(d, lo, x, lane);
+  win.load(d, s, lane);
+  return s;
+}
+
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l);
@@ -425,28 +463,48 @@ __device__ __forceinline__ uint32_t digest_range_win(const DigestLaunch& a, uint
 //     step inside one bucket just byte-sums into the lane accumulators;
 //   * loads are buffer loads bounded by the wave range (no per-load address clamping; the last
 //     vector of the range may extend past its end, whose slots the prefix clamp at q excludes).
-// Needs value_stride == 8 and an 8-byte-aligned arena start (segpos multiples of 8), 4 KiB steps.
-__device__ __forceinline__ uint32_t rec8_swz(uint32_t w) { return w ^ (((w >> 6) & 1u) << 2); }
-constexpr uint32_t kRec8Sums = 528;                 // swizzled record words (512 + word 512 = 0)
-constexpr uint32_t kRec8WaveWords = kRec8Sums + 80;  // + 65 lane prefixes, padded
-constexpr uint32_t kRec8LdsBytes = kRec8WaveWords * 4u * (kThreads / 64);
+// Needs value_stride == 8 and an 8-byte-aligned arena start (segpos multiples of 8).
+// ROWS = 1 KiB rows per step: 4 (4 KiB steps, 8 records per lane) or 8 (8 KiB steps, 16 records
+// per lane: the per-step scan, window walk and LDS round trips amortised over twice the bytes, and
+// twice the bytes in flight per wave -- at 8 KiB steps, ~20 VGPRs more).
+// LDS swizzles (XOR inside 16-byte chunks): the row writes (lane l: words 128u + 2l, +1) and the
+// transposed ds_read_b128 (lane l: its 2 x ROWS records) both conflict-free.
+template <int ROWS>
+__device__ __forceinline__ uint32_t rec8_swz(uint32_t w) {
+  return ROWS == 4 ? w ^ (((w >> 6) & 1u) << 2) : w ^ (((w >> 5) & 3u) << 2);
+}
+__host__ __device__ constexpr uint32_t rec8_sums_words(int rows) { return 128u * (uint32_t)rows + 16u; }  // + word 128 x rows = 0
+__host__ __device__ constexpr uint32_t rec8_wave_words(int rows) { return rec8_sums_words(rows) + 80u; }  // + 65 lane prefixes
+__host__ __device__ constexpr uint32_t rec8_lds_bytes(int rows) { return rec8_wave_words(rows) * 4u * (kThreads / 64); }
 
-template <bool NT>
-__device__ __forceinline__ void load_rec8(u32x4 (&v)[4], __amdgpu_buffer_rsrc_t rs, uint32_t off, int lane) {
+#ifdef MDE_WAVE_STAMPS  // probe only: per-wave entry / first step / exit times (s_memrealtime, 100 MHz)
+constexpr uint32_t kStampWaves = 16384;
+__device__ unsigned long long g_wave_stamps[3 * kStampWaves];
+__device__ __forceinline__ void wave_stamp(int k) {
+  const uint32_t w = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0 && w < kStampWaves) g_wave_stamps[3 * w + k] = t;
+}
+#endif
+
+template <bool NT, int ROWS>
+__device__ __forceinline__ void load_rec8(u32x4 (&v)[ROWS], __amdgpu_buffer_rsrc_t rs, uint32_t off, int lane) {
 #pragma unroll
-  for (int u = 0; u < 4; u++)
+  for (int u = 0; u < ROWS; u++)
     v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(u * 64 + lane) * 16u,
                                                                           off, NT ? 2 : 0));
 }
 
-template <bool NT>
+template <bool NT, int ROWS>
 __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uint64_t beg, uint64_t end, uint32_t s_lo,
-                                                      int lane, uint32_t* lds) {
-  constexpr uint64_t kStep = 4096;
-  constexpr uint32_t kFoldSteps = 4096;  // fast steps per lane fold: 255 x 16 MiB < 2^32 exact
+                                                      int lane, uint32_t* lds, uint64_t first, uint64_t last) {
+  constexpr uint64_t kStep = 1024ull * ROWS;
+  constexpr uint32_t kRecs = 128u * ROWS;      // records per step
+  constexpr uint32_t kLaneRecs = 2u * ROWS;    // records per lane after the transpose
+  constexpr uint32_t kFoldSteps = 16384 / ROWS;  // fast steps per lane fold: 255 x 16 MiB < 2^32 exact
   const SegDesc& d = a.seg;
-  uint32_t* R = lds;               // record sums, then exclusive local prefixes (swizzled)
-  uint32_t* E = lds + kRec8Sums;   // lane exclusive prefixes; E[64] = the step's total
+  uint32_t* R = lds;                            // record sums, then exclusive local prefixes (swizzled)
+  uint32_t* E = lds + rec8_sums_words(ROWS);    // lane exclusive prefixes; E[64] = the step's total
   // beg / end stay where the compiler puts them (VGPRs: they derive from threadIdx.x >> 6), so the
   // resource below is a VGPR quadruple and every buffer load runs as a one-iteration readfirstlane
   // loop. Moving them to SGPRs was measured (r03): the digest alone unchanged (134-139 us at 8-byte
@@ -457,21 +515,25 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
   const uint64_t span = ((end - beg) + 15) & ~15ull;  // <= kMaxWaveBytes
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)(d.base + beg), (short)0, (int)span, 0x00020000);
-  u32x4 va[4], vb[4];
-  load_rec8<NT>(va, rs, 0, lane);  // the first step's loads before the bucket search
-  if (lane == 0) R[512] = 0;       // F(512) = E[64] + 0
-  uint32_t s = seg_search(d, s_lo, beg, lane);
+  u32x4 va[ROWS], vb[ROWS];
+  load_rec8<NT, ROWS>(va, rs, 0, lane);  // the first step's loads before the bucket search
+  if (lane == 0) R[kRecs] = 0;           // F(kRecs) = E[64] + 0 (rec8_swz(kRecs) == kRecs)
   SegWindow win;
-  win.load(d, s, lane);
-  uint64_t sb = readlane64(win.start, 0), se = readlane64(win.start, 1);
+  uint32_t s = seg_start(d, s_lo, beg, first, last, lane, win);
+  const uint32_t k_start = __builtin_amdgcn_readfirstlane(s - win.base);
+#ifdef MDE_WAVE_STAMPS
+  wave_stamp(1);
+#endif
+  uint64_t sb = readlane64(win.start, k_start), se = readlane64(win.start, k_start + 1u);
   uint64_t wsum = 0;       // this lane's window bucket (win.base + lane): its finished sum
   uint32_t acc = 0;        // lane accumulator of whole steps inside bucket s
   uint32_t acc_steps = 0;  // wave-uniform: fast steps in acc (0: acc is all zero)
   uint64_t accs = 0;       // wave-uniform: bucket s's bytes folded out of acc and from scan steps
-  // lane-invariant LDS addresses
-  uint32_t* const wrow = R + rec8_swz(2u * (uint32_t)lane);
-  uint32_t* const rd0 = R + rec8_swz(8u * (uint32_t)lane);
-  uint32_t* const rd1 = R + rec8_swz(8u * (uint32_t)lane + 4u);
+  // lane-invariant LDS addresses (a row offset 128u leaves the swizzle bits alone)
+  uint32_t* const wrow = R + rec8_swz<ROWS>(2u * (uint32_t)lane);
+  uint32_t* rd[ROWS / 2];
+#pragma unroll
+  for (int j = 0; j < ROWS / 2; j++) rd[j] = R + rec8_swz<ROWS>(kLaneRecs * (uint32_t)lane + 4u * j);
 
   auto fold = [&]() {  // acc -> accs (exact: acc_steps <= kFoldSteps)
     if (acc_steps) accs += wave_sum_u32(acc);
@@ -488,11 +550,11 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
     if (wsum) atomicAdd(a.sums + win.base + (uint32_t)lane, (unsigned long long)wsum);
     wsum = 0;
   };
-  auto process = [&](const u32x4 (&v)[4], uint64_t p) {
+  auto process = [&](const u32x4 (&v)[ROWS], uint64_t p) {
     const uint64_t q = min(p + kStep, end);
     if (q == p + kStep && sb <= p && q <= se) {  // the whole step inside bucket s
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < ROWS; u++) {
         acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
         acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
         acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
@@ -501,22 +563,30 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
       if (++acc_steps == kFoldSteps) fold();
       return;
     }
-    // record sums -> LDS at their record index (row u, lane l: records 128u + 2l, 128u + 2l + 1;
-    // rec8_swz only flips bit 2 from bit 6, so row u's words sit at wrow + 128u)
+    // record sums -> LDS at their record index (row u, lane l: records 128u + 2l, 128u + 2l + 1)
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < ROWS; u++) {
       const uint32_t r0 = __builtin_amdgcn_sad_u8(v[u].y, 0u, __builtin_amdgcn_sad_u8(v[u].x, 0u, 0u));
       const uint32_t r1 = __builtin_amdgcn_sad_u8(v[u].w, 0u, __builtin_amdgcn_sad_u8(v[u].z, 0u, 0u));
       *reinterpret_cast<uint2*>(wrow + 128u * u) = make_uint2(r0, r1);
     }
-    // transposed: this lane's records 8l .. 8l+7, their local prefix, one wave scan of the totals
-    const uint4 x = *reinterpret_cast<const uint4*>(rd0);
-    const uint4 y = *reinterpret_cast<const uint4*>(rd1);
-    const uint32_t c1 = x.x, c2 = c1 + x.y, c3 = c2 + x.z, c4 = c3 + x.w;
-    const uint32_t c5 = c4 + y.x, c6 = c5 + y.y, c7 = c6 + y.z, tot = c7 + y.w;
+    // transposed: this lane's records kLaneRecs * l .. +kLaneRecs-1, their local exclusive
+    // prefixes, one wave scan of the lane totals
+    uint32_t c[kLaneRecs + 1];
+    c[0] = 0u;
+#pragma unroll
+    for (int j = 0; j < ROWS / 2; j++) {
+      const uint4 x = *reinterpret_cast<const uint4*>(rd[j]);
+      c[4 * j + 1] = c[4 * j] + x.x;
+      c[4 * j + 2] = c[4 * j + 1] + x.y;
+      c[4 * j + 3] = c[4 * j + 2] + x.z;
+      c[4 * j + 4] = c[4 * j + 3] + x.w;
+    }
+    const uint32_t tot = c[kLaneRecs];
     const uint32_t incl = wave_incl_scan_u32(tot);
-    *reinterpret_cast<uint4*>(rd0) = make_uint4(0u, c1, c2, c3);
-    *reinterpret_cast<uint4*>(rd1) = make_uint4(c4, c5, c6, c7);
+#pragma unroll
+    for (int j = 0; j < ROWS / 2; j++)
+      *reinterpret_cast<uint4*>(rd[j]) = make_uint4(c[4 * j], c[4 * j + 1], c[4 * j + 2], c[4 * j + 3]);
     E[lane] = incl - tot;
     if (lane == 63) E[64] = incl;
     // F(y) for this lane's bucket start y, clamped to [p, q]: record slot k = (y - p) / 8
@@ -524,7 +594,7 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
     for (;;) {
       const uint64_t st = win.start;
       const uint32_t k = st <= p ? 0u : (st >= q ? kq : (uint32_t)((st - p) >> 3));
-      const uint32_t F = R[rec8_swz(k)] + E[k >> 3];
+      const uint32_t F = R[rec8_swz<ROWS>(k)] + E[k / kLaneRecs];
       // bucket base + lane's bytes in the step, lanes 0..62: F of the next lane (DPP wave_shl:1)
       const uint32_t c = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)F, 0x130, 0xf, 0xf, true) - F;
       const uint32_t k0 = __builtin_amdgcn_readfirstlane(s - win.base);
@@ -554,10 +624,10 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
   };
 
   for (uint64_t p = beg;; p += 2 * kStep) {
-    load_rec8<NT>(vb, rs, (uint32_t)(p + kStep - beg), lane);  // always issued (bounded by the range)
+    load_rec8<NT, ROWS>(vb, rs, (uint32_t)(p + kStep - beg), lane);  // always issued (bounded by the range)
     process(va, p);
     if (p + kStep >= end) break;
-    load_rec8<NT>(va, rs, (uint32_t)(p + 2 * kStep - beg), lane);
+    load_rec8<NT, ROWS>(va, rs, (uint32_t)(p + 2 * kStep - beg), lane);
     process(vb, p + kStep);
     if (p + 2 * kStep >= end) break;
   }
@@ -568,7 +638,7 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
 
 // One contiguous range of wave_bytes per wave. `block` = this workgroup's index among the digest
 // workgroups of the launch.
-template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, bool REC8 = false>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, int REC8 = 0>
 __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t block, uint32_t* lds = nullptr) {
   // Streaming waves issue little VALU; when tree waves (back-to-back SHA-256 VALU) share the CU,
   // a raised priority keeps the loads flowing and the SHA waves take the slack.
@@ -581,18 +651,25 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
   const uint64_t last = segpos(d, d.S);
   const uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
   if (beg >= last) return;
+#ifdef MDE_WAVE_STAMPS
+  wave_stamp(0);
+#endif
   if (REC8)
-    digest_range_rec8<NT>(a, beg, min(beg + a.wave_bytes, last), 0u, lane, lds + (threadIdx.x >> 6) * kRec8WaveWords);
+    digest_range_rec8<NT, REC8 ? REC8 : 4>(a, beg, min(beg + a.wave_bytes, last), 0u, lane,
+                                           lds + (threadIdx.x >> 6) * rec8_wave_words(REC8), first, last);
   else if (WIN)
     digest_range_win<U, NT, PIPE, A8>(a, beg, min(beg + a.wave_bytes, last), 0u, lane);
   else
     digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), 0u, lane);
+#ifdef MDE_WAVE_STAMPS
+  wave_stamp(2);
+#endif
 }
 
 // Interleaved pieces (DigestLaunch::pieces): the wave streams `pieces` ranges of wave_bytes,
 // piece_stride apart, so the whole grid sweeps the arena front to back together. Each piece is a
 // digest_range (its own bucket search, from the previous piece's last bucket on, and flush).
-template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, bool REC8 = false>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, int REC8 = 0>
 __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32_t block, uint32_t* lds = nullptr) {
   if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const int lane = threadIdx.x & 63;
@@ -604,8 +681,8 @@ __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32
   uint32_t s = 0;
   uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
   for (uint32_t j = 0; j < a.pieces && beg < last; j++, beg += a.piece_stride)
-    s = REC8  ? digest_range_rec8<NT>(a, beg, min(beg + a.wave_bytes, last), s, lane,
-                                      lds + (threadIdx.x >> 6) * kRec8WaveWords)
+    s = REC8  ? digest_range_rec8<NT, REC8 ? REC8 : 4>(a, beg, min(beg + a.wave_bytes, last), s, lane,
+                                                       lds + (threadIdx.x >> 6) * rec8_wave_words(REC8), first, last)
         : WIN ? digest_range_win<U, NT, PIPE, A8>(a, beg, min(beg + a.wave_bytes, last), s, lane)
               : digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), s, lane);
 }
@@ -805,15 +882,19 @@ __device__ __forceinline__ void digest_body_steal(const DigestLaunch& a, uint32_
 
 // MODE: 0 = one static range per wave, 1 = tail stealing, 2 = interleaved pieces; 3 and 4 = 0 and
 // 2 with the bucket bounds in a register window (SegWindow); 5 and 6 = 0 and 2 for fixed 8-byte
-// records with the prefix scan in record space (digest_range_rec8; LDS: kRec8LdsBytes).
+// records with the prefix scan in record space (digest_range_rec8, 4 KiB steps; LDS:
+// rec8_lds_bytes); 7 and 8 = 5 and 6 with 8 KiB steps.
+__host__ __device__ constexpr int mode_rec8_rows(int mode) {
+  return (mode == 5 || mode == 6) ? 4 : ((mode == 7 || mode == 8) ? 8 : 0);
+}
 template <int U, bool NT, int PIPE, int PRIO, int MODE, bool A8>
 __device__ __forceinline__ void digest_dispatch(const DigestLaunch& a, uint32_t block, uint32_t* lds) {
   if (MODE == 1)
     digest_body_steal<U, NT, PRIO>(a, block);
-  else if (MODE == 2 || MODE == 4 || MODE == 6)
-    digest_body_pieces<U, NT, PIPE, PRIO, MODE == 4, A8, MODE == 6>(a, block, lds);
+  else if (MODE == 2 || MODE == 4 || MODE == 6 || MODE == 8)
+    digest_body_pieces<U, NT, PIPE, PRIO, MODE == 4, A8, mode_rec8_rows(MODE)>(a, block, lds);
   else
-    digest_body<U, NT, PIPE, PRIO, MODE == 3, A8, MODE == 5>(a, block, lds);
+    digest_body<U, NT, PIPE, PRIO, MODE == 3, A8, mode_rec8_rows(MODE)>(a, block, lds);
 }
 
 template <int U, bool NT, int PIPE, int PRIO = 0, int MODE = 0>
@@ -990,7 +1071,8 @@ const Variant kVariants[] = {
     MDE_VARIANT(8, true, true, 2, 1),    MDE_VARIANT(4, true, 2, 2, 0),
     MDE_VARIANT(4, true, 2, 2, 2),      MDE_VARIANT(4, true, 2, 2, 3),
     MDE_VARIANT(4, true, 2, 2, 4),      MDE_VARIANT(4, true, 2, 2, 5),
-    MDE_VARIANT(4, true, 2, 2, 6),
+    MDE_VARIANT(4, true, 2, 2, 6),      MDE_VARIANT(4, true, 2, 2, 7),
+    MDE_VARIANT(4, true, 2, 2, 8),
 };
 #undef MDE_VARIANT
 
@@ -1001,6 +1083,14 @@ const Variant& variant(int v) { return kVariants[(v >= 0 && v < kNumVariants) ? 
 }  // namespace
 
 int bucket_digest_variants() { return kNumVariants; }
+
+#ifdef MDE_WAVE_STAMPS
+}  // namespace mde
+extern "C" int mde_probe_wave_stamps(unsigned long long* host, uint64_t n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mde::g_wave_stamps), n * 8 > sizeof(mde::g_wave_stamps) ? sizeof(mde::g_wave_stamps) : n * 8);
+}
+namespace mde {
+#endif
 
 // LDS of one small-build workgroup: tree regions, bucket sums and counts, and in the split-schedule
 // form the K+W ring.
@@ -1049,14 +1139,21 @@ hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t
 }
 
 bool bucket_digest_steals(int v) { return variant(v).mode == 1; }
-bool bucket_digest_pieces(int v) { return variant(v).mode == 2 || variant(v).mode == 4 || variant(v).mode == 6; }
-bool bucket_digest_rec8(int v) { return variant(v).mode == 5 || variant(v).mode == 6; }
-uint32_t bucket_digest_rec8_lds_bytes() { return kRec8LdsBytes; }
+bool bucket_digest_pieces(int v) {
+  const int m = variant(v).mode;
+  return m == 2 || m == 4 || m == 6 || m == 8;
+}
+bool bucket_digest_rec8(int v) { return mode_rec8_rows(variant(v).mode) != 0; }
+uint32_t bucket_digest_rec8_lds_bytes(int v) {
+  const int rows = mode_rec8_rows(variant(v).mode);
+  return rows ? rec8_lds_bytes(rows) : 0u;
+}
 int bucket_digest_pieces_sibling(int v) {  // the same kernel with interleaved pieces
   switch (v) {
     case 11: return 12;
     case 13: return 14;
     case 15: return 16;
+    case 17: return 18;
     default: return v;
   }
 }
@@ -1077,7 +1174,7 @@ void plan_steal(uint64_t wave_bytes, uint64_t* head_bytes, uint64_t* chunk_bytes
 
 int bucket_digest_blocks_per_cu(int v, int cap) {
   int blocks = 0;
-  const size_t lds = bucket_digest_rec8(v) ? kRec8LdsBytes : 0;
+  const size_t lds = bucket_digest_rec8_lds_bytes(v);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, variant(v).fn, kThreads, lds) != hipSuccess ||
       blocks <= 0)
     blocks = 4;

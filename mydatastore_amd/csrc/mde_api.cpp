@@ -401,7 +401,7 @@ int plan_digest(mde_ctx* c, uint64_t bytes, mde::DigestLaunch* a) {
                           &a->wave_bytes, &a->n_waves, &a->pieces);
   a->piece_stride = (uint64_t)a->n_waves * a->wave_bytes;
   a->lds_bytes = c->digest_oversub > 1 ? (uint32_t)((160u * 1024u) / (uint32_t)c->digest_blocks_per_cu) & ~255u : 0u;
-  if (mde::bucket_digest_rec8(a->variant)) a->lds_bytes = std::max(a->lds_bytes, mde::bucket_digest_rec8_lds_bytes());
+  if (mde::bucket_digest_rec8(a->variant)) a->lds_bytes = std::max(a->lds_bytes, mde::bucket_digest_rec8_lds_bytes(a->variant));
   // Tail stealing needs fixed-length values and a split range; otherwise the static sibling.
   if (steals) {
     mde::plan_steal(a->wave_bytes, &a->head_bytes, &a->chunk_bytes, &a->tail_chunks);

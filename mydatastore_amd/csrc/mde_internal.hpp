@@ -65,7 +65,7 @@ bool bucket_digest_steals(int variant);
 bool bucket_digest_pieces(int variant);  // interleaved-pieces variant (DigestLaunch::pieces)
 int bucket_digest_pieces_sibling(int variant);  // its interleaved-pieces form (itself if none)
 bool bucket_digest_rec8(int variant);  // fixed 8-byte records, record-space scan (needs LDS)
-uint32_t bucket_digest_rec8_lds_bytes();
+uint32_t bucket_digest_rec8_lds_bytes(int variant);
 constexpr uint64_t kStealScratchBytes = 512;
 // Head / tail split of each wave range for tail stealing (tail_chunks = 0: no split).
 void plan_steal(uint64_t wave_bytes, uint64_t* head_bytes, uint64_t* chunk_bytes, uint32_t* tail_chunks);

@@ -76,7 +76,7 @@ __device__ __forceinline__ uint32_t leaves_items(const TreeLaunch& a, uint32_t p
   return items;
 }
 
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+__device__ __forceinline__ uint32_t wave_add_u32(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
@@ -85,7 +85,7 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 __device__ __forceinline__ void leaves_waves(const TreeLaunch& a, uint32_t wave0, uint32_t waves, uint32_t p_end) {
   const uint32_t lane = threadIdx.x % 64;
   for (uint32_t p = wave0; p < p_end && p < a.P; p += waves) {
-    const uint32_t items = wave_sum_u32(leaves_items(a, p, lane, 64));
+    const uint32_t items = wave_add_u32(leaves_items(a, p, lane, 64));
     if (lane == 0 && a.items_out) a.items_out[p] = (int32_t)items;
   }
 }

@@ -10,9 +10,12 @@
  *                       B bucket ranges and appends every value to ONE arena, record by record:
  *                       value_off grows by each value's length, seg_rec by the record count per
  *                       bucket, n_partitions = 1, value_stride = 0 (variable-length values); an
- *                       empty arena gets one padding byte. -> mde_batch_build with the nodes
- *                       output, then the shim's mdeTree: the *merkletree.MerkleTree assembled from
- *                       the device's digests and node hashes (no host hashing; mirrored below).
+ *                       empty arena gets one padding byte. B > 256: -> mde_batch_build with the
+ *                       nodes output, then the shim's mdeTree: the *merkletree.MerkleTree assembled
+ *                       from the device's digests and node hashes (no host hashing; mirrored
+ *                       below). B <= 256 (mdeHostTreeMaxBuckets): a digest-only mde_batch_build
+ *                       (root = nodes = NULL), then NewTree on the host over the device digests
+ *                       (the checker's SHA-256 tree stands in for merkletree's).
  *   diff Ba Bb          DifferentMerkleTreeBuckets (main/merkle_tree.go:159-216), which the shim no
  *                       longer replaces: the reference's DFS over two trees of the shim's shape --
  *                       mdeTree over mde_tree_from_digests' nodes (a tree rebuilt from an odd-B
@@ -39,6 +42,9 @@
 #include "mde.h"
 
 void oracle_sha256(const uint8_t* msg, uint64_t len, uint8_t out[32]); /* checker's SHA-256 */
+/* stands in for merkletree.NewTree's hashing where the shim builds the tree on the host */
+int oracle_tree(const uint64_t* digest, uint32_t n_buckets, uint8_t* nodes, uint8_t* root);
+#define HOST_TREE_MAX_BUCKETS 256 /* merkle_gpu.go mdeHostTreeMaxBuckets */
 
 /* ---- the shim's mdeTree (integration/go/merkle_gpu.go), in C: merkletree v0.2.0's node graph
  * (leaf Hash = LE64(digest), a duplicate of the last leaf when B is odd -- same Hash, same
@@ -223,11 +229,13 @@ int main(int argc, char** argv) {
       int32_t items = 0;
       uint8_t root[32];
       uint8_t* nodes = xmalloc(mde_tree_internal_nodes(B) * 32);
-      mde_tree_out out = {digest, size, &items, root, nodes};
+      const int host_tree = B <= HOST_TREE_MAX_BUCKETS;
+      mde_tree_out out = {digest, size, &items, host_tree ? NULL : root, host_tree ? NULL : nodes};
       if ((rc = mde_batch_build(batcher, &rec, &out, err, sizeof err))) {
         fprintf(stderr, "mde_batch_build: %d %s\n", rc, err);
         return 1;
       }
+      if (host_tree) oracle_tree(digest, B, nodes, root);
       stree t = mde_tree(digest, B, nodes);
       uint8_t* wb = NULL;
       uint64_t wl = 0, wc = 0;

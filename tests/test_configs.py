@@ -28,6 +28,12 @@ pytestmark = pytest.mark.gpu
 C2 = (25_600_000, 256, 256, 64, "block")
 C3 = (64_000_000, 64, 1024, 64, "block")
 C4 = (10_000_000, 1024, 1024, 64, "mod")
+# The reference's own default shapes (not BASELINE configs): partition_buckets = 1000
+# (config/default-config.yaml:10). PROD is the production value shape -- every epoch-index record's
+# value is the 8-byte LE write timestamp (main/manager.go:816) -- 100M of them over 1,024
+# partitions, the bench's production_shape line; C4K is C4 at B = 1000.
+PROD = (100_000_000, 1024, 8, 1000, "mod")
+C4K = (10_000_000, 1024, 1024, 1000, "mod")
 
 
 def _torch_digests(w):
@@ -79,12 +85,15 @@ def _builds(engine, w):
     return outs + [(f"fused{i}", o) for i, (o, _) in enumerate(sets)]
 
 
-@pytest.mark.parametrize("cfg,sample", [(C2, [0, 1, 255]), (C3, [0, 63]), (C4, list(range(32)))],
-                         ids=["C2", "C3", "C4"])
+@pytest.mark.parametrize("cfg,sample", [(C2, [0, 1, 255]), (C3, [0, 63]), (C4, list(range(32))),
+                                        (PROD, list(range(32)) + [511, 1023]), (C4K, list(range(32)))],
+                         ids=["C2", "C3", "C4", "PROD", "C4K"])
 def test_baseline_config_full_size(engine, coracle, cfg, sample):
     """BASELINE configs[1] (C2, 6.55 GB), configs[2] (C3, 64 GiB) and configs[3] at N = 1 (C4,
-    10.24 GB): every digest, size, item count and root of every partition, standalone and fused;
-    the sampled partitions equal the C oracle's build of host-regenerated records, nodes included."""
+    10.24 GB), and the reference's default shapes at B = 1000 (PROD: 100M 8-byte timestamps, the
+    rec8 record-space digest; C4K: C4 at B = 1000, the register-window digest): every digest, size,
+    item count and root of every partition, standalone and fused; the sampled partitions equal the
+    C oracle's build of host-regenerated records, nodes included."""
     from mydatastore_amd.workload import make_workload
     n_keys, P, V, B, mode = cfg
     w = make_workload(engine, n_partitions=P, n_buckets=B, value_len=V, part_mode=mode,

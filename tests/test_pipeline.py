@@ -505,26 +505,33 @@ def test_default_variant_choice_b1000_full_size(engine, value_len, n_keys, n_buc
         engine.set_digest_piece_bytes(-1)
 
 
-REC8_VARIANTS = (15, 16)  # digest.hip: fixed 8-byte records, record-space prefix scan (+ pieces)
+# digest.hip: fixed 8-byte records, record-space prefix scan (+ pieces), 4 KiB and 8 KiB steps
+REC8_VARIANTS = (15, 16, 17, 18)
 
 
 @pytest.mark.parametrize("start", [0, 8])
 @pytest.mark.parametrize("P,B,max_count", [(37, 1000, 300), (64, 64, 3000)])
-def test_rec8_ragged_arena_matches_torch_sums(engine, start, P, B, max_count):
+def test_rec8_ragged_arena_matches_torch_sums(engine, coracle, start, P, B, max_count):
     """The 8-byte-record digest (production timestamps, main/manager.go:816): 37 or 64 partitions, a
     quarter of the buckets empty, an empty partition, three buckets of 12-24 MB (past the 16 MiB
     exact-u32 reduction), the arena 16-byte aligned or 8 bytes past it (record slots on 8-byte
     boundaries), both variants and piece sizes from 1 KiB (piece and range ends inside buckets and
     in the middle of 16-byte vectors), standalone and fused: digests equal torch byte sums, sizes
-    the record counts, and the automatic choice picks it."""
+    the record counts, items their per-partition sums, roots the C oracle's SHA-256 trees over
+    those digests, and the automatic choice picks it."""
     import torch
     import mydatastore_amd as mde
     dev = torch.device("cuda:0")
     engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     rec, counts, want, keep, (P, B) = _skewed_arena(dev, False, seed=3 + start, P=P, B=B, max_count=max_count,
                                                     big=(3_000_000, 1_500_000, 2_000_000), stride=8, start=start)
+    want_np = want.numpy().astype(np.uint64)
+    want_root = torch.from_numpy(np.concatenate(
+        [np.frombuffer(coracle.tree(want_np[p * B:(p + 1) * B], B)[0], np.uint8) for p in range(P)]).copy())
+    want_items = counts.view(P, B).sum(1).to(torch.int32)
     try:
-        for v, pbs in [(-1, (-1,)), (REC8_VARIANTS[0], (-1,)), (REC8_VARIANTS[1], (1024, 8192, 1 << 20))]:
+        for v, pbs in [(-1, (-1,)), (REC8_VARIANTS[0], (-1,)), (REC8_VARIANTS[1], (1024, 8192, 1 << 20)),
+                       (REC8_VARIANTS[2], (-1,)), (REC8_VARIANTS[3], (1024, 8192, 1 << 20))]:
             engine.set_tuning(v, -1)
             for pb in pbs:
                 engine.set_digest_piece_bytes(pb)
@@ -543,6 +550,8 @@ def test_rec8_ragged_arena_matches_torch_sums(engine, start, P, B, max_count):
                     engine.synchronize()
                     assert torch.equal(o["digest"].cpu(), want), (v, pb, fused)
                     assert torch.equal(o["size"].cpu().to(torch.int64), counts), (v, pb, fused)
+                    assert torch.equal(o["items"].cpu(), want_items), (v, pb, fused)
+                    assert torch.equal(o["root"].cpu(), want_root), (v, pb, fused)
     finally:
         engine.set_digest_piece_bytes(-1)
         engine.set_tuning(-1, -1)
