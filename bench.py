@@ -89,6 +89,11 @@ def parse():
                     help="N = 1: skip the 8-byte-timestamp, B = 1000 line (production_shape)")
     ap.add_argument("--no-gather-per-build", action="store_true",
                     help="N > 1: skip the second timed run with one root-gather collective per build")
+    ap.add_argument("--engine", default="auto", choices=["auto", "group", "ranks"],
+                    help="group: ONE process drives the N GPUs through mde_group (partition p on GPU p %% N, "
+                         "device-resident pipelined builds, RCCL all-gather of the root slabs inside libmde: "
+                         "the path a Go node calls); ranks: one process per GPU, torch.distributed root "
+                         "gather; auto (default): group for N > 1, the single-engine path at N = 1")
     return ap.parse_args()
 
 
@@ -284,8 +289,151 @@ def end_to_end(torch, eng, w, B, reps=3):
     return res
 
 
+def main_group(args):
+    """N GPUs driven by ONE process through mde_group (include/mde.h): the multi-GPU path a Go node
+    reaches (merkle_gpu.go's process owns the node's GPUs). Partition p lives on GPU p % N; each
+    step is one pipelined build launch per GPU (this build's digest + the previous build's trees)
+    and every GATHER_BUCKET builds ONE all-gather of the root slabs (RCCL over xGMI on
+    communicators libmde created once, ncclCommInitAll), enqueued in stream order on every GPU.
+    Under torch.distributed.run the other ranks only join the barriers (gloo, no GPU); rank 0's
+    clock brackets all N GPUs' work. --rehearse: every shard on GPU 0 (copy gather)."""
+    import torch
+    import torch.distributed as dist
+    import mydatastore_amd as mde
+    from mydatastore_amd.workload import make_workload
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+    if rank != 0:  # the node's one process is rank 0; the others wait at its three barriers
+        for _ in range(3):
+            dist.barrier()
+        dist.destroy_process_group()
+        return
+    N = args.gpus
+    n_dev = torch.cuda.device_count()
+    devices = [0] * N if args.rehearse else list(range(N))
+    if max(devices) >= n_dev:
+        raise SystemExit(f"--gpus {N} but {n_dev} GPUs visible (use --rehearse to place every shard on GPU 0)")
+    n_keys, P, V, B, mode, desc = CONFIGS[args.config]
+    g = mde.Group(devices)
+    engines = {}
+    for d in sorted(set(devices)):
+        engines[d] = mde.Engine(d)
+    shards = [make_workload(engines[devices[i]], n_partitions=P, n_buckets=B, value_len=V, part_mode=mode,
+                            keys_per_partition=-(-n_keys // P), n_keys=n_keys, rank=i, world=N) for i in range(N)]
+    bucket = GATHER_BUCKET
+    slab = -(-P // N)
+    sdev = [torch.device("cuda", d) for d in devices]
+    send = [torch.zeros(bucket * slab * 32, dtype=torch.uint8, device=sdev[i]) for i in range(N)]
+    recv = [torch.zeros(N * bucket * slab * 32, dtype=torch.uint8, device=sdev[i]) for i in range(N)]
+    # two output sets per shard (pipelined builds alternate); each build's roots go straight into
+    # its row of the bucket's send slab
+    sets = [[w._outs() for _ in range(2)] for w in shards]
+
+    def tree_out(i, L):
+        o, _ = sets[i][L % 2]
+        root = send[i][(L % bucket) * slab * 32:].data_ptr()
+        return mde.TreeOut(o["digest"].data_ptr(), o["size"].data_ptr(), o["items"].data_ptr(), root, o["nodes"].data_ptr())
+
+    # the per-launch argument arrays, built once (bucket is even: L % bucket fixes L % 2)
+    import ctypes
+    lib = mde.load_library()
+    recs = (mde.Records * N)(*[w.rec for w in shards])
+    outs_by_slot = [(mde.TreeOut * N)(*[tree_out(i, k) for i in range(N)]) for k in range(bucket)]
+    nbytes = slab * 32 * bucket
+    send_p = (ctypes.c_void_p * N)(*[t.data_ptr() for t in send])
+    recv_p = (ctypes.c_void_p * N)(*[t.data_ptr() for t in recv])
+
+    def check(rc):
+        if rc != mde.MDE_OK:
+            g._check(rc)
+
+    def run(steps):  # `steps` pipelined builds, gathers of every complete bucket, drained
+        for L in range(steps):
+            check(lib.mde_group_build_pipelined_async(g.g, recs, outs_by_slot[L % bucket]))
+            if L >= 1 and (L - 1) % bucket == bucket - 1:  # launch L completed build L-1's trees
+                check(lib.mde_group_gather_async(g.g, send_p, recv_p, nbytes))
+        check(lib.mde_group_build_pipeline_drain_async(g.g))
+        if steps and (steps - 1) % bucket != bucket - 1:
+            check(lib.mde_group_gather_async(g.g, send_p, recv_p, nbytes))
+
+    ext = torch.cuda.ExternalStream(mde.load_library().mde_get_stream(g.ctx(0)), device=sdev[0])
+    run(max(args.warmup, 1))
+    g.synchronize()
+    if world > 1:
+        dist.barrier()
+    for d in sorted(set(devices)):
+        torch.cuda.synchronize(d)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(ext)
+    run(args.steps)
+    e1.record(ext)
+    g.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    ms = (t1 - t0) * 1e3 / args.steps
+    dev0_ms = e0.elapsed_time(e1) / args.steps
+    # parity: the gathered slabs (device 0's copy, the last bucket) hold every shard's roots of its
+    # last build; shard 0's last build equals the C oracle on host-regenerated partitions
+    last = args.steps - 1
+    got = recv[0].view(N, bucket, slab, 32)[:, last % bucket].cpu().numpy()
+    ok_gather = all(np.array_equal(got[i, :shards[i].n_partitions],
+                                   send[i].view(bucket, slab, 32)[last % bucket, :shards[i].n_partitions].cpu().numpy())
+                    for i in range(N))
+    ok_same = all(torch.equal(recv[i].cpu(), recv[0].cpu()) for i in range(1, N))
+    info = host_cpu_info()
+    threads = cpu_share(info, 1)
+    co, s_vals, s_seg, s_n, ref = oracle_sample((n_keys, P, V, B, mode, desc), shards[0].partition_ids, threads)
+    o0 = {k: v.cpu().numpy() for k, v in sets[0][last % 2][0].items()}
+    r0 = send[0].view(bucket, slab, 32)[last % bucket, :s_n].cpu().numpy().reshape(-1)
+    ok_oracle = (np.array_equal(o0["digest"][:s_n * B].view(np.uint64), ref["digest"]) and
+                 np.array_equal(o0["size"][:s_n * B], ref["size"]) and np.array_equal(r0, ref["root"]))
+    total = sum(w.value_bytes for w in shards)
+    achieved = shards[0].value_bytes / (dev0_ms * 1e-3) / 1e9
+    result = {
+        "metric": METRIC, "value": round(total / 2**30 / (ms * 1e-3), 3), "unit": "GiB/s", "n_gpus": N,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (device-generated splitmix64 values, 'k%016x' keys, SHA-256 bucket tags)",
+        "config": {"workload": desc + (f"; strong scaling: the config's total over {N} GPUs" if N > 1 else ""),
+                   "layout": "A (sorted by partition, bucket)", "n_keys": n_keys, "value_len": V,
+                   "n_partitions": P, "n_buckets": B, "bytes_hashed_per_step": total,
+                   "partitions_per_gpu": [w.n_partitions for w in shards],
+                   "parallelism": f"partition-shard x{N}, one process (mde_group)",
+                   "engine": "group", "devices": devices,
+                   "root_gather": f"{g.gather_kind} of {N} x {bucket} x {slab} x 32 B slabs, one per {bucket} builds, "
+                                  "in stream order on every GPU"},
+        "roofline": {"bound": "hbm", "kernel": "build_step_kernel (GPU 0's launches + its gathers)",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel_ms": round(dev0_ms, 5), "algorithmic_bytes_per_launch": shards[0].value_bytes},
+        "parity": {"gathered_slabs_hold_every_shard_roots": bool(ok_gather),
+                   "every_gpu_received_the_same_slabs": bool(ok_same),
+                   "oracle_sample_partitions": int(s_n), "shard0_equals_c_oracle_on_sample": bool(ok_oracle),
+                   "all_ranks_ok": bool(ok_gather and ok_same and ok_oracle)},
+        "cpu_baseline": None,
+    }
+    if world > 1:
+        result["launcher_ranks"] = world
+    print(json.dumps(result), flush=True)
+    g.close()
+    for e in engines.values():
+        e.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.engine == "group" or (args.engine == "auto" and max(world_env, args.gpus) > 1 and args.config != "c5"
+                                  and args.layout == "a" and not args.rccl_selftest and not args.simulate_world):
+        return main_group(args)
     import torch
     import torch.distributed as dist
     import mydatastore_amd as mde

@@ -91,6 +91,8 @@ typedef struct mde_tree_out {
 
 int mde_abi_version(void);
 const char* mde_strerror(int code);
+/* Visible gfx950 devices (0 without a usable GPU); a node's Go shim spreads partitions over them. */
+int mde_device_count(void);
 
 /* Context: one HIP device, one stream, device scratch. */
 int mde_create(int device, mde_ctx** out);
@@ -289,29 +291,43 @@ int mde_verify_epochs(mde_ctx* ctx, uint32_t n_partitions, uint32_t n_buckets,
                       int32_t* peer_status, uint8_t* object_out, uint64_t object_stride,
                       uint32_t* object_len);
 
-/* Device groups: one process driving G GPUs (a Go node is one process). Partitions are split
- * into G contiguous blocks, block i built on device i: its records are one contiguous range of
- * the host arena, so each device receives a single H2D copy, and the shards run concurrently on
- * one host thread per device. Outputs land in the caller's arrays exactly as one mde_build over
- * all P partitions would write them (the split never changes a result). The same device may be
- * listed more than once (several contexts on one GPU). mde_group_ctx gives the per-device
- * contexts for device-resident (*_async) use, e.g. partition p on device p % G. */
+/* Device groups: one process driving the G GPUs of a node (a Go node is one process). Partition p
+ * lives on device p % G (the in-node analogue of the reference's partition sharding over nodes,
+ * hashring/hashring.go:126-154); every device builds its own partitions, and the one exchange step
+ * -- the per-partition roots -- is ONE all-gather of fixed-size root slabs: RCCL over xGMI on
+ * communicators created once by mde_group_create (ncclCommInitAll), or device copies when a device
+ * is listed more than once (several contexts on one GPU) -- mde_group_gather_kind says which.
+ * Shard i holds partitions i, i + G, i + 2G, ... (mde_group_partitions of them), in that order. */
 typedef struct mde_group mde_group;
 int mde_group_create(const int* devices, uint32_t n_devices, mde_group** out);
 void mde_group_destroy(mde_group* group);
 uint32_t mde_group_size(const mde_group* group);
 mde_ctx* mde_group_ctx(mde_group* group, uint32_t i);
+const char* mde_group_gather_kind(const mde_group* group); /* "rccl all_gather" or "device copies (why)" */
+uint32_t mde_group_partitions(const mde_group* group, uint32_t n_partitions, uint32_t i);
 const char* mde_group_last_error(const mde_group* group);
-/* mde_last_error_copy for a group (its multi-build calls are serialised by a group lock). */
+/* mde_last_error_copy for a group (its calls are serialised by a group lock). */
 uint64_t mde_group_last_error_copy(mde_group* group, char* buf, uint64_t cap);
 /* RawPartitionMerkleTree for P partitions over the group (host pointers, synchronous); same
- * contract as mde_build. */
+ * contract and results as mde_build: each device receives its partitions' records (one copy per
+ * partition range), builds them, the root slabs (ceil(P/G) roots each) are all-gathered, and the
+ * outputs land in the caller's arrays in partition order. root == NULL: digest-only, no gather. */
 int mde_multi_build(mde_group* group, const mde_records* rec, const mde_tree_out* out);
-/* Host ingest over the group: each device's contiguous partition block goes through
- * mde_build_streamed on that device (its own two-slot ring, chunk_bytes as there), concurrently --
- * one PCIe link per device. Same contract and results as mde_multi_build. */
+/* Host ingest over the group (arenas larger than HBM, nothing resident): each device streams one
+ * contiguous block of partitions (one contiguous host range per PCIe link) through
+ * mde_build_streamed on that device, concurrently. Same contract and results as mde_multi_build. */
 int mde_multi_build_streamed(mde_group* group, const mde_records* rec, const mde_tree_out* out,
                              uint64_t chunk_bytes);
+/* Device-resident use, each call enqueued on every device's context stream (mde_group_ctx,
+ * mde_set_stream): shard[i] / shard_out[i] hold device-i pointers (shard i's partitions, layout as
+ * in mde_build_async); a shard with n_partitions == 0 is skipped. */
+int mde_group_build_async(mde_group* group, const mde_records* shard, const mde_tree_out* shard_out);
+int mde_group_build_pipelined_async(mde_group* group, const mde_records* shard, const mde_tree_out* shard_out);
+int mde_group_build_pipeline_drain_async(mde_group* group);
+/* The exchange step: device i contributes `bytes` from send[i] (device i memory); recv[i] (device
+ * i memory, G x bytes) receives every device's slab, slab r = device r's. */
+int mde_group_gather_async(mde_group* group, const void* const* send, void* const* recv, uint64_t bytes);
+int mde_group_synchronize(mde_group* group);
 
 /* Request coalescing for the production call shape (one partition per call). The reference runs
  * RawPartitionMerkleTree and the VerifyEpoch decision for ONE (partition, epoch) per call, on any

@@ -44,6 +44,8 @@ EXPORTED_SYMBOLS = (
     "mde_memcpy_h2d", "mde_memcpy_d2h", "mde_verify_peer_capacity", "mde_verify_epochs",
     "mde_verify_epochs_async", "mde_group_create", "mde_group_destroy", "mde_group_size",
     "mde_group_ctx", "mde_group_last_error", "mde_multi_build", "mde_multi_build_streamed",
+    "mde_group_gather_kind", "mde_group_partitions", "mde_group_build_async", "mde_group_build_pipelined_async",
+    "mde_group_build_pipeline_drain_async", "mde_group_gather_async", "mde_group_synchronize", "mde_device_count",
     "mde_batcher_create", "mde_batcher_destroy", "mde_batcher_ctx", "mde_batcher_contexts", "mde_batcher_stats",
     "mde_batch_build", "mde_batch_verify", "mde_reserve_decode_scratch",
 )
@@ -146,6 +148,14 @@ def load_library() -> C.CDLL:
         "mde_group_last_error_copy": (C.c_uint64, [vp, C.c_char_p, C.c_uint64]),
         "mde_multi_build": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
         "mde_multi_build_streamed": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), C.c_uint64]),
+        "mde_group_gather_kind": (C.c_char_p, [vp]),
+        "mde_group_partitions": (u32, [vp, u32, u32]),
+        "mde_group_build_async": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
+        "mde_group_build_pipelined_async": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut)]),
+        "mde_group_build_pipeline_drain_async": (C.c_int, [vp]),
+        "mde_group_gather_async": (C.c_int, [vp, C.POINTER(vp), C.POINTER(vp), C.c_uint64]),
+        "mde_group_synchronize": (C.c_int, [vp]),
+        "mde_device_count": (C.c_int, []),
         "mde_batcher_create": (C.c_int, [C.c_int, u32, u32, C.POINTER(vp)]),
         "mde_batcher_destroy": (None, [vp]),
         "mde_batcher_ctx": (vp, [vp, u32]),
@@ -574,7 +584,8 @@ class Engine:
 
 
 class Group:
-    """mde_group: one process driving several GPUs (contiguous partition blocks per device)."""
+    """mde_group: one process driving several GPUs; partition p on device p % G, the roots
+    all-gathered over RCCL (or device copies when a device is listed twice)."""
 
     def __init__(self, devices):
         self._mu = threading.Lock()
@@ -599,6 +610,45 @@ class Group:
 
     def __len__(self):
         return int(self.lib.mde_group_size(self.g))
+
+    @property
+    def gather_kind(self) -> str:
+        return self.lib.mde_group_gather_kind(self.g).decode()
+
+    def partitions(self, n_partitions: int, i: int) -> int:
+        """Partitions on device i (i, i + G, ...)."""
+        return int(self.lib.mde_group_partitions(self.g, n_partitions, i))
+
+    def ctx(self, i: int):
+        return self.lib.mde_group_ctx(self.g, i)
+
+    def _check(self, rc):
+        if rc != MDE_OK:
+            buf = C.create_string_buffer(512)
+            self.lib.mde_group_last_error_copy(self.g, buf, len(buf))
+            raise MdeError(rc, buf.value.decode(errors="replace"))
+
+    def build_async(self, shards, outs, pipelined=False):
+        """mde_group_build[_pipelined]_async: shards / outs = one Records / TreeOut per device
+        (device-i pointers)."""
+        n = len(self)
+        recs = (Records * n)(*shards)
+        tos = (TreeOut * n)(*outs)
+        fn = self.lib.mde_group_build_pipelined_async if pipelined else self.lib.mde_group_build_async
+        self._check(fn(self.g, recs, tos))
+
+    def drain_async(self):
+        self._check(self.lib.mde_group_build_pipeline_drain_async(self.g))
+
+    def gather_async(self, send, recv, nbytes: int):
+        """mde_group_gather_async: send[i] / recv[i] device-i tensors (or pointers)."""
+        n = len(self)
+        s = (C.c_void_p * n)(*[_ptr(x) if not isinstance(x, int) else x for x in send])
+        r = (C.c_void_p * n)(*[_ptr(x) if not isinstance(x, int) else x for x in recv])
+        self._check(self.lib.mde_group_gather_async(self.g, s, r, nbytes))
+
+    def synchronize(self):
+        self._check(self.lib.mde_group_synchronize(self.g))
 
     def build(self, values, n_partitions, n_buckets, value_stride=0, value_off=None, seg_rec=None,
               part_rec=None, bucket_tag=None, want_nodes=True, streamed=False, chunk_bytes=0, want_tree=True):

@@ -55,7 +55,7 @@ def _run(cmd, verbose):
 def build_engine(verbose: bool = True) -> Path:
     OBJ.mkdir(exist_ok=True)
     headers = list(CSRC.glob("*.hpp")) + [ROOT / "include" / "mde.h"]
-    sources = sorted(CSRC.glob("*.hip")) + [CSRC / "mde_api.cpp", CSRC / "batch.cpp"]
+    sources = sorted(CSRC.glob("*.hip")) + [CSRC / "mde_api.cpp", CSRC / "batch.cpp", CSRC / "group.cpp"]
     objs = []
     for src in sources:
         obj = OBJ / (src.stem + ".o")
@@ -64,7 +64,7 @@ def build_engine(verbose: bool = True) -> Path:
             _run([HIPCC, *HIP_FLAGS, *lang, "-c", src, "-o", obj], verbose)
         objs.append(obj)
     if _stale(LIB, objs):
-        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-pthread", "-o", LIB, *objs], verbose)
+        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-pthread", "-o", LIB, *objs, "-ldl"], verbose)
     return LIB
 
 

@@ -1,0 +1,579 @@
+// group.cpp -- device groups: one process driving the G GPUs of a node (include/mde.h mde_group_*).
+//
+// The reference spreads partitions over nodes with consistent hashing (hashring/hashring.go:126-154);
+// a Go node is one process. Inside one MI355X node the engine spreads them over the node's GPUs:
+// partition p lives on device p % G. Each device builds its own partitions --
+// no data-path collective -- and the one exchange step, the per-partition roots, is ONE RCCL
+// all-gather of fixed-size root slabs over xGMI, on communicators created once (ncclCommInitAll)
+// with the group. RCCL is bound at run time (dlopen of librccl.so.1: torch's own copy carries the
+// same SONAME, so a torch process shares one RCCL, and libmde has no link-time RCCL dependency).
+// A group that lists a device more than once (several contexts on one GPU: the multi-device logic
+// rehearsed on a one-GPU box) gathers with device copies instead -- the same bytes land in the same
+// places -- and says so (mde_group_gather_kind).
+//
+// Written against the public C ABI plus HIP, like batch.cpp.
+#include "../../include/mde.h"
+
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+// RCCL entry points, resolved once.
+struct Rccl {
+  decltype(&ncclCommInitAll) init_all = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  std::string why;  // empty when usable
+};
+
+const Rccl& rccl() {
+  static const Rccl r = [] {
+    Rccl x;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      const char* e = dlerror();
+      x.why = std::string("librccl not loadable: ") + (e ? e : "?");
+      return x;
+    }
+    x.init_all = reinterpret_cast<decltype(x.init_all)>(dlsym(h, "ncclCommInitAll"));
+    x.destroy = reinterpret_cast<decltype(x.destroy)>(dlsym(h, "ncclCommDestroy"));
+    x.all_gather = reinterpret_cast<decltype(x.all_gather)>(dlsym(h, "ncclAllGather"));
+    x.group_start = reinterpret_cast<decltype(x.group_start)>(dlsym(h, "ncclGroupStart"));
+    x.group_end = reinterpret_cast<decltype(x.group_end)>(dlsym(h, "ncclGroupEnd"));
+    x.error_string = reinterpret_cast<decltype(x.error_string)>(dlsym(h, "ncclGetErrorString"));
+    if (!x.init_all || !x.destroy || !x.all_gather || !x.group_start || !x.group_end || !x.error_string)
+      x.why = "librccl lacks a required entry point";
+    return x;
+  }();
+  return r;
+}
+
+struct Buf {
+  void* p = nullptr;
+  uint64_t cap = 0;
+};
+
+}  // namespace
+
+struct mde_group {
+  std::vector<int> dev;
+  std::vector<mde_ctx*> ctx;
+  std::vector<ncclComm_t> comm;   // one per device (empty: copy gather)
+  std::vector<hipEvent_t> ready;  // copy gather: each device's send buffer is ready
+  std::string gather_kind;
+  std::mutex mu;  // held by the host-pointer builds for the whole call; guards err
+  std::string err;
+  // mde_multi_build staging, per device: values, value_off, seg_rec / part_rec, bucket_tag,
+  // digest, size, items, root slab, nodes, gathered roots
+  enum { kVals, kVoff, kSeg, kTag, kDig, kSize, kItems, kRoot, kNodes, kRecv, kBufs };
+  std::vector<std::vector<Buf>> stage;
+};
+
+namespace {
+
+// Error messages go to `msg` (g->err, or a per-thread string while shards build concurrently).
+int fail(std::string& msg, int code, const char* fmt, ...) {
+  char m[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(m, sizeof m, fmt, ap);
+  va_end(ap);
+  msg = m;
+  return code;
+}
+
+int grow(mde_group* g, uint32_t i, int which, uint64_t bytes, std::string& msg) {
+  Buf& b = g->stage[i][which];
+  if (b.p && b.cap >= bytes) return MDE_OK;
+  (void)hipSetDevice(g->dev[i]);
+  if (b.p) {
+    (void)hipStreamSynchronize(static_cast<hipStream_t>(mde_get_stream(g->ctx[i])));
+    (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  const uint64_t cap = std::max<uint64_t>(bytes + bytes / 8, 256);
+  if (hipMalloc(&b.p, cap) != hipSuccess) {
+    b.p = nullptr;
+    return fail(msg, MDE_E_NOMEM, "device %d: staging allocation of %llu bytes failed", g->dev[i], (unsigned long long)cap);
+  }
+  b.cap = cap;
+  return MDE_OK;
+}
+
+uint64_t parts_on(uint32_t P, uint32_t G, uint32_t i) { return i < P ? (uint64_t)(P - i + G - 1) / G : 0; }
+
+// The one exchange step: device i contributes `bytes` from send[i]; recv[i] receives G slabs of
+// `bytes`, slab r = device r's. Enqueued on every device's context stream.
+int gather(mde_group* g, const void* const* send, void* const* recv, uint64_t bytes, std::string& msg) {
+  const uint32_t G = (uint32_t)g->ctx.size();
+  if (!g->comm.empty()) {
+    const Rccl& r = rccl();
+    ncclResult_t e = r.group_start();
+    for (uint32_t i = 0; i < G && e == ncclSuccess; i++) {
+      (void)hipSetDevice(g->dev[i]);
+      e = r.all_gather(send[i], recv[i], bytes, ncclUint8, g->comm[i], static_cast<hipStream_t>(mde_get_stream(g->ctx[i])));
+    }
+    const ncclResult_t e2 = r.group_end();
+    if (e == ncclSuccess) e = e2;
+    if (e != ncclSuccess) return fail(msg, MDE_E_DEVICE, "ncclAllGather: %s", r.error_string(e));
+    return MDE_OK;
+  }
+  for (uint32_t i = 0; i < G; i++) {
+    (void)hipSetDevice(g->dev[i]);
+    if (hipEventRecord(g->ready[i], static_cast<hipStream_t>(mde_get_stream(g->ctx[i]))) != hipSuccess)
+      return fail(msg, MDE_E_DEVICE, "hipEventRecord failed");
+  }
+  for (uint32_t i = 0; i < G; i++) {
+    (void)hipSetDevice(g->dev[i]);
+    hipStream_t st = static_cast<hipStream_t>(mde_get_stream(g->ctx[i]));
+    for (uint32_t r = 0; r < G; r++) {
+      if (hipStreamWaitEvent(st, g->ready[r], 0) != hipSuccess ||
+          hipMemcpyAsync(static_cast<uint8_t*>(recv[i]) + (uint64_t)r * bytes, send[r], bytes, hipMemcpyDefault, st) !=
+              hipSuccess)
+        return fail(msg, MDE_E_DEVICE, "device copy gather failed");
+    }
+  }
+  return MDE_OK;
+}
+
+// Host-side validation of a host-pointer build (the checks mde_build makes), before slicing.
+int check(const mde_records* r, const mde_tree_out* o, std::string& msg) {
+  if (!r || !o) return fail(msg, MDE_E_INVAL, "records or out is NULL");
+  if (!r->n_buckets) return fail(msg, MDE_E_INVAL, "n_buckets must be >= 1");
+  if (r->layout > MDE_LAYOUT_TAGGED) return fail(msg, MDE_E_INVAL, "unknown layout %u", r->layout);
+  if ((uint64_t)r->n_partitions * r->n_buckets > 0xffffffffull)
+    return fail(msg, MDE_E_INVAL, "n_partitions * n_buckets exceeds 2^32");
+  if (!o->root && o->nodes) return fail(msg, MDE_E_INVAL, "out/nodes needs out/root");
+  if (!r->values && r->values_bytes) return fail(msg, MDE_E_INVAL, "values is NULL");
+  if (r->value_stride && (uint64_t)r->value_stride * r->n_records > r->values_bytes)
+    return fail(msg, MDE_E_INVAL, "n_records * value_stride exceeds values_bytes");
+  const uint32_t P = r->n_partitions, B = r->n_buckets;
+  if (r->layout == MDE_LAYOUT_TAGGED) {
+    if (!r->part_rec || (!r->bucket_tag && r->n_records)) return fail(msg, MDE_E_INVAL, "layout B needs part_rec and bucket_tag");
+    if (!r->value_stride) return fail(msg, MDE_E_INVAL, "layout B needs fixed-length values");
+    if (B > 65536) return fail(msg, MDE_E_INVAL, "layout B supports n_buckets <= 65536");
+    for (uint32_t p = 0; p < P; p++)
+      if (r->part_rec[p] > r->part_rec[p + 1]) return fail(msg, MDE_E_INVAL, "part_rec not nondecreasing");
+    if (r->part_rec[P] > r->n_records) return fail(msg, MDE_E_INVAL, "part_rec exceeds n_records");
+    for (uint64_t k = r->part_rec[0]; k < r->part_rec[P]; k++)
+      if (r->bucket_tag[k] >= B) return fail(msg, MDE_E_INVAL, "bucket_tag[%llu] out of range", (unsigned long long)k);
+    return MDE_OK;
+  }
+  if (!r->seg_rec) return fail(msg, MDE_E_INVAL, "seg_rec is NULL");
+  if (!r->value_stride && !r->value_off && r->n_records) return fail(msg, MDE_E_INVAL, "variable-length values need value_off");
+  const uint64_t S = (uint64_t)P * B;
+  for (uint64_t s = 0; s < S; s++)
+    if (r->seg_rec[s] > r->seg_rec[s + 1]) return fail(msg, MDE_E_INVAL, "seg_rec not nondecreasing at %llu", (unsigned long long)s);
+  if (r->seg_rec[S] > r->n_records) return fail(msg, MDE_E_INVAL, "seg_rec[%llu] exceeds n_records", (unsigned long long)S);
+  if (!r->value_stride && r->n_records) {
+    for (uint64_t k = 0; k < r->n_records; k++)
+      if (r->value_off[k] > r->value_off[k + 1]) return fail(msg, MDE_E_INVAL, "value_off not nondecreasing");
+    if (r->value_off[r->n_records] > r->values_bytes) return fail(msg, MDE_E_INVAL, "value_off exceeds values_bytes");
+  }
+  return MDE_OK;
+}
+
+int ctx_err(mde_group* g, uint32_t i, int rc, std::string& msg) {
+  char m[512];
+  mde_last_error_copy(g->ctx[i], m, sizeof m);
+  return fail(msg, rc, "device %d: %s", g->dev[i], m);
+}
+
+#define GHIP(expr)                                                                                   \
+  do {                                                                                               \
+    const hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess) return fail(msg, MDE_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_));    \
+  } while (0)
+
+// Shard i of a host-pointer build: its partitions' records copied to device i (one copy per
+// partition range: partition p's records are contiguous in the host arena), rebased, and the
+// build enqueued on the device's context stream.
+int upload_and_build(mde_group* g, uint32_t i, const mde_records* r, bool tree, bool want_nodes, uint64_t slab_parts,
+                     std::string& msg) {
+  const uint32_t G = (uint32_t)g->ctx.size(), P = r->n_partitions, B = r->n_buckets;
+  const uint64_t Pi = parts_on(P, G, i);
+  const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
+  const uint64_t NI = mde_tree_internal_nodes(B);
+  auto pos = [&](uint64_t k) { return r->value_stride ? k * r->value_stride : r->value_off[k]; };
+  auto first_rec = [&](uint64_t p) { return tagged ? r->part_rec[p] : r->seg_rec[p * B]; };
+  uint64_t recs = 0, bytes = 0;
+  for (uint64_t p = i; p < P; p += G) {
+    recs += first_rec(p + 1) - first_rec(p);
+    bytes += pos(first_rec(p + 1)) - pos(first_rec(p));
+  }
+  const uint64_t nseg = tagged ? Pi + 1 : Pi * B + 1;
+  int rc;
+  if ((rc = grow(g, i, mde_group::kVals, bytes + 16, msg)) || (rc = grow(g, i, mde_group::kSeg, nseg * 8, msg)) ||
+      (!r->value_stride && (rc = grow(g, i, mde_group::kVoff, (recs + 1) * 8, msg))) ||
+      (tagged && (rc = grow(g, i, mde_group::kTag, recs * 2 + 2, msg))) ||
+      (rc = grow(g, i, mde_group::kDig, Pi * B * 8, msg)) || (rc = grow(g, i, mde_group::kSize, Pi * B * 4, msg)) ||
+      (rc = grow(g, i, mde_group::kItems, Pi * 4, msg)) || (rc = grow(g, i, mde_group::kRoot, slab_parts * 32, msg)) ||
+      (want_nodes && (rc = grow(g, i, mde_group::kNodes, Pi * NI * 32, msg))) ||
+      (rc = grow(g, i, mde_group::kRecv, G * slab_parts * 32, msg)))
+    return rc;
+  auto dptr = [&](int k) { return static_cast<uint8_t*>(g->stage[i][k].p); };
+  // host-side rebased index arrays
+  std::vector<uint64_t> seg(nseg), voff(r->value_stride ? 0 : recs + 1);
+  uint64_t rb = 0, bb = 0, k = 0;
+  hipStream_t st = static_cast<hipStream_t>(mde_get_stream(g->ctx[i]));
+  GHIP(hipSetDevice(g->dev[i]));
+  for (uint64_t p = i; p < P; p += G, k++) {
+    const uint64_t r0 = first_rec(p), r1 = first_rec(p + 1), b0 = pos(r0), b1 = pos(r1);
+    if (tagged) {
+      seg[k] = rb;
+    } else {
+      for (uint32_t b = 0; b < B; b++) seg[k * B + b] = r->seg_rec[p * B + b] - r0 + rb;
+    }
+    if (!r->value_stride)
+      for (uint64_t j = r0; j < r1; j++) voff[rb + j - r0] = r->value_off[j] - b0 + bb;
+    if (b1 > b0) GHIP(hipMemcpyAsync(dptr(mde_group::kVals) + bb, r->values + b0, b1 - b0, hipMemcpyHostToDevice, st));
+    if (tagged && r1 > r0)
+      GHIP(hipMemcpyAsync(dptr(mde_group::kTag) + rb * 2, r->bucket_tag + r0, (r1 - r0) * 2, hipMemcpyHostToDevice, st));
+    rb += r1 - r0;
+    bb += b1 - b0;
+  }
+  seg[nseg - 1] = rb;
+  if (!r->value_stride) voff[recs] = bb;
+  GHIP(hipMemcpyAsync(dptr(mde_group::kSeg), seg.data(), nseg * 8, hipMemcpyHostToDevice, st));
+  if (!r->value_stride) GHIP(hipMemcpyAsync(dptr(mde_group::kVoff), voff.data(), (recs + 1) * 8, hipMemcpyHostToDevice, st));
+  // the root slab is fixed-size: rows past this shard's partitions stay zero
+  if (tree) GHIP(hipMemsetAsync(dptr(mde_group::kRoot), 0, slab_parts * 32, st));
+  mde_records dr{};
+  dr.values = dptr(mde_group::kVals);
+  dr.values_bytes = bb;
+  dr.value_stride = r->value_stride;
+  dr.layout = r->layout;
+  dr.value_off = r->value_stride ? nullptr : reinterpret_cast<const uint64_t*>(dptr(mde_group::kVoff));
+  dr.n_records = rb;
+  dr.n_partitions = (uint32_t)Pi;
+  dr.n_buckets = B;
+  if (tagged) {
+    dr.part_rec = reinterpret_cast<const uint64_t*>(dptr(mde_group::kSeg));
+    dr.bucket_tag = reinterpret_cast<const uint16_t*>(dptr(mde_group::kTag));
+  } else {
+    dr.seg_rec = reinterpret_cast<const uint64_t*>(dptr(mde_group::kSeg));
+  }
+  mde_tree_out dout{reinterpret_cast<uint64_t*>(dptr(mde_group::kDig)), reinterpret_cast<int32_t*>(dptr(mde_group::kSize)),
+                    reinterpret_cast<int32_t*>(dptr(mde_group::kItems)), tree ? dptr(mde_group::kRoot) : nullptr,
+                    want_nodes ? dptr(mde_group::kNodes) : nullptr};
+  // the host copies above must complete before the host vectors go out of scope
+  GHIP(hipStreamSynchronize(st));
+  rc = mde_build_async(g->ctx[i], &dr, &dout);
+  return rc ? ctx_err(g, i, rc, msg) : MDE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mde_group_create(const int* devices, uint32_t n, mde_group** out) {
+  if (!out) return MDE_E_INVAL;
+  *out = nullptr;
+  if (!devices || !n) return MDE_E_INVAL;
+  mde_group* g = new (std::nothrow) mde_group();
+  if (!g) return MDE_E_NOMEM;
+  for (uint32_t i = 0; i < n; i++) {
+    mde_ctx* c = nullptr;
+    const int rc = mde_create(devices[i], &c);
+    if (rc != MDE_OK) {
+      mde_group_destroy(g);
+      return rc;
+    }
+    g->ctx.push_back(c);
+    g->dev.push_back(devices[i]);
+  }
+  g->stage.assign(n, std::vector<Buf>(mde_group::kBufs));
+  std::vector<int> sorted(g->dev);
+  std::sort(sorted.begin(), sorted.end());
+  const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+  const char* force = std::getenv("MDE_GROUP_GATHER");  // "copy": device copies even on distinct GPUs
+  const bool want_rccl = distinct && !(force && !std::strcmp(force, "copy"));
+  if (want_rccl && rccl().why.empty()) {
+    g->comm.assign(n, nullptr);
+    const ncclResult_t e = rccl().init_all(g->comm.data(), (int)n, g->dev.data());
+    if (e != ncclSuccess) {
+      g->comm.clear();
+      g->gather_kind = std::string("device copies (ncclCommInitAll failed: ") + rccl().error_string(e) + ")";
+    } else {
+      g->gather_kind = "rccl all_gather";
+    }
+  } else {
+    g->gather_kind = !distinct ? "device copies (a device listed twice)"
+                     : want_rccl ? "device copies (" + rccl().why + ")" : "device copies (MDE_GROUP_GATHER=copy)";
+  }
+  if (g->comm.empty()) {
+    g->ready.assign(n, nullptr);
+    for (uint32_t i = 0; i < n; i++) {
+      (void)hipSetDevice(g->dev[i]);
+      if (hipEventCreateWithFlags(&g->ready[i], hipEventDisableTiming) != hipSuccess) {
+        mde_group_destroy(g);
+        return MDE_E_DEVICE;
+      }
+    }
+  }
+  *out = g;
+  return MDE_OK;
+}
+
+void mde_group_destroy(mde_group* g) {
+  if (!g) return;
+  for (mde_ctx* c : g->ctx) (void)mde_synchronize(c);
+  for (ncclComm_t c : g->comm)
+    if (c) (void)rccl().destroy(c);
+  for (size_t i = 0; i < g->ready.size(); i++)
+    if (g->ready[i]) {
+      (void)hipSetDevice(g->dev[i]);
+      (void)hipEventDestroy(g->ready[i]);
+    }
+  for (size_t i = 0; i < g->stage.size(); i++) {
+    (void)hipSetDevice(g->dev[i]);
+    for (Buf& b : g->stage[i])
+      if (b.p) (void)hipFree(b.p);
+  }
+  for (mde_ctx* c : g->ctx) mde_destroy(c);
+  delete g;
+}
+
+uint32_t mde_group_size(const mde_group* g) { return g ? (uint32_t)g->ctx.size() : 0u; }
+
+mde_ctx* mde_group_ctx(mde_group* g, uint32_t i) { return g && i < g->ctx.size() ? g->ctx[i] : nullptr; }
+
+const char* mde_group_gather_kind(const mde_group* g) { return g ? g->gather_kind.c_str() : "null group"; }
+
+uint32_t mde_group_partitions(const mde_group* g, uint32_t n_partitions, uint32_t i) {
+  return g && i < g->ctx.size() ? (uint32_t)parts_on(n_partitions, (uint32_t)g->ctx.size(), i) : 0u;
+}
+
+const char* mde_group_last_error(const mde_group* g) { return g ? g->err.c_str() : "null group"; }
+
+uint64_t mde_group_last_error_copy(mde_group* g, char* buf, uint64_t cap) {
+  std::string m = "null group";
+  if (g) {
+    std::lock_guard<std::mutex> lk(g->mu);
+    m = g->err;
+  }
+  if (buf && cap) {
+    const uint64_t k = std::min<uint64_t>(m.size(), cap - 1);
+    std::memcpy(buf, m.data(), k);
+    buf[k] = 0;
+  }
+  return m.size();
+}
+
+int mde_group_build_async(mde_group* g, const mde_records* shard, const mde_tree_out* shard_out) {
+  if (!g || !shard || !shard_out) return MDE_E_INVAL;
+  for (uint32_t i = 0; i < g->ctx.size(); i++) {
+    if (!shard[i].n_partitions) continue;
+    const int rc = mde_build_async(g->ctx[i], &shard[i], &shard_out[i]);
+    if (rc) {
+      std::lock_guard<std::mutex> lk(g->mu);
+      return ctx_err(g, i, rc, g->err);
+    }
+  }
+  return MDE_OK;
+}
+
+int mde_group_build_pipelined_async(mde_group* g, const mde_records* shard, const mde_tree_out* shard_out) {
+  if (!g || !shard || !shard_out) return MDE_E_INVAL;
+  for (uint32_t i = 0; i < g->ctx.size(); i++) {
+    if (!shard[i].n_partitions) continue;
+    const int rc = mde_build_pipelined_async(g->ctx[i], &shard[i], &shard_out[i]);
+    if (rc) {
+      std::lock_guard<std::mutex> lk(g->mu);
+      return ctx_err(g, i, rc, g->err);
+    }
+  }
+  return MDE_OK;
+}
+
+int mde_group_build_pipeline_drain_async(mde_group* g) {
+  if (!g) return MDE_E_INVAL;
+  for (uint32_t i = 0; i < g->ctx.size(); i++) {
+    const int rc = mde_build_pipeline_drain_async(g->ctx[i]);
+    if (rc) {
+      std::lock_guard<std::mutex> lk(g->mu);
+      return ctx_err(g, i, rc, g->err);
+    }
+  }
+  return MDE_OK;
+}
+
+int mde_group_gather_async(mde_group* g, const void* const* send, void* const* recv, uint64_t bytes) {
+  if (!g || !send || !recv) return MDE_E_INVAL;
+  std::lock_guard<std::mutex> lk(g->mu);
+  return gather(g, send, recv, bytes, g->err);
+}
+
+int mde_group_synchronize(mde_group* g) {
+  if (!g) return MDE_E_INVAL;
+  for (uint32_t i = 0; i < g->ctx.size(); i++) {
+    const int rc = mde_synchronize(g->ctx[i]);
+    if (rc) {
+      std::lock_guard<std::mutex> lk(g->mu);
+      return ctx_err(g, i, rc, g->err);
+    }
+  }
+  return MDE_OK;
+}
+
+int mde_multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o) {
+  if (!g || g->ctx.empty()) return MDE_E_INVAL;
+  std::lock_guard<std::mutex> lk(g->mu);
+  g->err.clear();
+  std::string& msg = g->err;
+  int rc = check(r, o, msg);
+  if (rc) return rc;
+  const uint32_t G = (uint32_t)g->ctx.size(), P = r->n_partitions, B = r->n_buckets;
+  if (!P) return MDE_OK;
+  const uint64_t NI = mde_tree_internal_nodes(B), slab = (P + G - 1) / G;
+  const bool tree = o->root != nullptr, nodes = o->nodes != nullptr;
+  // every shard's copies and build, concurrently (one host thread per device: pageable copies
+  // block the calling thread)
+  std::vector<int> rcs(G, MDE_OK);
+  std::vector<std::string> errs(G);
+  {
+    std::vector<std::thread> th;
+    for (uint32_t i = 0; i < G && i < P; i++)
+      th.emplace_back([&, i] { rcs[i] = upload_and_build(g, i, r, tree, nodes, slab, errs[i]); });
+    for (auto& t : th) t.join();
+  }
+  for (uint32_t i = 0; i < G; i++)
+    if (rcs[i]) {
+      g->err = errs[i];
+      return rcs[i];
+    }
+  // the exchange step: every device's root slab to every device (device 0's copy comes home)
+  std::vector<const void*> send(G);
+  std::vector<void*> recv(G);
+  for (uint32_t i = 0; i < G; i++) {
+    if ((rc = grow(g, i, mde_group::kRoot, slab * 32, msg)) || (rc = grow(g, i, mde_group::kRecv, G * slab * 32, msg)))
+      return rc;
+    send[i] = g->stage[i][mde_group::kRoot].p;
+    recv[i] = g->stage[i][mde_group::kRecv].p;
+    if (i >= P) {  // a device without partitions still takes part with a zero slab
+      (void)hipSetDevice(g->dev[i]);
+      GHIP(hipMemsetAsync(g->stage[i][mde_group::kRoot].p, 0, slab * 32,
+                          static_cast<hipStream_t>(mde_get_stream(g->ctx[i]))));
+    }
+  }
+  if (tree && (rc = gather(g, send.data(), recv.data(), slab * 32, msg))) return rc;
+  // results home, in partition order
+  std::vector<uint8_t> h;
+  for (uint32_t i = 0; i < G && i < P; i++) {
+    const uint64_t Pi = parts_on(P, G, i);
+    hipStream_t st = static_cast<hipStream_t>(mde_get_stream(g->ctx[i]));
+    GHIP(hipSetDevice(g->dev[i]));
+    auto home = [&](int which, uint64_t row_bytes, uint8_t* dst) -> int {
+      h.resize(Pi * row_bytes);
+      GHIP(hipMemcpyAsync(h.data(), g->stage[i][which].p, Pi * row_bytes, hipMemcpyDeviceToHost, st));
+      GHIP(hipStreamSynchronize(st));
+      for (uint64_t k = 0; k < Pi; k++) std::memcpy(dst + (i + k * G) * row_bytes, h.data() + k * row_bytes, row_bytes);
+      return MDE_OK;
+    };
+    if (o->digest && (rc = home(mde_group::kDig, (uint64_t)B * 8, reinterpret_cast<uint8_t*>(o->digest)))) return rc;
+    if (o->size && (rc = home(mde_group::kSize, (uint64_t)B * 4, reinterpret_cast<uint8_t*>(o->size)))) return rc;
+    if (o->items && (rc = home(mde_group::kItems, 4, reinterpret_cast<uint8_t*>(o->items)))) return rc;
+    if (nodes && (rc = home(mde_group::kNodes, NI * 32, o->nodes))) return rc;
+  }
+  if (tree) {  // the gathered slabs on device 0: slab r row k = partition r + k * G
+    h.resize(G * slab * 32);
+    hipStream_t st = static_cast<hipStream_t>(mde_get_stream(g->ctx[0]));
+    GHIP(hipSetDevice(g->dev[0]));
+    GHIP(hipMemcpyAsync(h.data(), g->stage[0][mde_group::kRecv].p, G * slab * 32, hipMemcpyDeviceToHost, st));
+    GHIP(hipStreamSynchronize(st));
+    for (uint32_t rr = 0; rr < G; rr++)
+      for (uint64_t k = 0; k < slab; k++) {
+        const uint64_t p = rr + k * G;
+        if (p < P) std::memcpy(o->root + p * 32, h.data() + (rr * slab + k) * 32, 32);
+      }
+  }
+  for (uint32_t i = 0; i < G; i++) {
+    (void)hipSetDevice(g->dev[i]);
+    GHIP(hipStreamSynchronize(static_cast<hipStream_t>(mde_get_stream(g->ctx[i]))));
+  }
+  return MDE_OK;
+}
+
+// Host ingest over the group (arenas larger than HBM): nothing stays resident, so each device
+// streams one contiguous block of partitions -- one contiguous host range per PCIe link -- through
+// mde_build_streamed's two-slot ring, concurrently. Same results as mde_multi_build.
+int mde_multi_build_streamed(mde_group* g, const mde_records* r, const mde_tree_out* o, uint64_t chunk_bytes) {
+  if (!g || g->ctx.empty()) return MDE_E_INVAL;
+  std::lock_guard<std::mutex> lk(g->mu);
+  g->err.clear();
+  int rc = check(r, o, g->err);
+  if (rc) return rc;
+  if (!o->root) return fail(g->err, MDE_E_INVAL, "out/root is NULL");
+  const uint32_t G = (uint32_t)g->ctx.size(), P = r->n_partitions, B = r->n_buckets;
+  const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
+  const uint64_t NI = mde_tree_internal_nodes(B);
+  struct Shard {
+    mde_records rec;
+    mde_tree_out out;
+    std::vector<uint64_t> seg, voff;
+    int rc = MDE_OK;
+    bool live = false;
+  };
+  std::vector<Shard> sh(G);
+  for (uint32_t i = 0; i < G; i++) {
+    const uint64_t p0 = (uint64_t)P * i / G, p1 = (uint64_t)P * (i + 1) / G;
+    if (p0 == p1) continue;
+    Shard& s = sh[i];
+    s.live = true;
+    s.rec = *r;
+    s.rec.n_partitions = (uint32_t)(p1 - p0);
+    const uint64_t r0 = tagged ? r->part_rec[p0] : r->seg_rec[p0 * B];
+    const uint64_t r1 = tagged ? r->part_rec[p1] : r->seg_rec[p1 * B];
+    const uint64_t b0 = r->value_stride ? r0 * r->value_stride : r->value_off[r0];
+    const uint64_t b1 = r->value_stride ? r1 * r->value_stride : r->value_off[r1];
+    s.rec.values = r->values + b0;
+    s.rec.values_bytes = b1 - b0;
+    s.rec.n_records = r1 - r0;
+    if (tagged) {
+      s.seg.assign(r->part_rec + p0, r->part_rec + p1 + 1);
+      s.rec.part_rec = s.seg.data();
+      s.rec.bucket_tag = r->bucket_tag ? r->bucket_tag + r0 : nullptr;
+    } else {
+      s.seg.assign(r->seg_rec + p0 * B, r->seg_rec + p1 * B + 1);
+      s.rec.seg_rec = s.seg.data();
+    }
+    for (uint64_t& x : s.seg) x -= r0;
+    if (!r->value_stride) {
+      s.voff.assign(r->value_off + r0, r->value_off + r1 + 1);
+      for (uint64_t& x : s.voff) x -= b0;
+      s.rec.value_off = s.voff.data();
+    }
+    s.out.digest = o->digest ? o->digest + p0 * B : nullptr;
+    s.out.size = o->size ? o->size + p0 * B : nullptr;
+    s.out.items = o->items ? o->items + p0 : nullptr;
+    s.out.root = o->root + p0 * 32;
+    s.out.nodes = o->nodes ? o->nodes + p0 * NI * 32 : nullptr;
+  }
+  std::vector<std::thread> th;
+  for (uint32_t i = 0; i < G; i++)
+    if (sh[i].live) th.emplace_back([&, i] { sh[i].rc = mde_build_streamed(g->ctx[i], &sh[i].rec, &sh[i].out, chunk_bytes); });
+  for (auto& t : th) t.join();
+  for (uint32_t i = 0; i < G; i++)
+    if (sh[i].rc != MDE_OK) return ctx_err(g, i, sh[i].rc, g->err);
+  return MDE_OK;
+}
+
+}  // extern "C"

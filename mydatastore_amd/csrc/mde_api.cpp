@@ -749,6 +749,16 @@ extern "C" {
 
 int mde_abi_version(void) { return MDE_ABI_VERSION; }
 
+int mde_device_count(void) {
+  int n = 0, k = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  for (int d = 0; d < n; d++) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) k++;
+  }
+  return k;
+}
+
 int mde_reserve_decode_scratch(mde_ctx* c, uint64_t n_objects, uint64_t object_bytes) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
@@ -1673,139 +1683,4 @@ int mde_memcpy_d2h(mde_ctx* c, void* dst, const void* src, uint64_t bytes) {
 
 }  // extern "C"
 
-// ---------------------------------------------------------------------------------------------
-// Device groups: one process driving G GPUs (mde_multi_build).
-struct mde_group {
-  std::vector<mde_ctx*> ctx;
-  std::mutex mu;  // held by mde_multi_build[_streamed] for the whole call; guards err
-  std::string err;
-};
-
-int mde_group_create(const int* devices, uint32_t n, mde_group** out) {
-  if (!out) return MDE_E_INVAL;
-  *out = nullptr;
-  if (!devices || !n) return MDE_E_INVAL;
-  mde_group* g = new (std::nothrow) mde_group();
-  if (!g) return MDE_E_NOMEM;
-  for (uint32_t i = 0; i < n; i++) {
-    mde_ctx* c = nullptr;
-    const int rc = mde_create(devices[i], &c);
-    if (rc != MDE_OK) {
-      mde_group_destroy(g);
-      return rc;
-    }
-    g->ctx.push_back(c);
-  }
-  *out = g;
-  return MDE_OK;
-}
-
-void mde_group_destroy(mde_group* g) {
-  if (!g) return;
-  for (mde_ctx* c : g->ctx) mde_destroy(c);
-  delete g;
-}
-
-uint32_t mde_group_size(const mde_group* g) { return g ? (uint32_t)g->ctx.size() : 0u; }
-
-mde_ctx* mde_group_ctx(mde_group* g, uint32_t i) { return g && i < g->ctx.size() ? g->ctx[i] : nullptr; }
-
-const char* mde_group_last_error(const mde_group* g) { return g ? g->err.c_str() : "null group"; }
-
-uint64_t mde_group_last_error_copy(mde_group* g, char* buf, uint64_t cap) {
-  if (!g) return copy_message("null group", buf, cap);
-  std::lock_guard<std::mutex> lk(g->mu);
-  return copy_message(g->err, buf, cap);
-}
-
-namespace {
-// mde_multi_build / mde_multi_build_streamed: split P partitions into G contiguous blocks and
-// build each on its own device, one host thread per device (streamed: chunk_bytes ring per device).
-int multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o, bool streamed, uint64_t chunk_bytes) {
-  if (!g || g->ctx.empty()) return MDE_E_INVAL;
-  std::lock_guard<std::mutex> glk(g->mu);
-  g->err.clear();
-  mde_ctx* c0 = g->ctx[0];
-  {
-    Guard gd(c0);
-    int rc = check_records(c0, r);
-    if (!rc) rc = check_host_records(c0, r);
-    if (!rc && (!o || !o->root)) rc = set_err(c0, MDE_E_INVAL, "out/root is NULL");
-    if (rc) {
-      g->err = c0->err;
-      return rc;
-    }
-  }
-  const uint32_t G = (uint32_t)g->ctx.size(), P = r->n_partitions, B = r->n_buckets;
-  const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
-  const uint64_t NI = mde::tree_internal(B);
-  struct Shard {
-    mde_records rec;
-    mde_tree_out out;
-    std::vector<uint64_t> seg, voff;
-    int rc = MDE_OK;
-    bool live = false;
-  };
-  std::vector<Shard> sh(G);
-  for (uint32_t i = 0; i < G; i++) {
-    // contiguous partition blocks: one contiguous record range (and byte range) per device
-    const uint64_t p0 = (uint64_t)P * i / G, p1 = (uint64_t)P * (i + 1) / G;
-    if (p0 == p1) continue;
-    Shard& s = sh[i];
-    s.live = true;
-    s.rec = *r;
-    s.rec.n_partitions = (uint32_t)(p1 - p0);
-    const uint64_t r0 = tagged ? r->part_rec[p0] : r->seg_rec[p0 * B];
-    const uint64_t r1 = tagged ? r->part_rec[p1] : r->seg_rec[p1 * B];
-    const uint64_t b0 = r->value_stride ? r0 * r->value_stride : r->value_off[r0];
-    const uint64_t b1 = r->value_stride ? r1 * r->value_stride : r->value_off[r1];
-    s.rec.values = r->values + b0;
-    s.rec.values_bytes = b1 - b0;
-    s.rec.n_records = r1 - r0;
-    if (tagged) {
-      s.seg.assign(r->part_rec + p0, r->part_rec + p1 + 1);
-      s.rec.part_rec = s.seg.data();
-      s.rec.bucket_tag = r->bucket_tag ? r->bucket_tag + r0 : nullptr;
-    } else {
-      s.seg.assign(r->seg_rec + p0 * B, r->seg_rec + p1 * B + 1);
-      s.rec.seg_rec = s.seg.data();
-    }
-    for (uint64_t& x : s.seg) x -= r0;
-    if (!r->value_stride) {
-      s.voff.assign(r->value_off + r0, r->value_off + r1 + 1);
-      for (uint64_t& x : s.voff) x -= b0;
-      s.rec.value_off = s.voff.data();
-    }
-    s.out.digest = o->digest ? o->digest + p0 * B : nullptr;
-    s.out.size = o->size ? o->size + p0 * B : nullptr;
-    s.out.items = o->items ? o->items + p0 : nullptr;
-    s.out.root = o->root + p0 * 32;
-    s.out.nodes = o->nodes ? o->nodes + p0 * NI * 32 : nullptr;
-  }
-  // one host thread per device: each shard's H2D, build and D2H run concurrently
-  std::vector<std::thread> th;
-  for (uint32_t i = 0; i < G; i++)
-    if (sh[i].live)
-      th.emplace_back([&, i] {
-        sh[i].rc = streamed ? mde_build_streamed(g->ctx[i], &sh[i].rec, &sh[i].out, chunk_bytes)
-                            : mde_build(g->ctx[i], &sh[i].rec, &sh[i].out);
-      });
-  for (auto& t : th) t.join();
-  for (uint32_t i = 0; i < G; i++)
-    if (sh[i].rc != MDE_OK) {
-      char m[512];
-      mde_last_error_copy(g->ctx[i], m, sizeof m);
-      g->err = "device " + std::to_string(g->ctx[i]->device) + ": " + m;
-      return sh[i].rc;
-    }
-  return MDE_OK;
-}
-}  // namespace
-
-int mde_multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o) {
-  return multi_build(g, r, o, false, 0);
-}
-
-int mde_multi_build_streamed(mde_group* g, const mde_records* r, const mde_tree_out* o, uint64_t chunk_bytes) {
-  return multi_build(g, r, o, true, chunk_bytes);
-}
+// Device groups (mde_group_*, mde_multi_build*): group.cpp.

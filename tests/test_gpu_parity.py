@@ -498,42 +498,6 @@ def test_layout_b_full_size_equals_layout_a(engine):
         assert torch.equal(oa[k], ob[k]), k
 
 
-@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
-@pytest.mark.parametrize("streamed", [False, True], ids=["direct", "streamed"])
-def test_multi_build_group(golden, coracle, devices, streamed):
-    """mde_multi_build / mde_multi_build_streamed over a device group (several contexts on the one
-    GPU of the box: the split into contiguous partition blocks, per-shard rebasing and concurrent
-    shard threads are the same code an 8-GPU node runs) equals the golden single builds, layouts A
-    and B. Streamed: 4 KiB chunks, so each shard's ring turns over many times."""
-    import mydatastore_amd as mde
-    from tests.datasets import MODES
-    g = mde.Group(devices)
-    assert len(g) == len(devices)
-    kw = {"streamed": True, "chunk_bytes": 4096} if streamed else {}
-    for case in golden("synth_cases.json"):
-        values, voff, stride, seg = synth_arrays(case, coracle)
-        P, B = case["P"], case["B"]
-        out = g.build(values, P, B, stride, voff, seg_rec=seg, **kw)
-        assert out["digest"].tolist() == case["digest"], case["name"]
-        assert out["size"].tolist() == case["size"], case["name"]
-        assert out["items"].tolist() == case["items"], case["name"]
-        assert _roots(out, P) == case["root"], case["name"]
-        assert _node_shas(out, P, B) == case["nodes_sha256"], case["name"]
-        if case["var_len"]:
-            continue
-        n, V = case["n"], case["value_len"]
-        gids = np.arange(n, dtype=np.uint64)
-        part, bk = coracle.synth_tags(gids, P, B, MODES[case["part_mode"]], case["keys_per_partition"])
-        order = np.argsort(part, kind="stable")
-        part_rec = np.zeros(P + 1, np.uint64)
-        np.cumsum(np.bincount(part, minlength=P), out=part_rec[1:])
-        vb = coracle.synth_values(gids[order], V, case["seed"])
-        ob = g.build(vb, P, B, V, part_rec=part_rec, bucket_tag=bk[order].astype(np.uint16), **kw)
-        assert ob["digest"].tolist() == case["digest"], case["name"]
-        assert _roots(ob, P) == case["root"], case["name"]
-    g.close()
-
-
 def test_extract_layout_b(engine):
     """Range extract over layout B (write order + tags): the records of the requested buckets
     (duplicates / out-of-range ids ignored), per partition in arrival order, values included."""

@@ -1,0 +1,175 @@
+"""Device groups (include/mde.h mde_group_*, csrc/group.cpp): one process driving the GPUs of a
+node, partition p on device p % G, the roots all-gathered by RCCL (or device copies when a device
+is listed twice) -- the in-node analogue of the reference's partition sharding over nodes
+(hashring/hashring.go:126-154). On the one-GPU box a group lists device 0
+once (RCCL, one rank) or several times (several contexts, copy gather): the sharding, rebasing,
+slab layout and concurrent shard code are the ones an 8-GPU node runs. Plus two real processes
+(gloo ranks sharing the GPU) running the engine on their shards."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT
+from tests.datasets import MODES, synth_arrays
+
+
+def _roots(out, P):
+    return [out["root"][32 * p:32 * (p + 1)].tobytes().hex() for p in range(P)]
+
+
+def _node_shas(out, P, B):
+    import hashlib
+    import mydatastore_amd as mde
+    ni = mde.tree_internal_nodes(B) * 32
+    return [hashlib.sha256(out["nodes"][ni * p:ni * (p + 1)].tobytes()).hexdigest() for p in range(P)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+@pytest.mark.parametrize("streamed", [False, True], ids=["direct", "streamed"])
+def test_multi_build_group(golden, coracle, devices, streamed):
+    """mde_multi_build (partition p on device p % G, per-partition copies, RCCL or copy root
+    gather) and mde_multi_build_streamed (contiguous blocks through each device's ring, 4 KiB
+    chunks) equal the golden single builds, layouts A and B, nodes included."""
+    import mydatastore_amd as mde
+    g = mde.Group(devices)
+    assert len(g) == len(devices)
+    assert g.gather_kind == ("rccl all_gather" if len(devices) == 1 else "device copies (a device listed twice)")
+    kw = {"streamed": True, "chunk_bytes": 4096} if streamed else {}
+    for case in golden("synth_cases.json"):
+        values, voff, stride, seg = synth_arrays(case, coracle)
+        P, B = case["P"], case["B"]
+        out = g.build(values, P, B, stride, voff, seg_rec=seg, **kw)
+        assert out["digest"].tolist() == case["digest"], case["name"]
+        assert out["size"].tolist() == case["size"], case["name"]
+        assert out["items"].tolist() == case["items"], case["name"]
+        assert _roots(out, P) == case["root"], case["name"]
+        assert _node_shas(out, P, B) == case["nodes_sha256"], case["name"]
+        if not streamed:  # digest-only over the group: no tree, no gather
+            d = g.build(values, P, B, stride, voff, seg_rec=seg, want_tree=False)
+            assert d["digest"].tolist() == case["digest"] and d["root"] is None, case["name"]
+        if case["var_len"]:
+            continue
+        n, V = case["n"], case["value_len"]
+        gids = np.arange(n, dtype=np.uint64)
+        part, bk = coracle.synth_tags(gids, P, B, MODES[case["part_mode"]], case["keys_per_partition"])
+        order = np.argsort(part, kind="stable")
+        part_rec = np.zeros(P + 1, np.uint64)
+        np.cumsum(np.bincount(part, minlength=P), out=part_rec[1:])
+        vb = coracle.synth_values(gids[order], V, case["seed"])
+        ob = g.build(vb, P, B, V, part_rec=part_rec, bucket_tag=bk[order].astype(np.uint16), **kw)
+        assert ob["digest"].tolist() == case["digest"], case["name"]
+        assert _roots(ob, P) == case["root"], case["name"]
+    g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+@pytest.mark.parametrize("B", [64, 1000])
+def test_group_device_resident_build_and_gather(engine, devices, B):
+    """The path bench.py times at N > 1: every device's shard (partition p on device p % G,
+    generated on the device) built by mde_group_build_async and by a run of pipelined builds, then
+    ONE all-gather of the fixed-size root slabs: every device receives the same slabs, and they
+    assemble to exactly the roots of one engine build of the whole workload."""
+    import torch
+    import mydatastore_amd as mde
+    from mydatastore_amd.workload import make_workload
+    G, P, V, n = len(devices), 100, 64, 300_000
+    g = mde.Group(devices)
+    dev = torch.device("cuda:0")
+    shards = [make_workload(engine, n_partitions=P, n_buckets=B, value_len=V, part_mode="mod", n_keys=n,
+                            rank=i, world=G) for i in range(G)]
+    for i, w in enumerate(shards):
+        assert w.n_partitions == g.partitions(P, i)
+    whole = make_workload(engine, n_partitions=P, n_buckets=B, value_len=V, part_mode="mod", n_keys=n)
+    want = whole.build()["root"].cpu().numpy().reshape(P, 32)
+    slab = -(-P // G)
+    for pipelined in (False, True):
+        outs = [w._outs() for w in shards]
+        g.build_async([w.rec for w in shards], [o[1] for o in outs], pipelined=pipelined)
+        if pipelined:  # the second build of the run carries the first one's trees
+            outs2 = [w._outs() for w in shards]
+            g.build_async([w.rec for w in shards], [o[1] for o in outs2], pipelined=True)
+            g.drain_async()
+        g.synchronize()
+        send = [torch.zeros(slab * 32, dtype=torch.uint8, device=dev) for _ in range(G)]
+        recv = [torch.zeros(G * slab * 32, dtype=torch.uint8, device=dev) for _ in range(G)]
+        for i in range(G):
+            send[i][:shards[i].n_partitions * 32].copy_(outs[i][0]["root"])
+        torch.cuda.synchronize(dev)
+        g.gather_async(send, recv, slab * 32)
+        g.synchronize()
+        got = recv[0].cpu().numpy().reshape(G, slab, 32)
+        for i in range(1, G):
+            assert torch.equal(recv[i], recv[0])
+        assembled = np.zeros((P, 32), np.uint8)
+        for r in range(G):
+            pids = shards[r].partition_ids
+            assembled[pids] = got[r, :len(pids)]
+        assert np.array_equal(assembled, want), pipelined
+    g.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.gpu
+def test_two_gloo_ranks_run_the_engine():
+    """Two fresh processes (torch.distributed.run, gloo, both on cuda:0) each build their shard
+    with the ENGINE (not the oracle); the gathered roots equal one process's engine build of the
+    whole workload."""
+    env = {**os.environ, "MASTER_ADDR": "127.0.0.1"}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           str(ROOT / "tests" / "dist_engine_worker.py")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["world"] == 2
+    assert d["gathered_roots_equal_single_process"] and d["rank0_digests_equal_single_process"], d
+    assert d["engine"].endswith("libmde.so")
+
+
+def test_group_symbols_and_cpu_behaviour():
+    """CPU: the group entry points exist; without a GPU mde_group_create fails loudly."""
+    import ctypes as C
+    import torch
+    import mydatastore_amd as mde
+    lib = mde.load_library()
+    for name in ("mde_group_gather_kind", "mde_group_partitions", "mde_group_build_async",
+                 "mde_group_gather_async", "mde_device_count"):
+        assert hasattr(lib, name)
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    assert lib.mde_device_count() == 0
+    devs = (C.c_int * 1)(0)
+    h = C.c_void_p()
+    assert lib.mde_group_create(devs, 1, C.byref(h)) == mde.MDE_E_DEVICE and not h.value
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_bench_group_mode(gpus):
+    """bench.py's N-GPU path (--engine group) end to end on the box: one process, the shards of
+    BASELINE config 4 over `gpus` groups members (GPU 0 listed `gpus` times: --rehearse), pipelined
+    builds and bucketed root gathers; its parity block (gathered slabs, the C-oracle sample of
+    shard 0) is all true."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--engine", "group", "--gpus", str(gpus), "--steps", "9",
+           "--warmup", "2"] + (["--rehearse"] if gpus > 1 else [])
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["parity"]["all_ranks_ok"], d["parity"]
+    assert d["config"]["engine"] == "group" and d["n_gpus"] == gpus
+    assert ("rccl" in d["config"]["root_gather"]) == (gpus == 1)

@@ -9,6 +9,7 @@ for src in mydatastore_amd/csrc/*.hip; do
 done
 hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -Iinclude "$@" -c mydatastore_amd/csrc/mde_api.cpp -o $out/mde_api.o
 hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -Iinclude "$@" -c mydatastore_amd/csrc/batch.cpp -o $out/batch.o
-hipcc -shared --offload-arch=gfx950 -pthread -o tools/ab/libmde_$name.so $out/*.o
+hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -Iinclude "$@" -c mydatastore_amd/csrc/group.cpp -o $out/group.o
+hipcc -shared --offload-arch=gfx950 -pthread -o tools/ab/libmde_$name.so $out/*.o -ldl
 rm -rf $out
 echo tools/ab/libmde_$name.so
