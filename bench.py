@@ -50,6 +50,9 @@ CONFIGS = {
     # not a BASELINE config: C4 at the reference's default PartitionBuckets (config/default-config.yaml:8)
     "c4k": (10_000_000, 1024, 1024, 1000, "mod",
             "C4 at B=1000 (the reference's default PartitionBuckets): 10M keys x 1 KiB values, 1024 partitions"),
+    # not a BASELINE config: the production value shape (PROD_SHAPE below) as the timed workload
+    "prod": (100_000_000, 1024, 8, 1000, "mod",
+             "production shape: 100M 8-byte LE timestamps (main/manager.go:816), 1024 partitions, B=1000"),
 }
 
 

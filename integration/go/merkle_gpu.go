@@ -30,13 +30,16 @@ import (
 
 var (
 	mdeOnce sync.Once
-	// mdeBatcher serves RawPartitionMerkleTree and verifyEpochDecision: VerifyEpoch runs one
-	// partition per call on a pool of worker goroutines (main/manager.go:166-170,491), up to
-	// PartitionConcurrency at once (config/default-config.yaml:9); the batcher coalesces the calls
+	// mdeBatchers serve RawPartitionMerkleTree and verifyEpochDecision, one per GPU of the node:
+	// partition p goes to GPU p % G, the in-node analogue of the ring's partition sharding
+	// (hashring/hashring.go:126-154; the same placement as mde_group / mde_multi_build, which a
+	// caller building many partitions at once uses instead). VerifyEpoch runs one partition per
+	// call on a pool of worker goroutines (main/manager.go:166-170,491), up to
+	// PartitionConcurrency at once (config/default-config.yaml:9); each batcher coalesces the calls
 	// in flight into one device build / verify (group commit, mde_batch_build / mde_batch_verify).
 	// Each call gets its own error message back in its own buffer, so no lock is needed.
-	mdeBatcher *C.mde_batcher
-	mdeErr     error
+	mdeBatchers []*C.mde_batcher
+	mdeErr      error
 	// mdeHostTree: build every returned tree with merkletree.NewTree over the device digests (a
 	// digest-only device build; B-1 host SHA-256s per call) instead of assembling it from the
 	// device's node hashes. Callers of merkletree's own methods need it -- MerkleRoot(),
@@ -53,18 +56,33 @@ var (
 // (profiles/r04/*batch_bench*: shim_hosttree vs shim, INTEGRATION.md section 3).
 const mdeHostTreeMaxBuckets = 256
 
-func mdeEngine() (*C.mde_batcher, error) {
+// mdeEngine returns the batcher of the GPU that holds partitionId.
+func mdeEngine(partitionId int) (*C.mde_batcher, error) {
 	mdeOnce.Do(func() {
-		var b *C.mde_batcher
-		// at most 256 partitions per batch, no wait window: a batch is whatever queued while the
-		// previous batches ran
-		if rc := C.mde_batcher_create(0, 256, 0, &b); rc != C.MDE_OK {
-			mdeErr = errors.Errorf("mde_batcher_create: %s", C.GoString(C.mde_strerror(rc)))
+		n := int(C.mde_device_count())
+		if n < 1 {
+			mdeErr = errors.New("mde: no gfx950 GPU visible")
 			return
 		}
-		mdeBatcher = b
+		for d := 0; d < n; d++ {
+			var b *C.mde_batcher
+			// at most 256 partitions per batch, no wait window: a batch is whatever queued while the
+			// previous batches ran
+			if rc := C.mde_batcher_create(C.int(d), 256, 0, &b); rc != C.MDE_OK {
+				mdeErr = errors.Errorf("mde_batcher_create(%d): %s", d, C.GoString(C.mde_strerror(rc)))
+				for _, x := range mdeBatchers {
+					C.mde_batcher_destroy(x)
+				}
+				mdeBatchers = nil
+				return
+			}
+			mdeBatchers = append(mdeBatchers, b)
+		}
 	})
-	return mdeBatcher, mdeErr
+	if mdeErr != nil {
+		return nil, mdeErr
+	}
+	return mdeBatchers[partitionId%len(mdeBatchers)], nil
 }
 
 // mdeTree -- the *merkletree.MerkleTree NewTree would build over these buckets (cbergoon/merkletree
@@ -112,7 +130,7 @@ func cU64(v []uint64) unsafe.Pointer { return C.CBytes(unsafe.Slice((*byte)(unsa
 // partitions' calls in flight: bucket digests always on the device; for B > mdeHostTreeMaxBuckets
 // the SHA-256 tree too, returned as its node hashes and assembled without hashing (mdeTree).
 func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, upperEpoch int64) (*merkletree.MerkleTree, error) {
-	batcher, err := mdeEngine()
+	batcher, err := mdeEngine(partitionId)
 	if err != nil {
 		return nil, err
 	}
@@ -194,7 +212,7 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 // calls PoliteStreamRequest(partitionId, epoch, epoch+1, diffSet).
 func verifyEpochDecision(myTree *merkletree.MerkleTree, partitionId int, epoch int64,
 	epochTreeObjects []*rpc.RpcEpochTreeObject, replicaCount int) (bool, int, []int32, []byte, error) {
-	batcher, err := mdeEngine()
+	batcher, err := mdeEngine(partitionId)
 	if err != nil {
 		return false, 0, nil, nil, err
 	}

@@ -5,7 +5,8 @@
 #   tests   -m gpu parity suite            -> gpurun_out/$TAG/pytest_gpu.log
 #   smoke   __graft_entry__.smoke()        -> smoke.log
 #   bench   default bench line (N=1)       -> bench_default.json
-#   batch   tests/cpp/batch_bench (all)    -> batch_bench.jsonl
+#   batch   tests/cpp/batch_bench, 3 runs  -> batch_bench_r{1,2,3}.jsonl
+#   group1  bench.py --engine group --gpus 1 (the N-GPU path as a 1-GPU group, RCCL) -> bench_group1.json
 #   prod    bench.py --config prod line    -> bench_prod.json
 #   prof    rocprofv3 trace + FETCH/WRITE PMC of the default bench (tools/profile.sh)
 #   sq      SQ counters of the default bench workload (one --pmc pass)
@@ -37,8 +38,14 @@ for s in "$@"; do
       cat $O/bench_prod.json ;;
     batch)
       step batch
-      timeout -k 10 300 tests/cpp/build/batch_bench 0.4 > $O/batch_bench.jsonl 2> $O/batch_bench.err || { tail -20 $O/batch_bench.err; exit 1; }
-      tail -1 $O/batch_bench.jsonl ;;
+      for rep in 1 2 3; do
+        timeout -k 10 300 tests/cpp/build/batch_bench 0.4 > $O/batch_bench_r$rep.jsonl 2> $O/batch_bench_r$rep.err || { tail -20 $O/batch_bench_r$rep.err; exit 1; }
+        tail -1 $O/batch_bench_r$rep.jsonl
+      done ;;
+    group1)
+      step group1
+      timeout -k 10 300 python bench.py --engine group --gpus 1 ${BENCH_ARGS:-} > $O/bench_group1.json 2> $O/bench_group1.err || { tail -20 $O/bench_group1.err; exit 1; }
+      cat $O/bench_group1.json ;;
     prof)
       step prof
       bash tools/profile.sh $TAG c4 c4 || exit 1 ;;
