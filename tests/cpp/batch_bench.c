@@ -432,8 +432,11 @@ int main(int argc, char** argv) {
     fprintf(stderr, "mde_create: %d (%s)\n", rc, mde_strerror(rc));
     return 1;
   }
-  if ((rc = mde_batcher_create(0, 256, 0, &batcher))) return 1;
-  printf("{\"host_sha_extensions\": %s}\n", oracle_sha_ni() ? "true" : "false");
+  /* MDE_BATCH_WAIT_US: the batcher's collection window (0 = none, the shim's setting) */
+  const char* wait_env = getenv("MDE_BATCH_WAIT_US");
+  const uint32_t wait_us = wait_env ? (uint32_t)atoi(wait_env) : 0u;
+  if ((rc = mde_batcher_create(0, 256, wait_us, &batcher))) return 1;
+  printf("{\"host_sha_extensions\": %s, \"batcher_wait_us\": %u}\n", oracle_sha_ni() ? "true" : "false", wait_us);
   if (argc > 3) {
     const int only = argc > 4 ? case_by_name(argv[4]) : -1;
     if (argc > 4 && only < 0) {
