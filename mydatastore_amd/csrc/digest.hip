@@ -513,15 +513,8 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
   // chain bounds that step; a deliberate s_sleep per scan step or priority 0 did not do as well
   // (profiles/r03y_rec8_scalar_ab.txt, r03z_rec8_throttle_ab.txt).
   const uint64_t span = ((end - beg) + 15) & ~15ull;  // <= kMaxWaveBytes
-#ifdef MDE_REC8_SGPR  // probe only (A/B): the resource in SGPRs, no per-load readfirstlane loop
-  const uint64_t base_u = (uint64_t)(uintptr_t)(d.base + beg);
-  const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)base_u), bhi = __builtin_amdgcn_readfirstlane((uint32_t)(base_u >> 32));
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(uintptr_t)(((uint64_t)bhi << 32) | blo), (short)0, (int)__builtin_amdgcn_readfirstlane((uint32_t)span), 0x00020000);
-#else
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)(d.base + beg), (short)0, (int)span, 0x00020000);
-#endif
   u32x4 va[ROWS], vb[ROWS];
   load_rec8<NT, ROWS>(va, rs, 0, lane);  // the first step's loads before the bucket search
   if (lane == 0) R[kRecs] = 0;           // F(kRecs) = E[64] + 0 (rec8_swz(kRecs) == kRecs)
