@@ -152,6 +152,10 @@ struct mde_batcher {
   // copy; above ~16 KB such a copy starts ~11 us after the kernel, profiles/r03q_call_trace.txt);
   // MDE_DIRECT_OUT=0 turns it off (A/B)
   bool direct_out = true;
+  // inputs of a small batch read by the kernels straight from the slot's pinned in buffer (no H2D
+  // copy command: at one small partition the copy, its gap to the kernel and its host call cost
+  // more than reading ~10 KB over PCIe); MDE_DIRECT_IN=0/1 overrides (A/B)
+  bool direct_in = false;
   bool blocking_sync = false;  // MDE_BATCH_BLOCKING_SYNC=1: leaders sleep on their batch's event (A/B)
   // MDE_BATCH_PROFILE=1: host-side phase times summed over batches, printed by mde_batcher_destroy
   bool profile = false;
@@ -288,6 +292,19 @@ uint8_t* mapped_out(mde_batcher* b, mde_batcher::Slot* sl) {
   return static_cast<uint8_t*>(p);
 }
 
+// Batches whose inputs are at most this many bytes may be read in place from pinned memory.
+constexpr uint64_t kDirectInMax = 64ull << 10;
+
+// Device address of the slot's pinned in buffer for a small batch (NULL: copy to the device).
+const uint8_t* mapped_in(mde_batcher* b, mde_batcher::Slot* sl, uint64_t in_bytes) {
+  void* p = nullptr;
+  if (!b->direct_in || in_bytes > kDirectInMax || hipHostGetDevicePointer(&p, sl->pin_in.p, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return static_cast<const uint8_t*>(p);
+}
+
 // Stage + launch one build batch (records rebased into one arena): ONE H2D copy, mde_build_async,
 // ONE D2H copy and an event, all enqueued on the batcher context's stream.
 void launch_build(mde_batcher* b, mde_batcher::Slot* sl) {
@@ -348,12 +365,13 @@ void launch_build(mde_batcher* b, mde_batcher::Slot* sl) {
   if (!stride) hvoff[N] = V;
   hseg[S] = N;
   hipStream_t st = static_cast<hipStream_t>(mde_get_stream(sl->ctx));
-  uint8_t* din = static_cast<uint8_t*>(sl->dev_in.p);
+  const uint8_t* min_ = mapped_in(b, sl, in_bytes);
+  const uint8_t* din = min_ ? min_ : static_cast<const uint8_t*>(sl->dev_in.p);
   // every build output is stored once by the tree pass (trees wider than the LDS levels re-read
   // their nodes: device memory and a copy for those)
   uint8_t* mapped = B <= 4096u ? mapped_out(b, sl) : nullptr;
   uint8_t* dout = mapped ? mapped : static_cast<uint8_t*>(sl->dev_out.p);
-  BHIP(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, st));
+  if (!min_) BHIP(hipMemcpyAsync(sl->dev_in.p, hin, in_bytes, hipMemcpyHostToDevice, st));
   mde_records dr{};
   dr.values = din + o_vals;
   dr.values_bytes = V;
@@ -469,12 +487,13 @@ void launch_verify(mde_batcher* b, mde_batcher::Slot* sl) {
   }
   hoff[P * R] = base;
   hipStream_t st = static_cast<hipStream_t>(mde_get_stream(sl->ctx));
-  uint8_t* din = static_cast<uint8_t*>(sl->dev_in.p);
+  const uint8_t* min_ = mapped_in(b, sl, in_bytes);
+  const uint8_t* din = min_ ? min_ : static_cast<const uint8_t*>(sl->dev_in.p);
   uint8_t* dout = static_cast<uint8_t*>(sl->dev_out.p);
   // every verify output is stored once by the launch: straight into pinned memory
   uint8_t* mapped = mapped_out(b, sl);
   uint8_t* wout = mapped ? mapped : dout;
-  BHIP(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, st));
+  if (!min_) BHIP(hipMemcpyAsync(sl->dev_in.p, hin, in_bytes, hipMemcpyHostToDevice, st));
   const uint64_t* d_dig = reinterpret_cast<const uint64_t*>(din + i_dig);
   int rc = mde_reserve_decode_scratch(sl->ctx, P * R, nbytes);  // linear decode of any peer object
   if (rc) {
@@ -688,6 +707,7 @@ int mde_batcher_create(int device, uint32_t max_partitions, uint32_t max_wait_us
   }
   b->device = device;
   if (const char* e = std::getenv("MDE_DIRECT_OUT")) b->direct_out = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MDE_DIRECT_IN")) b->direct_in = std::atoi(e) != 0;
   if (const char* e = std::getenv("MDE_BATCH_BLOCKING_SYNC")) b->blocking_sync = std::atoi(e) != 0;
   if (const char* e = std::getenv("MDE_BATCH_PROFILE")) b->profile = std::atoi(e) != 0;
   if (const char* e = std::getenv("MDE_BATCH_EARLY")) b->early_handoff = std::atoi(e) != 0;
