@@ -371,6 +371,29 @@ int mde_batch_verify(mde_batcher* b, uint32_t n_buckets, int32_t partition, int6
                      int32_t* peer_status, uint8_t* object_out, uint64_t object_stride,
                      uint32_t* object_len, char* err, uint64_t err_cap);
 
+/* Resident build service for the one-partition calls (RawPartitionMerkleTree,
+ * main/merkle_tree.go:86-116, called once per VerifyEpoch, main/manager.go:1036). A persistent
+ * launch keeps one workgroup per request slot resident on `device`, polling the slot in coherent
+ * pinned host memory: a call packs its records into a free slot and spins until the slot's
+ * workgroup has built them (the one-launch small build: bucket digests, then the SHA-256 tree, or
+ * no tree when out->root is NULL) into the slot's pinned outputs -- no kernel launch, copy command
+ * or event per call. The launch ends itself after MDE_SERVER_LIFETIME_MS (default 100) and the
+ * next call relaunches it, so an idle process holds no GPU work. n_slots = 0: 16 (at most 256);
+ * max_buckets = 0: 1024 (at most 4096), which sizes the launch's LDS. mde_server_build has
+ * mde_batch_build's contract (layout A, host pointers read only during the call, its own error
+ * message in err); a request one workgroup cannot take (more partitions than it holds, more than
+ * 256 KiB of packed inputs, n_buckets > max_buckets) runs as mde_build on the service's own
+ * context. Thread-safe; mde_server_destroy must not race with calls in flight. */
+typedef struct mde_server mde_server;
+int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_server** out);
+void mde_server_destroy(mde_server* s);
+uint32_t mde_server_slots(const mde_server* s);
+int mde_server_build(mde_server* s, const mde_records* rec, const mde_tree_out* out, char* err,
+                     uint64_t err_cap);
+/* calls served, launches made (1 + relaunches after a lifetime ended) and calls run on the
+ * service's context */
+int mde_server_stats(mde_server* s, uint64_t* requests, uint64_t* launches, uint64_t* on_context);
+
 /* Write-time tagging of raw keys (device): bucket = BE64(SHA256(key)[:8]) % n_buckets
  * (main/manager.go:773-778), partition = XXH64(key, 0) % n_partitions (hashring.go:108-110).
  * key i = keys[key_off[i] .. key_off[i+1]). Either output may be NULL. */

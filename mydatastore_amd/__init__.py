@@ -48,6 +48,7 @@ EXPORTED_SYMBOLS = (
     "mde_group_build_pipeline_drain_async", "mde_group_gather_async", "mde_group_synchronize", "mde_device_count",
     "mde_batcher_create", "mde_batcher_destroy", "mde_batcher_ctx", "mde_batcher_contexts", "mde_batcher_stats",
     "mde_batch_build", "mde_batch_verify", "mde_reserve_decode_scratch",
+    "mde_server_create", "mde_server_destroy", "mde_server_slots", "mde_server_build", "mde_server_stats",
 )
 
 
@@ -162,6 +163,11 @@ def load_library() -> C.CDLL:
         "mde_batcher_contexts": (u32, [vp]),
         "mde_batcher_stats": (C.c_int, [vp, vp, vp, vp]),
         "mde_batch_build": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), C.c_char_p, u64]),
+        "mde_server_create": (C.c_int, [C.c_int, u32, u32, C.POINTER(vp)]),
+        "mde_server_destroy": (None, [vp]),
+        "mde_server_slots": (u32, [vp]),
+        "mde_server_build": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), C.c_char_p, u64]),
+        "mde_server_stats": (C.c_int, [vp, vp, vp, vp]),
         "mde_batch_verify": (C.c_int, [vp, u32, i32, C.c_int64, vp, vp, u32, vp, vp, u32, vp, vp, vp, vp,
                                        vp, vp, u64, vp, C.c_char_p, u64]),
         "mde_synth_tags_async": (C.c_int, [vp, vp, u64, u32, u32, C.c_int, u64, vp, vp]),
@@ -759,3 +765,51 @@ class Batcher:
         return {"valid": bool(valid[0]), "valid_count": int(vc[0]), "diff": ids[:int(dc[0])].tolist(),
                 "peer_status": st[:R].tolist(),
                 "object": obj[:int(olen[0])].tobytes() if want_object else None}
+
+
+class Server:
+    """mde_server: the resident build service -- one-partition builds served by a persistent
+    launch polling request slots in pinned host memory (no launch, copy or event per call).
+    Thread-safe; ctypes releases the GIL."""
+
+    def __init__(self, device: int = 0, n_slots: int = 0, max_buckets: int = 0):
+        self.lib = load_library()
+        h = C.c_void_p()
+        rc = self.lib.mde_server_create(device, n_slots, max_buckets, C.byref(h))
+        if rc != MDE_OK:
+            raise MdeError(rc, f"mde_server_create(device={device}) failed: {self.lib.mde_strerror(rc).decode()}")
+        self.s = h
+
+    def close(self):
+        if getattr(self, "s", None):
+            self.lib.mde_server_destroy(self.s)
+            self.s = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stats(self):
+        v = [C.c_uint64() for _ in range(3)]
+        self.lib.mde_server_stats(self.s, *(C.byref(x) for x in v))
+        return {"requests": v[0].value, "launches": v[1].value, "on_context": v[2].value}
+
+    def build(self, values, seg_rec, n_partitions, n_buckets, value_stride=0, value_off=None, want_nodes=True,
+              want_tree=True):
+        """mde_server_build: same outputs as Engine.build / Batcher.build."""
+        P, B = n_partitions, n_buckets
+        seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
+        values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)
+        if value_off is not None:
+            value_off = np.ascontiguousarray(value_off, dtype=np.uint64)
+        n_rec = (value_off.size - 1) if value_off is not None else (values.size // value_stride if value_stride else 0)
+        rec = Records(_ptr(values), values.nbytes, value_stride, 0, _ptr(value_off), n_rec, P, B, _ptr(seg_rec))
+        out = _build_outputs(P, B, want_nodes, want_tree)
+        to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
+        err = C.create_string_buffer(512)
+        rc = self.lib.mde_server_build(self.s, C.byref(rec), C.byref(to), err, len(err))
+        if rc != MDE_OK:
+            raise MdeError(rc, err.value.decode(errors="replace"))
+        return out

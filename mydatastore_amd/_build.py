@@ -10,6 +10,7 @@ Outputs (git-ignored, but shipped to the GPU box with the snapshot):
   tests/cpp/build/batch_test        concurrent callers of the batcher vs mde_build / the C oracle
   tests/cpp/build/batch_bench       production call shape: CPU oracle vs per-call vs batched, P callers
   tests/cpp/build/shim_replay       the Go shim's call sequences replayed from C (checked by pytest)
+  tests/cpp/build/server_test       concurrent callers of the resident build service vs mde_build / the C oracle
   oracle/build/liboracle.so         CPU restatement (test infrastructure only)
 """
 from __future__ import annotations
@@ -37,6 +38,7 @@ C_BENCH = ROOT / "tests" / "cpp" / "build" / "cabi_bench"
 BATCH_TEST = ROOT / "tests" / "cpp" / "build" / "batch_test"
 BATCH_BENCH = ROOT / "tests" / "cpp" / "build" / "batch_bench"
 SHIM_REPLAY = ROOT / "tests" / "cpp" / "build" / "shim_replay"
+SERVER_TEST = ROOT / "tests" / "cpp" / "build" / "server_test"
 
 
 def _stale(target: Path, deps) -> bool:
@@ -55,7 +57,7 @@ def _run(cmd, verbose):
 def build_engine(verbose: bool = True) -> Path:
     OBJ.mkdir(exist_ok=True)
     headers = list(CSRC.glob("*.hpp")) + [ROOT / "include" / "mde.h"]
-    sources = sorted(CSRC.glob("*.hip")) + [CSRC / "mde_api.cpp", CSRC / "batch.cpp", CSRC / "group.cpp"]
+    sources = sorted(CSRC.glob("*.hip")) + [CSRC / "mde_api.cpp", CSRC / "batch.cpp", CSRC / "group.cpp", CSRC / "server.cpp"]
     objs = []
     for src in sources:
         obj = OBJ / (src.stem + ".o")
@@ -88,7 +90,8 @@ def build_host(verbose: bool = True) -> Path:
               c_src, "-o", C_BENCH, f"-L{PKG}", "-lmde", f"-Wl,-rpath,{PKG}",
               "-Wl,-rpath,$ORIGIN/../../../mydatastore_amd"], verbose)
     # test programs that also link the C oracle (test infrastructure) as their checker
-    for name, out in (("batch_test.c", BATCH_TEST), ("batch_bench.c", BATCH_BENCH), ("shim_replay.c", SHIM_REPLAY)):
+    for name, out in (("batch_test.c", BATCH_TEST), ("batch_bench.c", BATCH_BENCH), ("shim_replay.c", SHIM_REPLAY),
+                      ("server_test.c", SERVER_TEST)):
         src = ROOT / "tests" / "cpp" / name
         if src.exists() and _stale(out, [src, ROOT / "include" / "mde.h", LIB, ORACLE_LIB]):
             out.parent.mkdir(parents=True, exist_ok=True)

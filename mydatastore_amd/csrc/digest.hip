@@ -985,15 +985,18 @@ __host__ __device__ __forceinline__ uint32_t small_build_kw_word(uint32_t groups
 // saves the second launch of the digest + tree pair.
 // kDuo: the trees run split-schedule (tree_body_duo, the latency form) with the workgroup's upper
 // half as schedule helpers, so a workgroup holds half as many partitions of B <= 128 buckets.
+// The body is a device function: the resident build service (server_kernel) runs it once per
+// request in a workgroup that stays resident between requests -- every barrier inside is reached
+// by all kThreads threads (no early exits), so the workgroup can loop.
 template <bool kDuo>
-__global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLaunch t, uint32_t G, uint32_t words) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+__device__ __forceinline__ void small_build_body(const SegDesc& d, const TreeLaunch& t, uint32_t G, uint32_t words,
+                                                 uint32_t blk, uint32_t* lds) {
 #ifdef MDE_SMALL_PROF  // probe only: digest-phase / tree-phase split of a one-workgroup launch
   const uint64_t prof0 = wall_clock64();
 #endif
   const u32x4* base = reinterpret_cast<const u32x4*>(d.base);
   const uint32_t groups = small_build_groups(G, kDuo);
-  const uint32_t s_beg = min(blockIdx.x * groups * t.B, d.S), s_end = min((blockIdx.x + 1) * groups * t.B, d.S);
+  const uint32_t s_beg = min(blk * groups * t.B, d.S), s_end = min((blk + 1) * groups * t.B, d.S);
   const uint32_t nb = s_end - s_beg;
   // this workgroup's bucket sums live in LDS after the tree levels (no global atomics, no fence)
   unsigned long long* sums = reinterpret_cast<unsigned long long*>(lds + small_build_sums_word(groups, words));
@@ -1029,7 +1032,7 @@ __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLa
   tl.sums_clear = nullptr;
   tl.sums_base = s_beg;
   if (!t.root_out) {  // digest-only build: the leaf outputs of this workgroup's partitions, no tree
-    const uint32_t p0 = blockIdx.x * groups;
+    const uint32_t p0 = blk * groups;
     leaves_waves(tl, p0 + threadIdx.x / 64u, (uint32_t)kThreads / 64u, p0 + groups);
     return;
   }
@@ -1038,15 +1041,116 @@ __global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLa
 #endif
   if (kDuo) {
     u32x4* kw = reinterpret_cast<u32x4*>(lds + small_build_kw_word(groups, words, t.B));
-    tree_body_duo(tl, G, words, blockIdx.x, lds, (uint32_t)kThreads / 2, kw);
+    tree_body_duo(tl, G, words, blk, lds, (uint32_t)kThreads / 2, kw);
   } else {
-    tree_body<true>(tl, G, words, blockIdx.x, lds, kThreads);
+    tree_body<true>(tl, G, words, blk, lds, kThreads);
   }
 #ifdef MDE_SMALL_PROF
   __syncthreads();
   if (gridDim.x == 1 && threadIdx.x == 0)
     printf("small_prof digest %lu tree %lu (x10ns)\n", prof1 - prof0, wall_clock64() - prof1);
 #endif
+}
+
+template <bool kDuo>
+__global__ __launch_bounds__(kThreads) void small_build_kernel(SegDesc d, TreeLaunch t, uint32_t G, uint32_t words) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  small_build_body<kDuo>(d, t, G, words, blockIdx.x, lds);
+}
+
+constexpr uint64_t kServerExit = ~0ull - 1ull;
+constexpr uint64_t kServerFinal = 1ull << 62;  // served after closing: the last request of this workgroup
+
+// The resident build service (mde_server, server.cpp): workgroup blockIdx.x serves slot
+// blockIdx.x -- a one-partition RawPartitionMerkleTree call without a kernel launch, a copy
+// command or an event per call. Thread 0 polls the slot's `req` word in coherent pinned host
+// memory (a relaxed system-scope load: a read over PCIe, no cache invalidation per poll), the
+// workgroup copies the posted request into LDS with per-lane vector loads (never the scalar cache:
+// the slot is rewritten for every request), optionally stages its inputs into device memory (one
+// PCIe round trip for all of them instead of one per dependent load), runs small_build_body
+// (outputs stored straight into the slot's pinned out region), makes every thread's stores
+// visible at system scope and publishes `done`. Exit: the host's kServerStop, or the lifetime --
+// then thread 0 sets `closed`, fences (seq_cst, system) and reads `req` once more, so a request
+// posted concurrently is either served here or seen by its host as closed (server.cpp relaunches).
+// Every wave reaches the exit: the decision is thread 0's, broadcast through LDS behind a barrier.
+__global__ __launch_bounds__(kThreads) void server_kernel(ServerSlot* slots, uint64_t lifetime) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  constexpr uint32_t kReqWords = (uint32_t)(sizeof(ServerReq) / 4);
+  static_assert(sizeof(ServerReq) % 4 == 0 && kReqWords <= (uint32_t)kThreads, "request fits one load per lane");
+  __shared__ uint64_t cmd;
+  __shared__ __attribute__((aligned(16))) uint32_t req[kReqWords];  // raw words (TreeLaunch has initializers)
+  ServerSlot* s = slots + blockIdx.x;
+  const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + lifetime;
+  uint64_t served = 0;
+  if (threadIdx.x == 0) served = __hip_atomic_load(&s->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (;;) {
+    if (threadIdx.x == 0) {
+      uint64_t c;
+      for (;;) {
+        const uint64_t r = __hip_atomic_load(&s->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (r == kServerStop) {
+          c = kServerExit;
+          break;
+        }
+        if (r != served) {
+          c = r;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() > t_end) {
+          __hip_atomic_store(&s->closed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __atomic_thread_fence(__ATOMIC_SEQ_CST);  // system scope: closed is visible before req is re-read
+          const uint64_t r2 = __hip_atomic_load(&s->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          c = (r2 != served && r2 != kServerStop) ? (r2 | kServerFinal) : kServerExit;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+      cmd = c;
+    }
+    __syncthreads();
+    const uint64_t c = cmd;
+    if (c == kServerExit) return;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the request's bytes, posted before req
+    if (threadIdx.x < kReqWords)
+      req[threadIdx.x] =
+          __hip_atomic_load(reinterpret_cast<const uint32_t*>(&s->r) + threadIdx.x, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    ServerReq q;
+    __builtin_memcpy(&q, req, sizeof q);
+    if (q.stage) {  // the inputs into device memory: every load in flight at once
+      const u32x4* src = reinterpret_cast<const u32x4*>(q.src);
+      u32x4* dst = reinterpret_cast<u32x4*>(q.dev_in);
+      const uint32_t n = (uint32_t)(q.stage_bytes / 16u);
+      constexpr uint32_t kU = 8;
+      for (uint32_t i0 = 0; i0 < n; i0 += kU * (uint32_t)kThreads) {
+        u32x4 v[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+          const uint32_t i = i0 + u * (uint32_t)kThreads + threadIdx.x;
+          if (i < n) v[u] = src[i];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+          const uint32_t i = i0 + u * (uint32_t)kThreads + threadIdx.x;
+          if (i < n) dst[i] = v[u];
+        }
+      }
+      __threadfence_block();
+      __syncthreads();
+    }
+    if (q.duo)
+      small_build_body<true>(q.d, q.t, q.G, q.words, 0, lds);
+    else
+      small_build_body<false>(q.d, q.t, q.G, q.words, 0, lds);
+    __threadfence_system();  // this thread's output stores, before done
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      served = c & ~kServerFinal;
+      __hip_atomic_store(&s->done, served, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (c & kServerFinal) return;
+  }
 }
 
 typedef void (*DigestKernel)(DigestLaunch);
@@ -1135,6 +1239,42 @@ hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t
     hipLaunchKernelGGL(small_build_kernel<true>, dim3(blocks), dim3(kThreads), lds, st, d, t, g.G, g.words);
   else
     hipLaunchKernelGGL(small_build_kernel<false>, dim3(blocks), dim3(kThreads), lds, st, d, t, g.G, g.words);
+  return hipGetLastError();
+}
+
+// Static LDS of server_kernel (the command word and the request copy), below the dynamic LDS.
+constexpr size_t kServerStaticLds = sizeof(ServerReq) + 64u;
+
+bool server_plan(uint32_t P, uint32_t B, size_t lds_bytes, uint32_t* G, uint32_t* words, uint32_t* duo) {
+  TreeGeometry g;
+  if (P < 1 || B < 1 || !tree_geometry(B, &g) || g.G > (uint32_t)kThreads) return false;
+  // one workgroup: the split-schedule form when its LDS fits the service's launch (kDuoMaxBlocks
+  // does not bind for one workgroup), else the plain form
+  bool d = tree_duo_enabled() && small_build_lds(g, B, true) <= lds_bytes;
+  if (P > small_build_groups(g.G, d)) d = false;
+  if (P > small_build_groups(g.G, d) || small_build_lds(g, B, d) > lds_bytes) return false;
+  *G = g.G;
+  *words = g.words;
+  *duo = d ? 1u : 0u;
+  return true;
+}
+
+size_t server_lds_bytes(uint32_t max_buckets) {
+  size_t m = 0;
+  for (uint32_t B = 1; B <= max_buckets; B++) {
+    TreeGeometry g;
+    if (!tree_geometry(B, &g) || g.G > (uint32_t)kThreads) continue;
+    size_t need = small_build_lds(g, B, tree_duo_enabled());
+    if (need + kServerStaticLds > kSmallBuildLdsMax) need = small_build_lds(g, B, false);
+    if (need + kServerStaticLds <= kSmallBuildLdsMax) m = std::max(m, need);
+  }
+  return (m + 15u) & ~size_t(15);
+}
+
+hipError_t launch_server(ServerSlot* slots, uint32_t n_slots, uint64_t lifetime_ticks, size_t lds_bytes,
+                         hipStream_t st) {
+  if (lds_bytes + kServerStaticLds > kSmallBuildLdsMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(server_kernel, dim3(n_slots), dim3(kThreads), lds_bytes, st, slots, lifetime_ticks);
   return hipGetLastError();
 }
 

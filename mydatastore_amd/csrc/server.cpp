@@ -1,0 +1,441 @@
+// server.cpp -- the resident build service (mde_server, include/mde.h): one-partition builds
+// without a kernel launch per call.
+//
+// The reference builds ONE partition per VerifyEpoch (main/manager.go:1036 ->
+// RawPartitionMerkleTree, main/merkle_tree.go:86-116): a few KB of 8-byte timestamps
+// (main/manager.go:816) at partition_buckets = 1000 (config/default-config.yaml:10), on up to
+// partition_concurrency = 10 workers. Through mde_build or the batcher (batch.cpp) every call pays
+// a launch, a copy command each way and a completion event -- ~20 us of round trip around a few us
+// of digest work. Here a persistent launch (digest.hip server_kernel) keeps one workgroup per
+// request slot resident on the device; the slots live in coherent pinned host memory:
+//   * a caller takes a free slot, packs its records into the slot's pinned in region (values, the
+//     rebased seg_rec, value_off unless the records have one length), writes the request
+//     descriptor and then the slot's sequence word (release);
+//   * the slot's workgroup, polling that word over PCIe, copies the inputs into device memory in
+//     one round trip, runs the one-launch small build (small_build_body: bucket sums in LDS, then
+//     the split-schedule SHA-256 tree, or no tree for a digest-only build) with its outputs stored
+//     straight into the slot's pinned out region, and publishes `done` (system-scope release);
+//   * the caller spins on `done` and copies its outputs out.
+// Lifetime: the launch ends by itself after `lifetime` (MDE_SERVER_LIFETIME_MS, default 100 ms),
+// so an idle process holds no GPU work; the next request relaunches it. Each workgroup, when its
+// lifetime is over, sets its slot's `closed` word, fences and reads the slot once more; a caller
+// that posts and then reads `closed` set waits for the launch to end and relaunches (a request
+// is served either by the closing workgroup's last read or by the next launch, never lost).
+// The launch runs on a CU-masked stream: such a stream gets a hardware queue of its own, so no
+// other stream of the process queues behind the persistent kernel.
+// Requests the resident workgroups do not take (more partitions than one workgroup holds, inputs
+// or outputs beyond a slot, B beyond the launch's LDS) run as mde_build on the service's own
+// context. Each caller gets exactly what mde_build returns for its inputs (tests/cpp/server_test.c
+// against mde_build and the C oracle under concurrent callers).
+#include "../../include/mde.h"
+#include "mde_internal.hpp"
+
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+#include <immintrin.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+void put_msg(char* buf, uint64_t cap, const char* msg) {
+  if (!buf || !cap) return;
+  const uint64_t n = std::min<uint64_t>(std::strlen(msg), cap - 1);
+  std::memcpy(buf, msg, n);
+  buf[n] = 0;
+}
+
+int failf(char* buf, uint64_t cap, int code, const char* fmt, ...) {
+  char m[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(m, sizeof m, fmt, ap);
+  va_end(ap);
+  put_msg(buf, cap, m);
+  return code;
+}
+
+uint64_t a16(uint64_t x) { return (x + 15) & ~15ull; }
+
+constexpr uint32_t kDefaultSlots = 16;
+constexpr uint32_t kMaxSlots = 256;
+constexpr uint64_t kDefaultInCap = 256ull << 10;
+constexpr uint64_t kDefaultLifetimeMs = 100;
+constexpr double kWaitTimeoutS = 30.0;
+
+}  // namespace
+
+struct mde_server {
+  int device = 0;
+  uint32_t n_slots = kDefaultSlots;
+  uint32_t max_buckets = 1024;
+  uint64_t in_cap = kDefaultInCap, out_cap = 0;
+  size_t lds = 0;
+  uint64_t lifetime_ticks = kDefaultLifetimeMs * 100000ull;  // s_memrealtime: 100 MHz
+  bool stage = true;  // MDE_SERVER_STAGE=0: the build reads its inputs in place over PCIe (A/B)
+  uint8_t* pin = nullptr;      // [n_slots ServerSlot][n_slots x in_cap][n_slots x out_cap], coherent
+  uint8_t* pin_dev = nullptr;  // its device address
+  uint8_t* dev_in = nullptr;   // [n_slots x in_cap] device staging
+  hipStream_t stream = nullptr;
+  hipEvent_t exit_ev = nullptr;
+  bool running = false;
+  std::mutex launch_m;
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<uint32_t> free_slots;
+  std::vector<uint64_t> seq;  // per slot, owned by the caller holding the slot
+  std::atomic<uint64_t> n_req{0}, n_launch{0}, n_ctx{0};
+  mde_ctx* ctx = nullptr;  // requests the resident workgroups do not take
+  std::mutex ctx_m;
+
+  mde::ServerSlot* slot(uint32_t i) { return reinterpret_cast<mde::ServerSlot*>(pin) + i; }
+  uint64_t in_off(uint32_t i) const { return (uint64_t)n_slots * sizeof(mde::ServerSlot) + (uint64_t)i * in_cap; }
+  uint64_t out_off(uint32_t i) const {
+    return (uint64_t)n_slots * sizeof(mde::ServerSlot) + (uint64_t)n_slots * in_cap + (uint64_t)i * out_cap;
+  }
+};
+
+namespace {
+
+// Output layout of one request in a slot's out region.
+struct OutLayout {
+  uint64_t dig, size, items, root, nodes, total;
+};
+OutLayout out_layout(uint32_t P, uint32_t B, bool tree, bool nodes) {
+  OutLayout o{};
+  const uint64_t S = (uint64_t)P * B;
+  o.dig = 0;
+  o.size = a16(S * 8);
+  o.items = o.size + a16(S * 4);
+  o.root = o.items + a16((uint64_t)P * 4);
+  o.nodes = o.root + (tree ? a16((uint64_t)P * 32) : 0);
+  o.total = o.nodes + (nodes ? a16((uint64_t)P * mde::tree_internal(B) * 32) : 0);
+  return o;
+}
+
+// The checks mde_build makes on host records (layout A), with the caller's message buffer.
+int validate(const mde_records* r, const mde_tree_out* o, char* err, uint64_t cap) {
+  if (r->layout != MDE_LAYOUT_SORTED) return failf(err, cap, MDE_E_INVAL, "mde_server_build takes layout A records");
+  if (!r->seg_rec || !r->n_buckets || !r->n_partitions)
+    return failf(err, cap, MDE_E_INVAL, "seg_rec, n_buckets and n_partitions are required");
+  if (!o->root && o->nodes) return failf(err, cap, MDE_E_INVAL, "out/nodes needs out/root");
+  if ((uint64_t)r->n_partitions * r->n_buckets > 0xffffffffull)
+    return failf(err, cap, MDE_E_INVAL, "n_partitions * n_buckets exceeds 2^32");
+  if (r->value_stride == 0 && !r->value_off && r->n_records)
+    return failf(err, cap, MDE_E_INVAL, "variable-length values need value_off");
+  if (!r->values && r->values_bytes) return failf(err, cap, MDE_E_INVAL, "values is NULL");
+  if (r->value_stride && (uint64_t)r->value_stride * r->n_records > r->values_bytes)
+    return failf(err, cap, MDE_E_INVAL, "n_records * value_stride exceeds values_bytes");
+  const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
+  for (uint64_t s = 0; s < S; s++)
+    if (r->seg_rec[s] > r->seg_rec[s + 1])
+      return failf(err, cap, MDE_E_INVAL, "seg_rec not nondecreasing at %llu", (unsigned long long)s);
+  if (r->seg_rec[S] > r->n_records)
+    return failf(err, cap, MDE_E_INVAL, "seg_rec[%llu] exceeds n_records", (unsigned long long)S);
+  if (!r->value_stride && r->n_records) {
+    for (uint64_t i = 0; i < r->n_records; i++)
+      if (r->value_off[i] > r->value_off[i + 1])
+        return failf(err, cap, MDE_E_INVAL, "value_off not nondecreasing at %llu", (unsigned long long)i);
+    if (r->value_off[r->n_records] > r->values_bytes)
+      return failf(err, cap, MDE_E_INVAL, "value_off[n_records] exceeds values_bytes");
+  }
+  return MDE_OK;
+}
+
+// Make sure a launch is serving (or relaunch after the previous one ended its lifetime).
+int ensure_running(mde_server* s, std::string* msg) {
+  std::lock_guard<std::mutex> lk(s->launch_m);
+  if (s->running) {
+    hipError_t e = hipEventQuery(s->exit_ev);
+    if (e == hipErrorNotReady) {
+      bool closing = false;
+      for (uint32_t i = 0; i < s->n_slots && !closing; i++)
+        closing = __atomic_load_n(&s->slot(i)->closed, __ATOMIC_ACQUIRE) != 0;
+      if (!closing) return MDE_OK;
+      // its workgroups share one lifetime: the rest close within about one request
+      e = hipEventSynchronize(s->exit_ev);
+    }
+    if (e != hipSuccess) {
+      *msg = std::string("resident build launch failed: ") + hipGetErrorString(e);
+      return MDE_E_DEVICE;
+    }
+    s->running = false;
+  }
+  for (uint32_t i = 0; i < s->n_slots; i++) __atomic_store_n(&s->slot(i)->closed, 0u, __ATOMIC_RELAXED);
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  (void)hipSetDevice(s->device);
+  hipError_t e = mde::launch_server(reinterpret_cast<mde::ServerSlot*>(s->pin_dev), s->n_slots, s->lifetime_ticks,
+                                    s->lds, s->stream);
+  if (e == hipSuccess) e = hipEventRecord(s->exit_ev, s->stream);
+  if (e != hipSuccess) {
+    for (uint32_t i = 0; i < s->n_slots; i++) __atomic_store_n(&s->slot(i)->closed, 1u, __ATOMIC_RELAXED);
+    *msg = std::string("resident build launch: ") + hipGetErrorString(e);
+    return MDE_E_DEVICE;
+  }
+  s->running = true;
+  s->n_launch.fetch_add(1, std::memory_order_relaxed);
+  return MDE_OK;
+}
+
+// Post request `q` on slot i and wait for its `done`.
+int post_and_wait(mde_server* s, uint32_t i, std::string* msg) {
+  mde::ServerSlot* sl = s->slot(i);
+  const uint64_t q = ++s->seq[i];
+  __atomic_store_n(&sl->req, q, __ATOMIC_RELEASE);
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);  // req before closed (the workgroup: closed before req)
+  if (__atomic_load_n(&sl->closed, __ATOMIC_ACQUIRE)) {
+    const int rc = ensure_running(s, msg);
+    if (rc) return rc;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spin = 1;; spin++) {
+    if (__atomic_load_n(&sl->done, __ATOMIC_ACQUIRE) == q) return MDE_OK;
+    _mm_pause();
+    if ((spin & 63) == 0) {
+      if (__atomic_load_n(&sl->closed, __ATOMIC_ACQUIRE)) {
+        // the workgroup closed: served by its last read, or by the next launch
+        const int rc = ensure_running(s, msg);
+        if (rc) return rc;
+        continue;
+      }
+      const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (dt > 50e-6) std::this_thread::yield();  // oversubscribed callers: give the core away
+      if (dt > kWaitTimeoutS) {
+        const hipError_t e = hipEventQuery(s->exit_ev);
+        *msg = std::string("resident build request timed out (launch: ") + hipGetErrorString(e) + ")";
+        return MDE_E_DEVICE;
+      }
+      if ((spin & 4095) == 0) {
+        const hipError_t e = hipEventQuery(s->exit_ev);
+        if (e != hipSuccess && e != hipErrorNotReady) {
+          *msg = std::string("resident build launch failed: ") + hipGetErrorString(e);
+          return MDE_E_DEVICE;
+        }
+      }
+    }
+  }
+}
+
+uint32_t take_slot(mde_server* s) {
+  std::unique_lock<std::mutex> lk(s->m);
+  s->cv.wait(lk, [&] { return !s->free_slots.empty(); });
+  const uint32_t i = s->free_slots.back();
+  s->free_slots.pop_back();
+  return i;
+}
+
+void give_slot(mde_server* s, uint32_t i) {
+  {
+    std::lock_guard<std::mutex> lk(s->m);
+    s->free_slots.push_back(i);
+  }
+  s->cv.notify_one();
+}
+
+}  // namespace
+
+extern "C" {
+
+int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_server** out) {
+  if (!out) return MDE_E_INVAL;
+  *out = nullptr;
+  if (n_slots > kMaxSlots || max_buckets > mde::kTreeLdsMaxBuckets) return MDE_E_INVAL;
+  mde_server* s = new (std::nothrow) mde_server();
+  if (!s) return MDE_E_NOMEM;
+  s->device = device;
+  if (n_slots) s->n_slots = n_slots;
+  if (max_buckets) s->max_buckets = max_buckets;
+  if (const char* e = std::getenv("MDE_SERVER_LIFETIME_MS")) {
+    const long long ms = std::atoll(e);
+    if (ms >= 1) s->lifetime_ticks = (uint64_t)ms * 100000ull;
+  }
+  if (const char* e = std::getenv("MDE_SERVER_STAGE")) s->stage = std::atoi(e) != 0;
+  int rc = mde_create(device, &s->ctx);
+  if (rc != MDE_OK) {
+    delete s;
+    return rc;
+  }
+  auto bail = [&](int code) {
+    mde_server_destroy(s);
+    return code;
+  };
+  (void)hipSetDevice(device);
+  s->lds = mde::server_lds_bytes(s->max_buckets);
+  uint32_t G, words, duo;
+  if (!s->lds || !mde::server_plan(1, s->max_buckets, s->lds, &G, &words, &duo)) return bail(MDE_E_INVAL);
+  s->out_cap = a16(out_layout(1, s->max_buckets, true, true).total);
+  const uint64_t bytes = (uint64_t)s->n_slots * (sizeof(mde::ServerSlot) + s->in_cap + s->out_cap);
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    return bail(MDE_E_NOMEM);
+  }
+  s->pin = static_cast<uint8_t*>(p);
+  std::memset(s->pin, 0, bytes);
+  void* pd = nullptr;
+  if (hipHostGetDevicePointer(&pd, s->pin, 0) != hipSuccess) return bail(MDE_E_DEVICE);
+  s->pin_dev = static_cast<uint8_t*>(pd);
+  void* di = nullptr;
+  if (hipMalloc(&di, (uint64_t)s->n_slots * s->in_cap) != hipSuccess) {
+    (void)hipGetLastError();
+    return bail(MDE_E_NOMEM);
+  }
+  s->dev_in = static_cast<uint8_t*>(di);
+  // a CU-masked stream gets a hardware queue of its own (all CUs enabled): nothing else of this
+  // process queues behind the persistent launch
+  int cus = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  std::vector<uint32_t> mask((size_t)std::max(1, (cus + 31) / 32), 0u);
+  for (int c = 0; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
+  if (hipExtStreamCreateWithCUMask(&s->stream, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+    (void)hipGetLastError();
+    s->stream = nullptr;
+    return bail(MDE_E_DEVICE);
+  }
+  if (hipEventCreateWithFlags(&s->exit_ev, hipEventDisableTiming) != hipSuccess) {
+    s->exit_ev = nullptr;
+    return bail(MDE_E_DEVICE);
+  }
+  s->seq.assign(s->n_slots, 0);
+  for (uint32_t i = 0; i < s->n_slots; i++) {
+    s->free_slots.push_back(s->n_slots - 1 - i);
+    s->slot(i)->closed = 1;  // no launch yet
+  }
+  std::string msg;
+  if (ensure_running(s, &msg)) return bail(MDE_E_DEVICE);
+  *out = s;
+  return MDE_OK;
+}
+
+void mde_server_destroy(mde_server* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  if (s->pin) {
+    for (uint32_t i = 0; i < s->n_slots; i++) __atomic_store_n(&s->slot(i)->req, mde::kServerStop, __ATOMIC_RELEASE);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  }
+  if (s->running && s->exit_ev) (void)hipEventSynchronize(s->exit_ev);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  if (s->exit_ev) (void)hipEventDestroy(s->exit_ev);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  if (s->dev_in) (void)hipFree(s->dev_in);
+  if (s->pin) (void)hipHostFree(s->pin);
+  if (s->ctx) mde_destroy(s->ctx);
+  delete s;
+}
+
+int mde_server_stats(mde_server* s, uint64_t* requests, uint64_t* launches, uint64_t* on_context) {
+  if (!s) return MDE_E_INVAL;
+  if (requests) *requests = s->n_req.load();
+  if (launches) *launches = s->n_launch.load();
+  if (on_context) *on_context = s->n_ctx.load();
+  return MDE_OK;
+}
+
+uint32_t mde_server_slots(const mde_server* s) { return s ? s->n_slots : 0u; }
+
+int mde_server_build(mde_server* s, const mde_records* rec, const mde_tree_out* out, char* err, uint64_t err_cap) {
+  put_msg(err, err_cap, "");
+  if (!s || !rec || !out) return failf(err, err_cap, MDE_E_INVAL, "null server, records or out");
+  int rc = validate(rec, out, err, err_cap);
+  if (rc) return rc;
+  const uint32_t P = rec->n_partitions, B = rec->n_buckets;
+  const uint64_t S = (uint64_t)P * B;
+  const uint64_t r0 = rec->seg_rec[0], r1 = rec->seg_rec[S], n = r1 - r0;
+  // records of one length (given, or detected from value_off): no offsets to send
+  uint64_t stride = rec->value_stride;
+  if (!stride && n) {
+    const uint64_t d0 = rec->value_off[r0 + 1] - rec->value_off[r0];
+    bool uniform = d0 > 0;
+    for (uint64_t k = r0 + 1; k < r1 && uniform; k++) uniform = rec->value_off[k + 1] - rec->value_off[k] == d0;
+    if (uniform && d0 <= 0xffffffffull) stride = d0;
+  }
+  const uint64_t b0 = rec->value_stride ? r0 * rec->value_stride : (n ? rec->value_off[r0] : 0);
+  const uint64_t b1 = rec->value_stride ? r1 * rec->value_stride : (n ? rec->value_off[r1] : 0);
+  const uint64_t V = b1 - b0;
+  const uint64_t o_seg = a16(std::max<uint64_t>(V, 16));
+  const uint64_t o_off = o_seg + a16((S + 1) * 8);
+  const uint64_t in_bytes = o_off + (stride ? 0 : a16((n + 1) * 8));
+  const bool tree = out->root != nullptr, nodes = out->nodes != nullptr;
+  const OutLayout ol = out_layout(P, B, tree, nodes);
+  uint32_t G = 0, words = 0, duo = 0;
+  const bool fits = B <= s->max_buckets && in_bytes <= s->in_cap && ol.total <= s->out_cap &&
+                    mde::server_plan(P, B, s->lds, &G, &words, &duo);
+  s->n_req.fetch_add(1, std::memory_order_relaxed);
+  if (!fits) {  // the service's context: the ordinary synchronous build
+    s->n_ctx.fetch_add(1, std::memory_order_relaxed);
+    std::lock_guard<std::mutex> lk(s->ctx_m);
+    rc = mde_build(s->ctx, rec, out);
+    if (rc) put_msg(err, err_cap, mde_last_error(s->ctx));
+    return rc;
+  }
+  const uint32_t i = take_slot(s);
+  uint8_t* in_h = s->pin + s->in_off(i);
+  const uint64_t in_d_pin = reinterpret_cast<uint64_t>(s->pin_dev + s->in_off(i));
+  uint8_t* out_h = s->pin + s->out_off(i);
+  uint8_t* out_d = s->pin_dev + s->out_off(i);
+  // pack: values, seg_rec rebased to the first record, value_off rebased (variable lengths only)
+  if (V) std::memcpy(in_h, rec->values + b0, V);
+  std::memset(in_h + V, 0, o_seg - V);
+  uint64_t* seg = reinterpret_cast<uint64_t*>(in_h + o_seg);
+  for (uint64_t k = 0; k <= S; k++) seg[k] = rec->seg_rec[k] - r0;
+  if (!stride) {
+    uint64_t* off = reinterpret_cast<uint64_t*>(in_h + o_off);
+    for (uint64_t k = 0; k <= n; k++) off[k] = rec->value_off[r0 + k] - b0;
+  }
+  const uint64_t in_base = s->stage ? reinterpret_cast<uint64_t>(s->dev_in + (uint64_t)i * s->in_cap) : in_d_pin;
+  mde::ServerReq q{};
+  q.d.base = reinterpret_cast<const uint8_t*>(in_base);
+  q.d.shift = 0;
+  q.d.stride = (uint32_t)stride;
+  q.d.value_off = stride ? nullptr : reinterpret_cast<const uint64_t*>(in_base + o_off);
+  q.d.seg_rec = reinterpret_cast<const uint64_t*>(in_base + o_seg);
+  q.d.S = (uint32_t)S;
+  q.d.n_records = n;
+  q.d.end = V;
+  q.t.P = P;
+  q.t.B = B;
+  q.t.seg_rec = q.d.seg_rec;
+  q.t.digest_out = reinterpret_cast<uint64_t*>(out_d + ol.dig);
+  q.t.size_out = reinterpret_cast<int32_t*>(out_d + ol.size);
+  q.t.items_out = reinterpret_cast<int32_t*>(out_d + ol.items);
+  q.t.root_out = tree ? out_d + ol.root : nullptr;
+  q.t.nodes_out = nodes ? out_d + ol.nodes : nullptr;
+  q.t.n_int = mde::tree_internal(B);
+  q.G = G;
+  q.words = words;
+  q.duo = duo;
+  q.stage = s->stage ? 1u : 0u;
+  q.src = reinterpret_cast<const uint8_t*>(in_d_pin);
+  q.dev_in = s->dev_in + (uint64_t)i * s->in_cap;
+  q.stage_bytes = a16(in_bytes);
+  std::memcpy(&s->slot(i)->r, &q, sizeof q);
+  std::string msg;
+  rc = post_and_wait(s, i, &msg);
+  if (rc == MDE_OK) {
+    if (out->digest) std::memcpy(out->digest, out_h + ol.dig, S * 8);
+    if (out->size) std::memcpy(out->size, out_h + ol.size, S * 4);
+    if (out->items) std::memcpy(out->items, out_h + ol.items, (uint64_t)P * 4);
+    if (tree && out->root) std::memcpy(out->root, out_h + ol.root, (uint64_t)P * 32);
+    if (nodes) std::memcpy(out->nodes, out_h + ol.nodes, (uint64_t)P * q.t.n_int * 32);
+    give_slot(s, i);
+  } else {
+    // the slot's workgroup may still write it: it stays out of the free list
+    put_msg(err, err_cap, msg.c_str());
+  }
+  return rc;
+}
+
+}  // extern "C"

@@ -21,7 +21,11 @@
  *   shim_hosttree  the hybrid: mde_batch_build digest-only (root = NULL: no device tree), then
  *                  NewTree on the host over the device digests (oracle_graph_build);
  *   device_call    mde_batch_build alone (digests + root), no tree object: the ABI call only;
- *   percall        synchronous mde_build (nodes) on one shared context + tree assembly.
+ *   percall        synchronous mde_build (nodes) on one shared context + tree assembly;
+ *   server         mde_server_build (the resident build service: a persistent launch polling
+ *                  request slots in pinned memory, no launch / copy / event per call) with the
+ *                  nodes output, then the tree assembled from the node hashes;
+ *   server_hosttree  mde_server_build digest-only, then NewTree on the host.
  * VerifyEpoch decision step (main/manager.go:1072-1104; two peers, one agreeing, one differing):
  *   cpu_verify     per peer: EpochTreeObjectToMerkleTree (decode the 8-byte bucket hashes, NewTree)
  *                  and DifferentMerkleTreeBuckets against the local tree; validCount / diffSet fold;
@@ -91,6 +95,8 @@ enum {
   SHIM_HOSTTREE,
   DEVICE_CALL,
   PERCALL,
+  SERVER,
+  SERVER_HOSTTREE,
   CPU_VERIFY,
   V_BATCHED,
   DIFF_HOST,
@@ -98,8 +104,9 @@ enum {
   DIFF_DIGESTS,
   N_CASES
 };
-static const char* kCases[] = {"cpu",        "shim",           "shim_hosttree", "device_call",  "percall",
-                               "cpu_verify", "verify_batched", "diff_host",     "diff_device", "diff_digests"};
+static const char* kCases[] = {"cpu",          "shim",       "shim_hosttree",  "device_call", "percall",
+                               "server",       "server_hosttree", "cpu_verify", "verify_batched", "diff_host",
+                               "diff_device",  "diff_digests"};
 
 /* One partition-epoch of 8-byte timestamps, records spread evenly over B buckets; the oracle's
  * outputs for it; two peers (agreeing, differing at bucket B/2) as decoded objects (the 8-byte
@@ -126,6 +133,7 @@ typedef struct {
 
 static mde_ctx* ctx;
 static mde_batcher* batcher;
+static mde_server* server;
 static pthread_barrier_t bar;
 static double g_seconds = 0.4;
 static long g_bad = 0;
@@ -282,6 +290,23 @@ static int call(int mode, part_t* p) {
       oracle_graph_free(g);
       return 0;
     }
+    case SERVER: {
+      mde_tree_out o = {p->dig, p->size, &p->items, p->root, p->nodes};
+      if ((rc = mde_server_build(server, &r, &o, err, sizeof err))) return rc;
+      oracle_graph* g = oracle_graph_from_nodes(p->dig, B, p->nodes);
+      check_tree(p, g, "server");
+      if (memcmp(p->root, p->root_ref, 32)) bad("server root", p);
+      oracle_graph_free(g);
+      return 0;
+    }
+    case SERVER_HOSTTREE: {
+      mde_tree_out o = {p->dig, p->size, &p->items, NULL, NULL};
+      if ((rc = mde_server_build(server, &r, &o, err, sizeof err))) return rc;
+      oracle_graph* g = oracle_graph_build(p->dig, B);
+      check_tree(p, g, "server_hosttree");
+      oracle_graph_free(g);
+      return 0;
+    }
     case DEVICE_CALL: {
       mde_tree_out o = {p->dig, p->size, &p->items, p->root, NULL};
       if ((rc = mde_batch_build(batcher, &r, &o, err, sizeof err))) return rc;
@@ -377,13 +402,15 @@ static void run_case(int mode, int P, uint64_t n, uint32_t B, part_t* parts, int
     jobs[t].n = 0;
     pthread_create(&th[t], NULL, worker, &jobs[t]);
   }
-  uint64_t b0 = 0, r0 = 0, p0 = 0, b1 = 0, r1 = 0, p1 = 0;
+  uint64_t b0 = 0, r0 = 0, p0 = 0, b1 = 0, r1 = 0, p1 = 0, sc0 = 0, sc1 = 0;
   mde_batcher_stats(batcher, &b0, &r0, &p0);
+  mde_server_stats(server, NULL, NULL, &sc0);
   pthread_barrier_wait(&bar);
   const double t0 = now_s();
   for (int t = 0; t < P; t++) pthread_join(th[t], NULL);
   const double wall = now_s() - t0;
   mde_batcher_stats(batcher, &b1, &r1, &p1);
+  mde_server_stats(server, NULL, NULL, &sc1);
   long total = 0;
   for (int t = 0; t < P; t++) total += jobs[t].n;
   double* all = xmalloc(sizeof(double) * (size_t)total);
@@ -401,6 +428,7 @@ static void run_case(int mode, int P, uint64_t n, uint32_t B, part_t* parts, int
          kCases[mode], P, n, B, total, wall, (double)total / wall, all[total / 2] * 1e6, all[total * 9 / 10] * 1e6);
   if ((mode == SHIM || mode == SHIM_HOSTTREE || mode == DEVICE_CALL || mode == V_BATCHED) && batches > 0)
     printf(", \"mean_requests_per_batch\": %.2f", (double)(r1 - r0) / batches);
+  if (mode == SERVER || mode == SERVER_HOSTTREE) printf(", \"server_calls_on_context\": %" PRIu64, sc1 - sc0);
   printf("}\n");
   fflush(stdout);
   free(all);
@@ -436,6 +464,10 @@ int main(int argc, char** argv) {
   const char* wait_env = getenv("MDE_BATCH_WAIT_US");
   const uint32_t wait_us = wait_env ? (uint32_t)atoi(wait_env) : 0u;
   if ((rc = mde_batcher_create(0, 256, wait_us, &batcher))) return 1;
+  if ((rc = mde_server_create(0, 0, 0, &server))) {
+    fprintf(stderr, "mde_server_create: %d\n", rc);
+    return 1;
+  }
   printf("{\"host_sha_extensions\": %s, \"batcher_wait_us\": %u}\n", oracle_sha_ni() ? "true" : "false", wait_us);
   if (argc > 3) {
     const int only = argc > 4 ? case_by_name(argv[4]) : -1;
@@ -452,7 +484,7 @@ int main(int argc, char** argv) {
       for (int ni = 0; ni < 3; ni++) {
         part_t p;
         make_part(&p, ns[ni], Bs[bi], 1 + ni);
-        for (int mode = CPU; mode <= PERCALL; mode++) run_case(mode, 1, ns[ni], Bs[bi], &p, 1);
+        for (int mode = CPU; mode <= SERVER_HOSTTREE; mode++) run_case(mode, 1, ns[ni], Bs[bi], &p, 1);
         free_part(&p);
       }
     const int Ps[3] = {1, 10, 100};
@@ -461,6 +493,7 @@ int main(int argc, char** argv) {
   }
   printf("{\"outputs_equal_oracle\": %s}\n", g_bad ? "false" : "true");
   mde_batcher_destroy(batcher);
+  mde_server_destroy(server);
   mde_destroy(ctx);
   return g_bad ? 3 : 0;
 }

@@ -1,0 +1,84 @@
+"""The resident build service (mde_server_build, include/mde.h): one-partition builds -- the
+reference's production call shape, one RawPartitionMerkleTree per (partition, epoch) from
+VerifyEpoch (main/manager.go:1036, main/merkle_tree.go:86-116) on up to partition_concurrency = 10
+workers (config/default-config.yaml:9) -- served by a persistent launch polling request slots in
+pinned host memory. Every caller's result equals mde_build's and the C oracle's; the launch ends
+at its lifetime and relaunches without losing a request."""
+import json
+import subprocess
+import threading
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT
+
+BIN = ROOT / "tests" / "cpp" / "build" / "server_test"
+
+
+def test_server_test_builds_and_fails_loudly_without_gpu():
+    import torch
+    assert BIN.exists()
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    r = subprocess.run([str(BIN), "2", "1"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "mde_server_create: -3" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads,calls,lifetime_ms", [(10, 40, 100), (1, 8, 100), (32, 8, 100), (8, 30, 2)])
+def test_server_concurrent_callers_c(threads, calls, lifetime_ms):
+    """tests/cpp/server_test.c: `threads` pthreads released together, each making `calls` builds
+    (B = 1 / 2 / 30 / 64 / 1000 / 1024 in the service, 4096 and > 256 KiB inputs on its context;
+    8-byte, variable-length and uniform variable-length values; records outside the bucket ranges;
+    empty partitions; 2-3 partitions per call; full, root-only and digest-only outputs). Every
+    output == mde_build == the C oracle. A 2 ms lifetime relaunches the service while calls are in
+    flight; the last calls each find the launch ended (idle past the lifetime)."""
+    r = subprocess.run([str(BIN), str(threads), str(calls), str(lifetime_ms)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])["server_test"]
+    assert d["mismatches"] == 0 and d["calls"] == threads * calls + 6
+    assert d["idle_relaunches_ok"]
+    assert d["on_context"] < d["requests"]  # most calls ran in the resident workgroups
+    if lifetime_ms <= 2:
+        assert d["launches"] > 6, d
+
+
+@pytest.mark.gpu
+def test_server_python_threads_match_oracle(coracle):
+    """Ten Python threads (ctypes releases the GIL) on one Server: 8-byte timestamp records at the
+    reference's default B = 1000 and at B = 64, full and digest-only builds; every result equals
+    the C oracle's build."""
+    import mydatastore_amd as mde
+    sv = mde.Server(0)
+    errors = []
+
+    def caller(t):
+        rng = np.random.default_rng(300 + t)
+        try:
+            for k in range(12):
+                B = (64, 1000)[(t + k) % 2]
+                n = int(rng.integers(200, 4000))
+                ts = rng.integers(1, 1 << 40, n, dtype=np.uint64)
+                vals = ts.view(np.uint8).copy()  # LE64 timestamps (main/manager.go:816)
+                cuts = np.sort(rng.integers(0, n + 1, B - 1))
+                seg = np.concatenate([[0], cuts, [n]]).astype(np.uint64)
+                tree = k % 3 != 2
+                got = sv.build(vals, seg, 1, B, value_stride=8, want_tree=tree)
+                exp = coracle.build(vals, seg, 1, B, 8)
+                for key in ("digest", "size", "items") + (("root", "nodes") if tree else ()):
+                    if not np.array_equal(got[key], exp[key]):
+                        errors.append((t, k, key))
+        except Exception as e:  # pragma: no cover
+            errors.append((t, repr(e)))
+
+    ths = [threading.Thread(target=caller, args=(t,)) for t in range(10)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    st = sv.stats()
+    sv.close()
+    assert not errors, errors[:5]
+    assert st["requests"] == 10 * 12 and st["on_context"] == 0
