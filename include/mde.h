@@ -390,6 +390,16 @@ void mde_server_destroy(mde_server* s);
 uint32_t mde_server_slots(const mde_server* s);
 int mde_server_build(mde_server* s, const mde_records* rec, const mde_tree_out* out, char* err,
                      uint64_t err_cap);
+/* The VerifyEpoch decision step (main/manager.go:1072-1104) for ONE partition, served the same
+ * way (the fused decision step of mde_verify_epochs in the slot's workgroup): mde_batch_verify's
+ * contract. More than 16 peers, more than 256 KiB of packed inputs or n_buckets > max_buckets run
+ * as mde_verify_epochs on the service's context. */
+int mde_server_verify(mde_server* s, uint32_t n_buckets, int32_t partition, int64_t epoch,
+                      const uint64_t* digest, const int32_t* size, uint32_t n_peers,
+                      const uint8_t* peer_bytes, const uint64_t* peer_off, uint32_t replica_count,
+                      uint8_t* valid, int32_t* valid_count, int32_t* diff_ids, int32_t* diff_count,
+                      int32_t* peer_status, uint8_t* object_out, uint64_t object_stride,
+                      uint32_t* object_len, char* err, uint64_t err_cap);
 /* calls served, launches made (1 + relaunches after a lifetime ended) and calls run on the
  * service's context */
 int mde_server_stats(mde_server* s, uint64_t* requests, uint64_t* launches, uint64_t* on_context);

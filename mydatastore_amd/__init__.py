@@ -48,7 +48,7 @@ EXPORTED_SYMBOLS = (
     "mde_group_build_pipeline_drain_async", "mde_group_gather_async", "mde_group_synchronize", "mde_device_count",
     "mde_batcher_create", "mde_batcher_destroy", "mde_batcher_ctx", "mde_batcher_contexts", "mde_batcher_stats",
     "mde_batch_build", "mde_batch_verify", "mde_reserve_decode_scratch",
-    "mde_server_create", "mde_server_destroy", "mde_server_slots", "mde_server_build", "mde_server_stats",
+    "mde_server_create", "mde_server_destroy", "mde_server_slots", "mde_server_build", "mde_server_verify", "mde_server_stats",
 )
 
 
@@ -168,6 +168,8 @@ def load_library() -> C.CDLL:
         "mde_server_slots": (u32, [vp]),
         "mde_server_build": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), C.c_char_p, u64]),
         "mde_server_stats": (C.c_int, [vp, vp, vp, vp]),
+        "mde_server_verify": (C.c_int, [vp, u32, C.c_int32, C.c_int64, vp, vp, u32, vp, vp, u32, vp, vp, vp, vp,
+                                        vp, vp, u64, vp, C.c_char_p, u64]),
         "mde_batch_verify": (C.c_int, [vp, u32, i32, C.c_int64, vp, vp, u32, vp, vp, u32, vp, vp, vp, vp,
                                        vp, vp, u64, vp, C.c_char_p, u64]),
         "mde_synth_tags_async": (C.c_int, [vp, vp, u64, u32, u32, C.c_int, u64, vp, vp]),
@@ -813,3 +815,32 @@ class Server:
         if rc != MDE_OK:
             raise MdeError(rc, err.value.decode(errors="replace"))
         return out
+
+    def verify(self, n_buckets, digest, size, peer_objects, replica_count, epoch, partition=0, want_object=True):
+        """mde_server_verify: Batcher.verify's contract, served by the resident launch."""
+        B = n_buckets
+        digest = np.ascontiguousarray(digest, dtype=np.uint64).reshape(-1)
+        size = np.ascontiguousarray(size, dtype=np.int32).reshape(-1)
+        R = len(peer_objects)
+        flat = [o or b"" for o in peer_objects]
+        off = np.zeros(R + 1, np.uint64)
+        off[1:] = np.cumsum([len(o) for o in flat])
+        blob = np.frombuffer(b"".join(flat) or b"\0", dtype=np.uint8).copy()
+        valid = np.zeros(1, np.uint8)
+        vc = np.zeros(1, np.int32)
+        ids = np.zeros(B, np.int32)
+        dc = np.zeros(1, np.int32)
+        st = np.zeros(max(R, 1), np.int32)
+        stride = int(self.lib.mde_epoch_tree_object_max_bytes(B)) if want_object else 0
+        obj = np.zeros(max(stride, 1), np.uint8) if want_object else None
+        olen = np.zeros(1, np.uint32) if want_object else None
+        err = C.create_string_buffer(512)
+        rc = self.lib.mde_server_verify(self.s, B, int(partition), epoch, _ptr(digest), _ptr(size), R, _ptr(blob),
+                                        _ptr(off), replica_count, _ptr(valid), _ptr(vc), _ptr(ids), _ptr(dc),
+                                        _ptr(st), _ptr(obj), stride, _ptr(olen), err, len(err))
+        if rc != MDE_OK:
+            raise MdeError(rc, err.value.decode(errors="replace"))
+        return {"valid": bool(valid[0]), "valid_count": int(vc[0]), "diff": ids[:int(dc[0])].tolist(),
+                "peer_status": st[:R].tolist(),
+                "object": obj[:int(olen[0])].tobytes() if want_object else None}
+

@@ -17,10 +17,13 @@
 // at most (#buckets touched) atomics per wave.
 //
 // Algorithmic bytes per launch: sum of value lengths.
+#include "mde.h"
 #include "mde_device.hpp"
 #include "mde_internal.hpp"
 #include "tree_body.hpp"
+#include "verify_body.hpp"
 #include <algorithm>
+#include <cstddef>
 
 
 namespace mde {
@@ -1062,8 +1065,8 @@ constexpr uint64_t kServerExit = ~0ull - 1ull;
 constexpr uint64_t kServerFinal = 1ull << 62;  // served after closing: the last request of this workgroup
 
 // The resident build service (mde_server, server.cpp): workgroup blockIdx.x serves slot
-// blockIdx.x -- a one-partition RawPartitionMerkleTree call without a kernel launch, a copy
-// command or an event per call. Thread 0 polls the slot's `req` word in coherent pinned host
+// blockIdx.x -- a one-partition RawPartitionMerkleTree call, or one VerifyEpoch decision step
+// (verify_fused_body), without a kernel launch, a copy command or an event per call. Thread 0 polls the slot's `req` word in coherent pinned host
 // memory (a relaxed system-scope load: a read over PCIe, no cache invalidation per poll), the
 // workgroup copies the posted request into LDS with per-lane vector loads (never the scalar cache:
 // the slot is rewritten for every request), optionally stages its inputs into device memory (one
@@ -1076,9 +1079,10 @@ constexpr uint64_t kServerFinal = 1ull << 62;  // served after closing: the last
 __global__ __launch_bounds__(kThreads) void server_kernel(ServerSlot* slots, uint64_t lifetime) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   constexpr uint32_t kReqWords = (uint32_t)(sizeof(ServerReq) / 4);
-  static_assert(sizeof(ServerReq) % 4 == 0 && kReqWords <= (uint32_t)kThreads, "request fits one load per lane");
+  static_assert(sizeof(ServerReq) % 4 == 0, "request in whole words");
   __shared__ uint64_t cmd;
   __shared__ __attribute__((aligned(16))) uint32_t req[kReqWords];  // raw words (TreeLaunch has initializers)
+  __shared__ VerifyShared vsh;  // the decision step's static LDS
   ServerSlot* s = slots + blockIdx.x;
   const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + lifetime;
   uint64_t served = 0;
@@ -1111,17 +1115,16 @@ __global__ __launch_bounds__(kThreads) void server_kernel(ServerSlot* slots, uin
     const uint64_t c = cmd;
     if (c == kServerExit) return;
     __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the request's bytes, posted before req
-    if (threadIdx.x < kReqWords)
-      req[threadIdx.x] =
-          __hip_atomic_load(reinterpret_cast<const uint32_t*>(&s->r) + threadIdx.x, __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_SYSTEM);
+    for (uint32_t w = threadIdx.x; w < kReqWords; w += (uint32_t)kThreads)
+      req[w] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(&s->r) + w, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
     __syncthreads();
-    ServerReq q;
-    __builtin_memcpy(&q, req, sizeof q);
-    if (q.stage) {  // the inputs into device memory: every load in flight at once
-      const u32x4* src = reinterpret_cast<const u32x4*>(q.src);
-      u32x4* dst = reinterpret_cast<u32x4*>(q.dev_in);
-      const uint32_t n = (uint32_t)(q.stage_bytes / 16u);
+    const char* rq = reinterpret_cast<const char*>(req);
+#define MDE_REQ_FIELD(x) ({ decltype(ServerReq::x) v_; __builtin_memcpy(&v_, rq + offsetof(ServerReq, x), sizeof v_); v_; })
+    if (MDE_REQ_FIELD(stage)) {  // the inputs into device memory: every load in flight at once
+      const u32x4* src = reinterpret_cast<const u32x4*>(MDE_REQ_FIELD(src));
+      u32x4* dst = reinterpret_cast<u32x4*>(MDE_REQ_FIELD(dev_in));
+      const uint32_t n = (uint32_t)(MDE_REQ_FIELD(stage_bytes) / 16u);
       constexpr uint32_t kU = 8;
       for (uint32_t i0 = 0; i0 < n; i0 += kU * (uint32_t)kThreads) {
         u32x4 v[kU];
@@ -1139,10 +1142,25 @@ __global__ __launch_bounds__(kThreads) void server_kernel(ServerSlot* slots, uin
       __threadfence_block();
       __syncthreads();
     }
-    if (q.duo)
-      small_build_body<true>(q.d, q.t, q.G, q.words, 0, lds);
-    else
-      small_build_body<false>(q.d, q.t, q.G, q.words, 0, lds);
+    // the descriptors are read in place from LDS (the bodies take references): held in registers,
+    // a decision step's ~0.6 KB descriptor alone would take ~160 VGPRs
+    if (MDE_REQ_FIELD(kind) == 1) {  // VerifyEpoch's decision step for one partition
+      const VerifyFusedLaunch& v = *reinterpret_cast<const VerifyFusedLaunch*>(rq + offsetof(ServerReq, v));
+      const uint32_t vg = MDE_REQ_FIELD(v_G), vw = MDE_REQ_FIELD(v_words), vs = MDE_REQ_FIELD(v_stage);
+      if (MDE_REQ_FIELD(v_deep))
+        verify_fused_body<true>(v, 0, vg, vw, vs, lds, vsh);
+      else
+        verify_fused_body<false>(v, 0, vg, vw, vs, lds, vsh);
+    } else {
+      const SegDesc& d = *reinterpret_cast<const SegDesc*>(rq + offsetof(ServerReq, d));
+      const TreeLaunch& t = *reinterpret_cast<const TreeLaunch*>(rq + offsetof(ServerReq, t));
+      const uint32_t g = MDE_REQ_FIELD(G), w = MDE_REQ_FIELD(words);
+      if (MDE_REQ_FIELD(duo))
+        small_build_body<true>(d, t, g, w, 0, lds);
+      else
+        small_build_body<false>(d, t, g, w, 0, lds);
+    }
+#undef MDE_REQ_FIELD
     __threadfence_system();  // this thread's output stores, before done
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1243,7 +1261,7 @@ hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t
 }
 
 // Static LDS of server_kernel (the command word and the request copy), below the dynamic LDS.
-constexpr size_t kServerStaticLds = sizeof(ServerReq) + 64u;
+constexpr size_t kServerStaticLds = sizeof(ServerReq) + sizeof(VerifyShared) + 64u;
 
 bool server_plan(uint32_t P, uint32_t B, size_t lds_bytes, uint32_t* G, uint32_t* words, uint32_t* duo) {
   TreeGeometry g;
@@ -1260,7 +1278,8 @@ bool server_plan(uint32_t P, uint32_t B, size_t lds_bytes, uint32_t* G, uint32_t
 }
 
 size_t server_lds_bytes(uint32_t max_buckets) {
-  size_t m = 0;
+  uint32_t vg, vw, vs;
+  size_t m = verify_fused_lds(mde_verify_peer_capacity(max_buckets), &vg, &vw, &vs);
   for (uint32_t B = 1; B <= max_buckets; B++) {
     TreeGeometry g;
     if (!tree_geometry(B, &g) || g.G > (uint32_t)kThreads) continue;

@@ -154,42 +154,6 @@ constexpr uint64_t kSmallBuildMaxBytes = 96u * 1024u;
 bool small_build_fits(uint64_t bytes, uint32_t P, uint32_t B);
 hipError_t launch_small_build(const SegDesc& d, const TreeLaunch& t, hipStream_t st);
 
-// Resident build service (server.cpp, mde_server_* in include/mde.h): a persistent launch whose
-// workgroup i serves request slot i. The slots live in coherent pinned host memory, mapped into
-// the device's address space; the host posts a request by writing `r` and then `req` (release),
-// the workgroup polls `req`, runs the one-launch small build on it (small_build_body) and stores
-// `done` = `req` after its outputs (system-scope release). `closed` is set by a workgroup that
-// stops polling at the end of its lifetime (it then checks `req` once more), so a host that posts
-// and then reads `closed` == 1 knows its request may not be seen and relaunches the service.
-struct ServerReq {
-  SegDesc d;
-  TreeLaunch t;
-  uint32_t G, words;  // tree_geometry(t.B)
-  uint32_t duo;       // small_build_duo: split-schedule trees
-  uint32_t stage;     // copy the request's inputs into dev_in before the build (1) or read them in place
-  const uint8_t* src;  // stage: [src, src + stage_bytes) -> dev_in, 16-byte multiples
-  uint8_t* dev_in;
-  uint64_t stage_bytes;
-};
-struct alignas(128) ServerSlot {
-  uint64_t req;          // host: sequence number of the posted request; kServerStop: exit
-  uint64_t pad0[15];
-  uint64_t done;         // device: sequence number of the last request served
-  uint32_t closed;       // device: the workgroup has stopped polling this slot
-  uint32_t pad1[29];
-  ServerReq r;           // host: the posted request
-};
-constexpr uint64_t kServerStop = ~0ull;
-// LDS of the service's workgroups for requests of up to max_buckets buckets (0: none fit).
-size_t server_lds_bytes(uint32_t max_buckets);
-// The request plan of one build of P partitions x B buckets in one service workgroup: false when
-// it does not fit (more partitions than one workgroup holds, or B beyond the LDS).
-bool server_plan(uint32_t P, uint32_t B, size_t lds_bytes, uint32_t* G, uint32_t* words, uint32_t* duo);
-// n_slots workgroups, each polling slots[i] (device address) until s_memrealtime passes its start
-// + lifetime ticks (100 MHz) or it reads kServerStop.
-hipError_t launch_server(ServerSlot* slots, uint32_t n_slots, uint64_t lifetime_ticks, size_t lds_bytes,
-                         hipStream_t st);
-
 struct DiffLaunch {
   uint32_t n_pairs;
   uint32_t Ba, Bb;
@@ -309,6 +273,51 @@ struct VerifyFusedLaunch {
 };
 bool verify_fused_fits(uint32_t R, uint32_t cap);
 hipError_t launch_verify_fused(const VerifyFusedLaunch& a, hipStream_t st);
+// Dynamic LDS of one fused decision-step workgroup for peer capacity `cap`, and its geometry.
+size_t verify_fused_lds(uint32_t cap, uint32_t* G, uint32_t* words, uint32_t* stage_bytes);
+
+// Resident build service (server.cpp, mde_server_* in include/mde.h): a persistent launch whose
+// workgroup i serves request slot i. The slots live in coherent pinned host memory, mapped into
+// the device's address space; the host posts a request by writing `r` and then `req` (release),
+// the workgroup polls `req`, runs the one-launch small build on it (small_build_body) and stores
+// `done` = `req` after its outputs (system-scope release). `closed` is set by a workgroup that
+// stops polling at the end of its lifetime (it then checks `req` once more), so a host that posts
+// and then reads `closed` == 1 knows its request may not be seen and relaunches the service.
+// kind 0: a build (d, t: small_build_body); kind 1: a VerifyEpoch decision step of one partition
+// (v: verify_fused_body with the geometry v_G / v_words / v_stage, v_deep for B > 64).
+struct ServerReq {
+  uint32_t kind;
+  uint32_t stage;     // copy the request's inputs into dev_in first (1) or read them in place
+  const uint8_t* src;  // stage: [src, src + stage_bytes) -> dev_in, 16-byte multiples
+  uint8_t* dev_in;
+  uint64_t stage_bytes;
+  SegDesc d;
+  TreeLaunch t;
+  uint32_t G, words;  // tree_geometry(t.B)
+  uint32_t duo;       // small_build_duo: split-schedule trees
+  uint32_t v_G, v_words, v_stage, v_deep;
+  VerifyFusedLaunch v;
+};
+struct alignas(128) ServerSlot {
+  uint64_t req;          // host: sequence number of the posted request; kServerStop: exit
+  uint64_t pad0[15];
+  uint64_t done;         // device: sequence number of the last request served
+  uint32_t closed;       // device: the workgroup has stopped polling this slot
+  uint32_t pad1[29];
+  ServerReq r;           // host: the posted request
+};
+constexpr uint64_t kServerStop = ~0ull;
+// LDS of the service's workgroups for builds and decision steps of up to max_buckets buckets (0:
+// none fit).
+size_t server_lds_bytes(uint32_t max_buckets);
+// The request plan of one build of P partitions x B buckets in one service workgroup: false when
+// it does not fit (more partitions than one workgroup holds, or B beyond the LDS).
+bool server_plan(uint32_t P, uint32_t B, size_t lds_bytes, uint32_t* G, uint32_t* words, uint32_t* duo);
+// n_slots workgroups, each polling slots[i] (device address) until s_memrealtime passes its start
+// + lifetime ticks (100 MHz) or it reads kServerStop.
+hipError_t launch_server(ServerSlot* slots, uint32_t n_slots, uint64_t lifetime_ticks, size_t lds_bytes,
+                         hipStream_t st);
+
 
 hipError_t launch_tag_keys(const uint8_t* keys, const uint64_t* key_off, uint64_t n, uint32_t B,
                            uint32_t P, uint32_t* bucket, uint32_t* partition, hipStream_t st);

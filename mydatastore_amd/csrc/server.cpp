@@ -74,6 +74,7 @@ constexpr uint32_t kMaxSlots = 256;
 constexpr uint64_t kDefaultInCap = 256ull << 10;
 constexpr uint64_t kDefaultLifetimeMs = 100;
 constexpr double kWaitTimeoutS = 30.0;
+constexpr uint32_t kMaxPeers = 16;  // decision steps with more peers run on the service's context
 
 }  // namespace
 
@@ -88,6 +89,8 @@ struct mde_server {
   uint8_t* pin = nullptr;      // [n_slots ServerSlot][n_slots x in_cap][n_slots x out_cap], coherent
   uint8_t* pin_dev = nullptr;  // its device address
   uint8_t* dev_in = nullptr;   // [n_slots x in_cap] device staging
+  uint8_t* vscr = nullptr;     // [n_slots x vscr_cap] decision-step scratch (peer digests, nodes, diffs, ...)
+  uint64_t vscr_cap = 0;
   hipStream_t stream = nullptr;
   hipEvent_t exit_ev = nullptr;
   bool running = false;
@@ -123,6 +126,23 @@ OutLayout out_layout(uint32_t P, uint32_t B, bool tree, bool nodes) {
   o.nodes = o.root + (tree ? a16((uint64_t)P * 32) : 0);
   o.total = o.nodes + (nodes ? a16((uint64_t)P * mde::tree_internal(B) * 32) : 0);
   return o;
+}
+
+// Device scratch of one decision step (mde_api.cpp verify_async, P = 1): peer digests, sizes,
+// bucket counts, valid flags, nodes, roots, diff ids, statuses; the local tree's nodes and root
+// (built in the launch only when a peer of another shape needs them); the partition's valid flag
+// (read back by the encoder); the decoder's spill area for nested unknown groups.
+struct VerifyScratch {
+  uint64_t off[13];
+};
+VerifyScratch verify_scratch(uint32_t B, uint32_t R, uint64_t peer_bytes) {
+  const uint32_t cap = mde_verify_peer_capacity(B);
+  const uint64_t T = R, NI = mde::tree_internal(cap), idcap = mde_diff_capacity(B, cap), NL = mde::tree_internal(B);
+  const uint64_t part[12] = {T * cap * 8, T * cap * 4, T * 4, T, T * NI * 32, T * 32, T * idcap * 4, T * 4,
+                             NL * 32, 32, 1, mde::wire_deep_entries(T, peer_bytes) * 4};
+  VerifyScratch v{};
+  for (int i = 0; i < 12; i++) v.off[i + 1] = v.off[i] + ((part[i] + 255) & ~255ull);
+  return v;
 }
 
 // The checks mde_build makes on host records (layout A), with the caller's message buffer.
@@ -275,7 +295,10 @@ int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_se
   s->lds = mde::server_lds_bytes(s->max_buckets);
   uint32_t G, words, duo;
   if (!s->lds || !mde::server_plan(1, s->max_buckets, s->lds, &G, &words, &duo)) return bail(MDE_E_INVAL);
-  s->out_cap = a16(out_layout(1, s->max_buckets, true, true).total);
+  // outputs of a build with nodes, or of a decision step with its object and kMaxPeers statuses
+  s->out_cap = a16(std::max<uint64_t>(out_layout(1, s->max_buckets, true, true).total,
+                                      64 + a16((uint64_t)s->max_buckets * 4) + a16(kMaxPeers * 4) +
+                                          a16(mde_epoch_tree_object_max_bytes(s->max_buckets))));
   const uint64_t bytes = (uint64_t)s->n_slots * (sizeof(mde::ServerSlot) + s->in_cap + s->out_cap);
   void* p = nullptr;
   if (hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
@@ -293,6 +316,13 @@ int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_se
     return bail(MDE_E_NOMEM);
   }
   s->dev_in = static_cast<uint8_t*>(di);
+  s->vscr_cap = verify_scratch(s->max_buckets, kMaxPeers, s->in_cap).off[12];
+  void* vs = nullptr;
+  if (hipMalloc(&vs, (uint64_t)s->n_slots * s->vscr_cap) != hipSuccess) {
+    (void)hipGetLastError();
+    return bail(MDE_E_NOMEM);
+  }
+  s->vscr = static_cast<uint8_t*>(vs);
   // a CU-masked stream gets a hardware queue of its own (all CUs enabled): nothing else of this
   // process queues behind the persistent launch
   int cus = 0;
@@ -331,6 +361,7 @@ void mde_server_destroy(mde_server* s) {
   if (s->exit_ev) (void)hipEventDestroy(s->exit_ev);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   if (s->dev_in) (void)hipFree(s->dev_in);
+  if (s->vscr) (void)hipFree(s->vscr);
   if (s->pin) (void)hipHostFree(s->pin);
   if (s->ctx) mde_destroy(s->ctx);
   delete s;
@@ -414,6 +445,7 @@ int mde_server_build(mde_server* s, const mde_records* rec, const mde_tree_out* 
   q.t.root_out = tree ? out_d + ol.root : nullptr;
   q.t.nodes_out = nodes ? out_d + ol.nodes : nullptr;
   q.t.n_int = mde::tree_internal(B);
+  q.kind = 0;
   q.G = G;
   q.words = words;
   q.duo = duo;
@@ -433,6 +465,129 @@ int mde_server_build(mde_server* s, const mde_records* rec, const mde_tree_out* 
     give_slot(s, i);
   } else {
     // the slot's workgroup may still write it: it stays out of the free list
+    put_msg(err, err_cap, msg.c_str());
+  }
+  return rc;
+}
+
+int mde_server_verify(mde_server* s, uint32_t n_buckets, int32_t partition, int64_t epoch, const uint64_t* digest,
+                      const int32_t* size, uint32_t n_peers, const uint8_t* peer_bytes, const uint64_t* peer_off,
+                      uint32_t replica_count, uint8_t* valid, int32_t* valid_count, int32_t* diff_ids,
+                      int32_t* diff_count, int32_t* peer_status, uint8_t* object_out, uint64_t object_stride,
+                      uint32_t* object_len, char* err, uint64_t err_cap) {
+  put_msg(err, err_cap, "");
+  if (!s) return failf(err, err_cap, MDE_E_INVAL, "null server");
+  const uint32_t B = n_buckets, R = n_peers;
+  // mde_batch_verify's checks
+  if (!B || !mde_verify_peer_capacity(B) || B > 65536u) return failf(err, err_cap, MDE_E_INVAL, "bad n_buckets %u", B);
+  if (!digest || !valid || !valid_count || !diff_ids || !diff_count)
+    return failf(err, err_cap, MDE_E_INVAL, "bad verify arguments");
+  if (R && !peer_off) return failf(err, err_cap, MDE_E_INVAL, "peer_off is NULL");
+  if (object_out && (!size || !object_len))
+    return failf(err, err_cap, MDE_E_INVAL, "object_out needs size and object_len");
+  if (object_out && object_stride < mde_epoch_tree_object_max_bytes(B))
+    return failf(err, err_cap, MDE_E_CAPACITY, "object_stride too small");
+  for (uint32_t r = 0; r < R; r++)
+    if (peer_off[r] > peer_off[r + 1]) return failf(err, err_cap, MDE_E_INVAL, "peer_off not nondecreasing");
+  const uint64_t nbytes = R ? peer_off[R] - peer_off[0] : 0;
+  if (nbytes && !peer_bytes) return failf(err, err_cap, MDE_E_INVAL, "peer_bytes is NULL");
+  // the slot's in region: digests, sizes, partition, peer offsets (rebased), peer bytes
+  const uint64_t i_dig = 0, i_size = a16((uint64_t)B * 8), i_part = i_size + a16((uint64_t)B * 4),
+                 i_off = i_part + 16, i_peer = i_off + a16(((uint64_t)R + 1) * 8);
+  const uint64_t in_bytes = i_peer + a16(nbytes + 1);
+  // out region: valid, valid_count, diff_count, object_len, then diff ids, statuses, the object
+  const uint64_t o_ids = 64, o_st = o_ids + a16((uint64_t)B * 4), o_obj = o_st + a16((uint64_t)R * 4);
+  const uint64_t ostride = object_out ? mde_epoch_tree_object_max_bytes(B) : 0;
+  const uint64_t out_bytes = o_obj + a16(ostride);
+  const uint32_t cap = mde_verify_peer_capacity(B);
+  const VerifyScratch vs = verify_scratch(B, R, nbytes);
+  s->n_req.fetch_add(1, std::memory_order_relaxed);
+  if (B > s->max_buckets || R > kMaxPeers || !mde::verify_fused_fits(R, cap) || in_bytes > s->in_cap ||
+      out_bytes > s->out_cap || vs.off[12] > s->vscr_cap) {  // the service's context
+    s->n_ctx.fetch_add(1, std::memory_order_relaxed);
+    std::lock_guard<std::mutex> lk(s->ctx_m);
+    const int rc = mde_verify_epochs(s->ctx, 1, B, &partition, epoch, digest, size, nullptr, R, peer_bytes, peer_off,
+                                     replica_count, valid, valid_count, diff_ids, diff_count, peer_status, object_out,
+                                     object_stride, object_len);
+    if (rc) put_msg(err, err_cap, mde_last_error(s->ctx));
+    return rc;
+  }
+  const uint32_t i = take_slot(s);
+  uint8_t* in_h = s->pin + s->in_off(i);
+  const uint8_t* in_pin_d = s->pin_dev + s->in_off(i);
+  uint8_t* out_h = s->pin + s->out_off(i);
+  uint8_t* out_d = s->pin_dev + s->out_off(i);
+  std::memcpy(in_h + i_dig, digest, (uint64_t)B * 8);
+  if (size) std::memcpy(in_h + i_size, size, (uint64_t)B * 4);
+  std::memcpy(in_h + i_part, &partition, 4);
+  uint64_t* off = reinterpret_cast<uint64_t*>(in_h + i_off);
+  for (uint32_t r = 0; r <= R; r++) off[r] = R ? peer_off[r] - peer_off[0] : 0;
+  if (nbytes) std::memcpy(in_h + i_peer, peer_bytes + peer_off[0], nbytes);
+  const uint8_t* in = s->stage ? s->dev_in + (uint64_t)i * s->in_cap : in_pin_d;
+  uint8_t* sc = s->vscr + (uint64_t)i * s->vscr_cap;
+  auto at = [&](int k) { return static_cast<void*>(sc + vs.off[k]); };
+  const uint64_t T = R, NI = mde::tree_internal(cap), idcap = mde_diff_capacity(B, cap);
+  const uint64_t* d_dig = reinterpret_cast<const uint64_t*>(in + i_dig);
+  uint64_t* pd = static_cast<uint64_t*>(at(0));
+  int32_t* nbk = static_cast<int32_t*>(at(2));
+  uint8_t* pvalid = static_cast<uint8_t*>(at(3));
+  uint8_t* pnodes = static_cast<uint8_t*>(at(4));
+  int32_t* pids = static_cast<int32_t*>(at(6));
+  int32_t* pst = static_cast<int32_t*>(at(7));
+  uint8_t* lnodes = static_cast<uint8_t*>(at(8));
+  uint8_t* vdev = static_cast<uint8_t*>(at(10));
+  mde::ServerReq q{};
+  q.kind = 1;
+  q.v.dec = mde::WireDecodeLaunch{(uint32_t)T, in + i_peer, reinterpret_cast<const uint64_t*>(in + i_off), cap,
+                                  nullptr, nullptr, nullptr, pd, static_cast<int32_t*>(at(1)), pvalid, nullptr, nbk};
+  q.v.dec.deep = static_cast<uint32_t*>(at(11));
+  q.v.dec.deep_cap = (vs.off[12] - vs.off[11]) / 4;
+  q.v.tree.B = cap;
+  q.v.tree.digest_in = pd;
+  q.v.tree.root_out = static_cast<uint8_t*>(at(5));
+  q.v.tree.nodes_out = pnodes;
+  q.v.tree.n_int = NI;
+  q.v.diff = mde::DiffLaunch{(uint32_t)T, B, cap, d_dig, lnodes, pd, pnodes, pids, idcap, pst, R, nbk};
+  q.v.fold = mde::VerifyLaunch{1, R, B, pst, pids, idcap, pvalid, replica_count, vdev,
+                               reinterpret_cast<int32_t*>(out_d + 4), reinterpret_cast<int32_t*>(out_d + o_ids),
+                               reinterpret_cast<int32_t*>(out_d + 8), out_d, reinterpret_cast<int32_t*>(out_d + o_st)};
+  if (object_out)
+    q.v.enc = mde::WireEncodeLaunch{1, B, reinterpret_cast<const int32_t*>(in + i_part), epoch, epoch + 1, d_dig,
+                                    reinterpret_cast<const int32_t*>(in + i_size), vdev, nullptr, out_d + o_obj, ostride,
+                                    reinterpret_cast<uint32_t*>(out_d + 12)};
+  q.v.local.P = 1;
+  q.v.local.B = B;
+  q.v.local.digest_in = d_dig;
+  q.v.local.root_out = static_cast<uint8_t*>(at(9));
+  q.v.local.nodes_out = lnodes;
+  q.v.local.n_int = mde::tree_internal(B);
+  uint32_t vst = 0;
+  (void)mde::verify_fused_lds(cap, &q.v_G, &q.v_words, &vst);
+  q.v_stage = vst;
+  q.v_deep = B > 64 ? 1u : 0u;
+  q.stage = s->stage ? 1u : 0u;
+  q.src = in_pin_d;
+  q.dev_in = s->dev_in + (uint64_t)i * s->in_cap;
+  q.stage_bytes = a16(in_bytes);
+  std::memcpy(&s->slot(i)->r, &q, sizeof q);
+  std::string msg;
+  const int rc = post_and_wait(s, i, &msg);
+  if (rc == MDE_OK) {
+    *valid = out_h[0];
+    std::memcpy(valid_count, out_h + 4, 4);
+    std::memcpy(diff_count, out_h + 8, 4);
+    int32_t dc = 0;
+    std::memcpy(&dc, out_h + 8, 4);
+    if (dc > 0) std::memcpy(diff_ids, out_h + o_ids, (uint64_t)std::min<uint32_t>((uint32_t)dc, B) * 4);
+    if (peer_status && R) std::memcpy(peer_status, out_h + o_st, (uint64_t)R * 4);
+    if (object_out) {
+      uint32_t len = 0;
+      std::memcpy(&len, out_h + 12, 4);
+      *object_len = len;
+      std::memcpy(object_out, out_h + o_obj, std::min<uint64_t>(len, ostride));
+    }
+    give_slot(s, i);
+  } else {
     put_msg(err, err_cap, msg.c_str());
   }
   return rc;

@@ -30,7 +30,8 @@
  *   cpu_verify     per peer: EpochTreeObjectToMerkleTree (decode the 8-byte bucket hashes, NewTree)
  *                  and DifferentMerkleTreeBuckets against the local tree; validCount / diffSet fold;
  *   verify_batched the shim's verifyEpochDecision: proto.Marshal of the peer objects (a C encoder
- *                  here) + mde_batch_verify.
+ *                  here) + mde_batch_verify;
+ *   verify_server  the same through the resident service (mde_server_verify).
  * DifferentMerkleTreeBuckets of two trees the caller already holds (one pair per call):
  *   diff_host      the reference's DFS over the two node graphs (oracle_graph_diff);
  *   diff_device    mde_diff with both trees' nodes (one shared context);
@@ -99,13 +100,14 @@ enum {
   SERVER_HOSTTREE,
   CPU_VERIFY,
   V_BATCHED,
+  V_SERVER,
   DIFF_HOST,
   DIFF_DEVICE,
   DIFF_DIGESTS,
   N_CASES
 };
 static const char* kCases[] = {"cpu",          "shim",       "shim_hosttree",  "device_call", "percall",
-                               "server",       "server_hosttree", "cpu_verify", "verify_batched", "diff_host",
+                               "server",       "server_hosttree", "cpu_verify", "verify_batched", "verify_server", "diff_host",
                                "diff_device",  "diff_digests"};
 
 /* One partition-epoch of 8-byte timestamps, records spread evenly over B buckets; the oracle's
@@ -344,6 +346,18 @@ static int call(int mode, part_t* p) {
       if (!rc && (vc != 1 || dc != 1 || p->ids[0] != (int32_t)(B / 2) || valid)) bad("verify_batched", p);
       return rc;
     }
+    case V_SERVER: {
+      uint64_t off[3] = {0, 0, 0};
+      for (int k = 0; k < 2; k++)
+        off[k + 1] = off[k] + marshal_object(p->wire + off[k], part, 9, 10, p->peer_hash[k], p->size_ref, B);
+      uint8_t valid;
+      int32_t vc, dc, st[2];
+      uint32_t olen;
+      rc = mde_server_verify(server, B, part, 9, p->dig_ref, p->size_ref, 2, p->wire, off, 2, &valid, &vc, p->ids, &dc,
+                             st, p->obj, ost, &olen, err, sizeof err);
+      if (!rc && (vc != 1 || dc != 1 || p->ids[0] != (int32_t)(B / 2) || valid)) bad("verify_server", p);
+      return rc;
+    }
     case DIFF_HOST: {
       const int32_t nd = oracle_graph_diff(p->tree, p->peer_tree[1], p->ids, (int32_t)(2 * B));
       if (nd != p->n_diff_ref || memcmp(p->ids, p->diff_ref, (uint64_t)nd * 4)) bad("diff_host", p);
@@ -428,7 +442,7 @@ static void run_case(int mode, int P, uint64_t n, uint32_t B, part_t* parts, int
          kCases[mode], P, n, B, total, wall, (double)total / wall, all[total / 2] * 1e6, all[total * 9 / 10] * 1e6);
   if ((mode == SHIM || mode == SHIM_HOSTTREE || mode == DEVICE_CALL || mode == V_BATCHED) && batches > 0)
     printf(", \"mean_requests_per_batch\": %.2f", (double)(r1 - r0) / batches);
-  if (mode == SERVER || mode == SERVER_HOSTTREE) printf(", \"server_calls_on_context\": %" PRIu64, sc1 - sc0);
+  if (mode == SERVER || mode == SERVER_HOSTTREE || mode == V_SERVER) printf(", \"server_calls_on_context\": %" PRIu64, sc1 - sc0);
   printf("}\n");
   fflush(stdout);
   free(all);

@@ -1,5 +1,6 @@
 /*
- * server_test.c -- concurrent callers of the resident build service (mde_server_build), in plain
+ * server_test.c -- concurrent callers of the resident build service (mde_server_build and
+ * mde_server_verify), in plain
  * C through include/mde.h, checked bit for bit against mde_build on a shared context and the C
  * oracle (oracle/mde_oracle.c, test infrastructure).
  *
@@ -13,7 +14,8 @@
  * 8-byte timestamps (main/manager.go:816), variable-length values and variable offsets that
  * happen to be uniform (sent as a stride), records outside the bucket ranges, empty partitions,
  * two or three partitions in one call, full builds with and without inner nodes and digest-only
- * builds (root NULL). With a short lifetime (third argument) the launch ends and relaunches many
+ * builds (root NULL); after every one-partition build, the VerifyEpoch decision step through the
+ * service (mde_server_verify) against mde_verify_epochs. With a short lifetime (third argument) the launch ends and relaunches many
  * times while calls are in flight; a final phase sleeps past the lifetime between calls. Prints
  * one JSON line; exit 0 iff every output matched.
  */
@@ -35,7 +37,7 @@ static mde_server* server;
 static mde_ctx* ctx; /* per-call reference path, shared by all threads (the context locks) */
 static pthread_barrier_t start;
 static int n_calls = 40;
-static long mismatches = 0, checked = 0;
+static long mismatches = 0, checked = 0, verified = 0;
 static pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
 
 static uint64_t rng(uint64_t* s) {
@@ -59,6 +61,78 @@ static void bad(const char* what, int t, int k, uint32_t P, uint32_t B) {
   if (mismatches < 20) fprintf(stderr, "mismatch: %s (thread %d call %d, P=%u B=%u)\n", what, t, k, P, B);
   mismatches++;
   pthread_mutex_unlock(&mu);
+}
+
+/* The VerifyEpoch decision step for the partition just built (digests d, sizes z): peers that
+ * agree, differ in one bucket, are absent, are garbage, carry another bucket count (every third
+ * call), and every seventh call 20 peers (beyond the service's 16: its context). The service's
+ * answer == mde_verify_epochs on the shared context. */
+static void verify_call(int t, int k, uint32_t B, const uint64_t* d, const int32_t* z, uint64_t* s) {
+  char err[256];
+  const uint64_t stride_o = mde_epoch_tree_object_max_bytes(B + 2);
+  uint8_t* peers = xmalloc(2 * stride_o + 64);
+  uint32_t plen[2];
+  uint64_t* dp = xmalloc((B + 2) * 8ull);
+  int32_t* zp = xmalloc((B + 2) * 4ull);
+  memcpy(dp, d, B * 8ull);
+  memcpy(zp, z, B * 4ull);
+  const int32_t part = t * 100 + k;
+  const int64_t epoch = 7 + (k % 2);
+  if (mde_encode_epoch_tree_objects(ctx, 1, B, &part, epoch, epoch + 1, dp, zp, NULL, NULL, peers, stride_o, plen))
+    exit(1);
+  const uint32_t pb = (k % 3 == 2) ? B + 2 : B; /* other-shape peer */
+  for (uint32_t b = B; b < pb; b++) {
+    dp[b] = rng(s) % 999999u;
+    zp[b] = 1;
+  }
+  dp[(uint32_t)k % B] = (dp[(uint32_t)k % B] + 1) % 999999u;
+  if (mde_encode_epoch_tree_objects(ctx, 1, pb, &part, epoch, epoch + 1, dp, zp, NULL, NULL, peers + plen[0], stride_o,
+                                    plen + 1))
+    exit(1);
+  const uint32_t R = (k % 7 == 6) ? 20u : (k % 2) ? 4u : 3u;
+  uint64_t* off = xmalloc((R + 1) * 8ull);
+  const uint32_t glen = 9; /* garbage: a truncated varint field */
+  memset(peers + plen[0] + plen[1], 0xff, glen);
+  off[0] = 0;
+  for (uint32_t r = 0; r < R; r++) { /* agreeing, differing, absent, garbage, then agreeing again */
+    const uint32_t kind = r < 4 ? r : 0;
+    off[r + 1] = off[r] + (kind == 0 ? plen[0] : kind == 1 ? plen[1] : kind == 2 ? 0 : glen);
+  }
+  /* lay the peer bytes out in that order */
+  uint8_t* blob = xmalloc(off[R] + 1);
+  for (uint32_t r = 0; r < R; r++) {
+    const uint32_t kind = r < 4 ? r : 0;
+    const uint8_t* src = kind == 0 ? peers : kind == 1 ? peers + plen[0] : peers + plen[0] + plen[1];
+    memcpy(blob + off[r], src, off[r + 1] - off[r]);
+  }
+  const int want_obj = k % 4 != 3;
+  const uint64_t ostride = want_obj ? mde_epoch_tree_object_max_bytes(B) : 0;
+  uint8_t va = 0, vb = 0;
+  int32_t ca = 0, cb = 0, na = 0, nb = 0;
+  int32_t *sa = xmalloc(R * 4ull), *sb = xmalloc(R * 4ull);
+  int32_t *ia = xmalloc(B * 4ull), *ib = xmalloc(B * 4ull);
+  uint8_t *oa = xmalloc(ostride), *ob = xmalloc(ostride);
+  uint32_t la = 0, lb = 0;
+  int rc = mde_server_verify(server, B, part, epoch, d, z, R, blob, off, 2, &va, &ca, ia, &na, sa,
+                             want_obj ? oa : NULL, ostride, want_obj ? &la : NULL, err, sizeof err);
+  if (rc) {
+    fprintf(stderr, "mde_server_verify: %d %s\n", rc, err);
+    exit(1);
+  }
+  if ((rc = mde_verify_epochs(ctx, 1, B, &part, epoch, d, z, NULL, R, blob, off, 2, &vb, &cb, ib, &nb, sb,
+                              want_obj ? ob : NULL, ostride, want_obj ? &lb : NULL))) {
+    fprintf(stderr, "mde_verify_epochs: %d\n", rc);
+    exit(1);
+  }
+  if (va != vb || ca != cb || na != nb || memcmp(ia, ib, (size_t)(na > 0 ? na : 0) * 4) || memcmp(sa, sb, R * 4) ||
+      la != lb || memcmp(oa, ob, la))
+    bad("verify", t, k, 1, B);
+  if (pb == B && (na != 1 || ia[0] != (int32_t)((uint32_t)k % B))) bad("verify diff", t, k, 1, B);
+  if (sa[0] != 0 || (R > 3 && sa[3] != MDE_E_DECODE)) bad("peer status", t, k, 1, B);
+  pthread_mutex_lock(&mu);
+  verified++;
+  pthread_mutex_unlock(&mu);
+  free(peers), free(dp), free(zp), free(off), free(blob), free(sa), free(sb), free(ia), free(ib), free(oa), free(ob);
 }
 
 /* One call of shape (t, k): build through the service, mde_build and the oracle; compare. */
@@ -132,6 +206,7 @@ static void one_call(int t, int k) {
   if (memcmp(i1, i2, P * 4) || memcmp(i1, i3, P * 4)) bad("items", t, k, P, B);
   if (shape < 2 && (memcmp(r1, r2, P * 32) || memcmp(r1, r3, P * 32))) bad("root", t, k, P, B);
   if (shape == 0 && (memcmp(n1, n2, P * NI * 32) || memcmp(n1, n3, P * NI * 32))) bad("nodes", t, k, P, B);
+  if (P == 1) verify_call(t, k, B, d3, z3, &s);
   pthread_mutex_lock(&mu);
   checked++;
   pthread_mutex_unlock(&mu);
@@ -177,8 +252,8 @@ int main(int argc, char** argv) {
   mde_server_destroy(server);
   mde_destroy(ctx);
   const int relaunched = launches1 >= launches0 + 6;
-  printf("{\"server_test\": {\"threads\": %d, \"calls\": %ld, \"mismatches\": %ld, \"requests\": %" PRIu64
+  printf("{\"server_test\": {\"threads\": %d, \"calls\": %ld, \"verifies\": %ld, \"mismatches\": %ld, \"requests\": %" PRIu64
          ", \"launches\": %" PRIu64 ", \"on_context\": %" PRIu64 ", \"lifetime_ms\": %ld, \"idle_relaunches_ok\": %s}}\n",
-         threads, checked, mismatches, requests, launches1, on_ctx, life_ms, relaunched ? "true" : "false");
+         threads, checked, verified, mismatches, requests, launches1, on_ctx, life_ms, relaunched ? "true" : "false");
   return (mismatches == 0 && relaunched && checked == (long)threads * n_calls + 6) ? 0 : 1;
 }
