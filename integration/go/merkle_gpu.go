@@ -39,6 +39,12 @@ var (
 	// in flight into one device build / verify (group commit, mde_batch_build / mde_batch_verify).
 	// Each call gets its own error message back in its own buffer, so no lock is needed.
 	mdeBatchers []*C.mde_batcher
+	// mdeServers: the resident build service of each GPU (mde_server_build / mde_server_verify): a
+	// persistent launch polling request slots in pinned memory serves each call without a kernel
+	// launch, copy command or event (INTEGRATION.md section 3). mdeResident picks it over the
+	// batcher for RawPartitionMerkleTree and verifyEpochDecision.
+	mdeServers  []*C.mde_server
+	mdeResident = true
 	mdeErr      error
 	// mdeHostTree: build every returned tree with merkletree.NewTree over the device digests (a
 	// digest-only device build; B-1 host SHA-256s per call) instead of assembling it from the
@@ -73,16 +79,41 @@ func mdeEngine(partitionId int) (*C.mde_batcher, error) {
 				for _, x := range mdeBatchers {
 					C.mde_batcher_destroy(x)
 				}
-				mdeBatchers = nil
+				for _, x := range mdeServers {
+					C.mde_server_destroy(x)
+				}
+				mdeBatchers, mdeServers = nil, nil
 				return
 			}
 			mdeBatchers = append(mdeBatchers, b)
+			var sv *C.mde_server
+			// 16 request slots (>= partition_concurrency), buckets up to 1,024 in the resident launch
+			if rc := C.mde_server_create(C.int(d), 16, 1024, &sv); rc != C.MDE_OK {
+				mdeErr = errors.Errorf("mde_server_create(%d): %s", d, C.GoString(C.mde_strerror(rc)))
+				for _, x := range mdeBatchers {
+					C.mde_batcher_destroy(x)
+				}
+				for _, x := range mdeServers {
+					C.mde_server_destroy(x)
+				}
+				mdeBatchers, mdeServers = nil, nil
+				return
+			}
+			mdeServers = append(mdeServers, sv)
 		}
 	})
 	if mdeErr != nil {
 		return nil, mdeErr
 	}
 	return mdeBatchers[partitionId%len(mdeBatchers)], nil
+}
+
+// mdeServer returns the resident build service of the GPU that holds partitionId.
+func mdeServer(partitionId int) (*C.mde_server, error) {
+	if _, err := mdeEngine(partitionId); err != nil {
+		return nil, err
+	}
+	return mdeServers[partitionId%len(mdeServers)], nil
 }
 
 // mdeTree -- the *merkletree.MerkleTree NewTree would build over these buckets (cbergoon/merkletree
@@ -186,7 +217,15 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 		out.root, out.nodes = (*C.uint8_t)(cRoot), (*C.uint8_t)(cNodes)
 	}
 	var errBuf [512]C.char
-	if rc := C.mde_batch_build(batcher, &rec, &out, &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
+	if mdeResident {
+		server, err := mdeServer(partitionId)
+		if err != nil {
+			return nil, err
+		}
+		if rc := C.mde_server_build(server, &rec, &out, &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
+			return nil, errors.Errorf("mde_server_build: %s", C.GoString(&errBuf[0]))
+		}
+	} else if rc := C.mde_batch_build(batcher, &rec, &out, &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
 		return nil, errors.Errorf("mde_batch_build: %s", C.GoString(&errBuf[0]))
 	}
 	digest := append([]uint64(nil), unsafe.Slice((*uint64)(cDigest), B)...)
@@ -266,7 +305,19 @@ func verifyEpochDecision(myTree *merkletree.MerkleTree, partitionId int, epoch i
 	defer C.free(cOut)
 	outs := unsafe.Slice((*int32)(cOut), 4)
 	var errBuf [512]C.char
-	if rc := C.mde_batch_verify(batcher, C.uint32_t(B), C.int32_t(partitionId), C.int64_t(epoch),
+	if mdeResident {
+		server, err := mdeServer(partitionId)
+		if err != nil {
+			return false, 0, nil, nil, err
+		}
+		if rc := C.mde_server_verify(server, C.uint32_t(B), C.int32_t(partitionId), C.int64_t(epoch),
+			(*C.uint64_t)(cDigest), (*C.int32_t)(cSize), C.uint32_t(R), (*C.uint8_t)(cBlob), (*C.uint64_t)(cOff),
+			C.uint32_t(replicaCount), (*C.uint8_t)(unsafe.Pointer(&outs[0])), (*C.int32_t)(unsafe.Pointer(&outs[1])),
+			(*C.int32_t)(cIds), (*C.int32_t)(unsafe.Pointer(&outs[2])), (*C.int32_t)(cStatus), (*C.uint8_t)(cObj),
+			stride, (*C.uint32_t)(unsafe.Pointer(&outs[3])), &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
+			return false, 0, nil, nil, errors.Errorf("mde_server_verify: %s", C.GoString(&errBuf[0]))
+		}
+	} else if rc := C.mde_batch_verify(batcher, C.uint32_t(B), C.int32_t(partitionId), C.int64_t(epoch),
 		(*C.uint64_t)(cDigest), (*C.int32_t)(cSize), C.uint32_t(R), (*C.uint8_t)(cBlob), (*C.uint64_t)(cOff),
 		C.uint32_t(replicaCount), (*C.uint8_t)(unsafe.Pointer(&outs[0])), (*C.int32_t)(unsafe.Pointer(&outs[1])),
 		(*C.int32_t)(cIds), (*C.int32_t)(unsafe.Pointer(&outs[2])), (*C.int32_t)(cStatus), (*C.uint8_t)(cObj),

@@ -10,7 +10,8 @@
  *                       B bucket ranges and appends every value to ONE arena, record by record:
  *                       value_off grows by each value's length, seg_rec by the record count per
  *                       bucket, n_partitions = 1, value_stride = 0 (variable-length values); an
- *                       empty arena gets one padding byte. B > 256: -> mde_batch_build with the
+ *                       empty arena gets one padding byte. B > 256: -> mde_server_build (the
+ *                       shim's mdeResident; mde_batch_build with "batcher" as argv[2]) with the
  *                       nodes output, then the shim's mdeTree: the *merkletree.MerkleTree assembled
  *                       from the device's digests and node hashes (no host hashing; mirrored
  *                       below). B <= 256 (mdeHostTreeMaxBuckets): a digest-only mde_batch_build
@@ -22,7 +23,7 @@
  *                       object has B+1 leaves, no duplicate) -- mirrored below.
  *   verify B p E rc R   VerifyEpoch's peer loop (main/manager.go:1072-1104): the local tree's
  *                       digests and sizes, R peer objects as wire bytes (absent = empty range)
- *                       -> mde_batch_verify.
+ *                       -> mde_server_verify (mde_batch_verify with "batcher").
  *
  * Input: whitespace-separated tokens; values and peer objects as hex strings ("-" = empty).
  *   build B n  <bucket of each record, nondecreasing>  <hex value of each record>
@@ -181,9 +182,13 @@ int main(int argc, char** argv) {
   if (argc < 2) return 2;
   FILE* f = fopen(argv[1], "r");
   if (!f) return 2;
+  /* the shim's mdeResident: the resident service (default), or "batcher" as the second argument */
+  const int resident = !(argc > 2 && !strcmp(argv[2], "batcher"));
   mde_batcher* batcher = NULL;
+  mde_server* server = NULL;
   mde_ctx* ctx = NULL;
   int rc = mde_batcher_create(0, 256, 0, &batcher);
+  if (!rc) rc = mde_server_create(0, 16, 1024, &server);
   if (rc || (rc = mde_create(0, &ctx))) {
     fprintf(stderr, "create: %d (%s)\n", rc, mde_strerror(rc));
     return 1;
@@ -231,8 +236,10 @@ int main(int argc, char** argv) {
       uint8_t* nodes = xmalloc(mde_tree_internal_nodes(B) * 32);
       const int host_tree = B <= HOST_TREE_MAX_BUCKETS;
       mde_tree_out out = {digest, size, &items, host_tree ? NULL : root, host_tree ? NULL : nodes};
-      if ((rc = mde_batch_build(batcher, &rec, &out, err, sizeof err))) {
-        fprintf(stderr, "mde_batch_build: %d %s\n", rc, err);
+      rc = resident ? mde_server_build(server, &rec, &out, err, sizeof err)
+                    : mde_batch_build(batcher, &rec, &out, err, sizeof err);
+      if (rc) {
+        fprintf(stderr, "build: %d %s\n", rc, err);
         return 1;
       }
       if (host_tree) oracle_tree(digest, B, nodes, root);
@@ -303,9 +310,12 @@ int main(int argc, char** argv) {
       uint8_t valid = 0;
       int32_t vc = 0, dc = 0;
       uint32_t olen = 0;
-      if ((rc = mde_batch_verify(batcher, B, part, epoch, digest, size, R, blob, off, replicas, &valid, &vc, ids, &dc,
-                                 status, obj, stride, &olen, err, sizeof err))) {
-        fprintf(stderr, "mde_batch_verify: %d %s\n", rc, err);
+      rc = resident ? mde_server_verify(server, B, part, epoch, digest, size, R, blob, off, replicas, &valid, &vc, ids,
+                                        &dc, status, obj, stride, &olen, err, sizeof err)
+                    : mde_batch_verify(batcher, B, part, epoch, digest, size, R, blob, off, replicas, &valid, &vc, ids,
+                                       &dc, status, obj, stride, &olen, err, sizeof err);
+      if (rc) {
+        fprintf(stderr, "verify: %d %s\n", rc, err);
         return 1;
       }
       printf("verify %d %d ;", valid, vc);
@@ -322,6 +332,7 @@ int main(int argc, char** argv) {
     }
   }
   fclose(f);
+  mde_server_destroy(server);
   mde_batcher_destroy(batcher);
   mde_destroy(ctx);
   return 0;

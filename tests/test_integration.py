@@ -195,21 +195,23 @@ def _replay_scenarios():
 
 
 @pytest.mark.gpu
-def test_shim_call_sequences_replayed_from_c_match_oracle(tmp_path):
+@pytest.mark.parametrize("path", ["resident", "batcher"])
+def test_shim_call_sequences_replayed_from_c_match_oracle(tmp_path, path):
     """The Go shim's exact ABI call sequences (integration/go/merkle_gpu.go, which cannot be
     compiled here), replayed in C: RawPartitionMerkleTree's one-partition arena with value_off
-    built record by record -> mde_batch_build with nodes -> the tree assembled from the device's
+    built record by record -> mde_server_build (the shim's default; mde_batch_build for
+    path="batcher") with nodes -> the tree assembled from the device's
     node hashes (mdeTree: Root.Hash, leaf count and the whole pre-order walk equal NewTree's);
     the reference's DFS over trees of that shape, B local leaves against B + 1 peer leaves
     (odd-B object quirk, SURVEY App. A.2);
     verifyEpochDecision with agreeing, absent, garbage, Valid-differing and other-B peers ->
-    mde_batch_verify. Every output equals the oracle's restatement of the reference
+    mde_server_verify / mde_batch_verify. Every output equals the oracle's restatement of the reference
     (main/merkle_tree.go:86-216, main/manager.go:1072-1104)."""
     import subprocess
     lines, expect = _replay_scenarios()
     f = tmp_path / "scenarios.txt"
     f.write_text("\n".join(lines) + "\n")
-    r = subprocess.run([str(REPLAY), str(f)], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([str(REPLAY), str(f), path], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     got = r.stdout.strip().splitlines()
     assert len(got) == len(expect)
