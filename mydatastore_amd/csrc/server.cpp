@@ -84,7 +84,8 @@ struct mde_server {
   uint32_t max_buckets = 1024;
   uint64_t in_cap = kDefaultInCap, out_cap = 0;
   size_t lds = 0;
-  uint64_t lifetime_ticks = kDefaultLifetimeMs * 100000ull;  // s_memrealtime: 100 MHz
+  uint64_t lifetime_ticks = 0;  // s_memrealtime ticks (wall_khz per ms)
+  uint32_t wall_khz = 0;
   bool stage = true;  // MDE_SERVER_STAGE=0: the build reads its inputs in place over PCIe (A/B)
   uint8_t* pin = nullptr;      // [n_slots ServerSlot][n_slots x in_cap][n_slots x out_cap], coherent
   uint8_t* pin_dev = nullptr;  // its device address
@@ -277,10 +278,19 @@ int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_se
   s->device = device;
   if (n_slots) s->n_slots = n_slots;
   if (max_buckets) s->max_buckets = max_buckets;
+  uint64_t life_ms = kDefaultLifetimeMs;
   if (const char* e = std::getenv("MDE_SERVER_LIFETIME_MS")) {
     const long long ms = std::atoll(e);
-    if (ms >= 1) s->lifetime_ticks = (uint64_t)ms * 100000ull;
+    if (ms >= 1) life_ms = (uint64_t)ms;
   }
+  // s_memrealtime ticks at the device's wall-clock rate (kHz)
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) {
+    (void)hipGetLastError();
+    khz = 100000;
+  }
+  s->wall_khz = (uint32_t)khz;
+  s->lifetime_ticks = life_ms * (uint64_t)khz;
   if (const char* e = std::getenv("MDE_SERVER_STAGE")) s->stage = std::atoi(e) != 0;
   int rc = mde_create(device, &s->ctx);
   if (rc != MDE_OK) {
