@@ -22,7 +22,8 @@
 // that posts and then reads `closed` set waits for the launch to end and relaunches (a request
 // is served either by the closing workgroup's last read or by the next launch, never lost).
 // The launch runs on a CU-masked stream: such a stream gets a hardware queue of its own, so no
-// other stream of the process queues behind the persistent kernel.
+// other stream of the process queues behind the persistent kernel (kept for the process, see
+// mde_server_create).
 // Requests the resident workgroups do not take (more partitions than one workgroup holds, inputs
 // or outputs beyond a slot, B beyond the launch's LDS) run as mde_build on the service's own
 // context. Each caller gets exactly what mde_build returns for its inputs (tests/cpp/server_test.c
@@ -93,6 +94,7 @@ struct mde_server {
   uint8_t* vscr = nullptr;     // [n_slots x vscr_cap] decision-step scratch (peer digests, nodes, diffs, ...)
   uint64_t vscr_cap = 0;
   hipStream_t stream = nullptr;
+  bool keep_stream = false;  // a process-lifetime stream (MDE_SERVER_CUMASK=2)
   hipEvent_t exit_ev = nullptr;
   bool running = false;
   std::mutex launch_m;
@@ -339,7 +341,28 @@ int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_se
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
   std::vector<uint32_t> mask((size_t)std::max(1, (cus + 31) / 32), 0u);
   for (int c = 0; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
-  if (hipExtStreamCreateWithCUMask(&s->stream, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+  // The launch's stream: a CU-masked stream (all CUs) gets a hardware queue of its own, so no other
+  // stream of the process queues behind the persistent kernel. It is kept for the process and
+  // reused by the next service on the device: destroying a CU-masked stream made a later
+  // hipStreamDestroy of another stream hang (ROCm 7, profiles/r04/r04n_service_streams.txt).
+  // MDE_SERVER_CUMASK=0: a plain non-blocking stream instead; 1: a CU-masked stream destroyed
+  // with the service (probes).
+  const char* cm = std::getenv("MDE_SERVER_CUMASK");
+  const int cmode = cm ? std::atoi(cm) : 2;
+  s->keep_stream = cmode == 2;
+  static std::mutex kept_m;
+  static hipStream_t kept[64] = {};
+  hipError_t se = hipSuccess;
+  if (cmode == 0) {
+    se = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  } else if (cmode == 2 && device >= 0 && device < 64) {
+    std::lock_guard<std::mutex> lk(kept_m);
+    if (!kept[device]) se = hipExtStreamCreateWithCUMask(&kept[device], (uint32_t)mask.size(), mask.data());
+    s->stream = kept[device];
+  } else {
+    se = hipExtStreamCreateWithCUMask(&s->stream, (uint32_t)mask.size(), mask.data());
+  }
+  if (se != hipSuccess || !s->stream) {
     (void)hipGetLastError();
     s->stream = nullptr;
     return bail(MDE_E_DEVICE);
@@ -366,14 +389,50 @@ void mde_server_destroy(mde_server* s) {
     for (uint32_t i = 0; i < s->n_slots; i++) __atomic_store_n(&s->slot(i)->req, mde::kServerStop, __ATOMIC_RELEASE);
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
   }
-  if (s->running && s->exit_ev) (void)hipEventSynchronize(s->exit_ev);
-  if (s->stream) (void)hipStreamSynchronize(s->stream);
-  if (s->exit_ev) (void)hipEventDestroy(s->exit_ev);
-  if (s->stream) (void)hipStreamDestroy(s->stream);
-  if (s->dev_in) (void)hipFree(s->dev_in);
-  if (s->vscr) (void)hipFree(s->vscr);
-  if (s->pin) (void)hipHostFree(s->pin);
+  const bool dbg = std::getenv("MDE_SERVER_DEBUG") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto since = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+  // bounded wait for the launch to end (it reads the stop word within microseconds, and ends at
+  // its lifetime in any case); a launch that does not end keeps its buffers (never freed under it)
+  bool ended = true;
+  if (s->running && s->exit_ev) {
+    bool told = false;
+    for (;;) {
+      const hipError_t e = hipEventQuery(s->exit_ev);
+      if (e != hipErrorNotReady) {
+        if (dbg) std::fprintf(stderr, "mde_server_destroy: launch ended after %.6f s (%s)\n", since(), hipGetErrorString(e));
+        break;
+      }
+      const double dt = since();
+      if (dt > 1.0 && !told) {
+        told = true;
+        std::fprintf(stderr, "mde_server_destroy: launch still running after 1 s; slots (req done closed):");
+        for (uint32_t i = 0; i < s->n_slots; i++)
+          std::fprintf(stderr, " [%llx %llu %u]", (unsigned long long)__atomic_load_n(&s->slot(i)->req, __ATOMIC_ACQUIRE),
+                       (unsigned long long)__atomic_load_n(&s->slot(i)->done, __ATOMIC_ACQUIRE),
+                       __atomic_load_n(&s->slot(i)->closed, __ATOMIC_ACQUIRE));
+        std::fprintf(stderr, "\n");
+      }
+      if (dt > 10.0) {
+        std::fprintf(stderr, "mde_server_destroy: launch did not end within 10 s; its buffers are kept\n");
+        ended = false;
+        break;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
+  if (ended) {
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (dbg) std::fprintf(stderr, "mde_server_destroy: stream synchronized %.6f s\n", since());
+    if (s->exit_ev) (void)hipEventDestroy(s->exit_ev);
+    if (s->stream && !s->keep_stream) (void)hipStreamDestroy(s->stream);
+    if (s->dev_in) (void)hipFree(s->dev_in);
+    if (s->vscr) (void)hipFree(s->vscr);
+    if (s->pin) (void)hipHostFree(s->pin);
+    if (dbg) std::fprintf(stderr, "mde_server_destroy: freed %.6f s\n", since());
+  }
   if (s->ctx) mde_destroy(s->ctx);
+  if (dbg) std::fprintf(stderr, "mde_server_destroy: done %.6f s\n", since());
   delete s;
 }
 

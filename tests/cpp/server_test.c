@@ -259,12 +259,16 @@ int main(int argc, char** argv) {
     fprintf(stderr, "idle call %d: launches %" PRIu64 " -> %" PRIu64 "\n", k, l0, l1);
   }
   mde_server_stats(server, &requests, &launches1, &on_ctx);
+  fprintf(stderr, "destroying the service\n");
   mde_server_destroy(server);
+  fprintf(stderr, "service destroyed\n");
   mde_destroy(ctx);
+  fprintf(stderr, "context destroyed\n");
   const int relaunched = launches1 >= launches0 + 6;
   printf("{\"server_test\": {\"threads\": %d, \"calls\": %ld, \"verifies\": %ld, \"mismatches\": %ld, \"requests\": %" PRIu64
          ", \"launches_before_idle\": %" PRIu64 ", \"launches\": %" PRIu64 ", \"on_context\": %" PRIu64
          ", \"lifetime_ms\": %ld, \"idle_relaunches_ok\": %s}}\n",
          threads, checked, verified, mismatches, requests, launches0, launches1, on_ctx, life_ms, relaunched ? "true" : "false");
+  fflush(stdout);
   return (mismatches == 0 && relaunched && checked == (long)threads * n_calls + 6) ? 0 : 1;
 }
