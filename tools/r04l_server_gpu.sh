@@ -1,6 +1,6 @@
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r04l; mkdir -p $O
+O=gpurun_out/${TAG:-r04l}; mkdir -p $O
 echo "== server_test 1x8"; timeout -k 10 60 tests/cpp/build/server_test 1 8 100 > $O/st1.json 2> $O/st1.err; rc=$?; cat $O/st1.json; tail -5 $O/st1.err; [ $rc -eq 0 ] || exit $rc
 echo "== server_test 10x40"; timeout -k 10 90 tests/cpp/build/server_test 10 40 100 > $O/st2.json 2> $O/st2.err; rc=$?; cat $O/st2.json; tail -5 $O/st2.err; [ $rc -eq 0 ] || exit $rc
 echo "== server_test 8x30 lifetime 2ms"; timeout -k 10 90 tests/cpp/build/server_test 8 30 2 > $O/st3.json 2> $O/st3.err; rc=$?; cat $O/st3.json; tail -5 $O/st3.err; [ $rc -eq 0 ] || exit $rc
