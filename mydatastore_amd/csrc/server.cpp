@@ -75,6 +75,7 @@ constexpr uint32_t kMaxSlots = 256;
 constexpr uint64_t kDefaultInCap = 256ull << 10;
 constexpr uint64_t kDefaultLifetimeMs = 100;
 constexpr double kWaitTimeoutS = 30.0;
+constexpr double kSpinS = 10e-6;  // pure spinning before a waiting caller starts yielding
 constexpr uint32_t kMaxPeers = 16;  // decision steps with more peers run on the service's context
 
 }  // namespace
@@ -223,9 +224,18 @@ int post_and_wait(mde_server* s, uint32_t i, std::string* msg) {
     if (rc) return rc;
   }
   const auto t0 = std::chrono::steady_clock::now();
+  bool yielding = false;
   for (uint64_t spin = 1;; spin++) {
     if (__atomic_load_n(&sl->done, __ATOMIC_ACQUIRE) == q) return MDE_OK;
-    _mm_pause();
+    // spin through a short call's round trip, then give the core away between checks: with more
+    // callers than cores (100 goroutines on a 16-core share) spinning slot holders would starve
+    // the callers that pack requests or build host trees
+    if (yielding)
+      std::this_thread::yield();
+    else
+      _mm_pause();
+    if ((spin & 15) == 0 && !yielding)
+      yielding = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kSpinS;
     if ((spin & 63) == 0) {
       if (__atomic_load_n(&sl->closed, __ATOMIC_ACQUIRE)) {
         // the workgroup closed: served by its last read, or by the next launch
@@ -234,7 +244,6 @@ int post_and_wait(mde_server* s, uint32_t i, std::string* msg) {
         continue;
       }
       const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      if (dt > 50e-6) std::this_thread::yield();  // oversubscribed callers: give the core away
       if (dt > kWaitTimeoutS) {
         const hipError_t e = hipEventQuery(s->exit_ev);
         *msg = std::string("resident build request timed out (launch: ") + hipGetErrorString(e) + ")";
