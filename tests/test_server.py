@@ -82,3 +82,52 @@ def test_server_python_threads_match_oracle(coracle):
     sv.close()
     assert not errors, errors[:5]
     assert st["requests"] == 10 * 12 and st["on_context"] == 0
+
+
+@pytest.mark.gpu
+def test_server_python_decisions_match_oracle(coracle):
+    """The VerifyEpoch decision step through the service (Server.verify) from eight Python
+    threads at B = 64 and 1000: agreeing, one-bucket-differing, absent and garbage peers; every
+    result equals the oracle's VerifyEpoch restatement (oracle.py verify_epoch,
+    main/manager.go:1072-1104)."""
+    import mydatastore_amd as mde
+    from oracle import oracle as O
+    from oracle import wire_pb
+    sv = mde.Server(0)
+    errors = []
+
+    def caller(t):
+        rng = np.random.default_rng(700 + t)
+        try:
+            for k in range(10):
+                B = (64, 1000)[(t + k) % 2]
+                n = int(rng.integers(200, 3000))
+                ts = rng.integers(1, 1 << 40, n, dtype=np.uint64)
+                vals = ts.view(np.uint8).copy()
+                cuts = np.sort(rng.integers(0, n + 1, B - 1))
+                seg = np.concatenate([[0], cuts, [n]]).astype(np.uint64)
+                exp = coracle.build(vals, seg, 1, B, 8)
+                d = exp["digest"].astype(np.uint64)
+                z = exp["size"]
+                d2 = d.copy()
+                d2[(3 * k + t) % B] = (d2[(3 * k + t) % B] + 1) % 999999
+                peers = [wire_pb.marshal(5, 2, 3, d.tolist(), z.tolist()),
+                         wire_pb.marshal(5, 2, 3, d2.tolist(), z.tolist(), valid=bool(k % 2)),
+                         None, b"\xff\xff"]
+                res = sv.verify(B, d, z, peers, replica_count=2, epoch=2, partition=5)
+                want = O.verify_epoch(O.tree_from_digests(d.tolist(), z.tolist()), 5, 2, peers, 2)
+                if (res["valid"], res["valid_count"], res["diff"], res["object"]) != \
+                        (want["valid"], want["valid_count"], want["diff"], want["object"]):
+                    errors.append((t, k))
+        except Exception as e:  # pragma: no cover
+            errors.append((t, repr(e)))
+
+    ths = [threading.Thread(target=caller, args=(t,)) for t in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    st = sv.stats()
+    sv.close()
+    assert not errors, errors[:5]
+    assert st["requests"] == 8 * 10 and st["on_context"] == 0
