@@ -10,6 +10,10 @@
 #   prod    bench.py --config prod line    -> bench_prod.json
 #   prof    rocprofv3 trace + FETCH/WRITE PMC of the default bench (tools/profile.sh)
 #   sq      SQ counters of the default bench workload (one --pmc pass)
+#   service resident build service: server_test (1 / 10 / 8 callers, 100 and 2 ms lifetimes) and
+#           the service + shim-replay pytest                         -> st{1,2,3}.json, service_pytest.log
+#   callbench  batch_bench at B = 64 / 1,000 x 1 / 10 / 100 callers  -> bb.jsonl (+ summary)
+#   stress  resident service under 4-64 callers, 1-100 ms lifetimes -> stress{1..5}.json
 # Extra bench flags: BENCH_ARGS="...".
 set -o pipefail
 export TMPDIR=/tmp
@@ -54,6 +58,31 @@ for s in "$@"; do
       timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES \
         --output-format csv -d $O/sq -o run -- python3 bench.py --profile ${BENCH_ARGS:-} --steps 3 --warmup 1 \
         > $O/sq.json 2> $O/sq.err || { tail -20 $O/sq.err; exit 1; } ;;
+    service)
+      step service
+      i=0
+      for a in "1 8 100" "10 40 100" "8 30 2"; do
+        i=$((i+1))
+        timeout -k 10 120 tests/cpp/build/server_test $a > $O/st$i.json 2> $O/st$i.err || { tail -5 $O/st$i.err; exit 1; }
+        cat $O/st$i.json
+      done
+      timeout -k 10 300 python -u -m pytest tests/test_server.py tests/test_integration.py -m gpu -x -v -p no:cacheprovider \
+        --timeout 120 --timeout-method thread > $O/service_pytest.log 2>&1 || { tail -30 $O/service_pytest.log; exit 1; }
+      tail -3 $O/service_pytest.log ;;
+    callbench)
+      step callbench
+      for B in 64 1000; do for P in 1 10 100; do
+        timeout -k 10 150 tests/cpp/build/batch_bench 0.4 $B $P >> $O/bb.jsonl 2>> $O/bb.err || { tail $O/bb.err; exit 1; }
+      done; done
+      python tools/batch_summary.py $O/bb.jsonl ;;
+    stress)
+      step stress
+      i=0
+      for a in "32 40 1" "16 60 3" "64 10 1" "10 80 100" "4 200 1"; do
+        i=$((i+1))
+        timeout -k 10 150 tests/cpp/build/server_test $a > $O/stress$i.json 2> $O/stress$i.err || { tail -5 $O/stress$i.err; exit 1; }
+        cat $O/stress$i.json
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
