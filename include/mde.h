@@ -131,6 +131,9 @@ int mde_set_verify_mode(mde_ctx* ctx, int mode);
 /* Tree geometry (merkletree v0.2.0 shape: dup last leaf if odd, self-pair odd levels). */
 uint32_t mde_tree_depth(uint32_t n_buckets);          /* internal levels, root included */
 uint64_t mde_tree_internal_nodes(uint32_t n_buckets); /* nodes per tree in mde_tree_out.nodes */
+/* Nodes of levels 1 .. L, L = the first level of at most top_nodes nodes (top_nodes <= 1: every
+ * level, = mde_tree_internal_nodes): what mde_server_build_levels writes per partition. */
+uint64_t mde_tree_prefix_nodes(uint32_t n_buckets, uint32_t top_nodes);
 uint64_t mde_diff_capacity(uint32_t n_buckets_a, uint32_t n_buckets_b); /* max ids one diff emits */
 
 /* RawPartitionMerkleTree for P partitions: bucket digests + sizes + SHA-256 tree on device.
@@ -390,6 +393,16 @@ void mde_server_destroy(mde_server* s);
 uint32_t mde_server_slots(const mde_server* s);
 int mde_server_build(mde_server* s, const mde_records* rec, const mde_tree_out* out, char* err,
                      uint64_t err_cap);
+/* RawPartitionMerkleTree split between the device and the caller: digests, sizes, items and the
+ * tree's levels 1 .. L (L = the first level of at most top_nodes nodes; out->nodes required, at
+ * the usual stride of mde_tree_internal_nodes(B) per partition, of which the first
+ * mde_tree_prefix_nodes(B, top_nodes) are written; out->root is not written). The caller hashes
+ * the few top levels (node = SHA256(left || right), the last node of an odd level paired with
+ * itself): a tree's dependent top levels cost a CPU core ~40 ns per compression on its SHA
+ * extensions against ~2 us on the device. The Go shim assembles the tree from these nodes and
+ * hashes its top levels with crypto/sha256. */
+int mde_server_build_levels(mde_server* s, const mde_records* rec, const mde_tree_out* out, uint32_t top_nodes,
+                            char* err, uint64_t err_cap);
 /* The VerifyEpoch decision step (main/manager.go:1072-1104) for ONE partition, served the same
  * way (the fused decision step of mde_verify_epochs in the slot's workgroup): mde_batch_verify's
  * contract. More than 16 peers, more than 256 KiB of packed inputs or n_buckets > max_buckets run

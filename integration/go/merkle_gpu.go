@@ -18,6 +18,7 @@ package main
 import "C"
 
 import (
+	"crypto/sha256"
 	"sync"
 	"unsafe"
 
@@ -116,11 +117,18 @@ func mdeServer(partitionId int) (*C.mde_server, error) {
 	return mdeServers[partitionId%len(mdeServers)], nil
 }
 
+// mdeTopNodes: with the resident service the device builds a tree's levels down to the first of at
+// most this many nodes (mde_server_build_levels) and mdeTree hashes the few levels above it: a
+// tree's dependent top levels cost a core ~40 ns per compression on the SHA extensions
+// crypto/sha256 uses, the device ~2 us (INTEGRATION.md section 3).
+const mdeTopNodes = 64
+
 // mdeTree -- the *merkletree.MerkleTree NewTree would build over these buckets (cbergoon/merkletree
 // v0.2.0: a duplicate of the last leaf when B is odd, level nodes pairing (2j, 2j+1) and the last
-// node of an odd level paired with itself), assembled from the device's outputs without hashing:
-// nodes holds the internal node hashes level 1 .. root, 32 bytes each (mde_tree_out.nodes).
-func mdeTree(digest []uint64, size []int32, nodes []byte) *merkletree.MerkleTree {
+// node of an odd level paired with itself), assembled from the device's outputs: nodes holds the
+// internal node hashes level 1 .. root, 32 bytes each (mde_tree_out.nodes), of which the first
+// `have` are the device's; the rest are hashed here as NewTree does (SHA256(left || right)).
+func mdeTree(digest []uint64, size []int32, nodes []byte, have int) *merkletree.MerkleTree {
 	B := len(digest)
 	t := &merkletree.MerkleTree{}
 	level := make([]*merkletree.Node, B, B+1)
@@ -142,7 +150,13 @@ func mdeTree(digest []uint64, size []int32, nodes []byte) *merkletree.MerkleTree
 			if 2*j+1 < len(level) {
 				r = level[2*j+1]
 			}
-			h := nodes[(off+j)*32 : (off+j+1)*32 : (off+j+1)*32]
+			var h []byte
+			if off+j < have {
+				h = nodes[(off+j)*32 : (off+j+1)*32 : (off+j+1)*32]
+			} else {
+				sum := sha256.Sum256(append(append(make([]byte, 0, 64), l.Hash...), r.Hash...))
+				h = sum[:]
+			}
 			n := &merkletree.Node{Left: l, Right: r, Hash: h}
 			l.Parent, r.Parent = n, n
 			next[j] = n
@@ -217,12 +231,19 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 		out.root, out.nodes = (*C.uint8_t)(cRoot), (*C.uint8_t)(cNodes)
 	}
 	var errBuf [512]C.char
+	have := nodeBytes / 32 // device node hashes in cNodes (all of them unless the levels are split)
 	if mdeResident {
 		server, err := mdeServer(partitionId)
 		if err != nil {
 			return nil, err
 		}
-		if rc := C.mde_server_build(server, &rec, &out, &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
+		if !hostTree { // the device's levels down to <= mdeTopNodes nodes; mdeTree hashes the top
+			out.root = nil
+			if rc := C.mde_server_build_levels(server, &rec, &out, mdeTopNodes, &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
+				return nil, errors.Errorf("mde_server_build_levels: %s", C.GoString(&errBuf[0]))
+			}
+			have = int(C.mde_tree_prefix_nodes(C.uint32_t(B), mdeTopNodes))
+		} else if rc := C.mde_server_build(server, &rec, &out, &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
 			return nil, errors.Errorf("mde_server_build: %s", C.GoString(&errBuf[0]))
 		}
 	} else if rc := C.mde_batch_build(batcher, &rec, &out, &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
@@ -231,7 +252,7 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 	digest := append([]uint64(nil), unsafe.Slice((*uint64)(cDigest), B)...)
 	size := append([]int32(nil), unsafe.Slice((*int32)(cSize), B)...)
 	if !hostTree {
-		return mdeTree(digest, size, C.GoBytes(cNodes, C.int(nodeBytes))), nil
+		return mdeTree(digest, size, C.GoBytes(cNodes, C.int(nodeBytes)), have), nil
 	}
 	// merkletree.NewTree over the device digests (B-1 host SHA-256s)
 	bucketList := make([]merkletree.Content, B)

@@ -48,7 +48,8 @@ EXPORTED_SYMBOLS = (
     "mde_group_build_pipeline_drain_async", "mde_group_gather_async", "mde_group_synchronize", "mde_device_count",
     "mde_batcher_create", "mde_batcher_destroy", "mde_batcher_ctx", "mde_batcher_contexts", "mde_batcher_stats",
     "mde_batch_build", "mde_batch_verify", "mde_reserve_decode_scratch",
-    "mde_server_create", "mde_server_destroy", "mde_server_slots", "mde_server_build", "mde_server_verify", "mde_server_stats",
+    "mde_server_create", "mde_server_destroy", "mde_server_slots", "mde_server_build", "mde_server_build_levels", "mde_server_verify", "mde_server_stats",
+    "mde_tree_prefix_nodes",
 )
 
 
@@ -168,6 +169,8 @@ def load_library() -> C.CDLL:
         "mde_server_slots": (u32, [vp]),
         "mde_server_build": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), C.c_char_p, u64]),
         "mde_server_stats": (C.c_int, [vp, vp, vp, vp]),
+        "mde_server_build_levels": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), u32, C.c_char_p, u64]),
+        "mde_tree_prefix_nodes": (u64, [u32, u32]),
         "mde_server_verify": (C.c_int, [vp, u32, C.c_int32, C.c_int64, vp, vp, u32, vp, vp, u32, vp, vp, vp, vp,
                                         vp, vp, u64, vp, C.c_char_p, u64]),
         "mde_batch_verify": (C.c_int, [vp, u32, i32, C.c_int64, vp, vp, u32, vp, vp, u32, vp, vp, vp, vp,
@@ -814,6 +817,27 @@ class Server:
         rc = self.lib.mde_server_build(self.s, C.byref(rec), C.byref(to), err, len(err))
         if rc != MDE_OK:
             raise MdeError(rc, err.value.decode(errors="replace"))
+        return out
+
+    def build_levels(self, values, seg_rec, n_partitions, n_buckets, top_nodes, value_stride=0, value_off=None):
+        """mde_server_build_levels: digests, sizes, items and the tree's levels 1 .. the first of at
+        most top_nodes nodes (the first mde_tree_prefix_nodes(B, top_nodes) of every partition's
+        nodes; the rest stay zero, the caller hashes them)."""
+        P, B = n_partitions, n_buckets
+        seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
+        values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)
+        if value_off is not None:
+            value_off = np.ascontiguousarray(value_off, dtype=np.uint64)
+        n_rec = (value_off.size - 1) if value_off is not None else (values.size // value_stride if value_stride else 0)
+        rec = Records(_ptr(values), values.nbytes, value_stride, 0, _ptr(value_off), n_rec, P, B, _ptr(seg_rec))
+        out = _build_outputs(P, B, True, True)
+        out["root"] = None
+        to = TreeOut(*(_ptr(out[k]) for k in ("digest", "size", "items", "root", "nodes")))
+        err = C.create_string_buffer(512)
+        rc = self.lib.mde_server_build_levels(self.s, C.byref(rec), C.byref(to), top_nodes, err, len(err))
+        if rc != MDE_OK:
+            raise MdeError(rc, err.value.decode(errors="replace"))
+        out["prefix_nodes"] = int(self.lib.mde_tree_prefix_nodes(B, top_nodes))
         return out
 
     def verify(self, n_buckets, digest, size, peer_objects, replica_count, epoch, partition=0, want_object=True):

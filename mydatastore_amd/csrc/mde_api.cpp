@@ -919,6 +919,17 @@ int mde_device_info(mde_ctx* c, int* cu_count, char* arch, int cap) {
 
 uint32_t mde_tree_depth(uint32_t B) { return B ? mde::tree_levels(B, nullptr) - 1 : 0; }
 uint64_t mde_tree_internal_nodes(uint32_t B) { return B ? mde::tree_internal(B) : 0; }
+uint64_t mde_tree_prefix_nodes(uint32_t B, uint32_t top_nodes) {
+  if (!B) return 0;
+  uint64_t t = 0;
+  uint32_t n = (B + 1) / 2;  // level 1 (the duplicate leaf of an odd B included)
+  const uint32_t stop = top_nodes ? top_nodes : 1u;
+  for (;;) {
+    t += n;
+    if (n <= stop) return t;
+    n = (n + 1) / 2;
+  }
+}
 uint64_t mde_diff_capacity(uint32_t a, uint32_t b) {
   if (!a || !b) return 0;
   uint32_t d = mde_tree_depth(a) < mde_tree_depth(b) ? mde_tree_depth(a) : mde_tree_depth(b);

@@ -116,6 +116,11 @@ struct TreeLaunch {
   // Fused build step, one partition per tree workgroup (Q = 0): LDS word of the split-schedule
   // K+W ring (tree_body_duo), 0 = plain tree_body. Set by the step launchers (plan_step_trees).
   uint32_t duo_kw_word = 0;
+  // tree_body / tree_body_duo: stop at the first level of at most top_nodes nodes (0: the root).
+  // nodes_out then holds levels 1 .. that level and root_out that level's first node; the caller
+  // hashes the few top levels itself (mde_server_build_levels: a one-partition call's dependent
+  // top levels, where a CPU core's SHA extensions beat the device's dependent chain).
+  uint32_t top_nodes = 0;
 };
 constexpr uint32_t kTreeLdsMaxBuckets = 4096;
 constexpr uint32_t kTreePairLdsMax = 64u * 1024u;  // standalone pair-shape trees (B <= 2,728)

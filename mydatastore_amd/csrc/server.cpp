@@ -455,9 +455,24 @@ int mde_server_stats(mde_server* s, uint64_t* requests, uint64_t* launches, uint
 
 uint32_t mde_server_slots(const mde_server* s) { return s ? s->n_slots : 0u; }
 
-int mde_server_build(mde_server* s, const mde_records* rec, const mde_tree_out* out, char* err, uint64_t err_cap) {
+}  // extern "C"
+
+namespace {
+
+// A build through the service; top_nodes > 0: the tree stops at the first level of at most
+// top_nodes nodes (mde_server_build_levels).
+int server_build(mde_server* s, const mde_records* rec, const mde_tree_out* out_in, uint32_t top_nodes, char* err,
+                 uint64_t err_cap) {
   put_msg(err, err_cap, "");
-  if (!s || !rec || !out) return failf(err, err_cap, MDE_E_INVAL, "null server, records or out");
+  if (!s || !rec || !out_in) return failf(err, err_cap, MDE_E_INVAL, "null server, records or out");
+  mde_tree_out levels_out;
+  uint8_t root_sink[32];
+  if (top_nodes) {  // levels: nodes required, root not written (a scratch root keeps the tree phase)
+    if (!out_in->nodes) return failf(err, err_cap, MDE_E_INVAL, "mde_server_build_levels needs out->nodes");
+    levels_out = *out_in;
+    levels_out.root = root_sink;
+  }
+  const mde_tree_out* out = top_nodes ? &levels_out : out_in;
   int rc = validate(rec, out, err, err_cap);
   if (rc) return rc;
   const uint32_t P = rec->n_partitions, B = rec->n_buckets;
@@ -483,10 +498,16 @@ int mde_server_build(mde_server* s, const mde_records* rec, const mde_tree_out* 
   const bool fits = B <= s->max_buckets && in_bytes <= s->in_cap && ol.total <= s->out_cap &&
                     mde::server_plan(P, B, s->lds, &G, &words, &duo);
   s->n_req.fetch_add(1, std::memory_order_relaxed);
-  if (!fits) {  // the service's context: the ordinary synchronous build
+  if (!fits) {  // the service's context: the ordinary synchronous build (a levels call gets every level)
     s->n_ctx.fetch_add(1, std::memory_order_relaxed);
+    std::vector<uint8_t> roots;
+    mde_tree_out o = *out;
+    if (top_nodes) {
+      roots.resize((uint64_t)P * 32);
+      o.root = roots.data();
+    }
     std::lock_guard<std::mutex> lk(s->ctx_m);
-    rc = mde_build(s->ctx, rec, out);
+    rc = mde_build(s->ctx, rec, &o);
     if (rc) put_msg(err, err_cap, mde_last_error(s->ctx));
     return rc;
   }
@@ -523,6 +544,7 @@ int mde_server_build(mde_server* s, const mde_records* rec, const mde_tree_out* 
   q.t.root_out = tree ? out_d + ol.root : nullptr;
   q.t.nodes_out = nodes ? out_d + ol.nodes : nullptr;
   q.t.n_int = mde::tree_internal(B);
+  q.t.top_nodes = top_nodes;
   q.kind = 0;
   q.G = G;
   q.words = words;
@@ -538,14 +560,31 @@ int mde_server_build(mde_server* s, const mde_records* rec, const mde_tree_out* 
     if (out->digest) std::memcpy(out->digest, out_h + ol.dig, S * 8);
     if (out->size) std::memcpy(out->size, out_h + ol.size, S * 4);
     if (out->items) std::memcpy(out->items, out_h + ol.items, (uint64_t)P * 4);
-    if (tree && out->root) std::memcpy(out->root, out_h + ol.root, (uint64_t)P * 32);
-    if (nodes) std::memcpy(out->nodes, out_h + ol.nodes, (uint64_t)P * q.t.n_int * 32);
+    if (tree && !top_nodes) std::memcpy(out->root, out_h + ol.root, (uint64_t)P * 32);
+    if (nodes) {
+      const uint64_t per = top_nodes ? mde_tree_prefix_nodes(B, top_nodes) : q.t.n_int;
+      for (uint32_t p = 0; p < P; p++)
+        std::memcpy(out->nodes + (uint64_t)p * q.t.n_int * 32, out_h + ol.nodes + (uint64_t)p * q.t.n_int * 32, per * 32);
+    }
     give_slot(s, i);
   } else {
     // the slot's workgroup may still write it: it stays out of the free list
     put_msg(err, err_cap, msg.c_str());
   }
   return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mde_server_build(mde_server* s, const mde_records* rec, const mde_tree_out* out, char* err, uint64_t err_cap) {
+  return server_build(s, rec, out, 0, err, err_cap);
+}
+
+int mde_server_build_levels(mde_server* s, const mde_records* rec, const mde_tree_out* out, uint32_t top_nodes,
+                            char* err, uint64_t err_cap) {
+  return server_build(s, rec, out, top_nodes ? top_nodes : 1u, err, err_cap);
 }
 
 int mde_server_verify(mde_server* s, uint32_t n_buckets, int32_t partition, int64_t epoch, const uint64_t* digest,

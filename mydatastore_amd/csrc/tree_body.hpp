@@ -143,10 +143,11 @@ __device__ __forceinline__ void tree_body(const TreeLaunch& a, uint32_t G, uint3
   uint64_t level_off = 0;  // node index of the current level's first node in node_base
   uint32_t* cur = buf0;
   uint32_t* nxt = kLds ? buf1 : (node_base ? node_base + (uint64_t)n1 * 8 : nullptr);
-  while (n_max > 1) {
+  const uint32_t stop = a.top_nodes ? a.top_nodes : 1u;  // uniform B when top_nodes is set
+  while (n_max > stop) {
     __syncthreads();
     n_max = (n_max + 1) / 2;
-    if (n <= 1) continue;  // this group's tree is complete
+    if (n <= stop) continue;  // this group's tree is complete
     const uint32_t m = (n + 1) / 2;
     if (live) {
       for (uint32_t j = tid; j < m; j += G) {
@@ -427,7 +428,8 @@ __device__ __forceinline__ void tree_body_duo(const TreeLaunch& a, uint32_t G, u
 
   uint32_t n = n1;
   uint64_t level_off = 0;
-  while (n > 1) {
+  const uint32_t stop = a.top_nodes ? a.top_nodes : 1u;
+  while (n > stop) {
     __syncthreads();
     const uint32_t m = (n + 1) / 2;
     if (wide && m > half) {  // a wide level: every thread hashes whole nodes

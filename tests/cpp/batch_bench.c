@@ -25,7 +25,10 @@
  *   server         mde_server_build (the resident build service: a persistent launch polling
  *                  request slots in pinned memory, no launch / copy / event per call) with the
  *                  nodes output, then the tree assembled from the node hashes;
- *   server_hosttree  mde_server_build digest-only, then NewTree on the host.
+ *   server_hosttree  mde_server_build digest-only, then NewTree on the host;
+ *   server_levels  mde_server_build_levels: digests and the tree's levels down to the first of at
+ *                  most 64 nodes on the device, the top levels hashed on the host (the shim's
+ *                  mdeTree finishing them with crypto/sha256).
  * VerifyEpoch decision step (main/manager.go:1072-1104; two peers, one agreeing, one differing):
  *   cpu_verify     per peer: EpochTreeObjectToMerkleTree (decode the 8-byte bucket hashes, NewTree)
  *                  and DifferentMerkleTreeBuckets against the local tree; validCount / diffSet fold;
@@ -67,6 +70,31 @@ const uint8_t* oracle_graph_root(const oracle_graph* g);
 int32_t oracle_graph_diff(const oracle_graph* a, const oracle_graph* b, int32_t* out, int32_t cap);
 void oracle_graph_free(oracle_graph* g);
 int oracle_sha_ni(void);
+void oracle_sha256(const uint8_t* msg, uint64_t len, uint8_t out[32]);
+
+/* The shim's top levels (mdeTree with mde_server_build_levels): levels above the first one of at
+ * most top nodes, hashed on the host, node = SHA256(left || right), an odd level's last node
+ * paired with itself -- merkletree v0.2.0's rule, on the CPU's SHA extensions like crypto/sha256. */
+static void finish_top_levels(uint32_t B, uint32_t top, uint8_t* nodes) {
+  uint32_t n = (B + 1) / 2;
+  uint64_t off = 0;
+  while (n > top && n > 1) { /* levels the device wrote */
+    off += n;
+    n = (n + 1) / 2;
+  }
+  while (n > 1) {
+    const uint32_t m = (n + 1) / 2;
+    uint8_t msg[64];
+    for (uint32_t j = 0; j < m; j++) {
+      const uint32_t l = 2 * j, r = 2 * j + 1 < n ? 2 * j + 1 : 2 * j;
+      memcpy(msg, nodes + (off + l) * 32, 32);
+      memcpy(msg + 32, nodes + (off + r) * 32, 32);
+      oracle_sha256(msg, 64, nodes + (off + n + j) * 32);
+    }
+    off += n;
+    n = m;
+  }
+}
 
 static double now_s(void) {
   struct timespec t;
@@ -98,6 +126,7 @@ enum {
   PERCALL,
   SERVER,
   SERVER_HOSTTREE,
+  SERVER_LEVELS,
   CPU_VERIFY,
   V_BATCHED,
   V_SERVER,
@@ -107,7 +136,7 @@ enum {
   N_CASES
 };
 static const char* kCases[] = {"cpu",          "shim",       "shim_hosttree",  "device_call", "percall",
-                               "server",       "server_hosttree", "cpu_verify", "verify_batched", "verify_server", "diff_host",
+                               "server",       "server_hosttree", "server_levels", "cpu_verify", "verify_batched", "verify_server", "diff_host",
                                "diff_device",  "diff_digests"};
 
 /* One partition-epoch of 8-byte timestamps, records spread evenly over B buckets; the oracle's
@@ -309,6 +338,15 @@ static int call(int mode, part_t* p) {
       oracle_graph_free(g);
       return 0;
     }
+    case SERVER_LEVELS: { /* device: digests + levels up to <= 64 nodes; host: the top levels */
+      mde_tree_out o = {p->dig, p->size, &p->items, NULL, p->nodes};
+      if ((rc = mde_server_build_levels(server, &r, &o, 64, err, sizeof err))) return rc;
+      finish_top_levels(B, 64, p->nodes);
+      oracle_graph* g = oracle_graph_from_nodes(p->dig, B, p->nodes);
+      check_tree(p, g, "server_levels");
+      oracle_graph_free(g);
+      return 0;
+    }
     case DEVICE_CALL: {
       mde_tree_out o = {p->dig, p->size, &p->items, p->root, NULL};
       if ((rc = mde_batch_build(batcher, &r, &o, err, sizeof err))) return rc;
@@ -442,7 +480,7 @@ static void run_case(int mode, int P, uint64_t n, uint32_t B, part_t* parts, int
          kCases[mode], P, n, B, total, wall, (double)total / wall, all[total / 2] * 1e6, all[total * 9 / 10] * 1e6);
   if ((mode == SHIM || mode == SHIM_HOSTTREE || mode == DEVICE_CALL || mode == V_BATCHED) && batches > 0)
     printf(", \"mean_requests_per_batch\": %.2f", (double)(r1 - r0) / batches);
-  if (mode == SERVER || mode == SERVER_HOSTTREE || mode == V_SERVER) printf(", \"server_calls_on_context\": %" PRIu64, sc1 - sc0);
+  if (mode == SERVER || mode == SERVER_HOSTTREE || mode == SERVER_LEVELS || mode == V_SERVER) printf(", \"server_calls_on_context\": %" PRIu64, sc1 - sc0);
   printf("}\n");
   fflush(stdout);
   free(all);
@@ -498,7 +536,7 @@ int main(int argc, char** argv) {
       for (int ni = 0; ni < 3; ni++) {
         part_t p;
         make_part(&p, ns[ni], Bs[bi], 1 + ni);
-        for (int mode = CPU; mode <= SERVER_HOSTTREE; mode++) run_case(mode, 1, ns[ni], Bs[bi], &p, 1);
+        for (int mode = CPU; mode <= SERVER_LEVELS; mode++) run_case(mode, 1, ns[ni], Bs[bi], &p, 1);
         free_part(&p);
       }
     const int Ps[3] = {1, 10, 100};

@@ -14,7 +14,8 @@
  * 8-byte timestamps (main/manager.go:816), variable-length values and variable offsets that
  * happen to be uniform (sent as a stride), records outside the bucket ranges, empty partitions,
  * two or three partitions in one call, full builds with and without inner nodes and digest-only
- * builds (root NULL); after every one-partition build, the VerifyEpoch decision step through the
+ * builds (root NULL), and the split tree (mde_server_build_levels, the device's levels up to the
+ * first of at most 1 / 2 / 16 / 64 / 300 nodes); after every one-partition build, the VerifyEpoch decision step through the
  * service (mde_server_verify) against mde_verify_epochs. With a short lifetime (third argument) the launch ends and relaunches many
  * times while calls are in flight; a final phase sleeps past the lifetime between calls. Prints
  * one JSON line; exit 0 iff every output matched.
@@ -208,6 +209,26 @@ static void one_call(int t, int k) {
   if (memcmp(i1, i2, P * 4) || memcmp(i1, i3, P * 4)) bad("items", t, k, P, B);
   if (shape < 2 && (memcmp(r1, r2, P * 32) || memcmp(r1, r3, P * 32))) bad("root", t, k, P, B);
   if (shape == 0 && (memcmp(n1, n2, P * NI * 32) || memcmp(n1, n3, P * NI * 32))) bad("nodes", t, k, P, B);
+  /* levels 1 .. the first of at most `top` nodes (mde_server_build_levels): that prefix of every
+   * partition's nodes equals the oracle's */
+  {
+    static const uint32_t tops[5] = {64, 1, 2, 16, 300};
+    const uint32_t top = tops[k % 5];
+    uint8_t* n4 = xmalloc(P * NI * 32);
+    uint64_t* d4 = xmalloc(S * 8);
+    int32_t* z4 = xmalloc(S * 4);
+    int32_t* i4 = xmalloc(P * 4);
+    mde_tree_out o4 = {d4, z4, i4, NULL, n4};
+    if ((rc = mde_server_build_levels(server, &rec, &o4, top, err, sizeof err))) {
+      fprintf(stderr, "mde_server_build_levels: %d %s\n", rc, err);
+      exit(1);
+    }
+    const uint64_t pre = mde_tree_prefix_nodes(B, top);
+    for (uint32_t p = 0; p < P; p++)
+      if (memcmp(n4 + (uint64_t)p * NI * 32, n3 + (uint64_t)p * NI * 32, pre * 32)) bad("levels", t, k, P, B);
+    if (memcmp(d4, d3, S * 8) || memcmp(z4, z3, S * 4) || memcmp(i4, i3, P * 4)) bad("levels digests", t, k, P, B);
+    free(n4), free(d4), free(z4), free(i4);
+  }
   if (P == 1) verify_call(t, k, B, d3, z3, &s);
   pthread_mutex_lock(&mu);
   checked++;

@@ -10,8 +10,10 @@
  *                       B bucket ranges and appends every value to ONE arena, record by record:
  *                       value_off grows by each value's length, seg_rec by the record count per
  *                       bucket, n_partitions = 1, value_stride = 0 (variable-length values); an
- *                       empty arena gets one padding byte. B > 256: -> mde_server_build (the
- *                       shim's mdeResident; mde_batch_build with "batcher" as argv[2]) with the
+ *                       empty arena gets one padding byte. B > 256: -> mde_server_build_levels
+ *                       (the shim's mdeResident: the device's levels down to <= 64 nodes, the
+ *                       levels above hashed by mdeTree; mde_batch_build with the whole tree when
+ *                       "batcher" is argv[2]) with the
  *                       nodes output, then the shim's mdeTree: the *merkletree.MerkleTree assembled
  *                       from the device's digests and node hashes (no host hashing; mirrored
  *                       below). B <= 256 (mdeHostTreeMaxBuckets): a digest-only mde_batch_build
@@ -46,6 +48,7 @@ void oracle_sha256(const uint8_t* msg, uint64_t len, uint8_t out[32]); /* checke
 /* stands in for merkletree.NewTree's hashing where the shim builds the tree on the host */
 int oracle_tree(const uint64_t* digest, uint32_t n_buckets, uint8_t* nodes, uint8_t* root);
 #define HOST_TREE_MAX_BUCKETS 256 /* merkle_gpu.go mdeHostTreeMaxBuckets */
+#define TOP_NODES 64              /* merkle_gpu.go mdeTopNodes */
 
 /* ---- the shim's mdeTree (integration/go/merkle_gpu.go), in C: merkletree v0.2.0's node graph
  * (leaf Hash = LE64(digest), a duplicate of the last leaf when B is odd -- same Hash, same
@@ -236,11 +239,36 @@ int main(int argc, char** argv) {
       uint8_t* nodes = xmalloc(mde_tree_internal_nodes(B) * 32);
       const int host_tree = B <= HOST_TREE_MAX_BUCKETS;
       mde_tree_out out = {digest, size, &items, host_tree ? NULL : root, host_tree ? NULL : nodes};
-      rc = resident ? mde_server_build(server, &rec, &out, err, sizeof err)
-                    : mde_batch_build(batcher, &rec, &out, err, sizeof err);
+      if (resident && !host_tree) { /* merkle_gpu.go: the device's levels down to <= mdeTopNodes */
+        out.root = NULL;
+        rc = mde_server_build_levels(server, &rec, &out, TOP_NODES, err, sizeof err);
+      } else {
+        rc = resident ? mde_server_build(server, &rec, &out, err, sizeof err)
+                      : mde_batch_build(batcher, &rec, &out, err, sizeof err);
+      }
       if (rc) {
         fprintf(stderr, "build: %d %s\n", rc, err);
         return 1;
+      }
+      if (resident && !host_tree) { /* mdeTree hashes the levels above the device's (crypto/sha256) */
+        uint32_t n = (B + 1) / 2;
+        uint64_t off = 0;
+        while (n > TOP_NODES && n > 1) {
+          off += n;
+          n = (n + 1) / 2;
+        }
+        while (n > 1) {
+          const uint32_t m = (n + 1) / 2;
+          uint8_t msg[64];
+          for (uint32_t j = 0; j < m; j++) {
+            const uint32_t l = 2 * j, rr = 2 * j + 1 < n ? 2 * j + 1 : 2 * j;
+            memcpy(msg, nodes + (off + l) * 32, 32);
+            memcpy(msg + 32, nodes + (off + rr) * 32, 32);
+            oracle_sha256(msg, 64, nodes + (off + n + j) * 32);
+          }
+          off += n;
+          n = m;
+        }
       }
       if (host_tree) oracle_tree(digest, B, nodes, root);
       stree t = mde_tree(digest, B, nodes);
@@ -258,7 +286,7 @@ int main(int argc, char** argv) {
       printf(" ; %u ", t.n_leafs);
       print_hex(wsig, 32);
       printf("\n");
-      if (memcmp(root, t.root->hash, 32)) {
+      if (!(resident && !host_tree) && memcmp(root, t.root->hash, 32)) { /* split levels: no device root */
         fprintf(stderr, "device root differs from the assembled tree's root\n");
         return 1;
       }

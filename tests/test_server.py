@@ -131,3 +131,44 @@ def test_server_python_decisions_match_oracle(coracle):
     sv.close()
     assert not errors, errors[:5]
     assert st["requests"] == 8 * 10 and st["on_context"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [64, 1000, 1023])
+def test_server_levels_plus_host_top_equals_oracle(coracle, B):
+    """The split tree (mde_server_build_levels): the device's levels down to the first of at most
+    64 nodes, the top levels hashed here with hashlib (node = SHA256(left || right), an odd level's
+    last node paired with itself, merkletree v0.2.0's rule); every node and the root equal the
+    oracle's tree."""
+    import hashlib
+    import mydatastore_amd as mde
+    rng = np.random.default_rng(B)
+    n = 3000
+    vals = rng.integers(1, 1 << 40, n, dtype=np.uint64).view(np.uint8).copy()
+    seg = np.concatenate([[0], np.sort(rng.integers(0, n + 1, B - 1)), [n]]).astype(np.uint64)
+    sv = mde.Server(0)
+    try:
+        got = sv.build_levels(vals, seg, 1, B, 64, value_stride=8)
+    finally:
+        sv.close()
+    exp = coracle.build(vals, seg, 1, B, 8)
+    nodes = got["nodes"].reshape(-1, 32).copy()
+    pre = got["prefix_nodes"]
+    assert np.array_equal(nodes[:pre], exp["nodes"].reshape(-1, 32)[:pre])
+    assert not nodes[pre:].any()
+    sizes, m = [], (B + 1) // 2  # level sizes, level 1 .. the root
+    while True:
+        sizes.append(m)
+        if m == 1:
+            break
+        m = (m + 1) // 2
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(int)
+    for k in range(1, len(sizes)):
+        if offs[k] < pre:
+            continue  # a level the device wrote (the prefix covers whole levels)
+        for j in range(sizes[k]):
+            left, right = 2 * j, min(2 * j + 1, sizes[k - 1] - 1)
+            msg = nodes[offs[k - 1] + left].tobytes() + nodes[offs[k - 1] + right].tobytes()
+            nodes[offs[k] + j] = np.frombuffer(hashlib.sha256(msg).digest(), np.uint8)
+    assert np.array_equal(nodes.reshape(-1), exp["nodes"]) and np.array_equal(nodes[-1], exp["root"])
+    assert np.array_equal(got["digest"], exp["digest"]) and np.array_equal(got["size"], exp["size"])
