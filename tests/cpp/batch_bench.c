@@ -165,6 +165,7 @@ typedef struct {
 static mde_ctx* ctx;
 static mde_batcher* batcher;
 static mde_server* server;
+static uint32_t g_top = 64; /* server_levels: MDE_TOP_NODES overrides (sweep) */
 static pthread_barrier_t bar;
 static double g_seconds = 0.4;
 static long g_bad = 0;
@@ -340,8 +341,8 @@ static int call(int mode, part_t* p) {
     }
     case SERVER_LEVELS: { /* device: digests + levels up to <= 64 nodes; host: the top levels */
       mde_tree_out o = {p->dig, p->size, &p->items, NULL, p->nodes};
-      if ((rc = mde_server_build_levels(server, &r, &o, 64, err, sizeof err))) return rc;
-      finish_top_levels(B, 64, p->nodes);
+      if ((rc = mde_server_build_levels(server, &r, &o, g_top, err, sizeof err))) return rc;
+      finish_top_levels(B, g_top, p->nodes);
       oracle_graph* g = oracle_graph_from_nodes(p->dig, B, p->nodes);
       check_tree(p, g, "server_levels");
       oracle_graph_free(g);
@@ -513,6 +514,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   /* MDE_BATCH_WAIT_US: the batcher's collection window (0 = none, the shim's setting) */
+  if (getenv("MDE_TOP_NODES")) g_top = (uint32_t)atoi(getenv("MDE_TOP_NODES"));
   const char* wait_env = getenv("MDE_BATCH_WAIT_US");
   const uint32_t wait_us = wait_env ? (uint32_t)atoi(wait_env) : 0u;
   if ((rc = mde_batcher_create(0, 256, wait_us, &batcher))) return 1;
