@@ -70,6 +70,23 @@ int failf(char* buf, uint64_t cap, int code, const char* fmt, ...) {
 
 uint64_t a16(uint64_t x) { return (x + 15) & ~15ull; }
 
+// Selects a device for the HIP calls of a scope and restores the calling thread's device after
+// (the service's calls run on its callers' threads, which may use other devices).
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) {
+      (void)hipGetLastError();
+      prev = -1;
+    }
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~DeviceScope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
 constexpr uint32_t kDefaultSlots = 16;
 constexpr uint32_t kMaxSlots = 256;
 constexpr uint64_t kDefaultInCap = 256ull << 10;
@@ -104,6 +121,10 @@ struct mde_server {
   std::vector<uint32_t> free_slots;
   std::vector<uint64_t> seq;  // per slot, owned by the caller holding the slot
   std::atomic<uint64_t> n_req{0}, n_launch{0}, n_ctx{0};
+  // a launch failed or a request timed out: every later call fails at once with this message
+  // (a slot whose request failed is never reused -- its workgroup may still write it)
+  std::atomic<bool> broken{false};
+  std::string broken_msg;
   mde_ctx* ctx = nullptr;  // requests the resident workgroups do not take
   std::mutex ctx_m;
 
@@ -199,7 +220,7 @@ int ensure_running(mde_server* s, std::string* msg) {
   }
   for (uint32_t i = 0; i < s->n_slots; i++) __atomic_store_n(&s->slot(i)->closed, 0u, __ATOMIC_RELAXED);
   __atomic_thread_fence(__ATOMIC_SEQ_CST);
-  (void)hipSetDevice(s->device);
+  DeviceScope ds(s->device);
   hipError_t e = mde::launch_server(reinterpret_cast<mde::ServerSlot*>(s->pin_dev), s->n_slots, s->lifetime_ticks,
                                     s->lds, s->stream);
   if (e == hipSuccess) e = hipEventRecord(s->exit_ev, s->stream);
@@ -260,12 +281,28 @@ int post_and_wait(mde_server* s, uint32_t i, std::string* msg) {
   }
 }
 
+// A free slot, or UINT32_MAX once the service is broken.
 uint32_t take_slot(mde_server* s) {
   std::unique_lock<std::mutex> lk(s->m);
-  s->cv.wait(lk, [&] { return !s->free_slots.empty(); });
+  s->cv.wait(lk, [&] { return !s->free_slots.empty() || s->broken.load(); });
+  if (s->broken.load()) return UINT32_MAX;
   const uint32_t i = s->free_slots.back();
   s->free_slots.pop_back();
   return i;
+}
+
+void mark_broken(mde_server* s, const std::string& msg) {
+  {
+    std::lock_guard<std::mutex> lk(s->m);
+    if (!s->broken.load()) s->broken_msg = msg;
+    s->broken.store(true);
+  }
+  s->cv.notify_all();
+}
+
+int broken_error(mde_server* s, char* err, uint64_t cap) {
+  std::lock_guard<std::mutex> lk(s->m);
+  return failf(err, cap, MDE_E_DEVICE, "resident build service unusable: %s", s->broken_msg.c_str());
 }
 
 void give_slot(mde_server* s, uint32_t i) {
@@ -312,7 +349,7 @@ int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_se
     mde_server_destroy(s);
     return code;
   };
-  (void)hipSetDevice(device);
+  DeviceScope ds(device);
   s->lds = mde::server_lds_bytes(s->max_buckets);
   uint32_t G, words, duo;
   if (!s->lds || !mde::server_plan(1, s->max_buckets, s->lds, &G, &words, &duo)) return bail(MDE_E_INVAL);
@@ -393,7 +430,7 @@ int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_se
 
 void mde_server_destroy(mde_server* s) {
   if (!s) return;
-  (void)hipSetDevice(s->device);
+  DeviceScope ds(s->device);
   if (s->pin) {
     for (uint32_t i = 0; i < s->n_slots; i++) __atomic_store_n(&s->slot(i)->req, mde::kServerStop, __ATOMIC_RELEASE);
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
@@ -512,6 +549,7 @@ int server_build(mde_server* s, const mde_records* rec, const mde_tree_out* out_
     return rc;
   }
   const uint32_t i = take_slot(s);
+  if (i == UINT32_MAX) return broken_error(s, err, err_cap);
   uint8_t* in_h = s->pin + s->in_off(i);
   const uint64_t in_d_pin = reinterpret_cast<uint64_t>(s->pin_dev + s->in_off(i));
   uint8_t* out_h = s->pin + s->out_off(i);
@@ -570,6 +608,7 @@ int server_build(mde_server* s, const mde_records* rec, const mde_tree_out* out_
   } else {
     // the slot's workgroup may still write it: it stays out of the free list
     put_msg(err, err_cap, msg.c_str());
+    mark_broken(s, msg);
   }
   return rc;
 }
@@ -630,6 +669,7 @@ int mde_server_verify(mde_server* s, uint32_t n_buckets, int32_t partition, int6
     return rc;
   }
   const uint32_t i = take_slot(s);
+  if (i == UINT32_MAX) return broken_error(s, err, err_cap);
   uint8_t* in_h = s->pin + s->in_off(i);
   const uint8_t* in_pin_d = s->pin_dev + s->in_off(i);
   uint8_t* out_h = s->pin + s->out_off(i);
@@ -705,7 +745,8 @@ int mde_server_verify(mde_server* s, uint32_t n_buckets, int32_t partition, int6
     }
     give_slot(s, i);
   } else {
-    put_msg(err, err_cap, msg.c_str());
+    put_msg(err, err_cap, msg.c_str());  // the slot stays out of the free list (see above)
+    mark_broken(s, msg);
   }
   return rc;
 }
