@@ -172,3 +172,27 @@ def test_server_levels_plus_host_top_equals_oracle(coracle, B):
             nodes[offs[k] + j] = np.frombuffer(hashlib.sha256(msg).digest(), np.uint8)
     assert np.array_equal(nodes.reshape(-1), exp["nodes"]) and np.array_equal(nodes[-1], exp["root"])
     assert np.array_equal(got["digest"], exp["digest"]) and np.array_equal(got["size"], exp["size"])
+
+
+def test_tree_prefix_nodes_matches_level_walk():
+    """CPU: mde_tree_prefix_nodes (what mde_server_build_levels writes per partition) is the node
+    count of levels 1 .. the first level of at most top_nodes nodes, merkletree v0.2.0's level
+    sizes (level 1 = ceil(B / 2), the odd duplicate leaf included; each next level ceil(n / 2));
+    top <= 1 gives every level (mde_tree_internal_nodes)."""
+    import ctypes
+    lib = ctypes.CDLL(str(ROOT / "mydatastore_amd" / "libmde.so"))
+    lib.mde_tree_prefix_nodes.restype = ctypes.c_uint64
+    lib.mde_tree_prefix_nodes.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    lib.mde_tree_internal_nodes.restype = ctypes.c_uint64
+    lib.mde_tree_internal_nodes.argtypes = [ctypes.c_uint32]
+    for B in list(range(1, 300)) + [511, 512, 513, 1000, 1023, 1024, 4096, 65536]:
+        for top in (0, 1, 2, 3, 16, 63, 64, 65, 300, 100000):
+            t, n = 0, (B + 1) // 2
+            stop = max(top, 1)
+            while True:
+                t += n
+                if n <= stop:
+                    break
+                n = (n + 1) // 2
+            assert lib.mde_tree_prefix_nodes(B, top) == t, (B, top)
+        assert lib.mde_tree_prefix_nodes(B, 0) == lib.mde_tree_internal_nodes(B)
