@@ -613,7 +613,7 @@ int pipeline_drain(mde_ctx* c) {
 int attach_top(mde_ctx* c, mde::TreeLaunch* t) {
   static const int group = [] {
     const char* e = std::getenv("MDE_STEP_TOP_GROUP");
-    return e ? std::atoi(e) : 4;
+    return e ? std::atoi(e) : 0;  // off until measured on the GPU
   }();
   if (group <= 0 || !t->P) return MDE_OK;
   int rc = ensure_buf(c, c->top_scratch, (uint64_t)t->P * mde::kStepTopNodes * 32);
