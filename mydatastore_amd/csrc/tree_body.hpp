@@ -36,6 +36,18 @@ __device__ __forceinline__ void store_half_node(uint32_t* dst, const uint32_t v[
   reinterpret_cast<u32x4*>(dst)[is_a ? 0 : 1] = u32x4{bswap(v[0]), bswap(v[1]), bswap(v[2]), bswap(v[3])};
 }
 
+// The group pass's exchange (TreeLaunch::top_out) crosses XCDs, whose L2s are not coherent with
+// each other: agent-scope relaxed stores and loads (sc1: written through to, and read from, the
+// device-coherent level), ordered by a wait for the stores' completion before the arrival atomic --
+// no L2 writeback or invalidate (a device-scope fence per tree flushed and invalidated the whole
+// L2 under the streaming digest: the production step 165 -> 342 us, profiles/r04/r04v_*).
+__device__ __forceinline__ void top_store(uint8_t* base, uint64_t word, uint32_t v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(base) + word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t top_load(const uint8_t* base, uint64_t word) {
+  return __hip_atomic_load(reinterpret_cast<const uint32_t*>(base) + word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Leaf b of partition p: digest, and (when building from byte sums) its size/digest outputs.
 __device__ __forceinline__ uint64_t tree_leaf(const TreeLaunch& a, uint64_t s, uint32_t& items, uint32_t& sz_out) {
   uint64_t v;
@@ -175,7 +187,7 @@ __device__ __forceinline__ void tree_body(const TreeLaunch& a, uint32_t G, uint3
     if (tid == 0 && a.items_out) a.items_out[p] = (int32_t)counter[0];
     if (a.top_out)  // the level the tree stopped at, for the fused step's group pass
       for (uint32_t w = tid; w < n * 8u; w += G)
-        reinterpret_cast<uint32_t*>(a.top_out)[(uint64_t)p * kStepTopNodes * 8u + w] = cur[w];
+        top_store(a.top_out, (uint64_t)p * kStepTopNodes * 8u + w, cur[w]);
   }
 }
 
@@ -487,7 +499,7 @@ __device__ __forceinline__ void tree_body_duo(const TreeLaunch& a, uint32_t G, u
   }
   if (live && a.top_out)  // the level the tree stopped at, for the fused step's group pass
     for (uint32_t w = x; w < n * 8u; w += 2u * half)
-      reinterpret_cast<uint32_t*>(a.top_out)[(uint64_t)p * kStepTopNodes * 8u + w] = cur[w];
+      top_store(a.top_out, (uint64_t)p * kStepTopNodes * 8u + w, cur[w]);
 }
 
 // LDS words of one tree_body group for B buckets (counter slot + the two level buffers).
@@ -509,14 +521,15 @@ __device__ __forceinline__ void step_group_top(const TreeLaunch& t, uint32_t p, 
   constexpr uint32_t kT = kStepTreeWideThreads;
   const uint32_t T = t.top_group;
   const uint32_t g = p / T, p0 = g * T, members = min(T, t.P - p0);
-  __threadfence();  // this tree's top_out (and node / root / digest outputs) before its arrival
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's top_out stores have completed
   __syncthreads();
-  if (x == 0) lds[0] = atomicAdd(t.top_count + g, 1u) == members - 1u ? 1u : 0u;
+  if (x == 0)
+    lds[0] = __hip_atomic_fetch_add(t.top_count + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1u
+                 ? 1u : 0u;
   __syncthreads();
   if (!lds[0]) return;  // not the last of its group (uniform)
-  __threadfence();  // acquire the group's other trees' top_out
   __syncthreads();  // lds[0] read by every thread before the levels overwrite it
-  if (x == 0) t.top_count[g] = 0u;  // the next launch of this context (stream-ordered)
+  if (x == 0) __hip_atomic_store(t.top_count + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
   // the level the trees stopped at: its size n0 and node index off0 (uniform B)
   uint32_t n0 = (t.B + 1u) / 2u, off0 = 0;
   while (n0 > kStepTopNodes) {
@@ -526,10 +539,9 @@ __device__ __forceinline__ void step_group_top(const TreeLaunch& t, uint32_t p, 
   // group levels in LDS: cur = members x n nodes, nxt = members x ceil(n / 2) (compact per level)
   uint32_t* cur = lds;
   uint32_t* nxt = lds + members * kStepTopNodes * 8u;
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(t.top_out) + (uint64_t)p0 * kStepTopNodes * 8u;
   for (uint32_t i = x; i < members * n0 * 8u; i += kT) {
     const uint32_t q = i / (n0 * 8u), w = i % (n0 * 8u);
-    cur[i] = __builtin_nontemporal_load(src + (uint64_t)q * kStepTopNodes * 8u + w);
+    cur[i] = top_load(t.top_out, (uint64_t)(p0 + q) * kStepTopNodes * 8u + w);
   }
   __syncthreads();
   uint32_t n = n0, off = off0;
