@@ -37,15 +37,11 @@ __device__ __forceinline__ void store_half_node(uint32_t* dst, const uint32_t v[
 }
 
 // The group pass's exchange (TreeLaunch::top_out) crosses XCDs, whose L2s are not coherent with
-// each other: agent-scope relaxed stores and loads (sc1: written through to, and read from, the
-// device-coherent level), ordered by a wait for the stores' completion before the arrival atomic --
-// no L2 writeback or invalidate (a device-scope fence per tree flushed and invalidated the whole
-// L2 under the streaming digest: the production step 165 -> 342 us, profiles/r04/r04v_*).
+// each other: write-through (sc1, agent-scope relaxed) stores, so the producer needs no L2
+// writeback (a __threadfence() per tree wrote back and invalidated under the streaming digest: the
+// production step 165 -> 342 us, profiles/r04/r04v_*); the consumer acquires once (step_group_top).
 __device__ __forceinline__ void top_store(uint8_t* base, uint64_t word, uint32_t v) {
   __hip_atomic_store(reinterpret_cast<uint32_t*>(base) + word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t top_load(const uint8_t* base, uint64_t word) {
-  return __hip_atomic_load(reinterpret_cast<const uint32_t*>(base) + word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Leaf b of partition p: digest, and (when building from byte sums) its size/digest outputs.
@@ -521,11 +517,20 @@ __device__ __forceinline__ void step_group_top(const TreeLaunch& t, uint32_t p, 
   constexpr uint32_t kT = kStepTreeWideThreads;
   const uint32_t T = t.top_group;
   const uint32_t g = p / T, p0 = g * T, members = min(T, t.P - p0);
+  // publish (cdna_hip_programming.md section 6, Guideline 16, counter form): the sc1 stores
+  // complete, then one relaxed agent-scope ticket; the last arriver acquires at agent scope once
+  // (lane 0) before its plain loads of the group's levels
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's top_out stores have completed
   __syncthreads();
-  if (x == 0)
-    lds[0] = __hip_atomic_fetch_add(t.top_count + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1u
-                 ? 1u : 0u;
+  if (x == 0) {
+    const bool last =
+        __hip_atomic_fetch_add(t.top_count + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds[0] = last ? 1u : 0u;
+  }
   __syncthreads();
   if (!lds[0]) return;  // not the last of its group (uniform)
   __syncthreads();  // lds[0] read by every thread before the levels overwrite it
@@ -541,7 +546,7 @@ __device__ __forceinline__ void step_group_top(const TreeLaunch& t, uint32_t p, 
   uint32_t* nxt = lds + members * kStepTopNodes * 8u;
   for (uint32_t i = x; i < members * n0 * 8u; i += kT) {
     const uint32_t q = i / (n0 * 8u), w = i % (n0 * 8u);
-    cur[i] = top_load(t.top_out, (uint64_t)(p0 + q) * kStepTopNodes * 8u + w);
+    cur[i] = reinterpret_cast<const uint32_t*>(t.top_out)[(uint64_t)(p0 + q) * kStepTopNodes * 8u + w];
   }
   __syncthreads();
   uint32_t n = n0, off = off0;
