@@ -37,11 +37,12 @@ __device__ __forceinline__ void store_half_node(uint32_t* dst, const uint32_t v[
 }
 
 // The group pass's exchange (TreeLaunch::top_out) crosses XCDs, whose L2s are not coherent with
-// each other: write-through (sc1, agent-scope relaxed) stores, so the producer needs no L2
-// writeback (a __threadfence() per tree wrote back and invalidated under the streaming digest: the
-// production step 165 -> 342 us, profiles/r04/r04v_*); the consumer acquires once (step_group_top).
+// each other: plain stores, published by one agent-scope release per tree (lane 0, step_group_top)
+// -- the counter form of cdna_hip_programming.md section 6 Guideline 16. (Rejected, r04v-r04x: a
+// __threadfence() in every thread -- the production step 165 -> 342 us; sc1 stores with sc1 loads,
+// or with an acquire and plain loads, read stale levels.)
 __device__ __forceinline__ void top_store(uint8_t* base, uint64_t word, uint32_t v) {
-  __hip_atomic_store(reinterpret_cast<uint32_t*>(base) + word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  reinterpret_cast<uint32_t*>(base)[word] = v;
 }
 
 // Leaf b of partition p: digest, and (when building from byte sums) its size/digest outputs.
@@ -517,12 +518,14 @@ __device__ __forceinline__ void step_group_top(const TreeLaunch& t, uint32_t p, 
   constexpr uint32_t kT = kStepTreeWideThreads;
   const uint32_t T = t.top_group;
   const uint32_t g = p / T, p0 = g * T, members = min(T, t.P - p0);
-  // publish (cdna_hip_programming.md section 6, Guideline 16, counter form): the sc1 stores
-  // complete, then one relaxed agent-scope ticket; the last arriver acquires at agent scope once
-  // (lane 0) before its plain loads of the group's levels
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's top_out stores have completed
+  // publish (cdna_hip_programming.md section 6, Guideline 16, counter form): every wave's stores
+  // complete, lane 0 releases at agent scope and draws a relaxed ticket; the last arriver acquires
+  // at agent scope once (lane 0) before its plain loads of the group's levels
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: the fence's own wait may be dropped
     const bool last =
         __hip_atomic_fetch_add(t.top_count + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1u;
     if (last) {
