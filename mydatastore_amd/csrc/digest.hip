@@ -1472,7 +1472,6 @@ hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStre
   if (tree_blocks + digest_blocks == 0) return hipSuccess;
   TreeLaunch tl = t ? *t : TreeLaunch{};
   tl.duo_kw_word = kw_word;
-  if (Q != 0 || !tl.top_out || !tl.top_count) tl.top_group = 0;  // the group pass: wide trees only
   hipLaunchKernelGGL(variant(a.variant).step, dim3(tree_blocks + digest_blocks), dim3(kThreads), lds, st, a, tl,
                      tree_blocks, Q);
   return hipGetLastError();

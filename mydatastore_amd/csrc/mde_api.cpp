@@ -70,8 +70,6 @@ struct mde_ctx {
   Buf packed_in, packed_out, pin_in, pin_out;
   Buf extract_scratch;
   Buf verify_scratch;
-  Buf top_scratch;  // fused steps' group pass: [P][kStepTopNodes] nodes
-  Buf top_counts;   // ... and one arrival counter per group (zero between launches)
   Buf deep_scratch;  // spill area of deeply nested unknown groups (WireDecodeLaunch::deep)
   bool verify_chain = false;  // mde_set_verify_mode(1): the five-launch chain even when fusable
   // Host-ingest ring (mde_build_streamed): two slots of values / value_off / seg_rec.
@@ -606,28 +604,6 @@ int pipeline_drain(mde_ctx* c) {
   return MDE_OK;
 }
 
-// Scratch of the fused step's group pass over the trees' top levels (TreeLaunch::top_group; the
-// launcher uses it for wide trees only): the level each tree stops at, and one arrival counter per
-// group, zero between launches (zeroed here when the buffer is (re)allocated, reset in-kernel by
-// each group's last tree). MDE_STEP_TOP_GROUP=0 turns the pass off (A/B).
-int attach_top(mde_ctx* c, mde::TreeLaunch* t) {
-  static const int group = [] {
-    const char* e = std::getenv("MDE_STEP_TOP_GROUP");
-    return e ? std::atoi(e) : 0;  // off until measured on the GPU
-  }();
-  if (group <= 0 || !t->P) return MDE_OK;
-  int rc = ensure_buf(c, c->top_scratch, (uint64_t)t->P * mde::kStepTopNodes * 32);
-  if (rc) return rc;
-  if (c->top_counts.cap < (uint64_t)t->P * 4) {
-    if ((rc = ensure_buf(c, c->top_counts, (uint64_t)t->P * 4))) return rc;
-    MDE_HIP(c, hipMemsetAsync(c->top_counts.p, 0, c->top_counts.cap, c->stream));
-  }
-  t->top_out = static_cast<uint8_t*>(c->top_scratch.p);
-  t->top_count = static_cast<uint32_t*>(c->top_counts.p);
-  t->top_group = (uint32_t)group;
-  return MDE_OK;
-}
-
 // One pipelined build: digest `r` into the free slot and, in the same launch, build the trees of
 // the pending build; `r` becomes the pending build. Layout B and B too wide for the fused step's
 // LDS budget run as separate launches on the same stream (same results, no overlap).
@@ -683,7 +659,6 @@ int build_pipelined(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
       mde_ctx::Slot& ps = c->pipe[pd.slot];
       rc = tree_launch_for(c, &pd.rec, &pd.out, ps.sums, ps.counts, &t);
       if (rc) return rc;
-      if ((rc = attach_top(c, &t))) return rc;
     }
     hipError_t e = mde::launch_build_step(a, pd.active ? &t : nullptr, c->stream);
     if (e != hipSuccess) {
@@ -851,8 +826,6 @@ void mde_destroy(mde_ctx* c) {
     if (c->pin_out.p) (void)hipHostFree(c->pin_out.p);
     if (c->extract_scratch.p) (void)hipFree(c->extract_scratch.p);
     if (c->verify_scratch.p) (void)hipFree(c->verify_scratch.p);
-    if (c->top_scratch.p) (void)hipFree(c->top_scratch.p);
-    if (c->top_counts.p) (void)hipFree(c->top_counts.p);
     if (c->deep_scratch.p) (void)hipFree(c->deep_scratch.p);
     for (int i = 0; i < 2; i++) {
       for (auto* b : {&c->ring_vals[i], &c->ring_voff[i], &c->ring_seg[i]})

@@ -121,17 +121,7 @@ struct TreeLaunch {
   // hashes the few top levels itself (mde_server_build_levels: a one-partition call's dependent
   // top levels, where a CPU core's SHA extensions beat the device's dependent chain).
   uint32_t top_nodes = 0;
-  // Fused build step, wide trees (Q = 0): each tree stops at its first level of <= kStepTopNodes
-  // nodes and copies that level to top_out ([P][kStepTopNodes] nodes); the last tree of every
-  // group of top_group partitions to get there (top_count[P / top_group], zero between launches,
-  // reset by that last tree) hashes the group's top levels together, with every lane busy -- a
-  // tree's levels of <= 64 nodes leave most of its two waves idle yet cost them a full
-  // instruction stream per level (digest.hip step_group_top). 0 = off.
-  uint8_t* top_out = nullptr;
-  uint32_t* top_count = nullptr;
-  uint32_t top_group = 0;
 };
-constexpr uint32_t kStepTopNodes = 64;
 constexpr uint32_t kTreeLdsMaxBuckets = 4096;
 constexpr uint32_t kTreePairLdsMax = 64u * 1024u;  // standalone pair-shape trees (B <= 2,728)
 constexpr uint32_t kTreePairMinPartitions = 512;

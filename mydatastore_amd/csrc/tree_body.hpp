@@ -36,15 +36,6 @@ __device__ __forceinline__ void store_half_node(uint32_t* dst, const uint32_t v[
   reinterpret_cast<u32x4*>(dst)[is_a ? 0 : 1] = u32x4{bswap(v[0]), bswap(v[1]), bswap(v[2]), bswap(v[3])};
 }
 
-// The group pass's exchange (TreeLaunch::top_out) crosses XCDs, whose L2s are not coherent with
-// each other: plain stores, published by one agent-scope release per tree (lane 0, step_group_top)
-// -- the counter form of cdna_hip_programming.md section 6 Guideline 16. (Rejected, r04v-r04x: a
-// __threadfence() in every thread -- the production step 165 -> 342 us; sc1 stores with sc1 loads,
-// or with an acquire and plain loads, read stale levels.)
-__device__ __forceinline__ void top_store(uint8_t* base, uint64_t word, uint32_t v) {
-  reinterpret_cast<uint32_t*>(base)[word] = v;
-}
-
 // Leaf b of partition p: digest, and (when building from byte sums) its size/digest outputs.
 __device__ __forceinline__ uint64_t tree_leaf(const TreeLaunch& a, uint64_t s, uint32_t& items, uint32_t& sz_out) {
   uint64_t v;
@@ -182,9 +173,6 @@ __device__ __forceinline__ void tree_body(const TreeLaunch& a, uint32_t G, uint3
   if (live) {
     if (tid < 8) reinterpret_cast<uint32_t*>(a.root_out + (uint64_t)p * 32)[tid] = cur[tid];
     if (tid == 0 && a.items_out) a.items_out[p] = (int32_t)counter[0];
-    if (a.top_out)  // the level the tree stopped at, for the fused step's group pass
-      for (uint32_t w = tid; w < n * 8u; w += G)
-        top_store(a.top_out, (uint64_t)p * kStepTopNodes * 8u + w, cur[w]);
   }
 }
 
@@ -494,9 +482,6 @@ __device__ __forceinline__ void tree_body_duo(const TreeLaunch& a, uint32_t G, u
     if (tid < 8) reinterpret_cast<uint32_t*>(a.root_out + (uint64_t)p * 32)[tid] = cur[tid];
     if (tid == 0 && a.items_out) a.items_out[p] = (int32_t)counter[0];
   }
-  if (live && a.top_out)  // the level the tree stopped at, for the fused step's group pass
-    for (uint32_t w = x; w < n * 8u; w += 2u * half)
-      top_store(a.top_out, (uint64_t)p * kStepTopNodes * 8u + w, cur[w]);
 }
 
 // LDS words of one tree_body group for B buckets (counter slot + the two level buffers).
@@ -508,75 +493,6 @@ __host__ __device__ inline uint32_t tree_lds_words(uint32_t B) {
 // A tree workgroup of a fused build step (plan_step_trees): Q > 0 -> its first wave builds Q
 // partitions (tree_body_packed); Q == 0 -> its first kStepTreeWideThreads threads (two waves)
 // build one partition (tree_body; the other waves leave at once).
-// The group pass of the fused step's wide trees (TreeLaunch::top_group): called by every tree after
-// its body (levels down to the first of <= kStepTopNodes nodes, copied to top_out); the group's
-// last tree to arrive hashes the top levels of all its trees level by level over its 128 threads
-// (at B = 1,000: levels of 32, 16, ..., 1 nodes per tree, 4 trees in 6 passes where each tree
-// alone took 6 passes of two mostly idle waves). Leaves LDS free for its own use: the body is done.
-__device__ __forceinline__ void step_group_top(const TreeLaunch& t, uint32_t p, uint32_t* lds) {
-  const uint32_t x = threadIdx.x;  // < kStepTreeWideThreads
-  constexpr uint32_t kT = kStepTreeWideThreads;
-  const uint32_t T = t.top_group;
-  const uint32_t g = p / T, p0 = g * T, members = min(T, t.P - p0);
-  // publish (cdna_hip_programming.md section 6, Guideline 16, counter form): every wave's stores
-  // complete, lane 0 releases at agent scope and draws a relaxed ticket; the last arriver acquires
-  // at agent scope once (lane 0) before its plain loads of the group's levels
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: the fence's own wait may be dropped
-    const bool last =
-        __hip_atomic_fetch_add(t.top_count + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1u;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    lds[0] = last ? 1u : 0u;
-  }
-  __syncthreads();
-  if (!lds[0]) return;  // not the last of its group (uniform)
-  __syncthreads();  // lds[0] read by every thread before the levels overwrite it
-  if (x == 0) __hip_atomic_store(t.top_count + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-  // the level the trees stopped at: its size n0 and node index off0 (uniform B)
-  uint32_t n0 = (t.B + 1u) / 2u, off0 = 0;
-  while (n0 > kStepTopNodes) {
-    off0 += n0;
-    n0 = (n0 + 1u) / 2u;
-  }
-  // group levels in LDS: cur = members x n nodes, nxt = members x ceil(n / 2) (compact per level)
-  uint32_t* cur = lds;
-  uint32_t* nxt = lds + members * kStepTopNodes * 8u;
-  for (uint32_t i = x; i < members * n0 * 8u; i += kT) {
-    const uint32_t q = i / (n0 * 8u), w = i % (n0 * 8u);
-    cur[i] = reinterpret_cast<const uint32_t*>(t.top_out)[(uint64_t)(p0 + q) * kStepTopNodes * 8u + w];
-  }
-  __syncthreads();
-  uint32_t n = n0, off = off0;
-  while (n > 1) {
-    const uint32_t m = (n + 1u) / 2u;
-    for (uint32_t i = x; i < members * m; i += kT) {
-      const uint32_t q = i / m, j = i % m;
-      const uint32_t l = 2u * j, r = (2u * j + 1u < n) ? 2u * j + 1u : 2u * j;
-      uint32_t hl[8], hr[8], st[8];
-      load_node(cur + (q * n + l) * 8u, hl);
-      load_node(cur + (q * n + r) * 8u, hr);
-      sha256_node_pair(hl, hr, st);
-      store_node(nxt + (q * m + j) * 8u, st);
-      if (t.nodes_out)
-        store_node(reinterpret_cast<uint32_t*>(t.nodes_out + ((uint64_t)(p0 + q) * t.n_int + off + n + j) * 32u), st);
-    }
-    __syncthreads();
-    uint32_t* tmp = cur;
-    cur = nxt;
-    nxt = tmp;
-    off += n;
-    n = m;
-  }
-  for (uint32_t i = x; i < members * 8u; i += kT)
-    reinterpret_cast<uint32_t*>(t.root_out + (uint64_t)(p0 + i / 8u) * 32u)[i % 8u] = cur[i];
-}
-
 __device__ __forceinline__ void step_trees(const TreeLaunch& t, uint32_t Q, uint32_t block, uint32_t* lds) {
   if (Q)
     tree_body_packed(t, Q, block, lds);
@@ -584,16 +500,11 @@ __device__ __forceinline__ void step_trees(const TreeLaunch& t, uint32_t Q, uint
 #ifdef MDE_STEP_WIDE_PRIO  // probe only: wide-tree waves at this priority beside the stream
     __builtin_amdgcn_s_setprio(MDE_STEP_WIDE_PRIO);
 #endif
-    if (threadIdx.x >= kStepTreeWideThreads) return;  // two waves per tree; the others leave now
-    TreeLaunch tt = t;
-    if (t.top_group) tt.top_nodes = kStepTopNodes;
-    else tt.top_out = nullptr;
     if (t.duo_kw_word)  // the second wave computes the first's message schedules on its <= 64-node levels
-      tree_body_duo(tt, kStepTreeWideThreads, tree_lds_words(t.B), block, lds, kStepTreeWideThreads / 2,
+      tree_body_duo(t, kStepTreeWideThreads, tree_lds_words(t.B), block, lds, kStepTreeWideThreads / 2,
                     reinterpret_cast<u32x4*>(lds + t.duo_kw_word));
     else
-      tree_body<true>(tt, kStepTreeWideThreads, tree_lds_words(t.B), block, lds, kStepTreeWideThreads);
-    if (t.top_group) step_group_top(t, block, lds);
+      tree_body<true>(t, kStepTreeWideThreads, tree_lds_words(t.B), block, lds, kStepTreeWideThreads);
   }
 }
 

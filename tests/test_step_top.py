@@ -1,11 +1,10 @@
-"""GPU parity of the fused build step's group pass over the wide trees' top levels (digest.hip
-step_group_top, TreeLaunch::top_group): with at least 512 partitions of more than 128 buckets the
-step's trees stop at their first level of <= 64 nodes and the last tree of every group of four to
-get there hashes the group's top levels. Every digest, size, item count, internal node and root of
-every partition must equal the C oracle's NewTree (cbergoon/merkletree v0.2.0 as restated in
-oracle/), across runs of pipelined builds (the per-group arrival counters must return to zero
-between launches), partition counts that leave a ragged last group, odd bucket counts and builds
-without the nodes output."""
+"""GPU parity of the fused build step's wide trees (plan_step_trees Q = 0: at least 512 partitions
+of more than 128 buckets, two waves per tree beside the streaming digest), the production shape's
+tree form: every digest, size, item count, internal node and root of every partition must equal the
+C oracle's NewTree (cbergoon/merkletree v0.2.0 as restated in oracle/), across runs of pipelined
+builds alternating two arenas, partition counts that are not multiples of any grouping, odd bucket
+counts and a build without the nodes output. (Written for a grouped pass over the trees' top levels,
+measured and rejected in round 4: profiles/r04/r04y_group_top_rejected.txt)"""
 import numpy as np
 import pytest
 
@@ -25,7 +24,7 @@ def _arena(P, B, seed, per_bucket=2):
 
 
 @pytest.mark.parametrize("P,B", [(512, 1000), (515, 1000), (1027, 1000), (600, 999), (520, 130)])
-def test_fused_step_group_top_matches_oracle(engine, coracle, P, B):
+def test_fused_step_wide_trees_match_oracle(engine, coracle, P, B):
     import torch
     import mydatastore_amd as mde
     dev = torch.device("cuda:0")
@@ -49,8 +48,8 @@ def test_fused_step_group_top_matches_oracle(engine, coracle, P, B):
                            for k in ("digest", "size", "items", "root", "nodes")))
         return o, to
 
-    # a run of five builds alternating the two arenas: build i's trees (and group pass) run inside
-    # build i+1's launch; build 3 without the nodes output
+    # a run of five builds alternating the two arenas: build i's trees run inside build i+1's
+    # launch; build 3 without the nodes output
     run = [(k % 2, k != 3) for k in range(5)]
     results = []
     for a, with_nodes in run:
