@@ -58,10 +58,11 @@ var (
 
 // mdeHostTreeMaxBuckets: at most this many buckets, the tree is NewTree's on the host over a
 // digest-only device build. A tree is a chain of dependent SHA-256 compressions: the CPU's SHA
-// extensions (which crypto/sha256 uses on amd64) run it in ~5 us at B = 64, the device in ~25 us
-// of one workgroup; at B = 1,000 the device's wide levels win, 45 vs ~80 us
-// (profiles/r04/*batch_bench*: shim_hosttree vs shim, INTEGRATION.md section 3).
-const mdeHostTreeMaxBuckets = 256
+// extensions (which crypto/sha256 uses on amd64) run B = 64's 94 compressions in ~5 us, while the
+// device's share of the split tree (mde_server_build_levels) only starts paying above that:
+// 16.9 vs 18.4 us per call at B = 64, equal at 96, 26.0 vs 22.7 at 128, 27.8 vs 35.8 at 256 and
+// 48 vs 109 at 1,000 (profiles/r04/r04thr_hosttree_vs_levels.jsonl, INTEGRATION.md section 3).
+const mdeHostTreeMaxBuckets = 64
 
 // mdeEngine returns the batcher of the GPU that holds partitionId.
 func mdeEngine(partitionId int) (*C.mde_batcher, error) {

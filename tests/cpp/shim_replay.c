@@ -10,13 +10,13 @@
  *                       B bucket ranges and appends every value to ONE arena, record by record:
  *                       value_off grows by each value's length, seg_rec by the record count per
  *                       bucket, n_partitions = 1, value_stride = 0 (variable-length values); an
- *                       empty arena gets one padding byte. B > 256: -> mde_server_build_levels
+ *                       empty arena gets one padding byte. B > 64: -> mde_server_build_levels
  *                       (the shim's mdeResident: the device's levels down to <= 64 nodes, the
  *                       levels above hashed by mdeTree; mde_batch_build with the whole tree when
  *                       "batcher" is argv[2]) with the
  *                       nodes output, then the shim's mdeTree: the *merkletree.MerkleTree assembled
  *                       from the device's digests and node hashes (no host hashing; mirrored
- *                       below). B <= 256 (mdeHostTreeMaxBuckets): a digest-only mde_batch_build
+ *                       below). B <= 64 (mdeHostTreeMaxBuckets): a digest-only mde_batch_build
  *                       (root = nodes = NULL), then NewTree on the host over the device digests
  *                       (the checker's SHA-256 tree stands in for merkletree's).
  *   diff Ba Bb          DifferentMerkleTreeBuckets (main/merkle_tree.go:159-216), which the shim no
@@ -47,7 +47,7 @@
 void oracle_sha256(const uint8_t* msg, uint64_t len, uint8_t out[32]); /* checker's SHA-256 */
 /* stands in for merkletree.NewTree's hashing where the shim builds the tree on the host */
 int oracle_tree(const uint64_t* digest, uint32_t n_buckets, uint8_t* nodes, uint8_t* root);
-#define HOST_TREE_MAX_BUCKETS 256 /* merkle_gpu.go mdeHostTreeMaxBuckets */
+#define HOST_TREE_MAX_BUCKETS 64  /* merkle_gpu.go mdeHostTreeMaxBuckets */
 #define TOP_NODES 64              /* merkle_gpu.go mdeTopNodes */
 
 /* ---- the shim's mdeTree (integration/go/merkle_gpu.go), in C: merkletree v0.2.0's node graph
