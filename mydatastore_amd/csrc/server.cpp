@@ -95,6 +95,13 @@ constexpr double kWaitTimeoutS = 30.0;
 constexpr double kSpinS = 10e-6;  // pure spinning before a waiting caller starts yielding
 constexpr uint32_t kMaxPeers = 16;  // decision steps with more peers run on the service's context
 
+// CU-masked streams kept for the process (see mde_server_create), per device: a service takes one
+// no live service holds (two services on one stream would queue each launch behind the other's
+// lifetime) and hands it back when its launch has ended.
+constexpr int kKeptDevices = 64;
+std::mutex g_kept_m;
+std::vector<hipStream_t> g_kept_free[kKeptDevices];
+
 }  // namespace
 
 struct mde_server {
@@ -389,22 +396,26 @@ int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_se
   for (int c = 0; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
   // The launch's stream: a CU-masked stream (all CUs) gets a hardware queue of its own, so no other
   // stream of the process queues behind the persistent kernel. It is kept for the process and
-  // reused by the next service on the device: destroying a CU-masked stream made a later
+  // reused by a later service on the device, never by two live ones (g_kept_free): destroying a
+  // CU-masked stream made a later
   // hipStreamDestroy of another stream hang (ROCm 7, profiles/r04/r04n_service_streams.txt).
   // MDE_SERVER_CUMASK=0: a plain non-blocking stream instead; 1: a CU-masked stream destroyed
   // with the service (probes).
   const char* cm = std::getenv("MDE_SERVER_CUMASK");
   const int cmode = cm ? std::atoi(cm) : 2;
-  s->keep_stream = cmode == 2;
-  static std::mutex kept_m;
-  static hipStream_t kept[64] = {};
+  s->keep_stream = cmode == 2 && device >= 0 && device < kKeptDevices;
   hipError_t se = hipSuccess;
   if (cmode == 0) {
     se = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
-  } else if (cmode == 2 && device >= 0 && device < 64) {
-    std::lock_guard<std::mutex> lk(kept_m);
-    if (!kept[device]) se = hipExtStreamCreateWithCUMask(&kept[device], (uint32_t)mask.size(), mask.data());
-    s->stream = kept[device];
+  } else if (s->keep_stream) {
+    std::lock_guard<std::mutex> lk(g_kept_m);
+    std::vector<hipStream_t>& pool = g_kept_free[device];
+    if (!pool.empty()) {
+      s->stream = pool.back();
+      pool.pop_back();
+    } else {
+      se = hipExtStreamCreateWithCUMask(&s->stream, (uint32_t)mask.size(), mask.data());
+    }
   } else {
     se = hipExtStreamCreateWithCUMask(&s->stream, (uint32_t)mask.size(), mask.data());
   }
@@ -472,6 +483,10 @@ void mde_server_destroy(mde_server* s) {
     if (dbg) std::fprintf(stderr, "mde_server_destroy: stream synchronized %.6f s\n", since());
     if (s->exit_ev) (void)hipEventDestroy(s->exit_ev);
     if (s->stream && !s->keep_stream) (void)hipStreamDestroy(s->stream);
+    if (s->stream && s->keep_stream) {
+      std::lock_guard<std::mutex> lk(g_kept_m);
+      g_kept_free[s->device].push_back(s->stream);
+    }
     if (s->dev_in) (void)hipFree(s->dev_in);
     if (s->vscr) (void)hipFree(s->vscr);
     if (s->pin) (void)hipHostFree(s->pin);

@@ -134,6 +134,45 @@ def test_server_python_decisions_match_oracle(coracle):
 
 
 @pytest.mark.gpu
+def test_two_live_services_on_one_device_do_not_queue_behind_each_other(coracle):
+    """Two services alive on one device at once, each with its own caller thread: each launch runs
+    on a kept stream no other live service holds, so neither waits for the other's lifetime
+    (default 100 ms) -- every call returns in well under that; every result equals the oracle."""
+    import time
+    import mydatastore_amd as mde
+    svs = [mde.Server(0), mde.Server(0)]
+    worst, errors = [0.0, 0.0], []
+
+    def caller(t):
+        rng = np.random.default_rng(900 + t)
+        try:
+            for k in range(40):
+                n = int(rng.integers(100, 2000))
+                vals = rng.integers(1, 1 << 40, n, dtype=np.uint64).view(np.uint8).copy()
+                seg = np.concatenate([[0], np.sort(rng.integers(0, n + 1, 63)), [n]]).astype(np.uint64)
+                t0 = time.perf_counter()
+                got = svs[t].build(vals, seg, 1, 64, value_stride=8)
+                worst[t] = max(worst[t], time.perf_counter() - t0)
+                exp = coracle.build(vals, seg, 1, 64, 8)
+                if not (np.array_equal(got["root"], exp["root"]) and np.array_equal(got["digest"], exp["digest"])):
+                    errors.append((t, k))
+        except Exception as e:  # pragma: no cover
+            errors.append((t, repr(e)))
+
+    try:
+        ths = [threading.Thread(target=caller, args=(t,)) for t in range(2)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+    finally:
+        for sv in svs:
+            sv.close()
+    assert not errors, errors[:5]
+    assert max(worst) < 0.05, worst
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("B", [64, 1000, 1023])
 def test_server_levels_plus_host_top_equals_oracle(coracle, B):
     """The split tree (mde_server_build_levels): the device's levels down to the first of at most
