@@ -43,6 +43,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <new>
 #include <string>
@@ -102,6 +103,12 @@ constexpr int kKeptDevices = 64;
 std::mutex g_kept_m;
 std::vector<hipStream_t> g_kept_free[kKeptDevices];
 
+// A caller waiting for a request slot (take_slot / give_slot).
+struct SlotWaiter {
+  std::condition_variable cv;
+  uint32_t slot = UINT32_MAX;
+};
+
 }  // namespace
 
 struct mde_server {
@@ -124,10 +131,12 @@ struct mde_server {
   bool running = false;
   std::mutex launch_m;
   std::mutex m;
-  std::condition_variable cv;
   std::vector<uint32_t> free_slots;
+  std::deque<SlotWaiter*> slot_waiters;  // callers waiting for a slot, first come first served
   std::vector<uint64_t> seq;  // per slot, owned by the caller holding the slot
   std::atomic<uint64_t> n_req{0}, n_launch{0}, n_ctx{0};
+  // MDE_SERVER_DEBUG totals, printed by mde_server_destroy: time waiting for a slot and for `done`
+  std::atomic<uint64_t> ns_slot{0}, ns_done{0};
   // a launch failed or a request timed out: every later call fails at once with this message
   // (a slot whose request failed is never reused -- its workgroup may still write it)
   std::atomic<bool> broken{false};
@@ -243,6 +252,15 @@ int ensure_running(mde_server* s, std::string* msg) {
 
 // Post request `q` on slot i and wait for its `done`.
 int post_and_wait(mde_server* s, uint32_t i, std::string* msg) {
+  const auto tw = std::chrono::steady_clock::now();
+  struct WaitTime {
+    mde_server* s;
+    std::chrono::steady_clock::time_point t;
+    ~WaitTime() {
+      s->ns_done.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                               std::chrono::steady_clock::now() - t).count(), std::memory_order_relaxed);
+    }
+  } wait_time{s, tw};
   mde::ServerSlot* sl = s->slot(i);
   const uint64_t q = ++s->seq[i];
   __atomic_store_n(&sl->req, q, __ATOMIC_RELEASE);
@@ -288,23 +306,41 @@ int post_and_wait(mde_server* s, uint32_t i, std::string* msg) {
   }
 }
 
-// A free slot, or UINT32_MAX once the service is broken.
+// A free slot, or UINT32_MAX once the service is broken. Callers finding none queue in FIFO order
+// and sleep on a condition variable of their own; give_slot hands a returned slot straight to the
+// first of them (one wakeup per handoff: a shared condition variable woke callers that found the
+// slot already re-taken -- 25-56 k futile wakeups per 80-110 k calls at 100 callers, most of the
+// process's CPU time spent in the kernel, profiles/r04/r04cw_callers_wait.txt).
 uint32_t take_slot(mde_server* s) {
+  const auto t0 = std::chrono::steady_clock::now();
   std::unique_lock<std::mutex> lk(s->m);
-  s->cv.wait(lk, [&] { return !s->free_slots.empty() || s->broken.load(); });
-  if (s->broken.load()) return UINT32_MAX;
-  const uint32_t i = s->free_slots.back();
-  s->free_slots.pop_back();
+  uint32_t i = UINT32_MAX;
+  if (!s->broken.load() && !s->free_slots.empty()) {
+    i = s->free_slots.back();
+    s->free_slots.pop_back();
+  } else if (!s->broken.load()) {
+    SlotWaiter w;
+    s->slot_waiters.push_back(&w);
+    w.cv.wait(lk, [&] { return w.slot != UINT32_MAX || s->broken.load(); });
+    if (s->broken.load()) {  // give back a slot handed over meanwhile, leave the queue
+      if (w.slot != UINT32_MAX) s->free_slots.push_back(w.slot);
+      auto it = std::find(s->slot_waiters.begin(), s->slot_waiters.end(), &w);
+      if (it != s->slot_waiters.end()) s->slot_waiters.erase(it);
+    } else {
+      i = w.slot;
+    }
+  }
+  lk.unlock();
+  s->ns_slot.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                           std::chrono::steady_clock::now() - t0).count(), std::memory_order_relaxed);
   return i;
 }
 
 void mark_broken(mde_server* s, const std::string& msg) {
-  {
-    std::lock_guard<std::mutex> lk(s->m);
-    if (!s->broken.load()) s->broken_msg = msg;
-    s->broken.store(true);
-  }
-  s->cv.notify_all();
+  std::lock_guard<std::mutex> lk(s->m);
+  if (!s->broken.load()) s->broken_msg = msg;
+  s->broken.store(true);
+  for (SlotWaiter* w : s->slot_waiters) w->cv.notify_one();  // under the lock: w lives on its caller's stack
 }
 
 int broken_error(mde_server* s, char* err, uint64_t cap) {
@@ -313,11 +349,15 @@ int broken_error(mde_server* s, char* err, uint64_t cap) {
 }
 
 void give_slot(mde_server* s, uint32_t i) {
-  {
-    std::lock_guard<std::mutex> lk(s->m);
+  std::lock_guard<std::mutex> lk(s->m);
+  if (!s->slot_waiters.empty()) {
+    SlotWaiter* w = s->slot_waiters.front();
+    s->slot_waiters.pop_front();
+    w->slot = i;
+    w->cv.notify_one();  // under the lock (see mark_broken)
+  } else {
     s->free_slots.push_back(i);
   }
-  s->cv.notify_one();
 }
 
 }  // namespace
@@ -493,7 +533,11 @@ void mde_server_destroy(mde_server* s) {
     if (dbg) std::fprintf(stderr, "mde_server_destroy: freed %.6f s\n", since());
   }
   if (s->ctx) mde_destroy(s->ctx);
-  if (dbg) std::fprintf(stderr, "mde_server_destroy: done %.6f s\n", since());
+  if (dbg)
+    std::fprintf(stderr,
+                 "mde_server_destroy: done %.6f s; requests %llu, waiting for a slot %.3f s, for done %.3f s\n",
+                 since(), (unsigned long long)s->n_req.load(), 1e-9 * (double)s->ns_slot.load(),
+                 1e-9 * (double)s->ns_done.load());
   delete s;
 }
 

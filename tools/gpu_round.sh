@@ -14,6 +14,8 @@
 #           the service + shim-replay pytest                         -> st{1,2,3}.json, service_pytest.log
 #   callbench  batch_bench at B = 64 / 1,000 x 1 / 10 / 100 callers  -> bb.jsonl (+ summary)
 #   stress  resident service under 4-64 callers, 1-100 ms lifetimes -> stress{1..5}.json
+#   callers the service at 10 / 100 callers with its wait totals (MDE_SERVER_DEBUG), user / system
+#           CPU seconds and the cgroup's cpu.stat; SLOTS="16 32" sweeps the slot count -> callers.txt
 # Extra bench flags: BENCH_ARGS="...".
 set -o pipefail
 export TMPDIR=/tmp
@@ -83,6 +85,18 @@ for s in "$@"; do
         timeout -k 10 150 tests/cpp/build/server_test $a > $O/stress$i.json 2> $O/stress$i.err || { tail -5 $O/stress$i.err; exit 1; }
         cat $O/stress$i.json
       done ;;
+    callers)
+      step callers
+      TIMEFORMAT="time user %U sys %S wall %R"
+      for sl in ${SLOTS:-16}; do
+        for a in "64 10 server_hosttree" "64 100 server_hosttree" "64 100 verify_server" "1000 100 server_levels"; do
+          echo "== $a slots $sl" >> $O/callers.txt
+          cat /sys/fs/cgroup/cpu.stat >> $O/callers.txt 2>/dev/null || true
+          { time MDE_SERVER_SLOTS=$sl MDE_SERVER_DEBUG=1 timeout -k 10 90 tests/cpp/build/batch_bench 0.4 $a \
+              >> $O/callers.txt 2>&1 ; } 2>> $O/callers.txt || { tail $O/callers.txt; exit 1; }
+        done
+      done
+      grep -E "^==|calls_per_s|for done|^time" $O/callers.txt | cut -c1-200 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
