@@ -295,15 +295,21 @@ def end_to_end(torch, eng, w, B, reps=3):
 def main_group(args):
     """N GPUs driven by ONE process through mde_group (include/mde.h): the multi-GPU path a Go node
     reaches (merkle_gpu.go's process owns the node's GPUs). Partition p lives on GPU p % N; each
-    step is one pipelined build launch per GPU (this build's digest + the previous build's trees)
-    and every GATHER_BUCKET builds ONE all-gather of the root slabs (RCCL over xGMI on
-    communicators libmde created once, ncclCommInitAll), enqueued in stream order on every GPU.
-    Under torch.distributed.run the other ranks only join the barriers (gloo, no GPU); rank 0's
-    clock brackets all N GPUs' work. --rehearse: every shard on GPU 0 (copy gather)."""
+    step is one pipelined build launch per GPU (this build's digest + the previous build's trees).
+    The exchange step -- ONE all-gather of the root slabs, RCCL over xGMI on communicators libmde
+    created once (ncclCommInitAll) -- runs on each GPU's side stream
+    (mde_group_gather_overlapped_async), overlapping the next builds: C4 gathers every
+    GATHER_BUCKET builds, then the same run is timed again with one gather per build
+    (`root_gather_per_build`, plus K bare gathers); C5 (BASELINE config 5) builds replicas A and B,
+    diffs and extracts on every GPU (mde_group_diff_async / mde_group_extract_async) and gathers
+    [A roots | B roots | diff counts] once per step. Under torch.distributed.run the other ranks
+    only join the barriers (gloo, no GPU); rank 0's clock brackets all N GPUs' work. --rehearse:
+    every shard on GPU 0 (copy gather)."""
+    import ctypes
     import torch
     import torch.distributed as dist
     import mydatastore_amd as mde
-    from mydatastore_amd.workload import make_workload
+    from mydatastore_amd.workload import Workload, make_workload, perturb_replica
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
@@ -315,88 +321,238 @@ def main_group(args):
         dist.destroy_process_group()
         return
     N = args.gpus
+    c5 = args.config == "c5"
     n_dev = torch.cuda.device_count()
     devices = [0] * N if args.rehearse else list(range(N))
     if max(devices) >= n_dev:
         raise SystemExit(f"--gpus {N} but {n_dev} GPUs visible (use --rehearse to place every shard on GPU 0)")
-    n_keys, P, V, B, mode, desc = CONFIGS[args.config]
+    n_keys, P, V, B, mode, desc = CONFIGS["c4" if c5 else args.config]
+    if c5:
+        desc = ("C5: C4 data as replica A + replica B with one bucket per partition perturbed; "
+                "build both, device DFS-order diff, out-of-sync range extract of B")
     g = mde.Group(devices)
+    lib = mde.load_library()
     engines = {}
     for d in sorted(set(devices)):
         engines[d] = mde.Engine(d)
     shards = [make_workload(engines[devices[i]], n_partitions=P, n_buckets=B, value_len=V, part_mode=mode,
                             keys_per_partition=-(-n_keys // P), n_keys=n_keys, rank=i, world=N) for i in range(N)]
-    bucket = GATHER_BUCKET
-    slab = -(-P // N)
     sdev = [torch.device("cuda", d) for d in devices]
-    send = [torch.zeros(bucket * slab * 32, dtype=torch.uint8, device=sdev[i]) for i in range(N)]
-    recv = [torch.zeros(N * bucket * slab * 32, dtype=torch.uint8, device=sdev[i]) for i in range(N)]
-    # two output sets per shard (pipelined builds alternate); each build's roots go straight into
-    # its row of the bucket's send slab
+    slab = -(-P // N)
+    width = 68 if c5 else 32  # bytes per partition row of a slab: [A root | B root | diff count] for C5
+    repl, touched = [], []
+    if c5:
+        for w in shards:
+            vb, t = perturb_replica(w)
+            repl.append(Workload(w.engine, vb, w.seg_rec, w.n_partitions, B, w.n_records, V, w.partition_ids))
+            touched.append(t)
+    # two output sets per shard and replica (pipelined builds alternate)
     sets = [[w._outs() for _ in range(2)] for w in shards]
-
-    def tree_out(i, L):
-        o, _ = sets[i][L % 2]
-        root = send[i][(L % bucket) * slab * 32:].data_ptr()
-        return mde.TreeOut(o["digest"].data_ptr(), o["size"].data_ptr(), o["items"].data_ptr(), root, o["nodes"].data_ptr())
-
-    # the per-launch argument arrays, built once (bucket is even: L % bucket fixes L % 2)
-    import ctypes
-    lib = mde.load_library()
+    sets_b = [[w._outs() for _ in range(2)] for w in repl]
     recs = (mde.Records * N)(*[w.rec for w in shards])
-    outs_by_slot = [(mde.TreeOut * N)(*[tree_out(i, k) for i in range(N)]) for k in range(bucket)]
-    nbytes = slab * 32 * bucket
-    send_p = (ctypes.c_void_p * N)(*[t.data_ptr() for t in send])
-    recv_p = (ctypes.c_void_p * N)(*[t.data_ptr() for t in recv])
+    recs_b = (mde.Records * N)(*[w.rec for w in repl]) if c5 else None
+    # C5 compare: diff ids per device, diff counts written straight into the step's send slab,
+    # extract outputs per device
+    cap = mde.diff_capacity(B, B)
+    diff_ids = [torch.zeros(w.n_partitions * cap, dtype=torch.int32, device=sdev[i]) for i, w in enumerate(shards)] if c5 else []
+    xo = []
+    for i, w in enumerate(repl):
+        rc_ = max(w.n_records // 8, 1024)
+        xo.append({"rec_cap": rc_, "part_off": torch.zeros(w.n_partitions + 1, dtype=torch.int64, device=sdev[i]),
+                   "out_rec": torch.zeros(rc_, dtype=torch.int64, device=sdev[i]),
+                   "out_vals": torch.zeros(rc_ * V, dtype=torch.uint8, device=sdev[i]),
+                   "out_voff": torch.zeros(rc_ + 1, dtype=torch.int64, device=sdev[i]),
+                   "status": torch.zeros(1, dtype=torch.int32, device=sdev[i])})
 
     def check(rc):
         if rc != mde.MDE_OK:
             g._check(rc)
 
-    def run(steps):  # `steps` pipelined builds, gathers of every complete bucket, drained
-        for L in range(steps):
-            check(lib.mde_group_build_pipelined_async(g.g, recs, outs_by_slot[L % bucket]))
-            if L >= 1 and (L - 1) % bucket == bucket - 1:  # launch L completed build L-1's trees
-                check(lib.mde_group_gather_async(g.g, send_p, recv_p, nbytes))
-        check(lib.mde_group_build_pipeline_drain_async(g.g))
-        if steps and (steps - 1) % bucket != bucket - 1:
-            check(lib.mde_group_gather_async(g.g, send_p, recv_p, nbytes))
+    class Run:
+        """The slabs of one timed configuration: two sets (double-buffered gathers), `bucket` rows of
+        `slab` partitions x `width` bytes per set and device; the per-launch argument arrays."""
 
-    ext = torch.cuda.ExternalStream(mde.load_library().mde_get_stream(g.ctx(0)), device=sdev[0])
-    run(max(args.warmup, 1))
-    g.synchronize()
-    if world > 1:
-        dist.barrier()
-    for d in sorted(set(devices)):
-        torch.cuda.synchronize(d)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record(ext)
-    run(args.steps)
-    e1.record(ext)
-    g.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    ms = (t1 - t0) * 1e3 / args.steps
-    dev0_ms = e0.elapsed_time(e1) / args.steps
-    # parity: the gathered slabs (device 0's copy, the last bucket) hold every shard's roots of its
-    # last build; shard 0's last build equals the C oracle on host-regenerated partitions
+        def __init__(self, bucket):
+            self.bucket = bucket
+            self.nbytes = bucket * slab * width
+            self.send = [[torch.zeros(self.nbytes, dtype=torch.uint8, device=sdev[i]) for i in range(N)] for _ in range(2)]
+            self.recv = [[torch.zeros(N * self.nbytes, dtype=torch.uint8, device=sdev[i]) for i in range(N)] for _ in range(2)]
+            self.send_p = [(ctypes.c_void_p * N)(*[t.data_ptr() for t in self.send[k]]) for k in range(2)]
+            self.recv_p = [(ctypes.c_void_p * N)(*[t.data_ptr() for t in self.recv[k]]) for k in range(2)]
+
+            def tree_out(o, base):
+                return mde.TreeOut(o["digest"].data_ptr(), o["size"].data_ptr(), o["items"].data_ptr(), base,
+                                   o["nodes"].data_ptr())
+            # build j: output set j % 2, its roots in slab set (j // bucket) % 2, row j % bucket
+            self.outs = [[(mde.TreeOut * N)(*[tree_out(sets[i][(k * bucket + r) % 2][0],
+                                                       self.send[k][i].data_ptr() + r * slab * width)
+                                              for i in range(N)]) for r in range(bucket)] for k in range(2)]
+            if c5:  # step j: A roots at [0, slab*32), B roots at [slab*32, slab*64), counts after
+                self.outs_b = [(mde.TreeOut * N)(*[tree_out(sets_b[i][k][0], self.send[k][i].data_ptr() + slab * 32)
+                                                   for i in range(N)]) for k in range(2)]
+                self.diff = [(mde.DiffArgs * N)(*[mde.DiffArgs(shards[i].n_partitions, B, B,
+                                                               sets[i][k][0]["digest"].data_ptr(), sets[i][k][0]["nodes"].data_ptr(),
+                                                               sets_b[i][k][0]["digest"].data_ptr(), sets_b[i][k][0]["nodes"].data_ptr(),
+                                                               diff_ids[i].data_ptr(), cap,
+                                                               self.send[k][i].data_ptr() + slab * 64) for i in range(N)])
+                             for k in range(2)]
+                self.extract = [(mde.ExtractArgs * N)(*[mde.ExtractArgs(diff_ids[i].data_ptr(), cap,
+                                                                        self.send[k][i].data_ptr() + slab * 64,
+                                                                        xo[i]["part_off"].data_ptr(), xo[i]["out_rec"].data_ptr(),
+                                                                        xo[i]["rec_cap"], xo[i]["out_vals"].data_ptr(),
+                                                                        xo[i]["out_voff"].data_ptr(), xo[i]["rec_cap"] * V,
+                                                                        xo[i]["status"].data_ptr()) for i in range(N)])
+                                for k in range(2)]
+            self.tickets = {}
+
+        def gather(self, b):  # the slabs of bucket (C5: step) b, on the side streams
+            t = ctypes.c_uint64()
+            check(lib.mde_group_gather_overlapped_async(g.g, self.send_p[b % 2], self.recv_p[b % 2], self.nbytes,
+                                                        ctypes.byref(t)))
+            self.tickets[b] = t.value
+
+        def wait(self, b):  # the context streams wait until bucket b's gather has read its slabs
+            if b in self.tickets:
+                check(lib.mde_group_gather_wait_async(g.g, self.tickets.pop(b)))
+
+        def run_c4(self, steps):
+            """`steps` pipelined builds: launch L digests build L and writes build L-1's trees (its
+            roots into slab set ((L-1) // bucket) % 2); once launch L has written the last build of
+            a bucket, that bucket's gather goes out on the side streams; before launch L writes the
+            first build of bucket b into set b % 2, the context streams wait for bucket b-2's gather."""
+            bk = self.bucket
+            for L in range(steps):
+                j = L - 1  # the build whose trees launch L writes
+                if j >= 0 and j % bk == 0:
+                    self.wait(j // bk - 2)
+                check(lib.mde_group_build_pipelined_async(g.g, recs, self.outs[(L // bk) % 2][L % bk]))
+                if j >= 0 and j % bk == bk - 1:
+                    self.gather(j // bk)
+            if steps and (steps - 1) % bk == 0:
+                self.wait((steps - 1) // bk - 2)
+            check(lib.mde_group_build_pipeline_drain_async(g.g))
+            if steps:
+                self.gather((steps - 1) // bk)
+
+        def run_c5(self, steps):
+            """Step L: launch 2L digests A(L) and writes B(L-1)'s trees; the compare of step L-1
+            (diff, extract, and its [A | B | counts] gather on the side streams); launch 2L+1
+            digests B(L) and writes A(L)'s trees. Slab set L % 2 is rewritten from launch 2L+1 on,
+            after step L-2's gather (the wait at the top of step L)."""
+            def compare(j):
+                k = j % 2
+                check(lib.mde_group_diff_async(g.g, self.diff[k]))
+                check(lib.mde_group_extract_async(g.g, recs_b, self.extract[k]))
+                self.gather(j)
+            for L in range(steps):
+                self.wait(L - 2)
+                check(lib.mde_group_build_pipelined_async(g.g, recs, self.outs[L % 2][0]))
+                if L >= 1:
+                    compare(L - 1)
+                check(lib.mde_group_build_pipelined_async(g.g, recs_b, self.outs_b[L % 2]))
+            check(lib.mde_group_build_pipeline_drain_async(g.g))
+            if steps:
+                compare(steps - 1)
+
+        def run(self, steps):
+            (self.run_c5 if c5 else self.run_c4)(steps)
+
+    ext = torch.cuda.ExternalStream(lib.mde_get_stream(g.ctx(0)), device=sdev[0])
+
+    def timed(run, steps, warmup):
+        run.run(max(warmup, 1))
+        g.synchronize()
+        run.tickets.clear()
+        if world > 1:
+            dist.barrier()
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(ext)
+        run.run(steps)
+        t_enq = time.perf_counter()
+        e1.record(ext)
+        g.synchronize()
+        t1 = time.perf_counter()
+        run.tickets.clear()
+        if world > 1:
+            dist.barrier()
+        ms = (t1 - t0) * 1e3 / steps
+        ht = {"enqueue_ms": round((t_enq - t0) * 1e3, 3), "enqueue_ms_per_step": round((t_enq - t0) * 1e3 / steps, 4),
+              "wall_ms": round((t1 - t0) * 1e3, 3), "launches_per_step": N * (2 if c5 else 1)}
+        return ms, e0.elapsed_time(e1) / steps, ht
+
+    main_run = Run(1 if c5 else GATHER_BUCKET)
+    ms, dev0_ms, host_timing = timed(main_run, args.steps, args.warmup)
     last = args.steps - 1
-    got = recv[0].view(N, bucket, slab, 32)[:, last % bucket].cpu().numpy()
-    ok_gather = all(np.array_equal(got[i, :shards[i].n_partitions],
-                                   send[i].view(bucket, slab, 32)[last % bucket, :shards[i].n_partitions].cpu().numpy())
+    # parity: the gathered slabs (device 0's copy) of the last bucket / step hold every shard's
+    # rows of its last build; every device received the same slabs; shard 0's last build equals
+    # the C oracle on host-regenerated partitions
+    bk = main_run.bucket
+    kset, row = (last // bk) % 2, last % bk
+    got = main_run.recv[kset][0].view(N, bk, slab, -1)[:, row].cpu().numpy()
+    ok_gather = all(np.array_equal(got[i].reshape(-1), main_run.send[kset][i].view(bk, slab, -1)[row].cpu().numpy().reshape(-1))
                     for i in range(N))
-    ok_same = all(torch.equal(recv[i].cpu(), recv[0].cpu()) for i in range(1, N))
+    ok_same = all(torch.equal(main_run.recv[kset][i].cpu(), main_run.recv[kset][0].cpu()) for i in range(1, N))
+    parity = {"gathered_slabs_hold_every_shard_rows": bool(ok_gather), "every_gpu_received_the_same_slabs": bool(ok_same)}
     info = host_cpu_info()
     threads = cpu_share(info, 1)
     co, s_vals, s_seg, s_n, ref = oracle_sample((n_keys, P, V, B, mode, desc), shards[0].partition_ids, threads)
     o0 = {k: v.cpu().numpy() for k, v in sets[0][last % 2][0].items()}
-    r0 = send[0].view(bucket, slab, 32)[last % bucket, :s_n].cpu().numpy().reshape(-1)
+    r0 = main_run.send[kset][0].view(bk, slab * width)[row, :s_n * 32].cpu().numpy()
     ok_oracle = (np.array_equal(o0["digest"][:s_n * B].view(np.uint64), ref["digest"]) and
                  np.array_equal(o0["size"][:s_n * B], ref["size"]) and np.array_equal(r0, ref["root"]))
-    total = sum(w.value_bytes for w in shards)
-    achieved = shards[0].value_bytes / (dev0_ms * 1e-3) / 1e9
+    parity["oracle_sample_partitions"] = int(s_n)
+    parity["shard0_equals_c_oracle_on_sample"] = bool(ok_oracle)
+    if c5:  # every shard's gathered diff counts: exactly its perturbed partitions; shard 0's diff and extract
+        ok_cnt = True
+        for i in range(N):
+            k = shards[i].n_partitions
+            cnt = got[i].reshape(-1)[slab * 64:slab * 64 + k * 4].view(np.int32)
+            ok_cnt &= bool(np.array_equal(cnt, np.array([1 if p in touched[i] else 0 for p in range(k)], np.int32)))
+        k0 = shards[0].n_partitions
+        ids = diff_ids[0].cpu().numpy().reshape(k0, cap)
+        ok_ids = all(ids[p, 0] == touched[0][p] for p in touched[0])
+        seg = shards[0].seg_rec.cpu().numpy()
+        want = sum(int(seg[p * B + b + 1] - seg[p * B + b]) for p, b in touched[0].items())
+        po = xo[0]["part_off"].cpu().numpy()
+        ok_ex = int(xo[0]["status"].item()) == 0 and int(po[-1]) == want
+        if ok_ex and want:
+            r = xo[0]["out_rec"][:want].cpu().numpy()
+            samp = slice(None, None, max(1, want // 64))
+            gotv = xo[0]["out_vals"][:want * V].view(want, V).cpu().numpy()[samp]
+            src = repl[0].values.view(-1, V)[torch.from_numpy(r[samp]).to(sdev[0])].cpu().numpy()
+            ok_ex = bool(np.array_equal(gotv, src))
+        parity["c5_gathered_diff_counts_are_the_perturbed_partitions"] = bool(ok_cnt)
+        parity["c5_shard0_diff_is_exactly_the_perturbed_bucket"] = bool(ok_ids)
+        parity["c5_shard0_extract_records_and_bytes"] = bool(ok_ex)
+        parity["c5_shard0_extracted_records_per_step"] = want
+    # C4: the same builds with ONE gather per build, and K bare gathers of one build's slabs: the
+    # fixed cost per build the >= 6x target at 8 GPUs depends on (SURVEY.md section 8e)
+    per_build = None
+    if not c5 and not args.no_gather_per_build and args.steps > 0:
+        one = Run(1)
+        ms1, dev1_ms, ht1 = timed(one, args.steps, 1)
+        k1 = (args.steps - 1) % 2
+        g1 = one.recv[k1][0].view(N, slab * 32).cpu().numpy()
+        ok1 = all(np.array_equal(g1[i], one.send[k1][i].cpu().numpy()) for i in range(N))
+        g.synchronize()
+        t0 = time.perf_counter()
+        for b in range(args.steps):
+            one.gather(b)
+        g.synchronize()
+        bare = (time.perf_counter() - t0) * 1e3 / args.steps
+        one.tickets.clear()
+        per_build = {"ms_per_step": round(ms1, 5), "gathers_per_step": 1, "kernel_ms_gpu0": round(dev1_ms, 5),
+                     "gather_cost_per_build_ms": round(ms1 - ms, 5),
+                     "bare_gather_ms": round(bare, 5), "gathered_roots_match_after_run": bool(ok1),
+                     "host_timing": ht1}
+        parity["per_build_gathered_roots_match"] = bool(ok1)
+    parity["all_ranks_ok"] = all(v for k, v in parity.items() if isinstance(v, bool))
+    total = sum(w.value_bytes for w in shards) * (2 if c5 else 1)
+    launches = 2 if c5 else 1
+    achieved = shards[0].value_bytes * launches / (dev0_ms * 1e-3) / 1e9
     result = {
         "metric": METRIC, "value": round(total / 2**30 / (ms * 1e-3), 3), "unit": "GiB/s", "n_gpus": N,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True,
@@ -408,18 +564,20 @@ def main_group(args):
                    "partitions_per_gpu": [w.n_partitions for w in shards],
                    "parallelism": f"partition-shard x{N}, one process (mde_group)",
                    "engine": "group", "devices": devices,
-                   "root_gather": f"{g.gather_kind} of {N} x {bucket} x {slab} x 32 B slabs, one per {bucket} builds, "
-                                  "in stream order on every GPU"},
-        "roofline": {"bound": "hbm", "kernel": "build_step_kernel (GPU 0's launches + its gathers)",
+                   "root_gather": f"{g.gather_kind} of {N} x {bk} x {slab} x {width} B slabs, one per "
+                                  + ("step (C5: [A roots | B roots | diff counts])" if c5 else f"{bk} builds")
+                                  + ", on a side stream per GPU, overlapped with the next builds"},
+        "roofline": {"bound": "hbm", "kernel": "build_step_kernel (GPU 0's launches"
+                                               + (" + the compare kernels, counted against it)" if c5 else ")"),
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel_ms": round(dev0_ms, 5), "algorithmic_bytes_per_launch": shards[0].value_bytes},
-        "parity": {"gathered_slabs_hold_every_shard_roots": bool(ok_gather),
-                   "every_gpu_received_the_same_slabs": bool(ok_same),
-                   "oracle_sample_partitions": int(s_n), "shard0_equals_c_oracle_on_sample": bool(ok_oracle),
-                   "all_ranks_ok": bool(ok_gather and ok_same and ok_oracle)},
+                     "kernel_ms": round(dev0_ms / launches, 5), "algorithmic_bytes_per_launch": shards[0].value_bytes},
+        "parity": parity,
+        "host_timing": host_timing,
         "cpu_baseline": None,
     }
+    if per_build is not None:
+        result["root_gather_per_build"] = per_build
     if world > 1:
         result["launcher_ranks"] = world
     print(json.dumps(result), flush=True)
@@ -434,7 +592,7 @@ def main_group(args):
 def main():
     args = parse()
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.engine == "group" or (args.engine == "auto" and max(world_env, args.gpus) > 1 and args.config != "c5"
+    if args.engine == "group" or (args.engine == "auto" and max(world_env, args.gpus) > 1
                                   and args.layout == "a" and not args.rccl_selftest and not args.simulate_world):
         return main_group(args)
     import torch

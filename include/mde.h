@@ -91,8 +91,12 @@ typedef struct mde_tree_out {
 
 int mde_abi_version(void);
 const char* mde_strerror(int code);
-/* Visible gfx950 devices (0 without a usable GPU); a node's Go shim spreads partitions over them. */
+/* Visible gfx950 devices (0 without a usable GPU); a node's Go shim spreads partitions over them.
+ * mde_device_list writes the HIP ordinals of the first `cap` of them (the ones mde_create and
+ * mde_group_create take; another GPU model visible at a lower index is skipped) and returns how
+ * many there are. */
 int mde_device_count(void);
+int mde_device_list(int* ordinals, int cap);
 
 /* Context: one HIP device, one stream, device scratch. */
 int mde_create(int device, mde_ctx** out);
@@ -330,7 +334,46 @@ int mde_group_build_pipeline_drain_async(mde_group* group);
 /* The exchange step: device i contributes `bytes` from send[i] (device i memory); recv[i] (device
  * i memory, G x bytes) receives every device's slab, slab r = device r's. */
 int mde_group_gather_async(mde_group* group, const void* const* send, void* const* recv, uint64_t bytes);
+/* The same exchange step overlapped with the next builds: each device's gather waits for the work
+ * already enqueued on the context streams (the producers of the send slabs) and runs on a side
+ * stream of that device, so the builds enqueued next on the context streams overlap it. *ticket
+ * (may be NULL) names it for mde_group_gather_wait_async, which makes every context stream wait
+ * until that gather has read every send slab and filled every recv -- call it before rewriting a
+ * send slab or reading a recv buffer in stream order. mde_group_synchronize also waits for it. */
+int mde_group_gather_overlapped_async(mde_group* group, const void* const* send, void* const* recv, uint64_t bytes,
+                                      uint64_t* ticket);
+int mde_group_gather_wait_async(mde_group* group, uint64_t ticket);
 int mde_group_synchronize(mde_group* group);
+/* BASELINE config 5 over the group (both replicas of a partition on the same device, so the
+ * compare and the extract are device-local): DifferentMerkleTreeBuckets
+ * (main/merkle_tree.go:159-216) of shard i's tree pairs on device i -- mde_diff_async's arguments,
+ * device-i pointers; n_pairs == 0 skips the device -- and StreamBucketsTask's range walk
+ * (main/manager.go:445-487) of shard i's records of the differing buckets -- mde_extract_async's
+ * arguments. Enqueued on every device's context stream. */
+typedef struct mde_diff_args {
+  uint32_t n_pairs, n_buckets_a, n_buckets_b;
+  const uint64_t* digest_a;
+  const uint8_t* nodes_a;
+  const uint64_t* digest_b;
+  const uint8_t* nodes_b;
+  int32_t* out_ids;
+  uint64_t out_stride;
+  int32_t* out_count;
+} mde_diff_args;
+typedef struct mde_extract_args {
+  const int32_t* ids;
+  uint64_t ids_stride;
+  const int32_t* counts;
+  uint64_t* part_off;
+  uint64_t* out_rec;
+  uint64_t rec_cap;
+  uint8_t* out_values;     /* optional */
+  uint64_t* out_value_off; /* optional */
+  uint64_t bytes_cap;
+  int32_t* status;
+} mde_extract_args;
+int mde_group_diff_async(mde_group* group, const mde_diff_args* shard);
+int mde_group_extract_async(mde_group* group, const mde_records* shard, const mde_extract_args* shard_args);
 
 /* Request coalescing for the production call shape (one partition per call). The reference runs
  * RawPartitionMerkleTree and the VerifyEpoch decision for ONE (partition, epoch) per call, on any
@@ -396,7 +439,9 @@ int mde_server_build(mde_server* s, const mde_records* rec, const mde_tree_out* 
 /* RawPartitionMerkleTree split between the device and the caller: digests, sizes, items and the
  * tree's levels 1 .. L (L = the first level of at most top_nodes nodes; out->nodes required, at
  * the usual stride of mde_tree_internal_nodes(B) per partition, of which the first
- * mde_tree_prefix_nodes(B, top_nodes) are written; out->root is not written). The caller hashes
+ * mde_tree_prefix_nodes(B, top_nodes) hold the tree's nodes; the nodes past that prefix are
+ * unspecified -- a call run on the service's context writes every level, one served resident
+ * leaves them untouched; out->root is not written). The caller hashes
  * the few top levels (node = SHA256(left || right), the last node of an odd level paired with
  * itself): a tree's dependent top levels cost a CPU core ~40 ns per compression on its SHA
  * extensions against ~2 us on the device. The Go shim assembles the tree from these nodes and
@@ -416,6 +461,13 @@ int mde_server_verify(mde_server* s, uint32_t n_buckets, int32_t partition, int6
 /* calls served, launches made (1 + relaunches after a lifetime ended) and calls run on the
  * service's context */
 int mde_server_stats(mde_server* s, uint64_t* requests, uint64_t* launches, uint64_t* on_context);
+/* 1 while the resident launch serves calls; 0 once it is out of service -- a launch failed, a
+ * request timed out (30 s), or mde_server_disable -- after which every call runs as mde_build /
+ * mde_verify_epochs on the service's context (same results, a launch per call), so one transient
+ * stall does not fail later calls. mde_server_disable takes the resident launch out of service
+ * (e.g. to give its CUs back to bulk builds); `why` is kept for diagnostics. */
+int mde_server_usable(mde_server* s);
+int mde_server_disable(mde_server* s, const char* why);
 
 /* Write-time tagging of raw keys (device): bucket = BE64(SHA256(key)[:8]) % n_buckets
  * (main/manager.go:773-778), partition = XXH64(key, 0) % n_partitions (hashring.go:108-110).

@@ -18,8 +18,13 @@ package main
 import "C"
 
 import (
+	"bytes"
 	"crypto/sha256"
+	"encoding/binary"
+	"hash"
+	"log"
 	"sync"
+	"sync/atomic"
 	"unsafe"
 
 	"github.com/cbergoon/merkletree"
@@ -47,13 +52,14 @@ var (
 	mdeServers  []*C.mde_server
 	mdeResident = true
 	mdeErr      error
-	// mdeHostTree: build every returned tree with merkletree.NewTree over the device digests (a
-	// digest-only device build; B-1 host SHA-256s per call) instead of assembling it from the
-	// device's node hashes. Callers of merkletree's own methods need it -- MerkleRoot(),
-	// VerifyTree(), RebuildTree() read unexported fields a tree literal cannot set; the reference
-	// calls MerkleRoot() in main/merkle_tree_test.go:90-92,150-152 only. Production reads the
-	// exported Root / Leafs / Left / Right / Hash / C (main/merkle_tree.go:122,160-216).
+	// mdeHostTree: build every returned tree with plain merkletree.NewTree over the device digests
+	// (a digest-only device build; B-1 host SHA-256s per call). Either way the tree is merkletree's
+	// own (mdeNewTree): MerkleRoot(), VerifyTree(), VerifyContent() and RebuildTree() all work on it.
 	mdeHostTree = false
+	// mdeHostCompressions counts the SHA-256 compressions this process ran on the host for the
+	// trees it returned (the memo's misses, or every node of a host tree); batch_bench reports the
+	// same count per call (tests/cpp/batch_bench.c).
+	mdeHostCompressions uint64
 )
 
 // mdeHostTreeMaxBuckets: at most this many buckets, the tree is NewTree's on the host over a
@@ -67,41 +73,34 @@ const mdeHostTreeMaxBuckets = 64
 // mdeEngine returns the batcher of the GPU that holds partitionId.
 func mdeEngine(partitionId int) (*C.mde_batcher, error) {
 	mdeOnce.Do(func() {
-		n := int(C.mde_device_count())
+		n := int(C.mde_device_list(nil, 0))
 		if n < 1 {
 			mdeErr = errors.New("mde: no gfx950 GPU visible")
 			return
 		}
-		for d := 0; d < n; d++ {
+		// the HIP ordinals of the gfx950 devices (another GPU model may sit at a lower index)
+		ords := make([]C.int, n)
+		C.mde_device_list(&ords[0], C.int(n))
+		for _, d := range ords {
 			var b *C.mde_batcher
+			var sv *C.mde_server
 			// at most 256 partitions per batch, no wait window: a batch is whatever queued while the
 			// previous batches ran
-			if rc := C.mde_batcher_create(C.int(d), 256, 0, &b); rc != C.MDE_OK {
-				mdeErr = errors.Errorf("mde_batcher_create(%d): %s", d, C.GoString(C.mde_strerror(rc)))
-				for _, x := range mdeBatchers {
-					C.mde_batcher_destroy(x)
-				}
-				for _, x := range mdeServers {
-					C.mde_server_destroy(x)
-				}
-				mdeBatchers, mdeServers = nil, nil
-				return
+			if rc := C.mde_batcher_create(d, 256, 0, &b); rc != C.MDE_OK {
+				log.Printf("mde: GPU %d skipped: mde_batcher_create: %s", int(d), C.GoString(C.mde_strerror(rc)))
+				continue
+			}
+			// 16 request slots (>= partition_concurrency), buckets up to 1,024 in the resident launch
+			if rc := C.mde_server_create(d, 16, 1024, &sv); rc != C.MDE_OK {
+				log.Printf("mde: GPU %d skipped: mde_server_create: %s", int(d), C.GoString(C.mde_strerror(rc)))
+				C.mde_batcher_destroy(b)
+				continue
 			}
 			mdeBatchers = append(mdeBatchers, b)
-			var sv *C.mde_server
-			// 16 request slots (>= partition_concurrency), buckets up to 1,024 in the resident launch
-			if rc := C.mde_server_create(C.int(d), 16, 1024, &sv); rc != C.MDE_OK {
-				mdeErr = errors.Errorf("mde_server_create(%d): %s", d, C.GoString(C.mde_strerror(rc)))
-				for _, x := range mdeBatchers {
-					C.mde_batcher_destroy(x)
-				}
-				for _, x := range mdeServers {
-					C.mde_server_destroy(x)
-				}
-				mdeBatchers, mdeServers = nil, nil
-				return
-			}
 			mdeServers = append(mdeServers, sv)
+		}
+		if len(mdeBatchers) == 0 {
+			mdeErr = errors.New("mde: no gfx950 GPU could be set up")
 		}
 	})
 	if mdeErr != nil {
@@ -119,54 +118,110 @@ func mdeServer(partitionId int) (*C.mde_server, error) {
 }
 
 // mdeTopNodes: with the resident service the device builds a tree's levels down to the first of at
-// most this many nodes (mde_server_build_levels) and mdeTree hashes the few levels above it: a
+// most this many nodes (mde_server_build_levels) and the host hashes the few levels above it: a
 // tree's dependent top levels cost a core ~40 ns per compression on the SHA extensions
 // crypto/sha256 uses, the device ~2 us (INTEGRATION.md section 3).
 const mdeTopNodes = 64
 
-// mdeTree -- the *merkletree.MerkleTree NewTree would build over these buckets (cbergoon/merkletree
-// v0.2.0: a duplicate of the last leaf when B is odd, level nodes pairing (2j, 2j+1) and the last
-// node of an odd level paired with itself), assembled from the device's outputs: nodes holds the
-// internal node hashes level 1 .. root, 32 bytes each (mde_tree_out.nodes), of which the first
-// `have` are the device's; the rest are hashed here as NewTree does (SHA256(left || right)).
-func mdeTree(digest []uint64, size []int32, nodes []byte, have int) *merkletree.MerkleTree {
+// mdeMemo -- what the device already hashed, in the order merkletree asks for it. cbergoon/merkletree
+// v0.2.0's construction (buildIntermediate) takes one hasher from the hash strategy per internal
+// node, level 1 first, left to right within a level -- the order of mde_tree_out.nodes -- and writes
+// it that node's message: left.Hash || right.Hash (two 8-byte LE64 leaves at level 1,
+// main/merkle_tree.go:64-71 and utils/utils.go:67-74; two 32-byte hashes above), the duplicate of
+// the last leaf when B is odd, the last node of an odd level paired with itself. The k-th hasher
+// answers with device node k's hash only when the message it was written is exactly node k's
+// message as the device hashed it; otherwise it runs SHA-256. A hit is therefore always the
+// SHA-256 of the bytes merkletree asked about, whatever order or tree it comes from (a tampered
+// leaf, another tree); the order only decides how often it hits. O(1) per node: no map, no copy
+// of the device's nodes.
+type mdeMemo struct {
+	leaf   [][]byte // LE64 leaf hashes (+ the odd-B duplicate)
+	nodes  []byte   // the device's node hashes, level 1 .. root, 32 bytes each
+	have   int      // how many of them the device wrote (its levels; all of them for a whole tree)
+	lvl    []int    // node count of each internal level, level 1 first
+	next   int      // the node merkletree's construction hashes next
+	active bool     // false once the tree exists: later hashers are plain SHA-256
+}
+
+func newMdeMemo(digest []uint64, nodes []byte, have int) *mdeMemo {
 	B := len(digest)
-	t := &merkletree.MerkleTree{}
-	level := make([]*merkletree.Node, B, B+1)
+	m := &mdeMemo{leaf: make([][]byte, B, B+1), nodes: nodes, have: have, active: true}
 	for i := 0; i < B; i++ {
-		c := &MerkleBucket{bucketId: int32(i), hasher: &CustomHash{value: int64(digest[i])}, size: size[i]}
-		h, _ := c.CalculateHash()
-		level[i] = &merkletree.Node{Hash: h, C: c}
+		m.leaf[i] = make([]byte, 8)
+		binary.LittleEndian.PutUint64(m.leaf[i], digest[i])
 	}
 	if B%2 == 1 {
-		last := level[B-1]
-		level = append(level, &merkletree.Node{Hash: last.Hash, C: last.C})
+		m.leaf = append(m.leaf, m.leaf[B-1])
 	}
-	t.Leafs = level
-	off := 0
-	for len(level) > 1 {
-		next := make([]*merkletree.Node, (len(level)+1)/2)
-		for j := range next {
-			l, r := level[2*j], level[2*j]
-			if 2*j+1 < len(level) {
-				r = level[2*j+1]
+	for n := len(m.leaf); n > 1; {
+		n = (n + 1) / 2
+		m.lvl = append(m.lvl, n)
+	}
+	return m
+}
+
+// message of device node k: its children's hashes (nil when k is past the device's nodes)
+func (m *mdeMemo) message(k int) ([]byte, []byte) {
+	if k >= m.have {
+		return nil, nil
+	}
+	off, below, prev := 0, len(m.leaf), -1
+	for _, n := range m.lvl {
+		if k < off+n {
+			j := k - off
+			li, ri := 2*j, 2*j
+			if 2*j+1 < below {
+				ri = 2*j + 1
 			}
-			var h []byte
-			if off+j < have {
-				h = nodes[(off+j)*32 : (off+j+1)*32 : (off+j+1)*32]
-			} else {
-				sum := sha256.Sum256(append(append(make([]byte, 0, 64), l.Hash...), r.Hash...))
-				h = sum[:]
+			if prev < 0 {
+				return m.leaf[li], m.leaf[ri]
 			}
-			n := &merkletree.Node{Left: l, Right: r, Hash: h}
-			l.Parent, r.Parent = n, n
-			next[j] = n
+			return m.nodes[(prev+li)*32 : (prev+li+1)*32], m.nodes[(prev+ri)*32 : (prev+ri+1)*32]
 		}
-		off += len(next)
-		level = next
+		prev, below, off = off, n, off+n
 	}
-	t.Root = level[0]
-	return t
+	return nil, nil
+}
+
+// mdeMemoHash -- the hash.Hash the strategy hands merkletree for node k: Write buffers the node's
+// message; Sum returns the device's hash of node k when the message is node k's, else SHA-256.
+type mdeMemoHash struct {
+	m   *mdeMemo
+	k   int
+	buf []byte
+}
+
+func (h *mdeMemoHash) Write(p []byte) (int, error) { h.buf = append(h.buf, p...); return len(p), nil }
+func (h *mdeMemoHash) Reset()                      { h.buf = h.buf[:0] }
+func (h *mdeMemoHash) Size() int                   { return sha256.Size }
+func (h *mdeMemoHash) BlockSize() int              { return sha256.BlockSize }
+func (h *mdeMemoHash) Sum(b []byte) []byte {
+	if l, r := h.m.message(h.k); l != nil && len(h.buf) == len(l)+len(r) &&
+		bytes.Equal(h.buf[:len(l)], l) && bytes.Equal(h.buf[len(l):], r) {
+		return append(b, h.m.nodes[h.k*32:(h.k+1)*32]...) // a copy: merkletree appends to node hashes
+	}
+	atomic.AddUint64(&mdeHostCompressions, uint64(len(h.buf)+8)/64+1)
+	sum := sha256.Sum256(h.buf)
+	return append(b, sum[:]...)
+}
+
+// mdeNewTree -- merkletree's own tree over the buckets, its internal hashes taken from the memo (no
+// host SHA-256 for the nodes the device built): merkletree.NewTreeWithHashStrategy runs its own
+// construction (leafs, the odd-B duplicate, parents, merkleRoot), so MerkleRoot(), VerifyTree(),
+// VerifyContent() and RebuildTree() behave as on a NewTree tree. Once the tree exists the memo is
+// switched off: a later VerifyTree / RebuildTree hashes with real SHA-256, as the reference's trees
+// do.
+func mdeNewTree(cs []merkletree.Content, m *mdeMemo) (*merkletree.MerkleTree, error) {
+	t, err := merkletree.NewTreeWithHashStrategy(cs, func() hash.Hash {
+		if !m.active {
+			return sha256.New()
+		}
+		h := &mdeMemoHash{m: m, k: m.next}
+		m.next++
+		return h
+	})
+	m.active, m.nodes = false, nil
+	return t, err
 }
 
 func cU64(v []uint64) unsafe.Pointer { return C.CBytes(unsafe.Slice((*byte)(unsafe.Pointer(&v[0])), len(v)*8)) }
@@ -174,7 +229,8 @@ func cU64(v []uint64) unsafe.Pointer { return C.CBytes(unsafe.Slice((*byte)(unsa
 // RawPartitionMerkleTree -- drop-in for main/merkle_tree.go:86-116. The per-bucket range scans are
 // unchanged; the values go into one arena that the MI355X engine reduces, batched with the other
 // partitions' calls in flight: bucket digests always on the device; for B > mdeHostTreeMaxBuckets
-// the SHA-256 tree too, returned as its node hashes and assembled without hashing (mdeTree).
+// the SHA-256 tree too, returned as its node hashes, from which merkletree's own construction takes
+// every node the device built (mdeNewTree).
 func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, upperEpoch int64) (*merkletree.MerkleTree, error) {
 	batcher, err := mdeEngine(partitionId)
 	if err != nil {
@@ -238,7 +294,7 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 		if err != nil {
 			return nil, err
 		}
-		if !hostTree { // the device's levels down to <= mdeTopNodes nodes; mdeTree hashes the top
+		if !hostTree { // the device's levels down to <= mdeTopNodes nodes; the memo misses the top ones
 			out.root = nil
 			if rc := C.mde_server_build_levels(server, &rec, &out, mdeTopNodes, &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
 				return nil, errors.Errorf("mde_server_build_levels: %s", C.GoString(&errBuf[0]))
@@ -250,16 +306,19 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 	} else if rc := C.mde_batch_build(batcher, &rec, &out, &errBuf[0], C.uint64_t(len(errBuf))); rc != C.MDE_OK {
 		return nil, errors.Errorf("mde_batch_build: %s", C.GoString(&errBuf[0]))
 	}
-	digest := append([]uint64(nil), unsafe.Slice((*uint64)(cDigest), B)...)
-	size := append([]int32(nil), unsafe.Slice((*int32)(cSize), B)...)
-	if !hostTree {
-		return mdeTree(digest, size, C.GoBytes(cNodes, C.int(nodeBytes)), have), nil
-	}
-	// merkletree.NewTree over the device digests (B-1 host SHA-256s)
+	digest := unsafe.Slice((*uint64)(cDigest), B)
+	size := unsafe.Slice((*int32)(cSize), B)
 	bucketList := make([]merkletree.Content, B)
 	for i := 0; i < B; i++ {
 		bucketList[i] = &MerkleBucket{bucketId: int32(i), hasher: &CustomHash{value: int64(digest[i])}, size: size[i]}
 	}
+	if !hostTree { // merkletree's construction, its node hashes from the device (the top levels of a split build hashed here)
+		return mdeNewTree(bucketList, newMdeMemo(digest, unsafe.Slice((*byte)(cNodes), nodeBytes), have))
+	}
+	// merkletree.NewTree over the device digests (B-1 host SHA-256s: one compression per 16-byte
+	// level-1 message, two per 64-byte message above)
+	n1 := uint64(B+1) / 2
+	atomic.AddUint64(&mdeHostCompressions, 2*uint64(C.mde_tree_internal_nodes(C.uint32_t(B)))-n1)
 	return merkletree.NewTree(bucketList)
 }
 

@@ -49,7 +49,9 @@ EXPORTED_SYMBOLS = (
     "mde_batcher_create", "mde_batcher_destroy", "mde_batcher_ctx", "mde_batcher_contexts", "mde_batcher_stats",
     "mde_batch_build", "mde_batch_verify", "mde_reserve_decode_scratch",
     "mde_server_create", "mde_server_destroy", "mde_server_slots", "mde_server_build", "mde_server_build_levels", "mde_server_verify", "mde_server_stats",
-    "mde_tree_prefix_nodes",
+    "mde_tree_prefix_nodes", "mde_group_gather_overlapped_async", "mde_group_gather_wait_async",
+    "mde_group_diff_async", "mde_group_extract_async", "mde_device_list", "mde_server_usable",
+    "mde_server_disable",
 )
 
 
@@ -73,6 +75,22 @@ class TreeOut(C.Structure):
     """struct mde_tree_out (include/mde.h)."""
     _fields_ = [("digest", C.c_void_p), ("size", C.c_void_p), ("items", C.c_void_p),
                 ("root", C.c_void_p), ("nodes", C.c_void_p)]
+
+
+class DiffArgs(C.Structure):
+    """struct mde_diff_args (include/mde.h): one device's mde_diff_async arguments."""
+    _fields_ = [("n_pairs", C.c_uint32), ("n_buckets_a", C.c_uint32), ("n_buckets_b", C.c_uint32),
+                ("digest_a", C.c_void_p), ("nodes_a", C.c_void_p), ("digest_b", C.c_void_p),
+                ("nodes_b", C.c_void_p), ("out_ids", C.c_void_p), ("out_stride", C.c_uint64),
+                ("out_count", C.c_void_p)]
+
+
+class ExtractArgs(C.Structure):
+    """struct mde_extract_args (include/mde.h): one device's mde_extract_async arguments."""
+    _fields_ = [("ids", C.c_void_p), ("ids_stride", C.c_uint64), ("counts", C.c_void_p),
+                ("part_off", C.c_void_p), ("out_rec", C.c_void_p), ("rec_cap", C.c_uint64),
+                ("out_values", C.c_void_p), ("out_value_off", C.c_void_p), ("bytes_cap", C.c_uint64),
+                ("status", C.c_void_p)]
 
 
 _lib = None
@@ -157,6 +175,11 @@ def load_library() -> C.CDLL:
         "mde_group_build_pipeline_drain_async": (C.c_int, [vp]),
         "mde_group_gather_async": (C.c_int, [vp, C.POINTER(vp), C.POINTER(vp), C.c_uint64]),
         "mde_group_synchronize": (C.c_int, [vp]),
+        "mde_group_gather_overlapped_async": (C.c_int, [vp, C.POINTER(vp), C.POINTER(vp), C.c_uint64,
+                                                        C.POINTER(C.c_uint64)]),
+        "mde_group_gather_wait_async": (C.c_int, [vp, C.c_uint64]),
+        "mde_group_diff_async": (C.c_int, [vp, C.POINTER(DiffArgs)]),
+        "mde_group_extract_async": (C.c_int, [vp, C.POINTER(Records), C.POINTER(ExtractArgs)]),
         "mde_device_count": (C.c_int, []),
         "mde_batcher_create": (C.c_int, [C.c_int, u32, u32, C.POINTER(vp)]),
         "mde_batcher_destroy": (None, [vp]),
@@ -169,6 +192,9 @@ def load_library() -> C.CDLL:
         "mde_server_slots": (u32, [vp]),
         "mde_server_build": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), C.c_char_p, u64]),
         "mde_server_stats": (C.c_int, [vp, vp, vp, vp]),
+        "mde_server_usable": (C.c_int, [vp]),
+        "mde_server_disable": (C.c_int, [vp, C.c_char_p]),
+        "mde_device_list": (C.c_int, [vp, C.c_int]),
         "mde_server_build_levels": (C.c_int, [vp, C.POINTER(Records), C.POINTER(TreeOut), u32, C.c_char_p, u64]),
         "mde_tree_prefix_nodes": (u64, [u32, u32]),
         "mde_server_verify": (C.c_int, [vp, u32, C.c_int32, C.c_int64, vp, vp, u32, vp, vp, u32, vp, vp, vp, vp,
@@ -658,6 +684,28 @@ class Group:
         r = (C.c_void_p * n)(*[_ptr(x) if not isinstance(x, int) else x for x in recv])
         self._check(self.lib.mde_group_gather_async(self.g, s, r, nbytes))
 
+    def gather_overlapped_async(self, send, recv, nbytes: int) -> int:
+        """mde_group_gather_overlapped_async: the gather on each device's side stream; returns its
+        ticket for gather_wait_async."""
+        n = len(self)
+        s = (C.c_void_p * n)(*[_ptr(x) if not isinstance(x, int) else x for x in send])
+        r = (C.c_void_p * n)(*[_ptr(x) if not isinstance(x, int) else x for x in recv])
+        t = C.c_uint64()
+        self._check(self.lib.mde_group_gather_overlapped_async(self.g, s, r, nbytes, C.byref(t)))
+        return int(t.value)
+
+    def gather_wait_async(self, ticket: int):
+        self._check(self.lib.mde_group_gather_wait_async(self.g, ticket))
+
+    def diff_async(self, args):
+        """mde_group_diff_async: one DiffArgs per device (device-i pointers)."""
+        self._check(self.lib.mde_group_diff_async(self.g, (DiffArgs * len(self))(*args)))
+
+    def extract_async(self, shards, args):
+        """mde_group_extract_async: one Records + ExtractArgs per device."""
+        n = len(self)
+        self._check(self.lib.mde_group_extract_async(self.g, (Records * n)(*shards), (ExtractArgs * n)(*args)))
+
     def synchronize(self):
         self._check(self.lib.mde_group_synchronize(self.g))
 
@@ -801,6 +849,18 @@ class Server:
         self.lib.mde_server_stats(self.s, *(C.byref(x) for x in v))
         return {"requests": v[0].value, "launches": v[1].value, "on_context": v[2].value}
 
+    @property
+    def usable(self) -> bool:
+        """mde_server_usable: the resident launch serves calls (else they run on its context)."""
+        return bool(self.lib.mde_server_usable(self.s))
+
+    def disable(self, why: str = ""):
+        """mde_server_disable: take the resident launch out of service; later calls run on the
+        service's context."""
+        rc = self.lib.mde_server_disable(self.s, why.encode())
+        if rc != MDE_OK:
+            raise MdeError(rc, "mde_server_disable failed")
+
     def build(self, values, seg_rec, n_partitions, n_buckets, value_stride=0, value_off=None, want_nodes=True,
               want_tree=True):
         """mde_server_build: same outputs as Engine.build / Batcher.build."""
@@ -822,7 +882,8 @@ class Server:
     def build_levels(self, values, seg_rec, n_partitions, n_buckets, top_nodes, value_stride=0, value_off=None):
         """mde_server_build_levels: digests, sizes, items and the tree's levels 1 .. the first of at
         most top_nodes nodes (the first mde_tree_prefix_nodes(B, top_nodes) of every partition's
-        nodes; the rest stay zero, the caller hashes them)."""
+        nodes; the nodes past that prefix are unspecified -- a call the service runs on its context
+        writes every level -- and the caller hashes them)."""
         P, B = n_partitions, n_buckets
         seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
         values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)

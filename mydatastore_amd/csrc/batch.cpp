@@ -31,6 +31,7 @@
 //
 // Written against the public C ABI plus HIP memory calls only, like any other client of mde.h.
 #include "../../include/mde.h"
+#include "device_scope.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -226,18 +227,19 @@ int check_build(Req* q) {
 
 bool same_key(const Req* a, const Req* b) { return std::memcmp(a->key, b->key, sizeof a->key) == 0; }
 
-// The leader's batch: its own request (still queued: a leader only leads for its own request, so
-// the batch it then waits for is the one its outputs come from) and every other compatible queued
-// request in arrival order, up to max_parts (and, for builds, up to 2^32 buckets in all:
-// mde_build's limit on n_partitions * n_buckets).
+// The leader's batch: its own request first (still queued: a leader only leads for its own
+// request, so the batch it then waits for is the one its outputs come from; alone it may exceed
+// max_parts), then every other compatible queued request in arrival order while the batch stays
+// within max_parts (and, for builds, within 2^32 buckets in all: mde_build's limit on
+// n_partitions * n_buckets, which every request already meets on its own).
 std::vector<Req*> take(mde_batcher* b, Req* first) {
-  std::vector<Req*> out;
+  std::vector<Req*> out{first};
   const uint64_t per_part = first->kind == Kind::Build ? first->rec.n_buckets : 1;
-  uint64_t parts = 0;
+  uint64_t parts = first->parts;
+  b->q.erase(std::find(b->q.begin(), b->q.end(), first));
   for (auto it = b->q.begin(); it != b->q.end();) {
     Req* x = *it;
-    if (x == first || (same_key(x, first) && parts + x->parts <= b->max_parts &&
-                       (parts + x->parts) * per_part <= 0xffffffffull)) {
+    if (same_key(x, first) && parts + x->parts <= b->max_parts && (parts + x->parts) * per_part <= 0xffffffffull) {
       out.push_back(x);
       parts += x->parts;
       it = b->q.erase(it);
@@ -312,7 +314,7 @@ void launch_build(mde_batcher* b, mde_batcher::Slot* sl) {
   const std::vector<Req*>& v = bt->v;
   // the batcher's device before any allocation (grow_slot) or event creation: the leader is
   // whichever caller thread leads, whatever device it has current
-  BHIP(hipSetDevice(b->device));
+  DeviceScope ds(b->device);  // the caller thread's device restored when the launch is enqueued
   const uint32_t B = v[0]->rec.n_buckets;
   const bool want_tree = v[0]->out.root != nullptr;  // same for the whole batch (request key)
   uint32_t stride = v[0]->rec.value_stride;
@@ -434,7 +436,7 @@ int check_verify(Req* q, uint64_t object_stride) {
 void launch_verify(mde_batcher* b, mde_batcher::Slot* sl) {
   Batch* bt = &sl->bt;
   const std::vector<Req*>& v = bt->v;
-  BHIP(hipSetDevice(b->device));  // before grow_slot (see launch_build)
+  DeviceScope ds(b->device);  // before grow_slot (see launch_build)
   const uint32_t B = v[0]->B;
   const int64_t epoch = v[0]->epoch;
   const uint32_t rcount = v[0]->replica_count;
@@ -726,7 +728,7 @@ void mde_batcher_destroy(mde_batcher* b) {
                  (unsigned long long)b->n_batches, (unsigned long long)b->n_requests, 1e6 * b->t_stage / b->n_batches,
                  1e6 * b->t_device / b->n_batches, 1e6 * b->t_scatter / b->n_batches, (unsigned long long)b->n_handoff,
                  b->n_handoff ? 1e6 * b->t_handoff / b->n_handoff : 0.0);
-  (void)hipSetDevice(b->device);
+  DeviceScope ds(b->device);
   for (auto& sl : b->slots) {
     if (!sl.ctx) continue;
     (void)mde_synchronize(sl.ctx);

@@ -13,6 +13,7 @@
 //
 // Written against the public C ABI plus HIP, like batch.cpp.
 #include "../../include/mde.h"
+#include "device_scope.hpp"
 
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
@@ -76,7 +77,14 @@ struct mde_group {
   std::vector<int> dev;
   std::vector<mde_ctx*> ctx;
   std::vector<ncclComm_t> comm;   // one per device (empty: copy gather)
-  std::vector<hipEvent_t> ready;  // copy gather: each device's send buffer is ready
+  std::vector<hipEvent_t> ready;  // each device's send buffer is ready (recorded on its context stream)
+  std::vector<hipEvent_t> copied; // copy gather in stream order: device i's copies are done
+  // overlapped gathers (mde_group_gather_overlapped_async): one side stream per device, and a ring
+  // of kRing "gather done" events per device; ticket t uses ring slot t % kRing
+  enum { kRing = 8 };
+  std::vector<hipStream_t> side;
+  std::vector<hipEvent_t> done;  // [slot * G + i]
+  uint64_t next_ticket = 1;
   std::string gather_kind;
   std::mutex mu;  // held by the host-pointer builds for the whole call; guards err
   std::string err;
@@ -149,6 +157,85 @@ int gather(mde_group* g, const void* const* send, void* const* recv, uint64_t by
           hipMemcpyAsync(static_cast<uint8_t*>(recv[i]) + (uint64_t)r * bytes, send[r], bytes, hipMemcpyDefault, st) !=
               hipSuccess)
         return fail(msg, MDE_E_DEVICE, "device copy gather failed");
+    }
+    if (hipEventRecord(g->copied[i], st) != hipSuccess) return fail(msg, MDE_E_DEVICE, "hipEventRecord failed");
+  }
+  // The collective's stream-order contract: work enqueued on stream r after the gather may rewrite
+  // send[r] -- so stream r waits until every device's copies (which read send[r]) are done.
+  for (uint32_t r = 0; r < G; r++) {
+    (void)hipSetDevice(g->dev[r]);
+    hipStream_t st = static_cast<hipStream_t>(mde_get_stream(g->ctx[r]));
+    for (uint32_t i = 0; i < G; i++)
+      if (i != r && hipStreamWaitEvent(st, g->copied[i], 0) != hipSuccess)
+        return fail(msg, MDE_E_DEVICE, "hipStreamWaitEvent failed");
+  }
+  return MDE_OK;
+}
+
+// The exchange step off the build streams: device i's side stream waits for the send slabs'
+// producers (the work already enqueued on the context streams: its own for RCCL, whose kernel on
+// device i reads only send[i]; every device's for the copies, which read every send[r]), gathers,
+// and records the ticket's ring event. The context streams go on with the next build at once.
+int gather_overlapped(mde_group* g, const void* const* send, void* const* recv, uint64_t bytes, uint64_t* ticket,
+                      std::string& msg) {
+  const uint32_t G = (uint32_t)g->ctx.size();
+  const uint64_t t = g->next_ticket++;
+  const uint64_t slot = t % mde_group::kRing;
+  for (uint32_t i = 0; i < G; i++) {
+    (void)hipSetDevice(g->dev[i]);
+    if (hipEventRecord(g->ready[i], static_cast<hipStream_t>(mde_get_stream(g->ctx[i]))) != hipSuccess)
+      return fail(msg, MDE_E_DEVICE, "hipEventRecord failed");
+  }
+  if (!g->comm.empty()) {
+    for (uint32_t i = 0; i < G; i++) {
+      (void)hipSetDevice(g->dev[i]);
+      if (hipStreamWaitEvent(g->side[i], g->ready[i], 0) != hipSuccess)
+        return fail(msg, MDE_E_DEVICE, "hipStreamWaitEvent failed");
+    }
+    const Rccl& r = rccl();
+    ncclResult_t e = r.group_start();
+    for (uint32_t i = 0; i < G && e == ncclSuccess; i++) {
+      (void)hipSetDevice(g->dev[i]);
+      e = r.all_gather(send[i], recv[i], bytes, ncclUint8, g->comm[i], g->side[i]);
+    }
+    const ncclResult_t e2 = r.group_end();
+    if (e == ncclSuccess) e = e2;
+    if (e != ncclSuccess) return fail(msg, MDE_E_DEVICE, "ncclAllGather: %s", r.error_string(e));
+  } else {
+    for (uint32_t i = 0; i < G; i++) {
+      (void)hipSetDevice(g->dev[i]);
+      for (uint32_t r = 0; r < G; r++) {
+        if (hipStreamWaitEvent(g->side[i], g->ready[r], 0) != hipSuccess ||
+            hipMemcpyAsync(static_cast<uint8_t*>(recv[i]) + (uint64_t)r * bytes, send[r], bytes, hipMemcpyDefault,
+                           g->side[i]) != hipSuccess)
+          return fail(msg, MDE_E_DEVICE, "device copy gather failed");
+      }
+    }
+  }
+  for (uint32_t i = 0; i < G; i++) {
+    (void)hipSetDevice(g->dev[i]);
+    if (hipEventRecord(g->done[slot * G + i], g->side[i]) != hipSuccess)
+      return fail(msg, MDE_E_DEVICE, "hipEventRecord failed");
+  }
+  if (ticket) *ticket = t;
+  return MDE_OK;
+}
+
+// Every context stream waits for gather `t`: RCCL -- device r's own side stream (its collective
+// completes only after it has sent send[r] and received recv[r]); copies -- every side stream (each
+// reads send[r]). A ticket whose ring slot a later gather re-recorded waits for that later gather:
+// later in every side stream's order, so the wait is longer, never wrong.
+int gather_wait(mde_group* g, uint64_t t, std::string& msg) {
+  const uint32_t G = (uint32_t)g->ctx.size();
+  if (!t || t >= g->next_ticket) return fail(msg, MDE_E_INVAL, "unknown gather ticket %llu", (unsigned long long)t);
+  const uint64_t slot = t % mde_group::kRing;
+  for (uint32_t r = 0; r < G; r++) {
+    (void)hipSetDevice(g->dev[r]);
+    hipStream_t st = static_cast<hipStream_t>(mde_get_stream(g->ctx[r]));
+    for (uint32_t i = 0; i < G; i++) {
+      if (!g->comm.empty() && i != r) continue;
+      if (hipStreamWaitEvent(st, g->done[slot * G + i], 0) != hipSuccess)
+        return fail(msg, MDE_E_DEVICE, "hipStreamWaitEvent failed");
     }
   }
   return MDE_OK;
@@ -288,6 +375,7 @@ int mde_group_create(const int* devices, uint32_t n, mde_group** out) {
   if (!out) return MDE_E_INVAL;
   *out = nullptr;
   if (!devices || !n) return MDE_E_INVAL;
+  DeviceScope keep(devices[0]);  // every hipSetDevice below undone on return
   mde_group* g = new (std::nothrow) mde_group();
   if (!g) return MDE_E_NOMEM;
   for (uint32_t i = 0; i < n; i++) {
@@ -319,14 +407,20 @@ int mde_group_create(const int* devices, uint32_t n, mde_group** out) {
     g->gather_kind = !distinct ? "device copies (a device listed twice)"
                      : want_rccl ? "device copies (" + rccl().why + ")" : "device copies (MDE_GROUP_GATHER=copy)";
   }
-  if (g->comm.empty()) {
-    g->ready.assign(n, nullptr);
-    for (uint32_t i = 0; i < n; i++) {
-      (void)hipSetDevice(g->dev[i]);
-      if (hipEventCreateWithFlags(&g->ready[i], hipEventDisableTiming) != hipSuccess) {
-        mde_group_destroy(g);
-        return MDE_E_DEVICE;
-      }
+  g->ready.assign(n, nullptr);
+  g->copied.assign(n, nullptr);
+  g->side.assign(n, nullptr);
+  g->done.assign((size_t)mde_group::kRing * n, nullptr);
+  for (uint32_t i = 0; i < n; i++) {
+    (void)hipSetDevice(g->dev[i]);
+    bool ok = hipEventCreateWithFlags(&g->ready[i], hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&g->copied[i], hipEventDisableTiming) == hipSuccess &&
+              hipStreamCreateWithFlags(&g->side[i], hipStreamNonBlocking) == hipSuccess;
+    for (uint32_t k = 0; ok && k < mde_group::kRing; k++)
+      ok = hipEventCreateWithFlags(&g->done[k * n + i], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+      mde_group_destroy(g);
+      return MDE_E_DEVICE;
     }
   }
   *out = g;
@@ -335,14 +429,24 @@ int mde_group_create(const int* devices, uint32_t n, mde_group** out) {
 
 void mde_group_destroy(mde_group* g) {
   if (!g) return;
+  DeviceScope keep(g->dev.empty() ? 0 : g->dev[0]);
   for (mde_ctx* c : g->ctx) (void)mde_synchronize(c);
+  for (size_t i = 0; i < g->side.size(); i++)
+    if (g->side[i]) {
+      (void)hipSetDevice(g->dev[i]);
+      (void)hipStreamSynchronize(g->side[i]);
+    }
   for (ncclComm_t c : g->comm)
     if (c) (void)rccl().destroy(c);
-  for (size_t i = 0; i < g->ready.size(); i++)
-    if (g->ready[i]) {
-      (void)hipSetDevice(g->dev[i]);
-      (void)hipEventDestroy(g->ready[i]);
-    }
+  const size_t n = g->dev.size();
+  for (size_t i = 0; i < g->ready.size(); i++) {
+    (void)hipSetDevice(g->dev[i]);
+    if (g->ready[i]) (void)hipEventDestroy(g->ready[i]);
+    if (i < g->copied.size() && g->copied[i]) (void)hipEventDestroy(g->copied[i]);
+    for (size_t k = 0; k < mde_group::kRing && k * n + i < g->done.size(); k++)
+      if (g->done[k * n + i]) (void)hipEventDestroy(g->done[k * n + i]);
+    if (i < g->side.size() && g->side[i]) (void)hipStreamDestroy(g->side[i]);
+  }
   for (size_t i = 0; i < g->stage.size(); i++) {
     (void)hipSetDevice(g->dev[i]);
     for (Buf& b : g->stage[i])
@@ -380,6 +484,7 @@ uint64_t mde_group_last_error_copy(mde_group* g, char* buf, uint64_t cap) {
 
 int mde_group_build_async(mde_group* g, const mde_records* shard, const mde_tree_out* shard_out) {
   if (!g || !shard || !shard_out) return MDE_E_INVAL;
+  DeviceScope keep(g->dev[0]);
   for (uint32_t i = 0; i < g->ctx.size(); i++) {
     if (!shard[i].n_partitions) continue;
     const int rc = mde_build_async(g->ctx[i], &shard[i], &shard_out[i]);
@@ -393,6 +498,7 @@ int mde_group_build_async(mde_group* g, const mde_records* shard, const mde_tree
 
 int mde_group_build_pipelined_async(mde_group* g, const mde_records* shard, const mde_tree_out* shard_out) {
   if (!g || !shard || !shard_out) return MDE_E_INVAL;
+  DeviceScope keep(g->dev[0]);
   for (uint32_t i = 0; i < g->ctx.size(); i++) {
     if (!shard[i].n_partitions) continue;
     const int rc = mde_build_pipelined_async(g->ctx[i], &shard[i], &shard_out[i]);
@@ -406,6 +512,7 @@ int mde_group_build_pipelined_async(mde_group* g, const mde_records* shard, cons
 
 int mde_group_build_pipeline_drain_async(mde_group* g) {
   if (!g) return MDE_E_INVAL;
+  DeviceScope keep(g->dev[0]);
   for (uint32_t i = 0; i < g->ctx.size(); i++) {
     const int rc = mde_build_pipeline_drain_async(g->ctx[i]);
     if (rc) {
@@ -418,14 +525,34 @@ int mde_group_build_pipeline_drain_async(mde_group* g) {
 
 int mde_group_gather_async(mde_group* g, const void* const* send, void* const* recv, uint64_t bytes) {
   if (!g || !send || !recv) return MDE_E_INVAL;
+  DeviceScope keep(g->dev[0]);
   std::lock_guard<std::mutex> lk(g->mu);
   return gather(g, send, recv, bytes, g->err);
 }
 
-int mde_group_synchronize(mde_group* g) {
+int mde_group_gather_overlapped_async(mde_group* g, const void* const* send, void* const* recv, uint64_t bytes,
+                                      uint64_t* ticket) {
+  if (!g || !send || !recv) return MDE_E_INVAL;
+  DeviceScope keep(g->dev[0]);
+  std::lock_guard<std::mutex> lk(g->mu);
+  return gather_overlapped(g, send, recv, bytes, ticket, g->err);
+}
+
+int mde_group_gather_wait_async(mde_group* g, uint64_t ticket) {
   if (!g) return MDE_E_INVAL;
+  DeviceScope keep(g->dev[0]);
+  std::lock_guard<std::mutex> lk(g->mu);
+  return gather_wait(g, ticket, g->err);
+}
+
+int mde_group_diff_async(mde_group* g, const mde_diff_args* shard) {
+  if (!g || !shard) return MDE_E_INVAL;
+  DeviceScope keep(g->dev[0]);
   for (uint32_t i = 0; i < g->ctx.size(); i++) {
-    const int rc = mde_synchronize(g->ctx[i]);
+    const mde_diff_args& a = shard[i];
+    if (!a.n_pairs) continue;
+    const int rc = mde_diff_async(g->ctx[i], a.n_pairs, a.n_buckets_a, a.digest_a, a.nodes_a, a.n_buckets_b, a.digest_b,
+                                  a.nodes_b, a.out_ids, a.out_stride, a.out_count);
     if (rc) {
       std::lock_guard<std::mutex> lk(g->mu);
       return ctx_err(g, i, rc, g->err);
@@ -434,8 +561,46 @@ int mde_group_synchronize(mde_group* g) {
   return MDE_OK;
 }
 
+int mde_group_extract_async(mde_group* g, const mde_records* shard, const mde_extract_args* args) {
+  if (!g || !shard || !args) return MDE_E_INVAL;
+  DeviceScope keep(g->dev[0]);
+  for (uint32_t i = 0; i < g->ctx.size(); i++) {
+    if (!shard[i].n_partitions) continue;
+    const mde_extract_args& a = args[i];
+    const int rc = mde_extract_async(g->ctx[i], &shard[i], a.ids, a.ids_stride, a.counts, a.part_off, a.out_rec,
+                                     a.rec_cap, a.out_values, a.out_value_off, a.bytes_cap, a.status);
+    if (rc) {
+      std::lock_guard<std::mutex> lk(g->mu);
+      return ctx_err(g, i, rc, g->err);
+    }
+  }
+  return MDE_OK;
+}
+
+int mde_group_synchronize(mde_group* g) {
+  if (!g) return MDE_E_INVAL;
+  DeviceScope keep(g->dev[0]);
+  for (uint32_t i = 0; i < g->ctx.size(); i++) {
+    const int rc = mde_synchronize(g->ctx[i]);
+    if (rc) {
+      std::lock_guard<std::mutex> lk(g->mu);
+      return ctx_err(g, i, rc, g->err);
+    }
+  }
+  for (uint32_t i = 0; i < g->side.size(); i++) {
+    (void)hipSetDevice(g->dev[i]);
+    const hipError_t e = hipStreamSynchronize(g->side[i]);
+    if (e != hipSuccess) {
+      std::lock_guard<std::mutex> lk(g->mu);
+      return fail(g->err, MDE_E_DEVICE, "device %d: gather stream: %s", g->dev[i], hipGetErrorString(e));
+    }
+  }
+  return MDE_OK;
+}
+
 int mde_multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o) {
   if (!g || g->ctx.empty()) return MDE_E_INVAL;
+  DeviceScope keep(g->dev[0]);
   std::lock_guard<std::mutex> lk(g->mu);
   g->err.clear();
   std::string& msg = g->err;
@@ -517,6 +682,7 @@ int mde_multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o) {
 // mde_build_streamed's two-slot ring, concurrently. Same results as mde_multi_build.
 int mde_multi_build_streamed(mde_group* g, const mde_records* r, const mde_tree_out* o, uint64_t chunk_bytes) {
   if (!g || g->ctx.empty()) return MDE_E_INVAL;
+  DeviceScope keep(g->dev[0]);
   std::lock_guard<std::mutex> lk(g->mu);
   g->err.clear();
   int rc = check(r, o, g->err);

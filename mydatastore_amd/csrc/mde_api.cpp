@@ -6,6 +6,7 @@
 // main/manager.go:166-170) or each thread can own one. Errors are returned as MDE_E_* codes with
 // the message kept per context; nothing throws or aborts across the ABI.
 #include "../../include/mde.h"
+#include "device_scope.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -315,10 +316,13 @@ int ensure_slot(mde_ctx* c, mde_ctx::Slot& sl, uint64_t S) {
   return MDE_OK;
 }
 
+// An entry point's critical section: the context lock, and the context's device selected for the
+// call (the caller thread's device restored after it).
 struct Guard {
   mde_ctx* c;
   std::lock_guard<std::mutex> lk;
-  explicit Guard(mde_ctx* ctx) : c(ctx), lk(ctx->mu) { (void)hipSetDevice(ctx->device); c->err.clear(); }
+  DeviceScope ds;
+  explicit Guard(mde_ctx* ctx) : c(ctx), lk(ctx->mu), ds(ctx->device) { c->err.clear(); }
 };
 
 int check_records(mde_ctx* c, const mde_records* r) {
@@ -749,15 +753,23 @@ extern "C" {
 
 int mde_abi_version(void) { return MDE_ABI_VERSION; }
 
-int mde_device_count(void) {
+int mde_device_list(int* ordinals, int cap) {
   int n = 0, k = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
   for (int d = 0; d < n; d++) {
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, d) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) k++;
+    if (hipGetDeviceProperties(&prop, d) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) {
+      if (ordinals && k < cap) ordinals[k] = d;
+      k++;
+    }
   }
   return k;
 }
+
+int mde_device_count(void) { return mde_device_list(nullptr, 0); }
 
 int mde_reserve_decode_scratch(mde_ctx* c, uint64_t n_objects, uint64_t object_bytes) {
   if (!c) return MDE_E_INVAL;
@@ -793,8 +805,8 @@ int mde_create(int device, mde_ctx** out) {
   c->device = device;
   c->cus = prop.multiProcessorCount;
   std::snprintf(c->arch, sizeof c->arch, "%s", prop.gcnArchName);
-  if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->own_stream, hipStreamDefault) != hipSuccess) {
+  DeviceScope ds(device);
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamDefault) != hipSuccess) {
     delete c;
     return MDE_E_DEVICE;
   }
@@ -808,7 +820,7 @@ void mde_destroy(mde_ctx* c) {
   if (!c) return;
   {
     std::lock_guard<std::mutex> lk(c->mu);
-    (void)hipSetDevice(c->device);
+    DeviceScope ds(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->sums) (void)hipFree(c->sums);
     if (c->counts) (void)hipFree(c->counts);

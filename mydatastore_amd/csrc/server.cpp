@@ -29,6 +29,7 @@
 // context. Each caller gets exactly what mde_build returns for its inputs (tests/cpp/server_test.c
 // against mde_build and the C oracle under concurrent callers).
 #include "../../include/mde.h"
+#include "device_scope.hpp"
 #include "mde_internal.hpp"
 
 #include <hip/hip_ext.h>
@@ -70,23 +71,6 @@ int failf(char* buf, uint64_t cap, int code, const char* fmt, ...) {
 }
 
 uint64_t a16(uint64_t x) { return (x + 15) & ~15ull; }
-
-// Selects a device for the HIP calls of a scope and restores the calling thread's device after
-// (the service's calls run on its callers' threads, which may use other devices).
-struct DeviceScope {
-  int prev = -1;
-  explicit DeviceScope(int d) {
-    if (hipGetDevice(&prev) != hipSuccess) {
-      (void)hipGetLastError();
-      prev = -1;
-    }
-    if (prev != d) (void)hipSetDevice(d);
-  }
-  ~DeviceScope() {
-    int cur = -1;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
 
 constexpr uint32_t kDefaultSlots = 16;
 constexpr uint32_t kMaxSlots = 256;
@@ -137,8 +121,8 @@ struct mde_server {
   std::atomic<uint64_t> n_req{0}, n_launch{0}, n_ctx{0};
   // MDE_SERVER_DEBUG totals, printed by mde_server_destroy: time waiting for a slot and for `done`
   std::atomic<uint64_t> ns_slot{0}, ns_done{0};
-  // a launch failed or a request timed out: every later call fails at once with this message
-  // (a slot whose request failed is never reused -- its workgroup may still write it)
+  // a launch failed, a request timed out or mde_server_disable: every later call runs on the
+  // service's context (a slot whose request failed is never reused -- its workgroup may still write it)
   std::atomic<bool> broken{false};
   std::string broken_msg;
   mde_ctx* ctx = nullptr;  // requests the resident workgroups do not take
@@ -341,11 +325,6 @@ void mark_broken(mde_server* s, const std::string& msg) {
   if (!s->broken.load()) s->broken_msg = msg;
   s->broken.store(true);
   for (SlotWaiter* w : s->slot_waiters) w->cv.notify_one();  // under the lock: w lives on its caller's stack
-}
-
-int broken_error(mde_server* s, char* err, uint64_t cap) {
-  std::lock_guard<std::mutex> lk(s->m);
-  return failf(err, cap, MDE_E_DEVICE, "resident build service unusable: %s", s->broken_msg.c_str());
 }
 
 void give_slot(mde_server* s, uint32_t i) {
@@ -594,7 +573,10 @@ int server_build(mde_server* s, const mde_records* rec, const mde_tree_out* out_
   const bool fits = B <= s->max_buckets && in_bytes <= s->in_cap && ol.total <= s->out_cap &&
                     mde::server_plan(P, B, s->lds, &G, &words, &duo);
   s->n_req.fetch_add(1, std::memory_order_relaxed);
-  if (!fits) {  // the service's context: the ordinary synchronous build (a levels call gets every level)
+  // the service's context: the ordinary synchronous build (a levels call gets every level) -- for
+  // requests the resident workgroups do not take, and for every request once the resident launch
+  // is out of service (a failed launch, a timed-out request, mde_server_disable)
+  auto on_context = [&](const char* why) {
     s->n_ctx.fetch_add(1, std::memory_order_relaxed);
     std::vector<uint8_t> roots;
     mde_tree_out o = *out;
@@ -603,12 +585,13 @@ int server_build(mde_server* s, const mde_records* rec, const mde_tree_out* out_
       o.root = roots.data();
     }
     std::lock_guard<std::mutex> lk(s->ctx_m);
-    rc = mde_build(s->ctx, rec, &o);
-    if (rc) put_msg(err, err_cap, mde_last_error(s->ctx));
-    return rc;
-  }
+    const int r = mde_build(s->ctx, rec, &o);
+    if (r) failf(err, err_cap, r, "%s%s", why, mde_last_error(s->ctx));
+    return r;
+  };
+  if (!fits) return on_context("");
   const uint32_t i = take_slot(s);
-  if (i == UINT32_MAX) return broken_error(s, err, err_cap);
+  if (i == UINT32_MAX) return on_context("resident build service unusable, on its context: ");
   uint8_t* in_h = s->pin + s->in_off(i);
   const uint64_t in_d_pin = reinterpret_cast<uint64_t>(s->pin_dev + s->in_off(i));
   uint8_t* out_h = s->pin + s->out_off(i);
@@ -665,9 +648,10 @@ int server_build(mde_server* s, const mde_records* rec, const mde_tree_out* out_
     }
     give_slot(s, i);
   } else {
-    // the slot's workgroup may still write it: it stays out of the free list
-    put_msg(err, err_cap, msg.c_str());
+    // the slot's workgroup may still write it: it stays out of the free list; this call and every
+    // later one run on the service's context
     mark_broken(s, msg);
+    rc = on_context((msg + "; on the service's context: ").c_str());
   }
   return rc;
 }
@@ -717,18 +701,21 @@ int mde_server_verify(mde_server* s, uint32_t n_buckets, int32_t partition, int6
   const uint32_t cap = mde_verify_peer_capacity(B);
   const VerifyScratch vs = verify_scratch(B, R, nbytes);
   s->n_req.fetch_add(1, std::memory_order_relaxed);
-  if (B > s->max_buckets || R > kMaxPeers || !mde::verify_fused_fits(R, cap) || in_bytes > s->in_cap ||
-      out_bytes > s->out_cap || vs.off[12] > s->vscr_cap) {  // the service's context
+  // the service's context (see server_build)
+  auto on_context = [&](const char* why) {
     s->n_ctx.fetch_add(1, std::memory_order_relaxed);
     std::lock_guard<std::mutex> lk(s->ctx_m);
-    const int rc = mde_verify_epochs(s->ctx, 1, B, &partition, epoch, digest, size, nullptr, R, peer_bytes, peer_off,
-                                     replica_count, valid, valid_count, diff_ids, diff_count, peer_status, object_out,
-                                     object_stride, object_len);
-    if (rc) put_msg(err, err_cap, mde_last_error(s->ctx));
-    return rc;
-  }
+    const int r = mde_verify_epochs(s->ctx, 1, B, &partition, epoch, digest, size, nullptr, R, peer_bytes, peer_off,
+                                    replica_count, valid, valid_count, diff_ids, diff_count, peer_status, object_out,
+                                    object_stride, object_len);
+    if (r) failf(err, err_cap, r, "%s%s", why, mde_last_error(s->ctx));
+    return r;
+  };
+  if (B > s->max_buckets || R > kMaxPeers || !mde::verify_fused_fits(R, cap) || in_bytes > s->in_cap ||
+      out_bytes > s->out_cap || vs.off[12] > s->vscr_cap)
+    return on_context("");
   const uint32_t i = take_slot(s);
-  if (i == UINT32_MAX) return broken_error(s, err, err_cap);
+  if (i == UINT32_MAX) return on_context("resident build service unusable, on its context: ");
   uint8_t* in_h = s->pin + s->in_off(i);
   const uint8_t* in_pin_d = s->pin_dev + s->in_off(i);
   uint8_t* out_h = s->pin + s->out_off(i);
@@ -787,7 +774,7 @@ int mde_server_verify(mde_server* s, uint32_t n_buckets, int32_t partition, int6
   q.stage_bytes = a16(in_bytes);
   std::memcpy(&s->slot(i)->r, &q, sizeof q);
   std::string msg;
-  const int rc = post_and_wait(s, i, &msg);
+  int rc = post_and_wait(s, i, &msg);
   if (rc == MDE_OK) {
     *valid = out_h[0];
     std::memcpy(valid_count, out_h + 4, 4);
@@ -803,11 +790,19 @@ int mde_server_verify(mde_server* s, uint32_t n_buckets, int32_t partition, int6
       std::memcpy(object_out, out_h + o_obj, std::min<uint64_t>(len, ostride));
     }
     give_slot(s, i);
-  } else {
-    put_msg(err, err_cap, msg.c_str());  // the slot stays out of the free list (see above)
+  } else {  // the slot stays out of the free list; on the service's context (see server_build)
     mark_broken(s, msg);
+    rc = on_context((msg + "; on the service's context: ").c_str());
   }
   return rc;
+}
+
+int mde_server_usable(mde_server* s) { return s && !s->broken.load() ? 1 : 0; }
+
+int mde_server_disable(mde_server* s, const char* why) {
+  if (!s) return MDE_E_INVAL;
+  mark_broken(s, why && *why ? why : "disabled by the caller");
+  return MDE_OK;
 }
 
 }  // extern "C"

@@ -28,7 +28,9 @@
  *   server_hosttree  mde_server_build digest-only, then NewTree on the host;
  *   server_levels  mde_server_build_levels: digests and the tree's levels down to the first of at
  *                  most 64 nodes on the device, the top levels hashed on the host (the shim's
- *                  mdeTree finishing them with crypto/sha256).
+ *                  memo misses, hashed with crypto/sha256).
+ * The build rows report host_compressions_per_call: the SHA-256 compressions the caller ran on the
+ * host (0 where every node hash comes from the device: shim, server, percall).
  * VerifyEpoch decision step (main/manager.go:1072-1104; two peers, one agreeing, one differing):
  *   cpu_verify     per peer: EpochTreeObjectToMerkleTree (decode the 8-byte bucket hashes, NewTree)
  *                  and DifferentMerkleTreeBuckets against the local tree; validCount / diffSet fold;
@@ -75,6 +77,16 @@ void oracle_sha256(const uint8_t* msg, uint64_t len, uint8_t out[32]);
 /* The shim's top levels (mdeTree with mde_server_build_levels): levels above the first one of at
  * most top nodes, hashed on the host, node = SHA256(left || right), an odd level's last node
  * paired with itself -- merkletree v0.2.0's rule, on the CPU's SHA extensions like crypto/sha256. */
+static uint64_t g_host_comp; /* host SHA-256 compressions of the current case (atomic adds) */
+
+static void count_comp(uint64_t c) { __atomic_fetch_add(&g_host_comp, c, __ATOMIC_RELAXED); }
+
+/* compressions of a whole host tree (NewTree): one per 16-byte level-1 message, two above */
+static uint64_t tree_comp(uint32_t B) {
+  const uint64_t n1 = (B + 1) / 2;
+  return 2 * mde_tree_internal_nodes(B) - n1;
+}
+
 static void finish_top_levels(uint32_t B, uint32_t top, uint8_t* nodes) {
   uint32_t n = (B + 1) / 2;
   uint64_t off = 0;
@@ -91,6 +103,7 @@ static void finish_top_levels(uint32_t B, uint32_t top, uint8_t* nodes) {
       memcpy(msg + 32, nodes + (off + r) * 32, 32);
       oracle_sha256(msg, 64, nodes + (off + n + j) * 32);
     }
+    count_comp(2ull * m);
     off += n;
     n = m;
   }
@@ -299,6 +312,7 @@ static int call(int mode, part_t* p) {
     case CPU: {
       oracle_bucket_digests(p->vals, 8, NULL, p->seg, 1, B, p->dig, p->size, &p->items);
       oracle_graph* g = oracle_graph_build(p->dig, B);
+      count_comp(tree_comp(B));
       check_tree(p, g, "cpu");
       oracle_graph_free(g);
       return 0;
@@ -318,6 +332,7 @@ static int call(int mode, part_t* p) {
       mde_tree_out o = {p->dig, p->size, &p->items, NULL, NULL};
       if ((rc = mde_batch_build(batcher, &r, &o, err, sizeof err))) return rc;
       oracle_graph* g = oracle_graph_build(p->dig, B);
+      count_comp(tree_comp(B));
       check_tree(p, g, "shim_hosttree");
       oracle_graph_free(g);
       return 0;
@@ -335,6 +350,7 @@ static int call(int mode, part_t* p) {
       mde_tree_out o = {p->dig, p->size, &p->items, NULL, NULL};
       if ((rc = mde_server_build(server, &r, &o, err, sizeof err))) return rc;
       oracle_graph* g = oracle_graph_build(p->dig, B);
+      count_comp(tree_comp(B));
       check_tree(p, g, "server_hosttree");
       oracle_graph_free(g);
       return 0;
@@ -458,6 +474,7 @@ static void run_case(int mode, int P, uint64_t n, uint32_t B, part_t* parts, int
   uint64_t b0 = 0, r0 = 0, p0 = 0, b1 = 0, r1 = 0, p1 = 0, sc0 = 0, sc1 = 0;
   mde_batcher_stats(batcher, &b0, &r0, &p0);
   mde_server_stats(server, NULL, NULL, &sc0);
+  __atomic_store_n(&g_host_comp, 0, __ATOMIC_RELAXED);
   pthread_barrier_wait(&bar);
   const double t0 = now_s();
   for (int t = 0; t < P; t++) pthread_join(th[t], NULL);
@@ -482,6 +499,8 @@ static void run_case(int mode, int P, uint64_t n, uint32_t B, part_t* parts, int
   if ((mode == SHIM || mode == SHIM_HOSTTREE || mode == DEVICE_CALL || mode == V_BATCHED) && batches > 0)
     printf(", \"mean_requests_per_batch\": %.2f", (double)(r1 - r0) / batches);
   if (mode == SERVER || mode == SERVER_HOSTTREE || mode == SERVER_LEVELS || mode == V_SERVER) printf(", \"server_calls_on_context\": %" PRIu64, sc1 - sc0);
+  if (mode <= SERVER_LEVELS)  /* the build rows: SHA-256 compressions the caller ran on the host per call */
+    printf(", \"host_compressions_per_call\": %.1f", total ? (double)__atomic_load_n(&g_host_comp, __ATOMIC_RELAXED) / (double)total : 0.0);
   printf("}\n");
   fflush(stdout);
   free(all);

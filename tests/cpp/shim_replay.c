@@ -12,13 +12,17 @@
  *                       bucket, n_partitions = 1, value_stride = 0 (variable-length values); an
  *                       empty arena gets one padding byte. B > 64: -> mde_server_build_levels
  *                       (the shim's mdeResident: the device's levels down to <= 64 nodes, the
- *                       levels above hashed by mdeTree; mde_batch_build with the whole tree when
- *                       "batcher" is argv[2]) with the
- *                       nodes output, then the shim's mdeTree: the *merkletree.MerkleTree assembled
- *                       from the device's digests and node hashes (no host hashing; mirrored
- *                       below). B <= 64 (mdeHostTreeMaxBuckets): a digest-only mde_batch_build
- *                       (root = nodes = NULL), then NewTree on the host over the device digests
- *                       (the checker's SHA-256 tree stands in for merkletree's).
+ *                       levels above hashed on the host; mde_batch_build with the whole tree when
+ *                       "batcher" is argv[2]) with the nodes output, then the shim's mdeNewTree:
+ *                       merkletree v0.2.0's own construction (NewTreeWithHashStrategy, mirrored
+ *                       below as mt_new_tree) with the memoising strategy mdeMemoHash: every node
+ *                       message the device hashed is looked up in mdeMemo, every other one is
+ *                       hashed with SHA-256 (counted: the host compressions of the call). B <= 64
+ *                       (mdeHostTreeMaxBuckets): a digest-only build (root = nodes = NULL), then
+ *                       NewTree on the host over the device digests (no memo: every node hashed).
+ *                       The memo is then offered a tampered tree (one bucket digest + 1): its root
+ *                       must be the SHA-256 tree of the tampered digests -- a miss is hashed, the
+ *                       memo never answers for bytes the device did not hash.
  *   diff Ba Bb          DifferentMerkleTreeBuckets (main/merkle_tree.go:159-216), which the shim no
  *                       longer replaces: the reference's DFS over two trees of the shim's shape --
  *                       mdeTree over mde_tree_from_digests' nodes (a tree rebuilt from an odd-B
@@ -33,7 +37,8 @@
  *   verify B p E rc R <B digests> <B sizes> <R hex objects>
  * Output, one line per op:
  *   build <digests> ; <sizes> ; <items> ; <Root.Hash hex> ; <leaf count> <SHA-256 of the pre-order
- *         walk: every node's Hash, and each leaf's bucketId as LE32>
+ *         walk: every node's Hash, and each leaf's bucketId as LE32> ; <host compressions>
+ *         <tampered tree's root == the SHA-256 tree of the tampered digests (1/0)>
  *   diff <count> <ids>            (count = MDE_E_TREE where the reference errors)
  *   verify <valid> <validCount> ; <diffSet> ; <peer statuses> ; <object hex>
  */
@@ -50,10 +55,9 @@ int oracle_tree(const uint64_t* digest, uint32_t n_buckets, uint8_t* nodes, uint
 #define HOST_TREE_MAX_BUCKETS 64  /* merkle_gpu.go mdeHostTreeMaxBuckets */
 #define TOP_NODES 64              /* merkle_gpu.go mdeTopNodes */
 
-/* ---- the shim's mdeTree (integration/go/merkle_gpu.go), in C: merkletree v0.2.0's node graph
- * (leaf Hash = LE64(digest), a duplicate of the last leaf when B is odd -- same Hash, same
- * content --, level nodes pairing (2j, 2j+1) with the last of an odd level paired with itself)
- * whose internal Hash fields are the device's node hashes, level 1 .. root. */
+/* ---- merkletree v0.2.0's node graph (leaf Hash = LE64(digest), a duplicate of the last leaf when B
+ * is odd -- same Hash, same content --, level nodes pairing (2j, 2j+1) with the last of an odd level
+ * paired with itself). */
 typedef struct snode {
   struct snode *left, *right;
   const uint8_t* hash;
@@ -66,15 +70,90 @@ typedef struct {
   snode* root;
   uint32_t n_leafs;
   uint8_t* leaf_hash;
+  uint8_t* node_hash; /* mt_new_tree: the internal nodes' hashes */
 } stree;
 
 static void* xmalloc(size_t n);
 
-static stree mde_tree(const uint64_t* digest, uint32_t B, const uint8_t* nodes) {
+/* ---- the shim's mdeMemo / mdeMemoHash (integration/go/merkle_gpu.go): the k-th hasher merkletree's
+ * construction takes answers with device node k's hash when the message written to it is exactly
+ * node k's message (its children's hashes as the device hashed them), else runs SHA-256 (counted:
+ * the host compressions of the call). */
+typedef struct {
+  uint8_t* leaf;         /* [n0 * 8] LE64 leaf hashes (+ the odd-B duplicate) */
+  uint32_t n0;
+  const uint8_t* nodes;  /* the device's node hashes, level 1 .. root */
+  uint64_t have;         /* how many of them the device wrote */
+  uint32_t lvl[40], n_lvl;
+  uint64_t next;         /* the node the construction hashes next */
+  uint64_t compressions;
+} memo_t;
+
+static memo_t memo_build(const uint64_t* digest, uint32_t B, const uint8_t* nodes, uint64_t have) {
+  memo_t m;
+  memset(&m, 0, sizeof m);
+  m.n0 = B + (B & 1u);
+  m.leaf = xmalloc((size_t)m.n0 * 8);
+  for (uint32_t i = 0; i < B; i++)
+    for (int k = 0; k < 8; k++) m.leaf[(size_t)i * 8 + k] = (uint8_t)(digest[i] >> (8 * k));
+  if (B & 1u) memcpy(m.leaf + (size_t)B * 8, m.leaf + (size_t)(B - 1) * 8, 8);
+  m.nodes = nodes;
+  m.have = have;
+  for (uint32_t n = m.n0; n > 1;) {
+    n = (n + 1) / 2;
+    m.lvl[m.n_lvl++] = n;
+  }
+  return m;
+}
+
+/* node k's message as the device hashed it; 0 when k is past the device's nodes */
+static uint32_t memo_message(const memo_t* m, uint64_t k, uint8_t msg[64]) {
+  if (k >= m->have) return 0;
+  uint64_t off = 0, below = m->n0;
+  int64_t prev = -1;
+  for (uint32_t i = 0; i < m->n_lvl; i++) {
+    const uint64_t n = m->lvl[i];
+    if (k < off + n) {
+      const uint64_t j = k - off, li = 2 * j, ri = 2 * j + 1 < below ? 2 * j + 1 : 2 * j;
+      if (prev < 0) {
+        memcpy(msg, m->leaf + li * 8, 8);
+        memcpy(msg + 8, m->leaf + ri * 8, 8);
+        return 16;
+      }
+      memcpy(msg, m->nodes + ((uint64_t)prev + li) * 32, 32);
+      memcpy(msg + 32, m->nodes + ((uint64_t)prev + ri) * 32, 32);
+      return 64;
+    }
+    prev = (int64_t)off;
+    below = n;
+    off += n;
+  }
+  return 0;
+}
+
+/* mdeMemoHash.Sum for the construction's next node; memo == NULL: plain NewTree */
+static void strategy_sum(memo_t* m, const uint8_t* msg, uint32_t n, uint8_t out[32], uint64_t* compressions) {
+  if (m) {
+    const uint64_t k = m->next++;
+    uint8_t want[64];
+    const uint32_t wn = memo_message(m, k, want);
+    if (wn && wn == n && !memcmp(want, msg, n)) {
+      memcpy(out, m->nodes + k * 32, 32);
+      return;
+    }
+  }
+  *compressions += (n + 8) / 64 + 1;
+  oracle_sha256(msg, n, out);
+}
+
+/* merkletree.NewTreeWithHashStrategy (v0.2.0 buildWithContent + buildIntermediate), the strategy
+ * being strategy_sum over `memo` */
+static stree mt_new_tree(const uint64_t* digest, uint32_t B, memo_t* memo, uint64_t* compressions) {
   stree t;
   const uint32_t n0 = B + (B & 1u);
   t.pool = xmalloc(sizeof(snode) * (2 * (size_t)n0 + 64)); /* every level rounds up: < 2 n0 + depth */
   t.leaf_hash = xmalloc((size_t)B * 8);
+  t.node_hash = xmalloc(mde_tree_internal_nodes(B) * 32);
   t.n_leafs = n0;
   snode* level = t.pool;
   for (uint32_t i = 0; i < B; i++) {
@@ -90,7 +169,12 @@ static stree mde_tree(const uint64_t* digest, uint32_t B, const uint8_t* nodes) 
     for (uint32_t j = 0; j < m; j++) {
       snode* l = &level[2 * j];
       snode* r = 2 * j + 1 < n ? &level[2 * j + 1] : l;
-      next[j] = (snode){l, r, nodes + (off + j) * 32, 32, -1};
+      uint8_t msg[64];
+      memcpy(msg, l->hash, l->hlen);
+      memcpy(msg + l->hlen, r->hash, r->hlen);
+      uint8_t* h = t.node_hash + (off + j) * 32;
+      strategy_sum(memo, msg, l->hlen + r->hlen, h, compressions);
+      next[j] = (snode){l, r, h, 32, -1};
     }
     off += m;
     level = next;
@@ -98,6 +182,20 @@ static stree mde_tree(const uint64_t* digest, uint32_t B, const uint8_t* nodes) 
     n = m;
   }
   t.root = level;
+  return t;
+}
+
+/* The reference's DFS (below) over two trees rebuilt from digests: node hashes the device built
+ * (mde_tree_from_digests), in the same graph. */
+static stree mde_tree(const uint64_t* digest, uint32_t B, const uint8_t* nodes) {
+  memo_t m = memo_build(digest, B, nodes, mde_tree_internal_nodes(B));
+  uint64_t c = 0;
+  stree t = mt_new_tree(digest, B, &m, &c);
+  free(m.leaf);
+  if (c) {
+    fprintf(stderr, "tree from device nodes needed %llu host compressions\n", (unsigned long long)c);
+    exit(1);
+  }
   return t;
 }
 
@@ -250,28 +348,23 @@ int main(int argc, char** argv) {
         fprintf(stderr, "build: %d %s\n", rc, err);
         return 1;
       }
-      if (resident && !host_tree) { /* mdeTree hashes the levels above the device's (crypto/sha256) */
-        uint32_t n = (B + 1) / 2;
-        uint64_t off = 0;
-        while (n > TOP_NODES && n > 1) {
-          off += n;
-          n = (n + 1) / 2;
-        }
-        while (n > 1) {
-          const uint32_t m = (n + 1) / 2;
-          uint8_t msg[64];
-          for (uint32_t j = 0; j < m; j++) {
-            const uint32_t l = 2 * j, rr = 2 * j + 1 < n ? 2 * j + 1 : 2 * j;
-            memcpy(msg, nodes + (off + l) * 32, 32);
-            memcpy(msg + 32, nodes + (off + rr) * 32, 32);
-            oracle_sha256(msg, 64, nodes + (off + n + j) * 32);
-          }
-          off += n;
-          n = m;
-        }
-      }
-      if (host_tree) oracle_tree(digest, B, nodes, root);
-      stree t = mde_tree(digest, B, nodes);
+      /* mdeNewTree: merkletree's construction over the memo of the device's nodes (the first
+       * `have`: every node through the batcher, the levels down to <= mdeTopNodes nodes through the
+       * service); or plain NewTree over the device digests (B <= mdeHostTreeMaxBuckets) */
+      const uint64_t have = host_tree ? 0 : resident ? mde_tree_prefix_nodes(B, TOP_NODES) : mde_tree_internal_nodes(B);
+      memo_t memo = memo_build(digest, B, nodes, have);
+      uint64_t compressions = 0;
+      stree t = mt_new_tree(digest, B, host_tree ? NULL : &memo, &compressions);
+      /* the memo offered a tampered tree: one bucket's digest + 1 */
+      uint64_t* tampered = xmalloc((uint64_t)B * 8);
+      memcpy(tampered, digest, (uint64_t)B * 8);
+      tampered[B / 2] = (tampered[B / 2] + 1) % MDE_HASH_MOD;
+      uint64_t tc = 0;
+      memo.next = 0; /* a second construction over the same memo */
+      stree tt = mt_new_tree(tampered, B, &memo, &tc);
+      uint8_t troot[32];
+      oracle_tree(tampered, B, NULL, troot);
+      const int tamper_ok = !memcmp(troot, tt.root->hash, 32) && tc > 0;
       uint8_t* wb = NULL;
       uint64_t wl = 0, wc = 0;
       walk(t.root, &wb, &wl, &wc);
@@ -285,12 +378,13 @@ int main(int argc, char** argv) {
       print_hex(t.root->hash, 32);
       printf(" ; %u ", t.n_leafs);
       print_hex(wsig, 32);
-      printf("\n");
-      if (!(resident && !host_tree) && memcmp(root, t.root->hash, 32)) { /* split levels: no device root */
+      printf(" ; %" PRIu64 " %d\n", compressions, tamper_ok);
+      if (!host_tree && !resident && memcmp(root, t.root->hash, 32)) { /* split levels: no device root */
         fprintf(stderr, "device root differs from the assembled tree's root\n");
         return 1;
       }
-      free(wb), free(t.pool), free(t.leaf_hash), free(nodes);
+      free(wb), free(t.pool), free(t.leaf_hash), free(t.node_hash), free(nodes);
+      free(tt.pool), free(tt.leaf_hash), free(tt.node_hash), free(tampered), free(memo.leaf);
       free(bucket), free(values), free(value_off), free(seg_rec), free(digest), free(size);
     } else if (!strcmp(op, "diff")) {
       const uint32_t Ba = (uint32_t)num(f), Bb = (uint32_t)num(f);
@@ -312,7 +406,8 @@ int main(int argc, char** argv) {
       printf("diff %d", count);
       for (int32_t i = 0; i < count; i++) printf(" %d", ids[i]);
       printf("\n");
-      free(ta.pool), free(ta.leaf_hash), free(tb.pool), free(tb.leaf_hash), free(na), free(nb);
+      free(ta.pool), free(ta.leaf_hash), free(ta.node_hash), free(tb.pool), free(tb.leaf_hash), free(tb.node_hash);
+      free(na), free(nb);
       free(da), free(db), free(ids);
     } else if (!strcmp(op, "verify")) {
       const uint32_t B = (uint32_t)num(f);

@@ -159,17 +159,178 @@ def test_group_symbols_and_cpu_behaviour():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gpus", [1, 2])
-def test_bench_group_mode(gpus):
+@pytest.mark.parametrize("gpus,config", [(1, "c4"), (2, "c4"), (8, "c4"), (1, "c5"), (8, "c5")])
+def test_bench_group_mode(gpus, config):
     """bench.py's N-GPU path (--engine group) end to end on the box: one process, the shards of
-    BASELINE config 4 over `gpus` groups members (GPU 0 listed `gpus` times: --rehearse), pipelined
-    builds and bucketed root gathers; its parity block (gathered slabs, the C-oracle sample of
-    shard 0) is all true."""
+    BASELINE config 4 (or 5: both replicas, diff, extract) over `gpus` group members (GPU 0 listed
+    `gpus` times: --rehearse), pipelined builds and side-stream root gathers; its parity block
+    (gathered slabs, the C-oracle sample of shard 0; C5: every gathered diff count and shard 0's
+    diff and extract) is all true, and the line carries the per-build gather cost and the host
+    enqueue time the >= 6x target depends on."""
     cmd = [sys.executable, str(ROOT / "bench.py"), "--engine", "group", "--gpus", str(gpus), "--steps", "9",
-           "--warmup", "2"] + (["--rehearse"] if gpus > 1 else [])
+           "--warmup", "2", "--config", config] + (["--rehearse"] if gpus > 1 else [])
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["parity"]["all_ranks_ok"], d["parity"]
     assert d["config"]["engine"] == "group" and d["n_gpus"] == gpus
     assert ("rccl" in d["config"]["root_gather"]) == (gpus == 1)
+    assert d["host_timing"]["enqueue_ms_per_step"] > 0
+    if config == "c4":
+        assert d["root_gather_per_build"]["gathered_roots_match_after_run"]
+        assert d["root_gather_per_build"]["bare_gather_ms"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("overlapped", [False, True], ids=["in_stream", "overlapped"])
+def test_gather_send_slab_rewritten_right_after_the_gather(overlapped):
+    """The exchange step's stream-order contract with the copy gather (a device listed three
+    times): work enqueued on a context stream after the gather -- here each device rewriting its
+    own send slab at once -- must not change what the other devices receive. The in-stream gather
+    makes every context stream wait for every device's copies; the overlapped one does once the
+    caller waits on its ticket (mde_group_gather_wait_async) before the rewrite."""
+    import torch
+    import mydatastore_amd as mde
+    G, nbytes = 3, 64 << 20
+    g = mde.Group([0] * G)
+    dev = torch.device("cuda:0")
+    lib = mde.load_library()
+    streams = [torch.cuda.ExternalStream(lib.mde_get_stream(g.ctx(i)), device=dev) for i in range(G)]
+    send = [torch.full((nbytes,), i + 1, dtype=torch.uint8, device=dev) for i in range(G)]
+    recv = [torch.zeros(G * nbytes, dtype=torch.uint8, device=dev) for _ in range(G)]
+    torch.cuda.synchronize(dev)
+    for rep in range(3):
+        if overlapped:
+            t = g.gather_overlapped_async(send, recv, nbytes)
+            g.gather_wait_async(t)
+        else:
+            g.gather_async(send, recv, nbytes)
+        for i in range(G):  # the rewrite, in stream order right after the gather
+            with torch.cuda.stream(streams[i]):
+                send[i].fill_(0xEE)
+        g.synchronize()
+        for i in range(G):
+            got = recv[i].view(G, nbytes)
+            for r in range(G):
+                assert bool((got[r] == r + 1 + 16 * rep).all()), (rep, i, r)
+        for i in range(G):
+            send[i].fill_(i + 1 + 16 * (rep + 1))
+            recv[i].zero_()
+        torch.cuda.synchronize(dev)
+    g.close()
+
+
+def _c5_single(engine, P, B, V, n):
+    """BASELINE config 5 in one engine: replicas A and B of the whole workload, diff + extract."""
+    import torch
+    import mydatastore_amd as mde
+    from mydatastore_amd.workload import Workload, make_workload, perturb_replica
+    w = make_workload(engine, n_partitions=P, n_buckets=B, value_len=V, part_mode="mod", n_keys=n)
+    vb, touched = perturb_replica(w)
+    wb = Workload(engine, vb, w.seg_rec, P, B, w.n_records, V, w.partition_ids)
+    oa, ob = w.build(), wb.build()
+    cap = mde.diff_capacity(B, B)
+    dev = w.values.device
+    ids = torch.zeros(P * cap, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(P, dtype=torch.int32, device=dev)
+    engine.diff_async(P, B, oa["digest"], oa["nodes"], B, ob["digest"], ob["nodes"], ids, cap, cnt)
+    rec_cap = max(w.n_records // 8, 1024)
+    part_off = torch.zeros(P + 1, dtype=torch.int64, device=dev)
+    out_rec = torch.zeros(rec_cap, dtype=torch.int64, device=dev)
+    out_vals = torch.zeros(rec_cap * V, dtype=torch.uint8, device=dev)
+    out_voff = torch.zeros(rec_cap + 1, dtype=torch.int64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    engine.extract_async(wb.rec, ids, cap, cnt, part_off, out_rec, rec_cap, out_vals, out_voff, rec_cap * V, status)
+    engine.synchronize()
+    po = part_off.cpu().numpy().astype(np.int64)
+    vals = out_vals.cpu().numpy()
+    per_part = [vals[po[p] * V:po[p + 1] * V].tobytes() for p in range(P)]
+    c = cnt.cpu().numpy()
+    idl = ids.cpu().numpy().reshape(P, cap)
+    return {"roots_a": oa["root"].cpu().numpy().reshape(P, 32), "roots_b": ob["root"].cpu().numpy().reshape(P, 32),
+            "counts": c, "ids": [idl[p, :c[p]].tolist() for p in range(P)], "extract": per_part,
+            "status": int(status.item()), "touched": touched}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [1, 2, 8])
+def test_group_c5_diff_extract_and_gather(engine, G):
+    """BASELINE config 5 on the mde_group path (the one the Go shim's process reaches): each
+    device builds both replicas of its partitions (pipelined, as bench.py times it), diffs them and
+    extracts replica B's records of the differing buckets on the device (mde_group_diff_async,
+    mde_group_extract_async), and the [A roots | B roots | diff counts] slabs are all-gathered on
+    the side streams (mde_group_gather_overlapped_async). The gathered slabs, every shard's diff
+    ids and extracted bytes equal the single-engine C5 result; the diff of every partition is
+    exactly its perturbed bucket."""
+    import torch
+    import mydatastore_amd as mde
+    from mydatastore_amd.workload import Workload, make_workload, perturb_replica
+    P, B, V, n = 48, 64, 64, 120_000
+    ref = _c5_single(engine, P, B, V, n)
+    assert ref["status"] == 0
+    for p in range(P):
+        assert ref["ids"][p] == ([ref["touched"][p]] if p in ref["touched"] else [])
+    g = mde.Group([0] * G)
+    dev = torch.device("cuda:0")
+    slab = -(-P // G)
+    cap = mde.diff_capacity(B, B)
+    shards, repl, outs, args_d, args_x, x, keep = [], [], [], [], [], [], []
+    send = [torch.zeros(slab * 68, dtype=torch.uint8, device=dev) for _ in range(G)]
+    recv = [torch.zeros(G * slab * 68, dtype=torch.uint8, device=dev) for _ in range(G)]
+    for i in range(G):
+        w = make_workload(engine, n_partitions=P, n_buckets=B, value_len=V, part_mode="mod", n_keys=n, rank=i, world=G)
+        vb, _ = perturb_replica(w)
+        wb = Workload(engine, vb, w.seg_rec, w.n_partitions, B, w.n_records, V, w.partition_ids)
+        Pl = w.n_partitions
+        oa, ob = w._outs()[0], wb._outs()[0]
+        keep.append((oa, ob))  # the output tensors live as long as the group's launches
+        base = send[i].data_ptr()
+        to_a = mde.TreeOut(oa["digest"].data_ptr(), oa["size"].data_ptr(), oa["items"].data_ptr(), base,
+                           oa["nodes"].data_ptr())
+        to_b = mde.TreeOut(ob["digest"].data_ptr(), ob["size"].data_ptr(), ob["items"].data_ptr(), base + slab * 32,
+                           ob["nodes"].data_ptr())
+        ids = torch.zeros(Pl * cap, dtype=torch.int32, device=dev)
+        rec_cap = max(w.n_records // 8, 1024)
+        t = {"ids": ids, "part_off": torch.zeros(Pl + 1, dtype=torch.int64, device=dev),
+             "out_rec": torch.zeros(rec_cap, dtype=torch.int64, device=dev),
+             "out_vals": torch.zeros(rec_cap * V, dtype=torch.uint8, device=dev),
+             "out_voff": torch.zeros(rec_cap + 1, dtype=torch.int64, device=dev),
+             "status": torch.zeros(1, dtype=torch.int32, device=dev)}
+        counts_ptr = base + slab * 64  # the diff counts land in the send slab itself
+        args_d.append(mde.DiffArgs(Pl, B, B, oa["digest"].data_ptr(), oa["nodes"].data_ptr(), ob["digest"].data_ptr(),
+                                   ob["nodes"].data_ptr(), ids.data_ptr(), cap, counts_ptr))
+        args_x.append(mde.ExtractArgs(ids.data_ptr(), cap, counts_ptr, t["part_off"].data_ptr(),
+                                      t["out_rec"].data_ptr(), rec_cap, t["out_vals"].data_ptr(),
+                                      t["out_voff"].data_ptr(), rec_cap * V, t["status"].data_ptr()))
+        shards.append(w)
+        repl.append(wb)
+        outs.append((to_a, to_b))
+        x.append(t)
+    torch.cuda.synchronize(dev)
+    # replica A then replica B, pipelined: B's launch completes A's trees, the drain B's
+    g.build_async([w.rec for w in shards], [o[0] for o in outs], pipelined=True)
+    g.build_async([w.rec for w in repl], [o[1] for o in outs], pipelined=True)
+    g.drain_async()
+    g.diff_async(args_d)
+    g.extract_async([w.rec for w in repl], args_x)
+    ticket = g.gather_overlapped_async(send, recv, slab * 68)
+    g.gather_wait_async(ticket)
+    g.synchronize()
+    for i in range(1, G):
+        assert torch.equal(recv[i], recv[0])
+    got = recv[0].cpu().numpy().reshape(G, slab * 68)
+    for r in range(G):
+        pids = shards[r].partition_ids
+        k = len(pids)
+        assert np.array_equal(got[r, :k * 32].reshape(k, 32), ref["roots_a"][pids]), r
+        assert np.array_equal(got[r, slab * 32:slab * 32 + k * 32].reshape(k, 32), ref["roots_b"][pids]), r
+        assert np.array_equal(got[r, slab * 64:slab * 64 + k * 4].view(np.int32), ref["counts"][pids]), r
+        assert int(x[r]["status"].item()) == 0
+        ids = x[r]["ids"].cpu().numpy().reshape(k, cap)
+        po = x[r]["part_off"].cpu().numpy().astype(np.int64)
+        vals = x[r]["out_vals"].cpu().numpy()
+        cnt = ref["counts"][pids]
+        for j, p in enumerate(pids):
+            assert ids[j, :cnt[j]].tolist() == ref["ids"][p], (r, p)
+            assert vals[po[j] * V:po[j + 1] * V].tobytes() == ref["extract"][p], (r, p)
+    g.close()

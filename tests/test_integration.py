@@ -70,15 +70,27 @@ def test_shim_names_exist_in_header():
 def test_shim_reimplements_the_reference_signatures():
     """The replaced function keeps the reference's Go signature (main/merkle_tree.go:86); the
     reference's own DifferentMerkleTreeBuckets (:159-216) stays, so the shim must not redefine it
-    (two definitions in package main would not compile), and the trees the shim returns carry the
-    exported fields that DFS reads (Root, Left, Right, Hash, C) plus Leafs (:122)."""
+    (two definitions in package main would not compile). Every tree the shim returns is built by
+    merkletree itself -- NewTree, or NewTreeWithHashStrategy fed by the memo of device node hashes
+    -- never as a struct literal, whose unexported merkleRoot / leaf / dup / Tree fields would stay
+    unset (MerkleRoot() nil, VerifyTree() walking into nil children)."""
     src = GO.read_text()
     code = re.sub(r"//.*", "", src)
     assert ("func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, upperEpoch int64) "
             "(*merkletree.MerkleTree, error)") in src
     assert "func DifferentMerkleTreeBuckets(" not in code
-    for field in ("t.Leafs", "t.Root", "Left: l, Right: r, Hash: h", "Hash: h, C: c"):
-        assert field in code, field
+    assert "merkletree.MerkleTree{" not in code and "merkletree.Node{" not in code
+    assert "merkletree.NewTreeWithHashStrategy(cs, func() hash.Hash" in code
+    assert "return merkletree.NewTree(bucketList)" in code
+    # mdeMemoHash is a hash.Hash (io.Writer + Sum + Reset + Size + BlockSize)
+    for method in ("Write(p []byte) (int, error)", "Sum(b []byte) []byte", "Reset()", "Size() int",
+                   "BlockSize() int"):
+        assert f"func (h *mdeMemoHash) {method}" in code, method
+    # Sum answers from the device only for node k's exact message, and copies out (merkletree
+    # appends to the hashes it gets back); the memo is switched off once the tree exists
+    assert "bytes.Equal(h.buf[:len(l)], l) && bytes.Equal(h.buf[len(l):], r)" in code
+    assert "return append(b, h.m.nodes[h.k*32:(h.k+1)*32]...)" in code
+    assert "m.active, m.nodes = false, nil" in code
 
 
 # ---------------------------------------------------------------------------------------------
@@ -107,7 +119,31 @@ def _walk_sig(root):
     return hashlib.sha256(bytes(out)).hexdigest()
 
 
-def _replay_scenarios():
+def _levels(B):
+    """Node counts of merkletree v0.2.0's internal levels for B buckets (level 1 .. root)."""
+    n, out = B + (B & 1), []
+    while n > 1:
+        n = (n + 1) // 2
+        out.append(n)
+    return out
+
+
+def _host_compressions(B, path):
+    """SHA-256 compressions the shim runs on the host for one B-bucket tree (mdeHostCompressions):
+    B <= 64 -- NewTree over the device digests, every node (one compression per 16-byte level-1
+    message, two per 64-byte message above); B > 64 through the resident service -- the nodes above
+    the device's levels (down to the first of at most mdeTopNodes = 64 nodes); through the batcher
+    -- none, every node hash comes from the device."""
+    lv = _levels(B)
+    if B <= 64:
+        return lv[0] + 2 * sum(lv[1:])
+    if path == "batcher":
+        return 0
+    k = next(i for i, n in enumerate(lv) if n <= 64)
+    return 2 * sum(lv[k + 1:])
+
+
+def _replay_scenarios(path="resident"):
     """(input tokens, expected output line) per op, from the oracle (oracle/oracle.py)."""
     import numpy as np
     from oracle import oracle as O
@@ -129,7 +165,8 @@ def _replay_scenarios():
         t = O.tree_from_digests(d, z)
         items = O.merkle_tree_to_partition_epoch_object(t, 0, 0, 1).items
         expect.append(f"build {' '.join(map(str, d))} ; {' '.join(map(str, z))} ; {items} ; "
-                      f"{t.merkle_root().hex()} ; {len(t.leafs)} {_walk_sig(t.root)}")
+                      f"{t.merkle_root().hex()} ; {len(t.leafs)} {_walk_sig(t.root)} ; "
+                      f"{_host_compressions(B, path)} 1")
         return list(map(int, d)), list(map(int, z))
 
     build(31, 300, rng.integers(0, 41, 300))                  # variable lengths, empty values, odd B
@@ -137,6 +174,10 @@ def _replay_scenarios():
     d1000, z1000 = build(1000, 5000, [8] * 5000)               # the reference's default B
     build(30, 0, [])                                           # no records: one padding byte
     d31, z31 = build(31, 200, rng.integers(1, 17, 200))
+    # the memoised merkletree construction just above the host-tree cutoff, at odd and even B, and
+    # past the service's 1,024-bucket launch (the service's context writes every level there)
+    for B, n in ((65, 400), (100, 700), (1023, 4000), (5000, 20000)):
+        build(B, n, [8] * n)
 
     # DifferentMerkleTreeBuckets (the reference's DFS over two trees of the shim's shape): local
     # B = 31 (merkletree duplicates the last leaf) against a tree rebuilt from an odd-B object
@@ -199,16 +240,19 @@ def _replay_scenarios():
 def test_shim_call_sequences_replayed_from_c_match_oracle(tmp_path, path):
     """The Go shim's exact ABI call sequences (integration/go/merkle_gpu.go, which cannot be
     compiled here), replayed in C: RawPartitionMerkleTree's one-partition arena with value_off
-    built record by record -> mde_server_build (the shim's default; mde_batch_build for
-    path="batcher") with nodes -> the tree assembled from the device's
-    node hashes (mdeTree: Root.Hash, leaf count and the whole pre-order walk equal NewTree's);
+    built record by record -> mde_server_build_levels (the shim's default; mde_batch_build for
+    path="batcher") with nodes -> merkletree's own construction fed by the memo of the device's
+    node hashes (mdeNewTree: Root.Hash, leaf count and the whole pre-order walk equal NewTree's;
+    host compressions = the nodes above the device's levels through the service, 0 through the
+    batcher, every node for B <= 64; a tampered tree misses the memo and is hashed for real) at
+    B in {30, 31, 64, 65, 100, 1000, 1023, 5000};
     the reference's DFS over trees of that shape, B local leaves against B + 1 peer leaves
     (odd-B object quirk, SURVEY App. A.2);
     verifyEpochDecision with agreeing, absent, garbage, Valid-differing and other-B peers ->
     mde_server_verify / mde_batch_verify. Every output equals the oracle's restatement of the reference
     (main/merkle_tree.go:86-216, main/manager.go:1072-1104)."""
     import subprocess
-    lines, expect = _replay_scenarios()
+    lines, expect = _replay_scenarios(path)
     f = tmp_path / "scenarios.txt"
     f.write_text("\n".join(lines) + "\n")
     r = subprocess.run([str(REPLAY), str(f), path], capture_output=True, text=True, timeout=120)

@@ -235,3 +235,84 @@ def test_tree_prefix_nodes_matches_level_walk():
                 n = (n + 1) // 2
             assert lib.mde_tree_prefix_nodes(B, top) == t, (B, top)
         assert lib.mde_tree_prefix_nodes(B, 0) == lib.mde_tree_internal_nodes(B)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,n", [(2000, 3000), (1000, 40000)])
+def test_server_levels_on_the_service_context(coracle, B, n):
+    """mde_server_build_levels for a request the resident workgroups do not take -- B beyond the
+    launch's 1,024 buckets, or more than 256 KiB of packed inputs -- runs as mde_build on the
+    service's context: the prefix of levels the caller reads equals the oracle's nodes (the nodes
+    past it are unspecified there: that path writes every level)."""
+    import mydatastore_amd as mde
+    rng = np.random.default_rng(B + n)
+    vals = rng.integers(1, 1 << 40, n, dtype=np.uint64).view(np.uint8).copy()
+    seg = np.concatenate([[0], np.sort(rng.integers(0, n + 1, B - 1)), [n]]).astype(np.uint64)
+    sv = mde.Server(0)
+    try:
+        before = sv.stats()["on_context"]
+        got = sv.build_levels(vals, seg, 1, B, 64, value_stride=8)
+        assert sv.stats()["on_context"] == before + 1
+    finally:
+        sv.close()
+    exp = coracle.build(vals, seg, 1, B, 8)
+    pre = got["prefix_nodes"]
+    assert np.array_equal(got["nodes"].reshape(-1, 32)[:pre], exp["nodes"].reshape(-1, 32)[:pre])
+    assert np.array_equal(got["digest"], exp["digest"]) and np.array_equal(got["size"], exp["size"])
+    assert np.array_equal(got["items"], exp["items"])
+
+
+@pytest.mark.gpu
+def test_disabled_service_serves_every_call_on_its_context(coracle):
+    """Once the resident launch is out of service (mde_server_disable here; a failed launch or a
+    30 s request timeout take the same path) every later build and decision runs on the service's
+    context instead of failing, with the oracle's results, from concurrent callers."""
+    from oracle import oracle as O
+    from oracle import wire_pb
+    import mydatastore_amd as mde
+    sv = mde.Server(0)
+    try:
+        assert sv.usable
+        sv.disable("test")
+        assert not sv.usable
+        errors = []
+
+        def caller(t):
+            try:
+                rng = np.random.default_rng(100 + t)
+                for k in range(4):
+                    B = (64, 1000)[k % 2]
+                    n = 1000
+                    vals = rng.integers(1, 1 << 40, n, dtype=np.uint64).view(np.uint8).copy()
+                    seg = np.concatenate([[0], np.sort(rng.integers(0, n + 1, B - 1)), [n]]).astype(np.uint64)
+                    got = sv.build(vals, seg, 1, B, value_stride=8)
+                    exp = coracle.build(vals, seg, 1, B, 8)
+                    for key in ("digest", "size", "items", "root", "nodes"):
+                        if not np.array_equal(got[key], exp[key]):
+                            errors.append((t, k, key))
+                    d = [int(x) for x in exp["digest"]]
+                    z = [int(x) for x in exp["size"]]
+                    peer = list(d)
+                    peer[3] = (peer[3] + 1) % 999999
+                    tree = O.tree_from_digests(peer, z)
+                    obj = O.merkle_tree_to_partition_epoch_object(tree, 5, 2, 3)
+                    blob = wire_pb.marshal(5, 2, 3, [O.decode_bytes_to_int64(h) for h in obj.buckets],
+                                           obj.buckets_size, valid=False, items=obj.items)
+                    v = sv.verify(B, exp["digest"], exp["size"], [blob, None], 2, 2, partition=5)
+                    w = O.verify_epoch(O.tree_from_digests(d, z), 5, 2, [blob, None], 2)
+                    if (v["valid"] != w["valid"] or v["valid_count"] != w["valid_count"] or v["diff"] != w["diff"]
+                            or v["object"] != w["object"]):
+                        errors.append((t, k, "verify"))
+            except Exception as e:  # noqa: BLE001
+                errors.append((t, repr(e)))
+
+        th = [threading.Thread(target=caller, args=(t,)) for t in range(4)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errors, errors[:5]
+        st = sv.stats()
+        assert st["on_context"] == st["requests"] == 32
+    finally:
+        sv.close()

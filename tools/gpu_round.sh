@@ -14,6 +14,9 @@
 #           the service + shim-replay pytest                         -> st{1,2,3}.json, service_pytest.log
 #   callbench  batch_bench at B = 64 / 1,000 x 1 / 10 / 100 callers  -> bb.jsonl (+ summary)
 #   stress  resident service under 4-64 callers, 1-100 ms lifetimes -> stress{1..5}.json
+#   teardown  tools/stream_teardown phases a (minimal) and b (the service's sequence), once each
+#           -> teardown_{a,b}.txt (run it last: a hang ends the call)
+#   testsall  -m gpu parity suite without -x (every failure listed)  -> pytest_gpu_all.log
 #   callers the service at 10 / 100 callers with its wait totals (MDE_SERVER_DEBUG), user / system
 #           CPU seconds and the cgroup's cpu.stat; SLOTS="16 32" sweeps the slot count -> callers.txt
 # Extra bench flags: BENCH_ARGS="...".
@@ -30,6 +33,17 @@ for s in "$@"; do
       timeout -k 10 1000 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread \
         > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
       tail -3 $O/pytest_gpu.log ;;
+    testsall)
+      step testsall
+      timeout -k 10 1100 python -u -m pytest tests -v -m gpu -p no:cacheprovider --timeout 150 --timeout-method thread \
+        > $O/pytest_gpu_all.log 2>&1 || { grep -E "FAILED|ERROR|Timeout" $O/pytest_gpu_all.log | head -40; tail -5 $O/pytest_gpu_all.log; exit 1; }
+      tail -3 $O/pytest_gpu_all.log ;;
+    teardown)
+      step teardown
+      for ph in a b; do
+        timeout -k 10 60 tools/stream_teardown $ph > $O/teardown_$ph.txt 2>&1 || { cat $O/teardown_$ph.txt; exit 1; }
+        cat $O/teardown_$ph.txt
+      done ;;
     smoke)
       step smoke
       timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
