@@ -483,6 +483,7 @@ __host__ __device__ constexpr uint32_t rec8_lds_bytes(int rows) { return rec8_wa
 #ifdef MDE_WAVE_STAMPS  // probe only: per-wave entry / first step / exit times (s_memrealtime, 100 MHz)
 constexpr uint32_t kStampWaves = 16384;
 __device__ unsigned long long g_wave_stamps[3 * kStampWaves];
+__device__ unsigned long long g_tree_stamps[2 * kStampWaves];  // fused step: tree waves' entry, exit
 __device__ __forceinline__ void wave_stamp(int k) {
   const uint32_t w = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
   const unsigned long long t = __builtin_amdgcn_s_memrealtime();
@@ -952,8 +953,18 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
   const uint32_t db = blockIdx.x;
 #else
   if (blockIdx.x < tree_blocks) {
+#ifdef MDE_WAVE_STAMPS  // probe only: every tree wave's entry and exit
+    const unsigned long long te = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifndef MDE_STEP_SKIP_TREES  // probe only: the dispatch shape without the tree work
     step_trees(t, Q, blockIdx.x, lds);
+#endif
+#ifdef MDE_WAVE_STAMPS
+    const uint32_t tw = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && tw < kStampWaves) {
+      g_tree_stamps[2 * tw] = te;
+      g_tree_stamps[2 * tw + 1] = __builtin_amdgcn_s_memrealtime();
+    }
 #endif
     return;
   }
@@ -1210,6 +1221,17 @@ int bucket_digest_variants() { return kNumVariants; }
 }  // namespace mde
 extern "C" int mde_probe_wave_stamps(unsigned long long* host, uint64_t n) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mde::g_wave_stamps), n * 8 > sizeof(mde::g_wave_stamps) ? sizeof(mde::g_wave_stamps) : n * 8);
+}
+extern "C" int mde_probe_tree_stamps(unsigned long long* host, uint64_t n, int reset) {
+  const size_t bytes = n * 8 > sizeof(mde::g_tree_stamps) ? sizeof(mde::g_tree_stamps) : n * 8;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(mde::g_tree_stamps), bytes) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long zero[3 * mde::kStampWaves] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(mde::g_tree_stamps), zero, sizeof(mde::g_tree_stamps)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(mde::g_wave_stamps), zero, sizeof(mde::g_wave_stamps)) != hipSuccess)
+      return -1;
+  }
+  return 0;
 }
 namespace mde {
 #endif

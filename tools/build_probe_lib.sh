@@ -10,6 +10,7 @@ done
 hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -Iinclude "$@" -c mydatastore_amd/csrc/mde_api.cpp -o $out/mde_api.o
 hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -Iinclude "$@" -c mydatastore_amd/csrc/batch.cpp -o $out/batch.o
 hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -Iinclude "$@" -c mydatastore_amd/csrc/group.cpp -o $out/group.o
+hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -Iinclude "$@" -c mydatastore_amd/csrc/server.cpp -o $out/server.o
 hipcc -shared --offload-arch=gfx950 -pthread -o tools/ab/libmde_$name.so $out/*.o -ldl
 rm -rf $out
 echo tools/ab/libmde_$name.so

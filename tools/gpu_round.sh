@@ -16,6 +16,12 @@
 #   stress  resident service under 4-64 callers, 1-100 ms lifetimes -> stress{1..5}.json
 #   teardown  tools/stream_teardown phases a (minimal) and b (the service's sequence), once each
 #           -> teardown_{a,b}.txt (run it last: a hang ends the call)
+#   stepprobe fused-step per-wave timeline at the production shape (tools/step_probe.py, probe
+#           library tools/ab/libmde_$PROBE_LIB.so, default stamps)        -> step_probe.jsonl
+#   groupbench bench.py --engine group at 1 GPU (RCCL) and 8 members on GPU 0 (--rehearse), C4 and C5
+#           -> bench_group_{1,8}_{c4,c5}.json
+#   serviceab bulk pipelined builds with no service / an idle one / one serving 10 callers
+#           (tools/service_ab.py, C4 and PROD)                        -> service_ab_{c4,prod}.jsonl
 #   testsall  -m gpu parity suite without -x (every failure listed)  -> pytest_gpu_all.log
 #   callers the service at 10 / 100 callers with its wait totals (MDE_SERVER_DEBUG), user / system
 #           CPU seconds and the cgroup's cpu.stat; SLOTS="16 32" sweeps the slot count -> callers.txt
@@ -38,11 +44,34 @@ for s in "$@"; do
       timeout -k 10 1100 python -u -m pytest tests -v -m gpu -p no:cacheprovider --timeout 150 --timeout-method thread \
         > $O/pytest_gpu_all.log 2>&1 || { grep -E "FAILED|ERROR|Timeout" $O/pytest_gpu_all.log | head -40; tail -5 $O/pytest_gpu_all.log; exit 1; }
       tail -3 $O/pytest_gpu_all.log ;;
+    stepprobe)
+      step stepprobe
+      MDE_LIBRARY=tools/ab/libmde_${PROBE_LIB:-stamps}.so timeout -k 10 180 python tools/step_probe.py ${PROBE_ARGS:-} \
+        > $O/step_probe.jsonl 2> $O/step_probe.err || { tail -20 $O/step_probe.err; exit 1; }
+      cat $O/step_probe.jsonl ;;
+    groupbench)
+      step groupbench
+      for spec in "1 c4" "1 c5" "8 c4" "8 c5"; do
+        set -- $spec
+        rh=""; [ $1 -gt 1 ] && rh="--rehearse"
+        timeout -k 10 300 python bench.py --engine group --gpus $1 --config $2 $rh ${BENCH_ARGS:-} \
+          > $O/bench_group_$1_$2.json 2> $O/bench_group_$1_$2.err || { tail -20 $O/bench_group_$1_$2.err; exit 1; }
+        cat $O/bench_group_$1_$2.json
+      done ;;
+    serviceab)
+      step serviceab
+      for shp in c4 prod; do
+        timeout -k 10 240 python tools/service_ab.py $shp 3 10 > $O/service_ab_$shp.jsonl 2> $O/service_ab_$shp.err || { tail -20 $O/service_ab_$shp.err; exit 1; }
+        cat $O/service_ab_$shp.jsonl
+      done ;;
     teardown)
       step teardown
-      for ph in a b; do
-        timeout -k 10 60 tools/stream_teardown $ph > $O/teardown_$ph.txt 2>&1 || { cat $O/teardown_$ph.txt; exit 1; }
+      for ph in ${TEARDOWN_PHASES:-a b}; do
+        timeout -k 10 60 tools/stream_teardown $ph > $O/teardown_$ph.txt 2>&1
+        rc=$?
+        echo "exit status $rc" >> $O/teardown_$ph.txt
         cat $O/teardown_$ph.txt
+        [ $rc -eq 0 ] || exit 1
       done ;;
     smoke)
       step smoke
