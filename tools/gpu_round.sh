@@ -22,6 +22,8 @@
 #           -> bench_group_{1,8}_{c4,c5}.json
 #   serviceab bulk pipelined builds with no service / an idle one / one serving 10 callers
 #           (tools/service_ab.py, C4 and PROD)                        -> service_ab_{c4,prod}.jsonl
+#   cumask1   the service with MDE_SERVER_CUMASK=1 (its CU-masked stream destroyed with it): server_test
+#           twice and tests/test_server.py once                        -> cumask1_*.txt / .log
 #   testsall  -m gpu parity suite without -x (every failure listed)  -> pytest_gpu_all.log
 #   callers the service at 10 / 100 callers with its wait totals (MDE_SERVER_DEBUG), user / system
 #           CPU seconds and the cgroup's cpu.stat; SLOTS="16 32" sweeps the slot count -> callers.txt
@@ -64,6 +66,19 @@ for s in "$@"; do
         timeout -k 10 240 python tools/service_ab.py $shp 3 10 > $O/service_ab_$shp.jsonl 2> $O/service_ab_$shp.err || { tail -20 $O/service_ab_$shp.err; exit 1; }
         cat $O/service_ab_$shp.jsonl
       done ;;
+    cumask1)
+      step cumask1  # the resident service destroying its CU-masked stream with itself (the r04m sequence)
+      export MDE_SERVER_CUMASK=1 MDE_SERVER_DEBUG=1
+      for a in "1 14 100" "10 40 100"; do
+        f=$O/cumask1_st_${a// /_}.txt
+        timeout -k 10 90 tests/cpp/build/server_test $a > $f 2>&1
+        rc=$?; echo "exit status $rc" >> $f; cat $f
+        [ $rc -eq 0 ] || exit 1
+      done
+      timeout -k 10 300 python -u -m pytest tests/test_server.py -m gpu -v -p no:cacheprovider --timeout 120 \
+        --timeout-method thread > $O/cumask1_pytest.log 2>&1 || { tail -30 $O/cumask1_pytest.log; exit 1; }
+      tail -3 $O/cumask1_pytest.log
+      unset MDE_SERVER_CUMASK MDE_SERVER_DEBUG ;;
     teardown)
       step teardown
       for ph in ${TEARDOWN_PHASES:-a b}; do
