@@ -818,10 +818,17 @@ int mde_create(int device, mde_ctx** out) {
 
 void mde_destroy(mde_ctx* c) {
   if (!c) return;
+  // MDE_TEARDOWN_TRACE=1: one stderr line before each step (a teardown that hangs names its step)
+  static const bool trace = std::getenv("MDE_TEARDOWN_TRACE") != nullptr;
+  auto step = [&](const char* what) {
+    if (trace) std::fprintf(stderr, "mde_destroy(%p): %s\n", static_cast<void*>(c), what), std::fflush(stderr);
+  };
   {
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceScope ds(c->device);
+    step("synchronize the stream");
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    step("free device buffers");
     if (c->sums) (void)hipFree(c->sums);
     if (c->counts) (void)hipFree(c->counts);
     if (c->steal) (void)hipFree(c->steal);
@@ -834,19 +841,25 @@ void mde_destroy(mde_ctx* c) {
     if (c->nodes_scratch.p) (void)hipFree(c->nodes_scratch.p);
     if (c->packed_in.p) (void)hipFree(c->packed_in.p);
     if (c->packed_out.p) (void)hipFree(c->packed_out.p);
+    step("free pinned host buffers");
     if (c->pin_in.p) (void)hipHostFree(c->pin_in.p);
     if (c->pin_out.p) (void)hipHostFree(c->pin_out.p);
+    step("free scratch");
     if (c->extract_scratch.p) (void)hipFree(c->extract_scratch.p);
     if (c->verify_scratch.p) (void)hipFree(c->verify_scratch.p);
     if (c->deep_scratch.p) (void)hipFree(c->deep_scratch.p);
+    step("free rings and events");
     for (int i = 0; i < 2; i++) {
       for (auto* b : {&c->ring_vals[i], &c->ring_voff[i], &c->ring_seg[i]})
         if (b->p) (void)hipFree(b->p);
       if (c->ev_loaded[i]) (void)hipEventDestroy(c->ev_loaded[i]);
       if (c->ev_done[i]) (void)hipEventDestroy(c->ev_done[i]);
     }
+    step(c->copy_stream ? "destroy the copy stream" : "no copy stream");
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    step("destroy the own stream");
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    step("done");
   }
   delete c;
 }

@@ -497,10 +497,18 @@ void mde_server_destroy(mde_server* s) {
       std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
   }
+  // MDE_SERVER_CTX_FIRST=1 (teardown probe): the service's context before its launch stream
+  const bool ctx_first = std::getenv("MDE_SERVER_CTX_FIRST") != nullptr;
   if (ended) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (dbg) std::fprintf(stderr, "mde_server_destroy: stream synchronized %.6f s\n", since());
+    if (ctx_first && s->ctx) {
+      mde_destroy(s->ctx);
+      s->ctx = nullptr;
+      if (dbg) std::fprintf(stderr, "mde_server_destroy: context destroyed first %.6f s\n", since());
+    }
     if (s->exit_ev) (void)hipEventDestroy(s->exit_ev);
+    if (dbg) std::fprintf(stderr, "mde_server_destroy: destroying the launch stream %.6f s\n", since());
     if (s->stream && !s->keep_stream) (void)hipStreamDestroy(s->stream);
     if (s->stream && s->keep_stream) {
       std::lock_guard<std::mutex> lk(g_kept_m);

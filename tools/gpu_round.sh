@@ -68,17 +68,15 @@ for s in "$@"; do
       done ;;
     cumask1)
       step cumask1  # the resident service destroying its CU-masked stream with itself (the r04m sequence)
-      export MDE_SERVER_CUMASK=1 MDE_SERVER_DEBUG=1
-      for a in "1 14 100" "10 40 100"; do
-        f=$O/cumask1_st_${a// /_}.txt
-        timeout -k 10 90 tests/cpp/build/server_test $a > $f 2>&1
+      export MDE_SERVER_CUMASK=1 MDE_SERVER_DEBUG=1 MDE_TEARDOWN_TRACE=1
+      for v in ${CUMASK_VARIANTS:-plain}; do
+        f=$O/cumask1_$v.txt
+        if [ $v = ctxfirst ]; then export MDE_SERVER_CTX_FIRST=1; else unset MDE_SERVER_CTX_FIRST; fi
+        timeout -k 10 90 tests/cpp/build/server_test 1 14 100 > $f 2>&1
         rc=$?; echo "exit status $rc" >> $f; cat $f
         [ $rc -eq 0 ] || exit 1
       done
-      timeout -k 10 300 python -u -m pytest tests/test_server.py -m gpu -v -p no:cacheprovider --timeout 120 \
-        --timeout-method thread > $O/cumask1_pytest.log 2>&1 || { tail -30 $O/cumask1_pytest.log; exit 1; }
-      tail -3 $O/cumask1_pytest.log
-      unset MDE_SERVER_CUMASK MDE_SERVER_DEBUG ;;
+      unset MDE_SERVER_CUMASK MDE_SERVER_DEBUG MDE_TEARDOWN_TRACE MDE_SERVER_CTX_FIRST ;;
     teardown)
       step teardown
       for ph in ${TEARDOWN_PHASES:-a b}; do
