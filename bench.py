@@ -315,13 +315,17 @@ def main_group(args):
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo")
-    if rank != 0:  # the node's one process is rank 0; the others wait at its three barriers
-        for _ in range(3):
+    c5 = args.config == "c5"
+    # rank 0's barriers: two around each timed run (the bucketed run, and for C4 the run with one
+    # gather per build) and one at the end; every other rank joins exactly as many
+    per_build_run = not c5 and not args.no_gather_per_build and args.steps > 0
+    n_barriers = 2 * (2 if per_build_run else 1) + 1
+    if rank != 0:  # the node's one process is rank 0; the others only join its barriers
+        for _ in range(n_barriers):
             dist.barrier()
         dist.destroy_process_group()
         return
     N = args.gpus
-    c5 = args.config == "c5"
     n_dev = torch.cuda.device_count()
     devices = [0] * N if args.rehearse else list(range(N))
     if max(devices) >= n_dev:
@@ -531,7 +535,7 @@ def main_group(args):
     # C4: the same builds with ONE gather per build, and K bare gathers of one build's slabs: the
     # fixed cost per build the >= 6x target at 8 GPUs depends on
     per_build = None
-    if not c5 and not args.no_gather_per_build and args.steps > 0:
+    if per_build_run:
         one = Run(1)
         ms1, dev1_ms, ht1 = timed(one, args.steps, 1)
         k1 = (args.steps - 1) % 2

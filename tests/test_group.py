@@ -334,3 +334,21 @@ def test_group_c5_diff_extract_and_gather(engine, G):
             assert ids[j, :cnt[j]].tolist() == ref["ids"][p], (r, p)
             assert vals[po[j] * V:po[j + 1] * V].tobytes() == ref["extract"][p], (r, p)
     g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["c4", "c5"])
+def test_bench_group_under_torchrun(config):
+    """The driver's N-GPU invocation (`torch.distributed.run --nproc-per-node N bench.py --gpus N`):
+    rank 0 drives the group, the other ranks only join its barriers -- the same number of them for
+    every config (two around each timed run, one at the end), or a rank would wait forever. Two
+    ranks, both shards on GPU 0 (--rehearse)."""
+    env = {**os.environ, "MASTER_ADDR": "127.0.0.1"}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+           "--gpus", "2", "--steps", "4", "--warmup", "1", "--rehearse", "--config", config]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["parity"]["all_ranks_ok"] and d["launcher_ranks"] == 2 and d["config"]["engine"] == "group"
+    assert ("root_gather_per_build" in d) == (config == "c4")
