@@ -236,7 +236,8 @@ std::vector<Req*> take(mde_batcher* b, Req* first) {
   std::vector<Req*> out{first};
   const uint64_t per_part = first->kind == Kind::Build ? first->rec.n_buckets : 1;
   uint64_t parts = first->parts;
-  b->q.erase(std::find(b->q.begin(), b->q.end(), first));
+  const auto self = std::find(b->q.begin(), b->q.end(), first);
+  if (self != b->q.end()) b->q.erase(self);
   for (auto it = b->q.begin(); it != b->q.end();) {
     Req* x = *it;
     if (same_key(x, first) && parts + x->parts <= b->max_parts && (parts + x->parts) * per_part <= 0xffffffffull) {

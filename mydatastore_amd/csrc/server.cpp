@@ -366,11 +366,6 @@ int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_se
   s->wall_khz = (uint32_t)khz;
   s->lifetime_ticks = life_ms * (uint64_t)khz;
   if (const char* e = std::getenv("MDE_SERVER_STAGE")) s->stage = std::atoi(e) != 0;
-  int rc = mde_create(device, &s->ctx);
-  if (rc != MDE_OK) {
-    delete s;
-    return rc;
-  }
   auto bail = [&](int code) {
     mde_server_destroy(s);
     return code;
@@ -447,6 +442,11 @@ int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_se
     s->exit_ev = nullptr;
     return bail(MDE_E_DEVICE);
   }
+  // The service's own context (requests the resident workgroups do not take), created AFTER the
+  // launch stream: a stream created before a CU-masked stream and destroyed after it hung in
+  // hipStreamDestroy (ROCm 7.2); created after it, either order completes (DESIGN.md section 7,
+  // profiles/r05/r05g_teardown_bisect.txt). mde_server_destroy also destroys it first.
+  if (int rc = mde_create(device, &s->ctx)) return bail(rc);
   s->seq.assign(s->n_slots, 0);
   for (uint32_t i = 0; i < s->n_slots; i++) {
     s->free_slots.push_back(s->n_slots - 1 - i);
@@ -497,15 +497,14 @@ void mde_server_destroy(mde_server* s) {
       std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
   }
-  // MDE_SERVER_CTX_FIRST=1 (teardown probe): the service's context before its launch stream
-  const bool ctx_first = std::getenv("MDE_SERVER_CTX_FIRST") != nullptr;
   if (ended) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (dbg) std::fprintf(stderr, "mde_server_destroy: stream synchronized %.6f s\n", since());
-    if (ctx_first && s->ctx) {
+    // the service's context before its launch stream (see mde_server_create)
+    if (s->ctx) {
       mde_destroy(s->ctx);
       s->ctx = nullptr;
-      if (dbg) std::fprintf(stderr, "mde_server_destroy: context destroyed first %.6f s\n", since());
+      if (dbg) std::fprintf(stderr, "mde_server_destroy: context destroyed %.6f s\n", since());
     }
     if (s->exit_ev) (void)hipEventDestroy(s->exit_ev);
     if (dbg) std::fprintf(stderr, "mde_server_destroy: destroying the launch stream %.6f s\n", since());

@@ -250,6 +250,34 @@ int main(int argc, char** argv) {
   const char* life = argc > 3 ? argv[3] : "100";
   setenv("MDE_SERVER_LIFETIME_MS", life, 1);
   const long life_ms = atol(life);
+  /* SERVER_TEST_EARLY_CTX=1: a context created before the service, used, and destroyed after it
+   * (the teardown order of a process whose other contexts outlive its services) */
+  mde_ctx* early = NULL;
+  if (getenv("SERVER_TEST_EARLY_CTX")) {
+    if (mde_create(0, &early)) {
+      fprintf(stderr, "mde_create (early): failed\n");
+      return 1;
+    }
+    uint8_t v[64] = {1, 2, 3};
+    uint64_t seg[3] = {0, 4, 8};
+    uint64_t dig[2];
+    int32_t sz[2], it;
+    uint8_t root[32];
+    mde_records r;
+    memset(&r, 0, sizeof r);
+    r.values = v;
+    r.values_bytes = sizeof v;
+    r.value_stride = 8;
+    r.n_records = 8;
+    r.n_partitions = 1;
+    r.n_buckets = 2;
+    r.seg_rec = seg;
+    mde_tree_out o = {dig, sz, &it, root, NULL};
+    if (mde_build(early, &r, &o)) {
+      fprintf(stderr, "mde_build (early): %s\n", mde_last_error(early));
+      return 1;
+    }
+  }
   int rc = mde_server_create(0, 0, 0, &server);
   if (rc) {
     fprintf(stderr, "mde_server_create: %d\n", rc);
@@ -285,6 +313,10 @@ int main(int argc, char** argv) {
   fprintf(stderr, "service destroyed\n");
   mde_destroy(ctx);
   fprintf(stderr, "context destroyed\n");
+  if (early) {
+    mde_destroy(early);
+    fprintf(stderr, "early context destroyed\n");
+  }
   const int relaunched = launches1 >= launches0 + 6;
   printf("{\"server_test\": {\"threads\": %d, \"calls\": %ld, \"verifies\": %ld, \"mismatches\": %ld, \"requests\": %" PRIu64
          ", \"launches_before_idle\": %" PRIu64 ", \"launches\": %" PRIu64 ", \"on_context\": %" PRIu64

@@ -67,16 +67,22 @@ for s in "$@"; do
         cat $O/service_ab_$shp.jsonl
       done ;;
     cumask1)
-      step cumask1  # the resident service destroying its CU-masked stream with itself (the r04m sequence)
+      step cumask1  # the resident service destroying its CU-masked stream with itself (MDE_SERVER_CUMASK=1)
       export MDE_SERVER_CUMASK=1 MDE_SERVER_DEBUG=1 MDE_TEARDOWN_TRACE=1
       for v in ${CUMASK_VARIANTS:-plain}; do
         f=$O/cumask1_$v.txt
-        if [ $v = ctxfirst ]; then export MDE_SERVER_CTX_FIRST=1; else unset MDE_SERVER_CTX_FIRST; fi
+        if [ $v = early ]; then export SERVER_TEST_EARLY_CTX=1; else unset SERVER_TEST_EARLY_CTX; fi
         timeout -k 10 90 tests/cpp/build/server_test 1 14 100 > $f 2>&1
         rc=$?; echo "exit status $rc" >> $f; cat $f
         [ $rc -eq 0 ] || exit 1
       done
-      unset MDE_SERVER_CUMASK MDE_SERVER_DEBUG MDE_TEARDOWN_TRACE MDE_SERVER_CTX_FIRST ;;
+      unset MDE_SERVER_DEBUG MDE_TEARDOWN_TRACE SERVER_TEST_EARLY_CTX
+      if [ -n "${CUMASK_PYTEST:-}" ]; then
+        timeout -k 10 400 python -u -m pytest tests/test_server.py tests/test_integration.py -m gpu -v -p no:cacheprovider \
+          --timeout 120 --timeout-method thread > $O/cumask1_pytest.log 2>&1 || { tail -30 $O/cumask1_pytest.log; exit 1; }
+        tail -3 $O/cumask1_pytest.log
+      fi
+      unset MDE_SERVER_CUMASK ;;
     teardown)
       step teardown
       for ph in ${TEARDOWN_PHASES:-a b}; do
