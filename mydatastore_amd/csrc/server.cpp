@@ -22,8 +22,8 @@
 // that posts and then reads `closed` set waits for the launch to end and relaunches (a request
 // is served either by the closing workgroup's last read or by the next launch, never lost).
 // The launch runs on a CU-masked stream: such a stream gets a hardware queue of its own, so no
-// other stream of the process queues behind the persistent kernel (kept for the process, see
-// mde_server_create).
+// other stream of the process queues behind the persistent kernel (destroyed with the service, its
+// context destroyed first: see mde_server_create).
 // Requests the resident workgroups do not take (more partitions than one workgroup holds, inputs
 // or outputs beyond a slot, B beyond the launch's LDS) run as mde_build on the service's own
 // context. Each caller gets exactly what mde_build returns for its inputs (tests/cpp/server_test.c
@@ -80,7 +80,7 @@ constexpr double kWaitTimeoutS = 30.0;
 constexpr double kSpinS = 10e-6;  // pure spinning before a waiting caller starts yielding
 constexpr uint32_t kMaxPeers = 16;  // decision steps with more peers run on the service's context
 
-// CU-masked streams kept for the process (see mde_server_create), per device: a service takes one
+// MDE_SERVER_CUMASK=2: CU-masked streams kept for the process (see mde_server_create), per device: a service takes one
 // no live service holds (two services on one stream would queue each launch behind the other's
 // lifetime) and hands it back when its launch has ended.
 constexpr int kKeptDevices = 64;
@@ -110,7 +110,7 @@ struct mde_server {
   uint8_t* vscr = nullptr;     // [n_slots x vscr_cap] decision-step scratch (peer digests, nodes, diffs, ...)
   uint64_t vscr_cap = 0;
   hipStream_t stream = nullptr;
-  bool keep_stream = false;  // a process-lifetime stream (MDE_SERVER_CUMASK=2)
+  bool keep_stream = false;  // a process-lifetime stream (MDE_SERVER_CUMASK=2, the round-4 pool)
   hipEvent_t exit_ev = nullptr;
   bool running = false;
   std::mutex launch_m;
@@ -409,14 +409,17 @@ int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_se
   std::vector<uint32_t> mask((size_t)std::max(1, (cus + 31) / 32), 0u);
   for (int c = 0; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
   // The launch's stream: a CU-masked stream (all CUs) gets a hardware queue of its own, so no other
-  // stream of the process queues behind the persistent kernel. It is kept for the process and
-  // reused by a later service on the device, never by two live ones (g_kept_free): destroying a
-  // CU-masked stream made a later
-  // hipStreamDestroy of another stream hang (ROCm 7, profiles/r04/r04n_service_streams.txt).
-  // MDE_SERVER_CUMASK=0: a plain non-blocking stream instead; 1: a CU-masked stream destroyed
-  // with the service (probes).
+  // stream of the process queues behind the persistent kernel; it is destroyed with the service.
+  // Round 4 kept it for the process instead, because destroying it made a later hipStreamDestroy
+  // hang (profiles/r04/r04n_service_streams.txt). Round 5 found the order that hangs: the
+  // service's own context, created before this stream and destroyed after it
+  // (profiles/r05/r05g_teardown_bisect.txt); the context is now created after the stream and
+  // destroyed before it, and destroy-with-service passes the service tests, including a context
+  // that outlives the service (r05h). MDE_SERVER_CUMASK=0: a plain non-blocking stream instead;
+  // 2: the round-4 pool (a CU-masked stream kept for the process, reused by a later service on
+  // the device, never by two live ones).
   const char* cm = std::getenv("MDE_SERVER_CUMASK");
-  const int cmode = cm ? std::atoi(cm) : 2;
+  const int cmode = cm ? std::atoi(cm) : 1;
   s->keep_stream = cmode == 2 && device >= 0 && device < kKeptDevices;
   hipError_t se = hipSuccess;
   if (cmode == 0) {
