@@ -663,6 +663,9 @@ int build_pipelined(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
       mde_ctx::Slot& ps = c->pipe[pd.slot];
       rc = tree_launch_for(c, &pd.rec, &pd.out, ps.sums, ps.counts, &t);
       if (rc) return rc;
+#ifdef MDE_PROBE_STEP_TOP_NODES  // probe only (wrong roots): the trees stop at their first level of <= N nodes
+      t.top_nodes = MDE_PROBE_STEP_TOP_NODES;
+#endif
     }
     hipError_t e = mde::launch_build_step(a, pd.active ? &t : nullptr, c->stream);
     if (e != hipSuccess) {

@@ -46,6 +46,15 @@ for s in "$@"; do
       timeout -k 10 1100 python -u -m pytest tests -v -m gpu -p no:cacheprovider --timeout 150 --timeout-method thread \
         > $O/pytest_gpu_all.log 2>&1 || { grep -E "FAILED|ERROR|Timeout" $O/pytest_gpu_all.log | head -40; tail -5 $O/pytest_gpu_all.log; exit 1; }
       tail -3 $O/pytest_gpu_all.log ;;
+    topprobe)
+      step topprobe  # A/B: the production-shape fused step with and without the wide trees' top levels
+      for rep in 1 2 3; do
+        for lib in mydatastore_amd/libmde.so tools/ab/libmde_${PROBE_LIB:-top64}.so; do
+          MDE_LIBRARY=$lib timeout -k 10 180 python tools/top_probe.py $(basename $lib) 2 >> $O/top_probe.jsonl 2>> $O/top_probe.err \
+            || { tail -20 $O/top_probe.err; exit 1; }
+        done
+      done
+      cat $O/top_probe.jsonl ;;
     stepprobe)
       step stepprobe
       MDE_LIBRARY=tools/ab/libmde_${PROBE_LIB:-stamps}.so timeout -k 10 180 python tools/step_probe.py ${PROBE_ARGS:-} \
