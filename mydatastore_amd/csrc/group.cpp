@@ -306,7 +306,7 @@ int check(const mde_records* r, const mde_tree_out* o, std::string& msg) {
 int ctx_err(mde_group* g, uint32_t i, int rc, std::string& msg) {
   char m[512];
   mde_last_error_copy(g->ctx[i], m, sizeof m);
-  return fail(msg, rc, "device %d: %s", g->dev[i], m);
+  return fail(msg, rc, "member %u (device %d): %s", i, g->dev[i], m);
 }
 
 // Enqueue threads. A device-resident group call launches work on every device (a pipelined build

@@ -347,6 +347,17 @@ int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_se
   if (!out) return MDE_E_INVAL;
   *out = nullptr;
   if (n_slots > kMaxSlots || max_buckets > mde::kTreeLdsMaxBuckets) return MDE_E_INVAL;
+  {  // the device checks mde_create makes, before any allocation (its context is created later)
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+      (void)hipGetLastError();
+      return MDE_E_DEVICE;
+    }
+    if (device < 0 || device >= n) return MDE_E_INVAL;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+      return MDE_E_DEVICE;
+  }
   mde_server* s = new (std::nothrow) mde_server();
   if (!s) return MDE_E_NOMEM;
   s->device = device;

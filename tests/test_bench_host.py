@@ -56,3 +56,29 @@ def test_cpu_share_rule():
     assert bench.cpu_share(info) == 8
     h = bench.host_cpu_info()
     assert h["nproc"] and "cpu_model" in h
+
+
+def test_group_bench_ranks_join_rank0s_barriers():
+    """CPU: under torch.distributed.run the group bench's rank 0 drives every GPU and the other
+    ranks only join its barriers, so their count must equal rank 0's: two around each timed run
+    (the bucketed run, plus for C4 the run with one gather per build) and one at the end. Counted
+    from bench.py's source, so a new barrier on one side fails here instead of hanging a launch."""
+    import ast
+    from tests.conftest import ROOT
+    src = (ROOT / "bench.py").read_text()
+    tree = ast.parse(src)
+    mg = next(n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "main_group")
+    timed = next(n for n in ast.walk(mg) if isinstance(n, ast.FunctionDef) and n.name == "timed")
+
+    def barriers(node):
+        return sum(1 for n in ast.walk(node) if isinstance(n, ast.Call) and isinstance(n.func, ast.Attribute)
+                   and n.func.attr == "barrier")
+    per_timed = barriers(timed)
+    calls_of_timed = sum(1 for n in ast.walk(mg) if isinstance(n, ast.Call) and isinstance(n.func, ast.Name)
+                         and n.func.id == "timed")
+    others = barriers(mg) - per_timed  # outside timed(): the non-zero ranks' loop + rank 0's final one
+    assert per_timed == 2 and calls_of_timed == 2 and others == 2
+    # the non-zero ranks' count: 2 per timed run + 1, the per-build run only for C4 with steps > 0
+    assert "n_barriers = 2 * (2 if per_build_run else 1) + 1" in src
+    assert "per_build_run = not c5 and not args.no_gather_per_build and args.steps > 0" in src
+    assert "if per_build_run:\n        one = Run(1)" in src

@@ -352,3 +352,35 @@ def test_bench_group_under_torchrun(config):
     d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert d["parity"]["all_ranks_ok"] and d["launcher_ranks"] == 2 and d["config"]["engine"] == "group"
     assert ("root_gather_per_build" in d) == (config == "c4")
+
+
+@pytest.mark.gpu
+def test_group_errors_name_the_failing_member(engine):
+    """With one enqueue thread per member, a failure on one member still comes back as the call's
+    error, naming that member; the other members' shares were enqueued and the group stays usable.
+    An unknown gather ticket is MDE_E_INVAL."""
+    import torch
+    import mydatastore_amd as mde
+    from mydatastore_amd.workload import make_workload
+    G, P, B, V, n = 3, 30, 64, 32, 30_000
+    g = mde.Group([0] * G)
+    shards = [make_workload(engine, n_partitions=P, n_buckets=B, value_len=V, part_mode="mod", n_keys=n, rank=i,
+                            world=G) for i in range(G)]
+    outs = [w._outs() for w in shards]
+    bad = mde.Records.from_buffer_copy(shards[2].rec)
+    bad.n_buckets = 0  # rejected by mde_build_async on member 2
+    with pytest.raises(mde.MdeError) as ei:
+        g.build_async([shards[0].rec, shards[1].rec, bad], [o[1] for o in outs])
+    assert ei.value.code == mde.MDE_E_INVAL and "member 2" in str(ei.value)
+    g.synchronize()
+    with pytest.raises(mde.MdeError) as ei:
+        g.gather_wait_async(12345)
+    assert ei.value.code == mde.MDE_E_INVAL
+    g.build_async([w.rec for w in shards], [o[1] for o in outs])  # still usable
+    g.synchronize()
+    whole = make_workload(engine, n_partitions=P, n_buckets=B, value_len=V, part_mode="mod", n_keys=n)
+    want = whole.build()["root"].cpu().numpy().reshape(P, 32)
+    for i, w in enumerate(shards):
+        assert np.array_equal(outs[i][0]["root"].cpu().numpy().reshape(-1, 32), want[w.partition_ids])
+    g.close()
+    torch.cuda.synchronize()
