@@ -253,19 +253,21 @@ def _c5_single(engine, P, B, V, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("G", [1, 2, 8])
-def test_group_c5_diff_extract_and_gather(engine, G):
+@pytest.mark.parametrize("G,P,B,V,n", [(1, 48, 64, 64, 120_000), (2, 48, 64, 64, 120_000), (8, 48, 64, 64, 120_000),
+                                       (8, 5, 64, 32, 20_000), (3, 37, 999, 8, 90_000), (5, 64, 130, 24, 70_000)],
+                         ids=["G1", "G2", "G8", "G8-P5-members-without-partitions", "G3-odd-B999-8B", "G5-B130"])
+def test_group_c5_diff_extract_and_gather(engine, G, P, B, V, n):
     """BASELINE config 5 on the mde_group path (the one the Go shim's process reaches): each
     device builds both replicas of its partitions (pipelined, as bench.py times it), diffs them and
     extracts replica B's records of the differing buckets on the device (mde_group_diff_async,
     mde_group_extract_async), and the [A roots | B roots | diff counts] slabs are all-gathered on
     the side streams (mde_group_gather_overlapped_async). The gathered slabs, every shard's diff
     ids and extracted bytes equal the single-engine C5 result; the diff of every partition is
-    exactly its perturbed bucket."""
+    exactly its perturbed bucket. Shapes: 1/2/8 members, more members than partitions (members
+    with nothing to build still take part in the gather), odd B with 8-byte values, B = 130."""
     import torch
     import mydatastore_amd as mde
     from mydatastore_amd.workload import Workload, make_workload, perturb_replica
-    P, B, V, n = 48, 64, 64, 120_000
     ref = _c5_single(engine, P, B, V, n)
     assert ref["status"] == 0
     for p in range(P):
