@@ -14,6 +14,7 @@ import sys
 import numpy as np
 import pytest
 
+from oracle import oracle as O
 from tests.conftest import ROOT
 from tests.datasets import MODES, synth_arrays
 
@@ -248,6 +249,7 @@ def _c5_single(engine, P, B, V, n):
     c = cnt.cpu().numpy()
     idl = ids.cpu().numpy().reshape(P, cap)
     return {"roots_a": oa["root"].cpu().numpy().reshape(P, 32), "roots_b": ob["root"].cpu().numpy().reshape(P, 32),
+            "digest_a": oa["digest"].cpu().numpy().reshape(P, B), "digest_b": ob["digest"].cpu().numpy().reshape(P, B),
             "counts": c, "ids": [idl[p, :c[p]].tolist() for p in range(P)], "extract": per_part,
             "status": int(status.item()), "touched": touched}
 
@@ -270,8 +272,13 @@ def test_group_c5_diff_extract_and_gather(engine, G, P, B, V, n):
     from mydatastore_amd.workload import Workload, make_workload, perturb_replica
     ref = _c5_single(engine, P, B, V, n)
     assert ref["status"] == 0
-    for p in range(P):
-        assert ref["ids"][p] == ([ref["touched"][p]] if p in ref["touched"] else [])
+    for p in range(P):  # the DFS diff of the perturbed bucket: repeated once per odd level on its
+        # path (the reference visits a self-paired node's child twice), nothing for the others
+        if p in ref["touched"]:
+            assert ref["ids"][p] == O.diff_from_digests(ref["digest_a"][p], ref["digest_b"][p])
+            assert set(ref["ids"][p]) == {ref["touched"][p]}
+        else:
+            assert ref["ids"][p] == [] and np.array_equal(ref["digest_a"][p], ref["digest_b"][p])
     g = mde.Group([0] * G)
     dev = torch.device("cuda:0")
     slab = -(-P // G)
