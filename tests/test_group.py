@@ -265,7 +265,7 @@ def test_group_c5_diff_extract_and_gather(engine, G, P, B, V, n):
     mde_group_extract_async), and the [A roots | B roots | diff counts] slabs are all-gathered on
     the side streams (mde_group_gather_overlapped_async). The gathered slabs, every shard's diff
     ids and extracted bytes equal the single-engine C5 result; the diff of every partition is
-    exactly its perturbed bucket. Shapes: 1/2/8 members, more members than partitions (members
+    the oracle's DFS diff: its perturbed bucket, once per odd level on the bucket's path. Shapes: 1/2/8 members, more members than partitions (members
     with nothing to build still take part in the gather), odd B with 8-byte values, B = 130."""
     import torch
     import mydatastore_amd as mde
