@@ -37,6 +37,11 @@ sys.path.insert(0, str(ROOT))
 METRIC = "Merkle-tree build GiB/s (device-resident KV bytes hashed/s) at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 GATHER_BUCKET = 8  # builds per root-gather collective in fused mode at N > 1
+# Default warm-up: at least 3 steps and at least this much device time. After an idle spell (the
+# host-side parity checks before the timed run) the shader clock takes ~10-20 ms of load to come
+# back: the production shape (VALU-issue bound) reads ~190 us per build after 3 warm-up builds and
+# ~170 after 100, while C4 (HBM bound) moves < 0.5 % (profiles/r05/r05p_clock_ramp.jsonl).
+WARMUP_MIN_MS = 25.0
 
 CONFIGS = {
     # name: (n_keys, n_partitions, value_len, n_buckets, part_mode, description)
@@ -60,7 +65,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps before the K timed ones (default: >= 3 steps covering >= "
+                         "WARMUP_MIN_MS of device time, calibrated on 3 extra untimed steps)")
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS) + ["c5"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -98,6 +105,15 @@ def parse():
                          "the path a Go node calls); ranks: one process per GPU, torch.distributed root "
                          "gather; auto (default): group for N > 1, the single-engine path at N = 1")
     return ap.parse_args()
+
+
+def resolve_warmup(args, calibrate):
+    """--warmup W as given; by default W >= 3 steps covering >= WARMUP_MIN_MS, from `calibrate(3)`:
+    3 extra untimed steps run to completion, returning their wall ms."""
+    if args.warmup is not None:
+        return args.warmup
+    ms = calibrate(3)
+    return max(3, int(np.ceil(WARMUP_MIN_MS / max(ms / 3, 1e-3))))
 
 
 SAMPLE_MAX_BYTES = 512 << 20  # host-regenerated oracle sample per rank (at least one partition)
@@ -224,8 +240,16 @@ def production_shape(torch, eng, dev, threads, reps=10):
             eng.build_pipelined_async(w.rec, sets[i % 2][1])
         eng.build_pipeline_drain_async()
 
+    # each timed run right behind >= WARMUP_MIN_MS of builds (this runs after the CPU baseline has
+    # left the GPU idle for seconds; the step is shader-clock sensitive, see WARMUP_MIN_MS)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run(reps)
+    torch.cuda.synchronize(dev)
+    n_warm = max(reps, int(np.ceil(WARMUP_MIN_MS / max((time.perf_counter() - t0) * 1e3 / reps, 1e-3))))
+
     def timed(fn):
-        fn()
+        run(n_warm)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(st)
         fn()
@@ -243,6 +267,7 @@ def production_shape(torch, eng, dev, threads, reps=10):
     ok = (np.array_equal(got["digest"][:s_n * B].view(np.uint64), ref["digest"]) and
           np.array_equal(got["size"][:s_n * B], ref["size"]) and np.array_equal(got["root"][:s_n * 32], ref["root"]))
     res = {"workload": desc, "bytes": w.value_bytes,
+           "warmup_builds_before_each_run": n_warm,
            "fused_us_per_build": round(fused_us, 2), "fused_frac": round(w.value_bytes / fused_us / 1e3 / HBM_PEAK_GBS, 4),
            "digest_kernel_us": round(digest_us, 2),
            "digest_frac": round(w.value_bytes / digest_us / 1e3 / HBM_PEAK_GBS, 4),
@@ -488,7 +513,16 @@ def main_group(args):
         return ms, e0.elapsed_time(e1) / steps, ht
 
     main_run = Run(1 if c5 else GATHER_BUCKET)
-    ms, dev0_ms, host_timing = timed(main_run, args.steps, args.warmup)
+
+    def calibrate(k):
+        t0 = time.perf_counter()
+        main_run.run(k)
+        g.synchronize()
+        main_run.tickets.clear()
+        return (time.perf_counter() - t0) * 1e3
+
+    warmup = resolve_warmup(args, calibrate)
+    ms, dev0_ms, host_timing = timed(main_run, args.steps, warmup)
     last = args.steps - 1
     # parity: the gathered slabs (device 0's copy) of the last bucket / step hold every shard's
     # rows of its last build; every device received the same slabs; shard 0's last build equals
@@ -559,7 +593,7 @@ def main_group(args):
     achieved = shards[0].value_bytes * launches / (dev0_ms * 1e-3) / 1e9
     result = {
         "metric": METRIC, "value": round(total / 2**30 / (ms * 1e-3), 3), "unit": "GiB/s", "n_gpus": N,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True,
+        "steps": args.steps, "warmup": warmup, "ms_per_step": round(ms, 5), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (device-generated splitmix64 values, 'k%016x' keys, SHA-256 bucket tags)",
         "config": {"workload": desc + (f"; strong scaling: the config's total over {N} GPUs" if N > 1 else ""),
@@ -941,7 +975,21 @@ def main():
         return bool(np.array_equal(allr[w.partition_ids].reshape(-1),
                                    outs[last % (2 * bucket)][0]["root"].cpu().numpy()))
 
-    ms, kern_ms, host_timing = timed_run(args.steps, args.warmup)
+    def calibrate(k):  # k untimed steps to completion (the same count on every rank)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        join()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) * 1e3
+
+    warmup = resolve_warmup(args, calibrate)
+    if use_dist and args.warmup is None:  # one count on every rank (the steps carry collectives)
+        wt = torch.tensor([warmup], dtype=torch.int64, device=dev)
+        dist.all_reduce(wt, op=dist.ReduceOp.MAX)
+        warmup = int(wt.item())
+    ms, kern_ms, host_timing = timed_run(args.steps, warmup)
     eng.set_stream(stream.cuda_stream)
     if use_dist and fused and not c5 and args.steps > 0:
         parity["gathered_roots_match_after_run"] = last_gathered_ok(args.steps)
@@ -1013,7 +1061,7 @@ def main():
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
-            "warmup": args.warmup,
+            "warmup": warmup,
             "ms_per_step": round(ms, 5),
             "higher_is_better": True,
             "scaling": "weak" if (weak and world > 1) else "strong",
