@@ -481,13 +481,20 @@ __host__ __device__ constexpr uint32_t rec8_wave_words(int rows) { return rec8_s
 __host__ __device__ constexpr uint32_t rec8_lds_bytes(int rows) { return rec8_wave_words(rows) * 4u * (kThreads / 64); }
 
 #ifdef MDE_WAVE_STAMPS  // probe only: per-wave entry / first step / exit times (s_memrealtime, 100 MHz)
+// and shader-clock counts at the same points (s_memtime): a wave's clock = d(memtime) / d(realtime)
 constexpr uint32_t kStampWaves = 16384;
 __device__ unsigned long long g_wave_stamps[3 * kStampWaves];
 __device__ unsigned long long g_tree_stamps[2 * kStampWaves];  // fused step: tree waves' entry, exit
+__device__ unsigned long long g_wave_clk[3 * kStampWaves];
+__device__ unsigned long long g_tree_clk[2 * kStampWaves];
 __device__ __forceinline__ void wave_stamp(int k) {
   const uint32_t w = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
   const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-  if ((threadIdx.x & 63) == 0 && w < kStampWaves) g_wave_stamps[3 * w + k] = t;
+  const unsigned long long c = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0 && w < kStampWaves) {
+    g_wave_stamps[3 * w + k] = t;
+    g_wave_clk[3 * w + k] = c;
+  }
 }
 #endif
 
@@ -955,6 +962,7 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
   if (blockIdx.x < tree_blocks) {
 #ifdef MDE_WAVE_STAMPS  // probe only: every tree wave's entry and exit
     const unsigned long long te = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long ce = __builtin_amdgcn_s_memtime();
 #endif
 #ifndef MDE_STEP_SKIP_TREES  // probe only: the dispatch shape without the tree work
     step_trees(t, Q, blockIdx.x, lds);
@@ -964,6 +972,8 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
     if ((threadIdx.x & 63) == 0 && tw < kStampWaves) {
       g_tree_stamps[2 * tw] = te;
       g_tree_stamps[2 * tw + 1] = __builtin_amdgcn_s_memrealtime();
+      g_tree_clk[2 * tw] = ce;
+      g_tree_clk[2 * tw + 1] = __builtin_amdgcn_s_memtime();
     }
 #endif
     return;
@@ -1228,10 +1238,19 @@ extern "C" int mde_probe_tree_stamps(unsigned long long* host, uint64_t n, int r
   if (reset) {
     static const unsigned long long zero[3 * mde::kStampWaves] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(mde::g_tree_stamps), zero, sizeof(mde::g_tree_stamps)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(mde::g_wave_stamps), zero, sizeof(mde::g_wave_stamps)) != hipSuccess)
+        hipMemcpyToSymbol(HIP_SYMBOL(mde::g_wave_stamps), zero, sizeof(mde::g_wave_stamps)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(mde::g_tree_clk), zero, sizeof(mde::g_tree_clk)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(mde::g_wave_clk), zero, sizeof(mde::g_wave_clk)) != hipSuccess)
       return -1;
   }
   return 0;
+}
+// which = 0: the streaming waves' shader-clock counts (3 per wave), 1: the tree waves' (2 per wave)
+extern "C" int mde_probe_clock_stamps(unsigned long long* host, uint64_t n, int which) {
+  const size_t cap = which ? sizeof(mde::g_tree_clk) : sizeof(mde::g_wave_clk);
+  const size_t bytes = n * 8 > cap ? cap : n * 8;
+  return which ? (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mde::g_tree_clk), bytes)
+               : (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mde::g_wave_clk), bytes);
 }
 namespace mde {
 #endif
