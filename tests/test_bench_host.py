@@ -82,3 +82,26 @@ def test_group_bench_ranks_join_rank0s_barriers():
     assert "n_barriers = 2 * (2 if per_build_run else 1) + 1" in src
     assert "per_build_run = not c5 and not args.no_gather_per_build and args.steps > 0" in src
     assert "if per_build_run:\n        one = Run(1)" in src
+
+
+def test_default_warmup_covers_the_clock_ramp():
+    """--warmup W is taken as given; the default is >= 3 steps covering >= WARMUP_MIN_MS of device
+    time, from 3 calibration steps (the VALU-bound production step reads
+    ~12 % slow after 3 warm-up builds that follow an idle spell)."""
+    import argparse
+    import bench
+    calls = []
+
+    def calibrate(ms_per_step):
+        def f(k):
+            calls.append(k)
+            return k * ms_per_step
+        return f
+    assert bench.resolve_warmup(argparse.Namespace(warmup=5), calibrate(1.0)) == 5 and calls == []
+    assert bench.resolve_warmup(argparse.Namespace(warmup=0), calibrate(1.0)) == 0 and calls == []
+    c4 = bench.resolve_warmup(argparse.Namespace(warmup=None), calibrate(1.48))
+    prod = bench.resolve_warmup(argparse.Namespace(warmup=None), calibrate(0.17))
+    c3 = bench.resolve_warmup(argparse.Namespace(warmup=None), calibrate(12.0))
+    assert calls == [3, 3, 3]
+    assert c4 * 1.48 >= bench.WARMUP_MIN_MS and (c4 - 1) * 1.48 < bench.WARMUP_MIN_MS
+    assert prod * 0.17 >= bench.WARMUP_MIN_MS and c3 == 3
