@@ -523,6 +523,10 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
   // issue of the stream leaves SIMD cycles to the co-resident tree waves, whose dependent SHA-256
   // chain bounds that step; a deliberate s_sleep per scan step or priority 0 did not do as well
   // (profiles/r03y_rec8_scalar_ab.txt, r03z_rec8_throttle_ab.txt).
+#ifdef MDE_PROBE_REC8_SRSRC  // probe only: the range (and so the buffer resource) wave-uniform in SGPRs
+  beg = readlane64(beg, 0);
+  end = readlane64(end, 0);
+#endif
   const uint64_t span = ((end - beg) + 15) & ~15ull;  // <= kMaxWaveBytes
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)(d.base + beg), (short)0, (int)span, 0x00020000);

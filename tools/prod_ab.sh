@@ -1,0 +1,8 @@
+# Alternating-process warm A/B of the production-shape fused step (tools/prod_ab.py):
+#   LIBS="ref srsrc" ROUNDS=3 bash tools/prod_ab.sh > out.jsonl
+set -o pipefail
+for r in $(seq ${ROUNDS:-3}); do
+  for lib in ${LIBS:-ref srsrc}; do
+    MDE_LIBRARY=tools/ab/libmde_$lib.so timeout -k 10 120 python tools/prod_ab.py $lib 3 40 || exit 1
+  done
+done
