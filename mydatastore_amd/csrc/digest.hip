@@ -964,6 +964,9 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
   const uint32_t db = blockIdx.x;
 #else
   if (blockIdx.x < tree_blocks) {
+#ifdef MDE_PROBE_TREE_PRIO  // probe only: the tree waves' issue priority (the stream's is PRIO)
+    __builtin_amdgcn_s_setprio(MDE_PROBE_TREE_PRIO);
+#endif
 #ifdef MDE_WAVE_STAMPS  // probe only: every tree wave's entry and exit
     const unsigned long long te = __builtin_amdgcn_s_memrealtime();
     const unsigned long long ce = __builtin_amdgcn_s_memtime();
@@ -1220,6 +1223,10 @@ const Variant kVariants[] = {
     MDE_VARIANT(4, true, 2, 2, 4),      MDE_VARIANT(4, true, 2, 2, 5),
     MDE_VARIANT(4, true, 2, 2, 6),      MDE_VARIANT(4, true, 2, 2, 7),
     MDE_VARIANT(4, true, 2, 2, 8),
+#ifdef MDE_PROBE_EXTRA_VARIANTS  // probe only: the rec8 stream (mode 5) at issue priority 0, 1, 3
+    MDE_VARIANT(4, true, 2, 0, 5),      MDE_VARIANT(4, true, 2, 1, 5),
+    MDE_VARIANT(4, true, 2, 3, 5),
+#endif
 };
 #undef MDE_VARIANT
 

@@ -3,7 +3,7 @@
 process; the last build's roots checked against a standalone build of the same records.
 One JSON line: the library, the per-build times, roots_ok.
 
-    MDE_LIBRARY=... python tools/prod_ab.py [tag] [reps] [warm_ms]
+    MDE_LIBRARY=... [MDE_AB_VARIANT=v] python tools/prod_ab.py [tag] [reps] [warm_ms]
 """
 import json
 import os
@@ -27,6 +27,9 @@ def main():
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream(dev)
     eng.set_stream(st.cuda_stream)
+    if os.environ.get("MDE_AB_VARIANT"):  # an explicit digest variant (e.g. 17: rec8 with 8 KiB steps)
+        eng.set_tuning(int(os.environ["MDE_AB_VARIANT"]))
+        tag += "+v" + os.environ["MDE_AB_VARIANT"]
     w = make_workload(eng, n_partitions=1024, n_buckets=1000, value_len=8, part_mode="mod", n_keys=100_000_000)
     sets = [w._outs() for _ in range(2)]
     ref = w.build()["root"].cpu().numpy()
