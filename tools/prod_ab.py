@@ -28,7 +28,7 @@ def main():
     st = torch.cuda.current_stream(dev)
     eng.set_stream(st.cuda_stream)
     if os.environ.get("MDE_AB_VARIANT"):  # an explicit digest variant (e.g. 17: rec8 with 8 KiB steps)
-        eng.set_tuning(int(os.environ["MDE_AB_VARIANT"]))
+        eng.set_tuning(*map(int, os.environ["MDE_AB_VARIANT"].split(",")))  # variant[,blocks/CU[,oversub]]
         tag += "+v" + os.environ["MDE_AB_VARIANT"]
     w = make_workload(eng, n_partitions=1024, n_buckets=1000, value_len=8, part_mode="mod", n_keys=100_000_000)
     sets = [w._outs() for _ in range(2)]
