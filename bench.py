@@ -327,7 +327,7 @@ def main_group(args):
     GATHER_BUCKET builds, then the same run is timed again with one gather per build
     (`root_gather_per_build`, plus K bare gathers); C5 (BASELINE config 5) builds replicas A and B,
     diffs and extracts on every GPU (mde_group_diff_async / mde_group_extract_async) and gathers
-    [A roots | B roots | diff counts] once per step. Under torch.distributed.run the other ranks
+    [A roots | B roots | diff counts | diff ids] once per step. Under torch.distributed.run the other ranks
     only join the barriers (gloo, no GPU); rank 0's clock brackets all N GPUs' work. --rehearse:
     every shard on GPU 0 (copy gather)."""
     import ctypes
@@ -368,7 +368,12 @@ def main_group(args):
                             keys_per_partition=-(-n_keys // P), n_keys=n_keys, rank=i, world=N) for i in range(N)]
     sdev = [torch.device("cuda", d) for d in devices]
     slab = -(-P // N)
-    width = 68 if c5 else 32  # bytes per partition row of a slab: [A root | B root | diff count] for C5
+    # C5 compare: the diff writes its counts and its id lists (cap ids per partition) straight into
+    # the step's send slab, so the exchange step carries them
+    cap = mde.diff_capacity(B, B)
+    # bytes per partition of a slab: C4 its root; C5 [A root | B root | diff count | diff ids], laid
+    # out as four arrays of `slab` rows (roots at 0 and slab*32, counts at slab*64, ids at slab*68)
+    width = 68 + 4 * cap if c5 else 32
     repl, touched = [], []
     if c5:
         for w in shards:
@@ -380,10 +385,7 @@ def main_group(args):
     sets_b = [[w._outs() for _ in range(2)] for w in repl]
     recs = (mde.Records * N)(*[w.rec for w in shards])
     recs_b = (mde.Records * N)(*[w.rec for w in repl]) if c5 else None
-    # C5 compare: diff ids per device, diff counts written straight into the step's send slab,
-    # extract outputs per device
-    cap = mde.diff_capacity(B, B)
-    diff_ids = [torch.zeros(w.n_partitions * cap, dtype=torch.int32, device=sdev[i]) for i, w in enumerate(shards)] if c5 else []
+    # C5 extract outputs per device
     xo = []
     for i, w in enumerate(repl):
         rc_ = max(w.n_records // 8, 1024)
@@ -422,10 +424,10 @@ def main_group(args):
                 self.diff = [(mde.DiffArgs * N)(*[mde.DiffArgs(shards[i].n_partitions, B, B,
                                                                sets[i][k][0]["digest"].data_ptr(), sets[i][k][0]["nodes"].data_ptr(),
                                                                sets_b[i][k][0]["digest"].data_ptr(), sets_b[i][k][0]["nodes"].data_ptr(),
-                                                               diff_ids[i].data_ptr(), cap,
+                                                               self.send[k][i].data_ptr() + slab * 68, cap,
                                                                self.send[k][i].data_ptr() + slab * 64) for i in range(N)])
                              for k in range(2)]
-                self.extract = [(mde.ExtractArgs * N)(*[mde.ExtractArgs(diff_ids[i].data_ptr(), cap,
+                self.extract = [(mde.ExtractArgs * N)(*[mde.ExtractArgs(self.send[k][i].data_ptr() + slab * 68, cap,
                                                                         self.send[k][i].data_ptr() + slab * 64,
                                                                         xo[i]["part_off"].data_ptr(), xo[i]["out_rec"].data_ptr(),
                                                                         xo[i]["rec_cap"], xo[i]["out_vals"].data_ptr(),
@@ -543,15 +545,16 @@ def main_group(args):
                  np.array_equal(o0["size"][:s_n * B], ref["size"]) and np.array_equal(r0, ref["root"]))
     parity["oracle_sample_partitions"] = int(s_n)
     parity["shard0_equals_c_oracle_on_sample"] = bool(ok_oracle)
-    if c5:  # every shard's gathered diff counts: exactly its perturbed partitions; shard 0's diff and extract
-        ok_cnt = True
+    if c5:  # every shard's gathered diff counts and id lists: exactly its perturbed partitions and
+        # buckets (B = 64: no odd level, so no DFS duplicates); shard 0's extract
+        ok_cnt = ok_ids = True
         for i in range(N):
             k = shards[i].n_partitions
-            cnt = got[i].reshape(-1)[slab * 64:slab * 64 + k * 4].view(np.int32)
+            row = got[i].reshape(-1)
+            cnt = row[slab * 64:slab * 64 + k * 4].view(np.int32)
             ok_cnt &= bool(np.array_equal(cnt, np.array([1 if p in touched[i] else 0 for p in range(k)], np.int32)))
-        k0 = shards[0].n_partitions
-        ids = diff_ids[0].cpu().numpy().reshape(k0, cap)
-        ok_ids = all(ids[p, 0] == touched[0][p] for p in touched[0])
+            ids = row[slab * 68:slab * 68 + k * cap * 4].view(np.int32).reshape(k, cap)
+            ok_ids &= all(ids[p, :cnt[p]].tolist() == ([touched[i][p]] if p in touched[i] else []) for p in range(k))
         seg = shards[0].seg_rec.cpu().numpy()
         want = sum(int(seg[p * B + b + 1] - seg[p * B + b]) for p, b in touched[0].items())
         po = xo[0]["part_off"].cpu().numpy()
@@ -563,7 +566,7 @@ def main_group(args):
             src = repl[0].values.view(-1, V)[torch.from_numpy(r[samp]).to(sdev[0])].cpu().numpy()
             ok_ex = bool(np.array_equal(gotv, src))
         parity["c5_gathered_diff_counts_are_the_perturbed_partitions"] = bool(ok_cnt)
-        parity["c5_shard0_diff_is_exactly_the_perturbed_bucket"] = bool(ok_ids)
+        parity["c5_gathered_diff_ids_are_the_perturbed_buckets"] = bool(ok_ids)
         parity["c5_shard0_extract_records_and_bytes"] = bool(ok_ex)
         parity["c5_shard0_extracted_records_per_step"] = want
     # C4: the same builds with ONE gather per build, and K bare gathers of one build's slabs: the
@@ -603,7 +606,7 @@ def main_group(args):
                    "parallelism": f"partition-shard x{N}, one process (mde_group)",
                    "engine": "group", "devices": devices,
                    "root_gather": f"{g.gather_kind} of {N} x {bk} x {slab} x {width} B slabs, one per "
-                                  + ("step (C5: [A roots | B roots | diff counts])" if c5 else f"{bk} builds")
+                                  + ("step (C5: [A roots | B roots | diff counts | diff id lists])" if c5 else f"{bk} builds")
                                   + ", on a side stream per GPU, overlapped with the next builds"},
         "roofline": {"bound": "hbm", "kernel": "build_step_kernel (GPU 0's launches"
                                                + (" + the compare kernels, counted against it)" if c5 else ")"),

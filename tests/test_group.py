@@ -262,8 +262,8 @@ def test_group_c5_diff_extract_and_gather(engine, G, P, B, V, n):
     """BASELINE config 5 on the mde_group path (the one the Go shim's process reaches): each
     device builds both replicas of its partitions (pipelined, as bench.py times it), diffs them and
     extracts replica B's records of the differing buckets on the device (mde_group_diff_async,
-    mde_group_extract_async), and the [A roots | B roots | diff counts] slabs are all-gathered on
-    the side streams (mde_group_gather_overlapped_async). The gathered slabs, every shard's diff
+    mde_group_extract_async), and the [A roots | B roots | diff counts | diff ids] slabs (the
+    diff writes its counts and id lists into the slab itself) are all-gathered on the side streams (mde_group_gather_overlapped_async). The gathered slabs, every shard's diff
     ids and extracted bytes equal the single-engine C5 result; the diff of every partition is
     the oracle's DFS diff: its perturbed bucket, once per odd level on the bucket's path. Shapes: 1/2/8 members, more members than partitions (members
     with nothing to build still take part in the gather), odd B with 8-byte values, B = 130."""
@@ -284,8 +284,9 @@ def test_group_c5_diff_extract_and_gather(engine, G, P, B, V, n):
     slab = -(-P // G)
     cap = mde.diff_capacity(B, B)
     shards, repl, outs, args_d, args_x, x, keep = [], [], [], [], [], [], []
-    send = [torch.zeros(slab * 68, dtype=torch.uint8, device=dev) for _ in range(G)]
-    recv = [torch.zeros(G * slab * 68, dtype=torch.uint8, device=dev) for _ in range(G)]
+    width = 68 + 4 * cap
+    send = [torch.zeros(slab * width, dtype=torch.uint8, device=dev) for _ in range(G)]
+    recv = [torch.zeros(G * slab * width, dtype=torch.uint8, device=dev) for _ in range(G)]
     for i in range(G):
         w = make_workload(engine, n_partitions=P, n_buckets=B, value_len=V, part_mode="mod", n_keys=n, rank=i, world=G)
         vb, _ = perturb_replica(w)
@@ -298,17 +299,17 @@ def test_group_c5_diff_extract_and_gather(engine, G, P, B, V, n):
                            oa["nodes"].data_ptr())
         to_b = mde.TreeOut(ob["digest"].data_ptr(), ob["size"].data_ptr(), ob["items"].data_ptr(), base + slab * 32,
                            ob["nodes"].data_ptr())
-        ids = torch.zeros(Pl * cap, dtype=torch.int32, device=dev)
+        ids_ptr = base + slab * 68  # the diff id lists land in the send slab too
         rec_cap = max(w.n_records // 8, 1024)
-        t = {"ids": ids, "part_off": torch.zeros(Pl + 1, dtype=torch.int64, device=dev),
+        t = {"part_off": torch.zeros(Pl + 1, dtype=torch.int64, device=dev),
              "out_rec": torch.zeros(rec_cap, dtype=torch.int64, device=dev),
              "out_vals": torch.zeros(rec_cap * V, dtype=torch.uint8, device=dev),
              "out_voff": torch.zeros(rec_cap + 1, dtype=torch.int64, device=dev),
              "status": torch.zeros(1, dtype=torch.int32, device=dev)}
         counts_ptr = base + slab * 64  # the diff counts land in the send slab itself
         args_d.append(mde.DiffArgs(Pl, B, B, oa["digest"].data_ptr(), oa["nodes"].data_ptr(), ob["digest"].data_ptr(),
-                                   ob["nodes"].data_ptr(), ids.data_ptr(), cap, counts_ptr))
-        args_x.append(mde.ExtractArgs(ids.data_ptr(), cap, counts_ptr, t["part_off"].data_ptr(),
+                                   ob["nodes"].data_ptr(), ids_ptr, cap, counts_ptr))
+        args_x.append(mde.ExtractArgs(ids_ptr, cap, counts_ptr, t["part_off"].data_ptr(),
                                       t["out_rec"].data_ptr(), rec_cap, t["out_vals"].data_ptr(),
                                       t["out_voff"].data_ptr(), rec_cap * V, t["status"].data_ptr()))
         shards.append(w)
@@ -322,12 +323,12 @@ def test_group_c5_diff_extract_and_gather(engine, G, P, B, V, n):
     g.drain_async()
     g.diff_async(args_d)
     g.extract_async([w.rec for w in repl], args_x)
-    ticket = g.gather_overlapped_async(send, recv, slab * 68)
+    ticket = g.gather_overlapped_async(send, recv, slab * width)
     g.gather_wait_async(ticket)
     g.synchronize()
     for i in range(1, G):
         assert torch.equal(recv[i], recv[0])
-    got = recv[0].cpu().numpy().reshape(G, slab * 68)
+    got = recv[0].cpu().numpy().reshape(G, slab * width)
     for r in range(G):
         pids = shards[r].partition_ids
         k = len(pids)
@@ -335,7 +336,7 @@ def test_group_c5_diff_extract_and_gather(engine, G, P, B, V, n):
         assert np.array_equal(got[r, slab * 32:slab * 32 + k * 32].reshape(k, 32), ref["roots_b"][pids]), r
         assert np.array_equal(got[r, slab * 64:slab * 64 + k * 4].view(np.int32), ref["counts"][pids]), r
         assert int(x[r]["status"].item()) == 0
-        ids = x[r]["ids"].cpu().numpy().reshape(k, cap)
+        ids = got[r, slab * 68:slab * 68 + k * cap * 4].view(np.int32).reshape(k, cap)
         po = x[r]["part_off"].cpu().numpy().astype(np.int64)
         vals = x[r]["out_vals"].cpu().numpy()
         cnt = ref["counts"][pids]
