@@ -435,16 +435,21 @@ def main_group(args):
                                                                         xo[i]["status"].data_ptr()) for i in range(N)])
                                 for k in range(2)]
             self.tickets = {}
+            self.gather_s = 0.0  # host time spent enqueueing gathers and their waits
 
         def gather(self, b):  # the slabs of bucket (C5: step) b, on the side streams
+            t0 = time.perf_counter()
             t = ctypes.c_uint64()
             check(lib.mde_group_gather_overlapped_async(g.g, self.send_p[b % 2], self.recv_p[b % 2], self.nbytes,
                                                         ctypes.byref(t)))
             self.tickets[b] = t.value
+            self.gather_s += time.perf_counter() - t0
 
         def wait(self, b):  # the context streams wait until bucket b's gather has read its slabs
             if b in self.tickets:
+                t0 = time.perf_counter()
                 check(lib.mde_group_gather_wait_async(g.g, self.tickets.pop(b)))
+                self.gather_s += time.perf_counter() - t0
 
         def run_c4(self, steps):
             """`steps` pipelined builds: launch L digests build L and writes build L-1's trees (its
@@ -499,6 +504,7 @@ def main_group(args):
         for d in sorted(set(devices)):
             torch.cuda.synchronize(d)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        run.gather_s = 0.0
         t0 = time.perf_counter()
         e0.record(ext)
         run.run(steps)
@@ -511,7 +517,11 @@ def main_group(args):
             dist.barrier()
         ms = (t1 - t0) * 1e3 / steps
         ht = {"enqueue_ms": round((t_enq - t0) * 1e3, 3), "enqueue_ms_per_step": round((t_enq - t0) * 1e3 / steps, 4),
-              "wall_ms": round((t1 - t0) * 1e3, 3), "launches_per_step": N * (2 if c5 else 1)}
+              "wall_ms": round((t1 - t0) * 1e3, 3), # per step, per device: C4 one pipelined build; C5 two builds, the diff and the extract
+              "device_calls_per_step": N * (4 if c5 else 1),
+              # of enqueue_ms: the gathers and their waits (the copy gather of a rehearsal issues
+              # N x N copies from this thread; the RCCL gather N grouped calls)
+              "gather_enqueue_ms_per_step": round(run.gather_s * 1e3 / steps, 4)}
         return ms, e0.elapsed_time(e1) / steps, ht
 
     main_run = Run(1 if c5 else GATHER_BUCKET)
