@@ -105,3 +105,19 @@ def test_default_warmup_covers_the_clock_ramp():
     assert calls == [3, 3, 3]
     assert c4 * 1.48 >= bench.WARMUP_MIN_MS and (c4 - 1) * 1.48 < bench.WARMUP_MIN_MS
     assert prod * 0.17 >= bench.WARMUP_MIN_MS and c3 == 3
+
+
+def test_gpurun_upload_keeps_what_the_bench_reads():
+    """bench.py reads profiles/pmc_traffic.json on the GPU box for roofline.traffic; a
+    .gpurunignore pattern that drops it from the upload silently nulls the field."""
+    import fnmatch
+    from tests.conftest import ROOT
+    pats = [p.strip() for p in (ROOT / ".gpurunignore").read_text().splitlines() if p.strip()]
+    for path in ("./profiles/pmc_traffic.json", "./bench.py", "./mydatastore_amd/libmde.so",
+                 "./oracle/build/liboracle.so"):
+        for p in pats:
+            parts = path.split("/")
+            prefixes = ["/".join(parts[:i]) for i in range(2, len(parts) + 1)]
+            hit = (any(fnmatch.fnmatch(x, p) for x in prefixes) if p.startswith("./")
+                   else any(fnmatch.fnmatch(x, p) for x in parts[1:]))
+            assert not hit, (path, p)

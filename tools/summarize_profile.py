@@ -72,10 +72,15 @@ def main(src, tag, cfg):
         durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows(tr[0])
                 if kern in r["Kernel_Name"]]
         if len(durs) > 1:
+            k = int(bench.get("steps", 0))
             out["dominant_kernel_trace"] = {
                 "launches": len(durs), "first_ns": durs[0],
                 "avg_ns_excluding_first": round(statistics.mean(durs[1:]), 1),
                 "median_ns": statistics.median(durs)}
+            # the bench's K timed launches are the last K (warm-up and calibration launches before)
+            if 0 < k <= len(durs):
+                out["dominant_kernel_trace"]["avg_ns_timed_launches"] = round(statistics.mean(durs[-k:]), 1)
+                out["dominant_kernel_trace"]["timed_launches"] = k
     dst = ROOT / "profiles" / f"{tag}_{cfg}.json"
     dst.write_text(json.dumps(out, indent=1) + "\n")
     shutil.copy(src / "trace" / "run_kernel_stats.csv", ROOT / "profiles" / f"{tag}_{cfg}_kernel_stats.csv")
