@@ -263,10 +263,38 @@ def test_group_c5_diff_extract_and_gather(engine, G, P, B, V, n):
     device builds both replicas of its partitions (pipelined, as bench.py times it), diffs them and
     extracts replica B's records of the differing buckets on the device (mde_group_diff_async,
     mde_group_extract_async), and the [A roots | B roots | diff counts | diff ids] slabs (the
-    diff writes its counts and id lists into the slab itself) are all-gathered on the side streams (mde_group_gather_overlapped_async). The gathered slabs, every shard's diff
-    ids and extracted bytes equal the single-engine C5 result; the diff of every partition is
-    the oracle's DFS diff: its perturbed bucket, once per odd level on the bucket's path. Shapes: 1/2/8 members, more members than partitions (members
-    with nothing to build still take part in the gather), odd B with 8-byte values, B = 130."""
+    diff writes its counts and id lists into the slab itself) are all-gathered on the side
+    streams (mde_group_gather_overlapped_async). The gathered slabs, every shard's diff ids and
+    extracted bytes equal the single-engine C5 result; the diff of every partition is the
+    oracle's DFS diff: its perturbed bucket, once per odd level on the bucket's path. Shapes:
+    1/2/8 members, more members than partitions (members with nothing to build still take part
+    in the gather), odd B with 8-byte values, B = 130."""
+    _check_group_c5(engine, G, P, B, V, n)
+
+
+def _random_c5_shapes(k, seed=20261018):
+    """Seeded random C5 shapes for the group: member counts 1-8, partition counts 1-79 (members
+    without partitions when G > P), B from 1 to 333 (odd levels: DFS duplicates), values of
+    1-33 bytes (the 8-byte record scan among them), a few to ~40 records per bucket."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(k):
+        G, P = int(rng.integers(1, 9)), int(rng.integers(1, 80))
+        B = int(rng.choice([1, 2, 3, 5, 31, 64, 65, 130, 333]))
+        V = int(rng.choice([1, 3, 8, 8, 16, 33]))
+        n = max(1, min(200_000, P * B * int(rng.integers(1, 40))))
+        out.append((G, P, B, V, n))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G,P,B,V,n", _random_c5_shapes(8))
+def test_group_c5_random_shapes(engine, G, P, B, V, n):
+    """The group C5 check of test_group_c5_diff_extract_and_gather over seeded random shapes."""
+    _check_group_c5(engine, G, P, B, V, n)
+
+
+def _check_group_c5(engine, G, P, B, V, n):
     import torch
     import mydatastore_amd as mde
     from mydatastore_amd.workload import Workload, make_workload, perturb_replica
