@@ -235,7 +235,7 @@ def _c5_single(engine, P, B, V, n):
     ids = torch.zeros(P * cap, dtype=torch.int32, device=dev)
     cnt = torch.zeros(P, dtype=torch.int32, device=dev)
     engine.diff_async(P, B, oa["digest"], oa["nodes"], B, ob["digest"], ob["nodes"], ids, cap, cnt)
-    rec_cap = max(w.n_records // 8, 1024)
+    rec_cap = max(w.n_records, 1024)  # B = 1 or 2 extracts all or half of the records
     part_off = torch.zeros(P + 1, dtype=torch.int64, device=dev)
     out_rec = torch.zeros(rec_cap, dtype=torch.int64, device=dev)
     out_vals = torch.zeros(rec_cap * V, dtype=torch.uint8, device=dev)
@@ -328,7 +328,7 @@ def _check_group_c5(engine, G, P, B, V, n):
         to_b = mde.TreeOut(ob["digest"].data_ptr(), ob["size"].data_ptr(), ob["items"].data_ptr(), base + slab * 32,
                            ob["nodes"].data_ptr())
         ids_ptr = base + slab * 68  # the diff id lists land in the send slab too
-        rec_cap = max(w.n_records // 8, 1024)
+        rec_cap = max(w.n_records, 1024)  # B = 1 or 2 extracts all or half of the records
         t = {"part_off": torch.zeros(Pl + 1, dtype=torch.int64, device=dev),
              "out_rec": torch.zeros(rec_cap, dtype=torch.int64, device=dev),
              "out_vals": torch.zeros(rec_cap * V, dtype=torch.uint8, device=dev),
