@@ -14,6 +14,7 @@
 // Written against the public C ABI plus HIP, like batch.cpp.
 #include "../../include/mde.h"
 #include "device_scope.hpp"
+#include "enq_pool.hpp"
 
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
@@ -78,16 +79,6 @@ struct Buf {
   uint64_t cap = 0;
 };
 
-// A host thread that enqueues one device's share of every group call (see run_all).
-struct EnqWorker {
-  std::thread th;
-  std::atomic<uint64_t> posted{0}, finished{0};
-  std::atomic<bool> sleeping{false}, quit{false};
-  std::mutex m;
-  std::condition_variable cv;
-  int rc = 0;
-};
-
 }  // namespace
 
 struct mde_group {
@@ -109,14 +100,12 @@ struct mde_group {
   // digest, size, items, root slab, nodes, gathered roots
   enum { kVals, kVoff, kSeg, kTag, kDig, kSize, kItems, kRoot, kNodes, kRecv, kBufs };
   std::vector<std::vector<Buf>> stage;
-  // Per-device enqueue threads (run_all): devices 1..G-1 each have one; the calling thread
-  // enqueues device 0's share. Started on the first device-resident call of a group of G > 1
-  // (MDE_GROUP_THREADS=0: the calling thread enqueues every device's share in turn).
+  // Per-device enqueue threads (run_all, enq_pool.hpp): devices 1..G-1 each have one; the calling
+  // thread enqueues device 0's share. Started on the first device-resident call of a group of
+  // G > 1 (MDE_GROUP_THREADS=0: the calling thread enqueues every device's share in turn).
   bool threaded = true;
-  std::vector<std::unique_ptr<EnqWorker>> workers;
-  const std::function<int(uint32_t)>* job = nullptr;
-  uint64_t job_seq = 0;
-  std::mutex run_mu;  // one group call at a time through the workers
+  std::unique_ptr<mde::EnqPool> pool;
+  std::mutex pool_mu;  // guards the pool's creation
 };
 
 namespace {
@@ -309,40 +298,8 @@ int ctx_err(mde_group* g, uint32_t i, int rc, std::string& msg) {
   return fail(msg, rc, "member %u (device %d): %s", i, g->dev[i], m);
 }
 
-// Enqueue threads. A device-resident group call launches work on every device (a pipelined build
-// per device, a diff, an extract, ...); each launch costs the host several microseconds (argument
-// setup, the HIP runtime's launch path), so one thread launching for 8 GPUs spends 8x that per
-// step against a device step of ~0.2 ms (C4 at N = 8). run_all hands device i's share to thread i
-// (device 0's to the caller) and returns when every share is enqueued: the host cost per step is
-// one device's, not G devices'. Workers spin on their job word for kWorkerSpin after each job --
-// a run of group calls keeps them hot -- then sleep on a condition variable.
-constexpr auto kWorkerSpin = std::chrono::microseconds(200);
-
-void worker_loop(mde_group* g, uint32_t i) {
-  EnqWorker& w = *g->workers[i];
-  uint64_t last = 0;
-  for (;;) {
-    uint64_t p = w.posted.load();
-    auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t spin = 1; p == last && !w.quit.load(); spin++) {
-      _mm_pause();
-      if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > kWorkerSpin) {
-        std::unique_lock<std::mutex> lk(w.m);
-        w.sleeping.store(true);
-        w.cv.wait(lk, [&] { return w.posted.load() != last || w.quit.load(); });
-        w.sleeping.store(false);
-        t0 = std::chrono::steady_clock::now();
-      }
-      p = w.posted.load();
-    }
-    if (p == last) return;  // quit
-    w.rc = (*g->job)(i);
-    last = p;
-    w.finished.store(p);
-  }
-}
-
 // fn(i) for every device i (fn returns an MDE code); the lowest failing device's code, or MDE_OK.
+// Device i's share runs on its enqueue thread (enq_pool.hpp), device 0's on the caller.
 int run_all(mde_group* g, const std::function<int(uint32_t)>& fn, uint32_t* failed) {
   const uint32_t G = (uint32_t)g->ctx.size();
   if (!g->threaded || G == 1) {
@@ -355,39 +312,11 @@ int run_all(mde_group* g, const std::function<int(uint32_t)>& fn, uint32_t* fail
     }
     return MDE_OK;
   }
-  std::lock_guard<std::mutex> lk(g->run_mu);
-  if (g->workers.empty()) {
-    g->workers.resize(G);
-    for (uint32_t i = 1; i < G; i++) g->workers[i].reset(new EnqWorker());
-    for (uint32_t i = 1; i < G; i++) g->workers[i]->th = std::thread(worker_loop, g, i);
+  {
+    std::lock_guard<std::mutex> lk(g->pool_mu);
+    if (!g->pool) g->pool.reset(new mde::EnqPool(G));
   }
-  g->job = &fn;
-  const uint64_t seq = ++g->job_seq;
-  for (uint32_t i = 1; i < G; i++) {
-    EnqWorker& w = *g->workers[i];
-    w.posted.store(seq);
-    if (w.sleeping.load()) {
-      { std::lock_guard<std::mutex> wl(w.m); }
-      w.cv.notify_one();
-    }
-  }
-  int rc = fn(0);
-  *failed = 0;
-  for (uint32_t i = 1; i < G; i++) {
-    EnqWorker& w = *g->workers[i];
-    for (uint32_t spin = 1; w.finished.load() != seq; spin++) {
-      if (spin < 4096)
-        _mm_pause();
-      else
-        std::this_thread::yield();
-    }
-    if (!rc && w.rc) {
-      rc = w.rc;
-      *failed = i;
-    }
-  }
-  g->job = nullptr;
-  return rc;
+  return g->pool->run(fn, failed);
 }
 
 // A device-resident group call: fn(i) enqueues device i's share on its context (run_all: one host
@@ -400,18 +329,7 @@ int group_call(mde_group* g, const std::function<int(uint32_t)>& fn) {
   return ctx_err(g, failed, rc, g->err);
 }
 
-void stop_workers(mde_group* g) {
-  for (auto& w : g->workers) {
-    if (!w) continue;
-    {
-      std::lock_guard<std::mutex> wl(w->m);
-      w->quit.store(true);
-    }
-    w->cv.notify_one();
-    if (w->th.joinable()) w->th.join();
-  }
-  g->workers.clear();
-}
+void stop_workers(mde_group* g) { g->pool.reset(); }
 
 #define GHIP(expr)                                                                                   \
   do {                                                                                               \
