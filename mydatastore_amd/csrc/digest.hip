@@ -695,11 +695,18 @@ __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32
   const uint64_t last = segpos(d, d.S);
   uint32_t s = 0;
   uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
+#ifdef MDE_WAVE_STAMPS
+  wave_stamp(0);
+  wave_stamp(1);
+#endif
   for (uint32_t j = 0; j < a.pieces && beg < last; j++, beg += a.piece_stride)
     s = REC8  ? digest_range_rec8<NT, REC8 ? REC8 : 4>(a, beg, min(beg + a.wave_bytes, last), s, lane,
                                                        lds + (threadIdx.x >> 6) * rec8_wave_words(REC8), first, last)
         : WIN ? digest_range_win<U, NT, PIPE, A8>(a, beg, min(beg + a.wave_bytes, last), s, lane)
               : digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), s, lane);
+#ifdef MDE_WAVE_STAMPS
+  wave_stamp(2);
+#endif
 }
 
 
