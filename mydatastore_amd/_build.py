@@ -7,6 +7,7 @@ Outputs (git-ignored, but shipped to the GPU box with the snapshot):
   mydatastore_amd/libmde_host.so    C++ mirror of main/merkle_tree.go over the C ABI
   tests/cpp/build/test_merkle_tree  C++ port of the reference's Merkle tests
   tests/cpp/build/cabi_bench        plain-C driver of the C ABI (C4 build, no PyTorch)
+  tests/cpp/build/group_cabi        plain-C driver of the multi-GPU path (mde_group, no PyTorch)
   tests/cpp/build/batch_test        concurrent callers of the batcher vs mde_build / the C oracle
   tests/cpp/build/batch_bench       production call shape: CPU oracle vs per-call vs batched, P callers
   tests/cpp/build/shim_replay       the Go shim's call sequences replayed from C (checked by pytest)
@@ -35,6 +36,7 @@ HOST_LIB = PKG / "libmde_host.so"
 ORACLE_LIB = ROOT / "oracle" / "build" / "liboracle.so"
 CPP_TEST = ROOT / "tests" / "cpp" / "build" / "test_merkle_tree"
 C_BENCH = ROOT / "tests" / "cpp" / "build" / "cabi_bench"
+GROUP_CABI = ROOT / "tests" / "cpp" / "build" / "group_cabi"
 BATCH_TEST = ROOT / "tests" / "cpp" / "build" / "batch_test"
 BATCH_BENCH = ROOT / "tests" / "cpp" / "build" / "batch_bench"
 SHIM_REPLAY = ROOT / "tests" / "cpp" / "build" / "shim_replay"
@@ -83,12 +85,13 @@ def build_host(verbose: bool = True) -> Path:
         _run(["g++", "-O2", "-std=c++17", "-Wall", f"-I{ROOT / 'include'}", f"-I{hdir}", test_src,
               "-o", CPP_TEST, f"-L{PKG}", "-lmde_host", "-lmde",
               f"-Wl,-rpath,{PKG}", "-Wl,-rpath,$ORIGIN/../../../mydatastore_amd"], verbose)
-    c_src = ROOT / "tests" / "cpp" / "cabi_bench.c"
-    if c_src.exists() and _stale(C_BENCH, [c_src, ROOT / "include" / "mde.h", LIB]):
-        C_BENCH.parent.mkdir(parents=True, exist_ok=True)
-        _run(["gcc", "-O2", "-std=c11", "-D_POSIX_C_SOURCE=199309L", "-Wall", f"-I{ROOT / 'include'}",
-              c_src, "-o", C_BENCH, f"-L{PKG}", "-lmde", f"-Wl,-rpath,{PKG}",
-              "-Wl,-rpath,$ORIGIN/../../../mydatastore_amd"], verbose)
+    for name, out in (("cabi_bench.c", C_BENCH), ("group_cabi.c", GROUP_CABI)):
+        c_src = ROOT / "tests" / "cpp" / name
+        if c_src.exists() and _stale(out, [c_src, ROOT / "include" / "mde.h", LIB]):
+            out.parent.mkdir(parents=True, exist_ok=True)
+            _run(["gcc", "-O2", "-std=c11", "-D_POSIX_C_SOURCE=199309L", "-Wall", f"-I{ROOT / 'include'}",
+                  c_src, "-o", out, f"-L{PKG}", "-lmde", f"-Wl,-rpath,{PKG}",
+                  "-Wl,-rpath,$ORIGIN/../../../mydatastore_amd"], verbose)
     # test programs that also link the C oracle (test infrastructure) as their checker
     for name, out in (("batch_test.c", BATCH_TEST), ("batch_bench.c", BATCH_BENCH), ("shim_replay.c", SHIM_REPLAY),
                       ("server_test.c", SERVER_TEST)):

@@ -422,3 +422,35 @@ def test_group_errors_name_the_failing_member(engine):
         assert np.array_equal(outs[i][0]["root"].cpu().numpy().reshape(-1, 32), want[w.partition_ids])
     g.close()
     torch.cuda.synchronize()
+
+
+GROUP_CABI = ROOT / "tests" / "cpp" / "build" / "group_cabi"
+
+
+def test_group_cabi_fails_loudly_without_gpu():
+    """The plain-C driver of the multi-GPU path builds, and without a gfx950 device it stops at
+    mde_device_list (there is no CPU fallback behind the ABI)."""
+    import torch
+    subprocess.run([sys.executable, "-m", "mydatastore_amd._build", "-q"], cwd=ROOT, check=True)
+    assert GROUP_CABI.exists()
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    r = subprocess.run([str(GROUP_CABI), "1000", "4", "64", "8", "2", "1"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "no gfx950 device" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("members,rehearse", [(1, 0), (3, 1), (8, 1)])
+def test_group_cabi_parity(members, rehearse):
+    """The multi-GPU path from plain C, no PyTorch (what one node process does with its GPUs): a
+    reduced C4-shaped workload sharded p % G, pipelined group builds with the roots in the send
+    slabs and one overlapped gather per build; the last build's gathered slabs hold every member's
+    roots on every member, equal a standalone group build's, and member 0's roots are the tree of
+    its digests. One GPU: 1 member over RCCL, 3 and 8 members rehearsed on it (device copies)."""
+    import json
+    r = subprocess.run([str(GROUP_CABI), "1000000", "256", "256", "64", "6", "2", str(members), str(rehearse)],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert all(d["parity"].values()), d
+    assert d["members"] == members and ("rccl" in d["gather"]) == (members == 1)
