@@ -18,6 +18,7 @@
 #           -> teardown_{a,b}.txt (run it last: a hang ends the call)
 #   stepprobe fused-step per-wave timeline at the production shape (tools/step_probe.py, probe
 #           library tools/ab/libmde_$PROBE_LIB.so, default stamps)        -> step_probe.jsonl
+#   groupc  the multi-GPU path from plain C (tests/cpp/group_cabi.c; GROUPC_ARGS) -> group_cabi.json
 #   groupbench bench.py --engine group at 1 GPU (RCCL) and 8 members on GPU 0 (--rehearse), C4 and C5
 #           -> bench_group_{1,8}_{c4,c5}.json
 #   serviceab bulk pipelined builds with no service / an idle one / one serving 10 callers
@@ -60,6 +61,10 @@ for s in "$@"; do
       MDE_LIBRARY=tools/ab/libmde_${PROBE_LIB:-stamps}.so timeout -k 10 180 python tools/step_probe.py ${PROBE_ARGS:-} \
         > $O/step_probe.jsonl 2> $O/step_probe.err || { tail -20 $O/step_probe.err; exit 1; }
       cat $O/step_probe.jsonl ;;
+    groupc)
+      step groupc
+      timeout -k 10 300 ./tests/cpp/build/group_cabi ${GROUPC_ARGS:-} > $O/group_cabi.json 2> $O/group_cabi.err || { tail -20 $O/group_cabi.err; exit 1; }
+      cat $O/group_cabi.json ;;
     groupbench)
       step groupbench
       for spec in "1 c4" "1 c5" "8 c4" "8 c5"; do
