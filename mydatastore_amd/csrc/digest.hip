@@ -638,6 +638,21 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
     }
   };
 
+#ifdef MDE_PROBE_REC8_DEPTH3  // probe only: three steps in flight per wave instead of two
+  u32x4 vc[ROWS];
+  load_rec8<NT, ROWS>(vb, rs, (uint32_t)kStep, lane);
+  for (uint64_t p = beg;; p += 3 * kStep) {
+    load_rec8<NT, ROWS>(vc, rs, (uint32_t)(p + 2 * kStep - beg), lane);  // always issued (bounded by the range)
+    process(va, p);
+    if (p + kStep >= end) break;
+    load_rec8<NT, ROWS>(va, rs, (uint32_t)(p + 3 * kStep - beg), lane);
+    process(vb, p + kStep);
+    if (p + 2 * kStep >= end) break;
+    load_rec8<NT, ROWS>(vb, rs, (uint32_t)(p + 4 * kStep - beg), lane);
+    process(vc, p + 2 * kStep);
+    if (p + 3 * kStep >= end) break;
+  }
+#else
   for (uint64_t p = beg;; p += 2 * kStep) {
     load_rec8<NT, ROWS>(vb, rs, (uint32_t)(p + kStep - beg), lane);  // always issued (bounded by the range)
     process(va, p);
@@ -646,6 +661,7 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
     process(vb, p + kStep);
     if (p + 2 * kStep >= end) break;
   }
+#endif
   retire();
   window_out();
   return s;
