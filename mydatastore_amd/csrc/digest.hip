@@ -487,6 +487,14 @@ __device__ unsigned long long g_wave_stamps[3 * kStampWaves];
 __device__ unsigned long long g_tree_stamps[2 * kStampWaves];  // fused step: tree waves' entry, exit
 __device__ unsigned long long g_wave_clk[3 * kStampWaves];
 __device__ unsigned long long g_tree_clk[2 * kStampWaves];
+// where each wave ran: HW_ID (wave, SIMD, CU, SH, SE ids) in the low word, XCC_ID in the high
+__device__ unsigned long long g_wave_hw[kStampWaves];
+__device__ unsigned long long g_tree_hw[kStampWaves];
+__device__ __forceinline__ unsigned long long hw_where() {
+  const unsigned hw = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID, 32 bits
+  const unsigned xcc = (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID, 4 bits
+  return ((unsigned long long)xcc << 32) | hw;
+}
 __device__ __forceinline__ void wave_stamp(int k) {
   const uint32_t w = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
   const unsigned long long t = __builtin_amdgcn_s_memrealtime();
@@ -494,6 +502,7 @@ __device__ __forceinline__ void wave_stamp(int k) {
   if ((threadIdx.x & 63) == 0 && w < kStampWaves) {
     g_wave_stamps[3 * w + k] = t;
     g_wave_clk[3 * w + k] = c;
+    if (k == 0) g_wave_hw[w] = hw_where();
   }
 }
 #endif
@@ -1004,6 +1013,7 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
       g_tree_stamps[2 * tw + 1] = __builtin_amdgcn_s_memrealtime();
       g_tree_clk[2 * tw] = ce;
       g_tree_clk[2 * tw + 1] = __builtin_amdgcn_s_memtime();
+      g_tree_hw[tw] = hw_where();
     }
 #endif
     return;
@@ -1278,6 +1288,13 @@ extern "C" int mde_probe_tree_stamps(unsigned long long* host, uint64_t n, int r
       return -1;
   }
   return 0;
+}
+// which = 0 / 1: the streaming / tree waves' placement (hw_where, one per wave)
+extern "C" int mde_probe_hw_where(unsigned long long* host, uint64_t n, int which) {
+  const size_t cap = which ? sizeof(mde::g_tree_hw) : sizeof(mde::g_wave_hw);
+  const size_t bytes = n * 8 > cap ? cap : n * 8;
+  return which ? (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mde::g_tree_hw), bytes)
+               : (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mde::g_wave_hw), bytes);
 }
 // which = 0: the streaming waves' shader-clock counts (3 per wave), 1: the tree waves' (2 per wave)
 extern "C" int mde_probe_clock_stamps(unsigned long long* host, uint64_t n, int which) {
