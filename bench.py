@@ -744,10 +744,11 @@ def main():
         out_vals = torch.zeros(bytes_cap, dtype=torch.uint8, device=dev)
         out_voff = torch.zeros(rec_cap + 1, dtype=torch.int64, device=dev)
         status = torch.zeros(1, dtype=torch.int32, device=dev)
-        # N > 1: each step's per-partition diff counts travel with the roots (SURVEY.md section 8e:
-        # C5 also gathers the diff results); staged per output set, as diff_cnt is rewritten by
-        # the next step's diff while the gather may still be in flight
+        # N > 1: each step's per-partition diff counts and id lists travel with the roots (SURVEY.md
+        # section 8e: C5 also gathers the diff-id lists); staged per output set, as diff_cnt and
+        # diff_ids are rewritten by the next step's diff while the gather may still be in flight
         cnt_stage = [torch.zeros(Pl, dtype=torch.int32, device=dev) for _ in range(2)]
+        ids_stage = [torch.zeros(Pl * cap, dtype=torch.int32, device=dev) for _ in range(2)]
 
     # Two output sets and two gather slabs: the RCCL root gather of build i runs on a side stream
     # and overlaps build i+1 (the exchange step overlapped with compute); a build's output set is
@@ -757,7 +758,8 @@ def main():
     bucket = GATHER_BUCKET if (fused and use_dist and not c5) else 1
     outs = [(w.out, w.tree_out)] + [w._outs() for _ in range(2 * bucket - 1)]
     outs_b = [(wb.out, wb.tree_out), wb._outs()] if c5 else None
-    gather = RootGather(P, world, dev, width=68 if c5 else 32, batch=bucket) if use_dist else None
+    # C5 slab row per partition: [A root | B root | diff count | cap diff ids] (as four arrays)
+    gather = RootGather(P, world, dev, width=68 + 4 * cap if c5 else 32, batch=bucket) if use_dist else None
     side = torch.cuda.Stream(dev) if use_dist else None
     ev_built = [torch.cuda.Event() for _ in range(2)]
     ev_gathered = [torch.cuda.Event() for _ in range(2)]
@@ -800,7 +802,8 @@ def main():
                           out_voff, bytes_cap, status)
         if use_dist:
             cnt_stage[k].copy_(diff_cnt)
-            roots = torch.cat([o["root"], ob["root"], cnt_stage[k].view(torch.uint8)])
+            ids_stage[k].copy_(diff_ids)
+            roots = torch.cat([o["root"], ob["root"], cnt_stage[k].view(torch.uint8), ids_stage[k].view(torch.uint8)])
             ev_built[k].record(stream)
             side.wait_event(ev_built[k])
             with torch.cuda.stream(side):
@@ -868,7 +871,8 @@ def main():
                               out_voff, bytes_cap, status)
             if use_dist:
                 cnt_stage[i].copy_(diff_cnt)
-                roots = torch.cat([o["root"], ob["root"], cnt_stage[i].view(torch.uint8)])
+                ids_stage[i].copy_(diff_ids)
+                roots = torch.cat([o["root"], ob["root"], cnt_stage[i].view(torch.uint8), ids_stage[i].view(torch.uint8)])
         if use_dist:
             ev_built[i].record(build_stream)
             side.wait_event(ev_built[i])
@@ -917,12 +921,16 @@ def main():
             got = out_vals[:want * V].view(want, V).cpu().numpy()[:: max(1, len(r) // 64)]
             src = vb.view(-1, V)[torch.from_numpy(samp).to(dev)].cpu().numpy()
             ok_ex = bool(np.array_equal(got, src))
-        if use_dist:  # step 0's gather (slab 0): [A roots | B roots | diff counts] per rank
+        if use_dist:  # step 0's gather (slab 0): [A roots | B roots | diff counts | diff ids] per rank
             slabs = gather.recv[0].view(world, -1).cpu().numpy()
-            counts = [slabs[r][len(local_partitions(P, r, world)) * 64:
-                               len(local_partitions(P, r, world)) * 68].view(np.int32) for r in range(world)]
+            nl = [len(local_partitions(P, r, world)) for r in range(world)]
+            counts = [slabs[r][nl[r] * 64:nl[r] * 68].view(np.int32) for r in range(world)]
+            gids = [slabs[r][nl[r] * 68:nl[r] * (68 + 4 * cap)].view(np.int32).reshape(nl[r], cap) for r in range(world)]
             parity["c5_gathered_diff_counts"] = bool(np.array_equal(counts[rank], cnt) and
                                                      all(((c == 0) | (c == 1)).all() for c in counts))
+            parity["c5_gathered_diff_ids"] = bool(np.array_equal(gids[rank], ids) and
+                                                  all(0 <= gids[r][p, 0] < B for r in range(world)
+                                                      for p in range(nl[r]) if counts[r][p] == 1))
         parity["c5_diff_is_exactly_the_perturbed_bucket"] = bool(ok)
         parity["c5_extract_records_and_bytes"] = bool(ok_ex)
         parity["c5_extracted_records_per_step"] = want
@@ -1087,7 +1095,7 @@ def main():
                        "partitions_per_gpu": Pl, "parallelism": f"partition-shard x{world}",
                        "root_gather": (("gloo all_gather (rehearsal, staged through the host)" if args.rehearse
                                         else "rccl all_gather_into_tensor")
-                                       + f" of ceil(P/N) x {68 if c5 else 32} B slabs on a side stream, "
+                                       + f" of ceil(P/N) x {68 + 4 * cap if c5 else 32} B slabs on a side stream, "
                                        + ("one per step (C5: both replicas' roots + diff counts)" if c5 else
                                           f"one per {GATHER_BUCKET if fused else 1} builds") + ", overlapped with the next build")
                        if use_dist else None},

@@ -454,3 +454,22 @@ def test_group_cabi_parity(members, rehearse):
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert all(d["parity"].values()), d
     assert d["members"] == members and ("rccl" in d["gather"]) == (members == 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["c4", "c5"])
+def test_bench_ranks_engine_under_torchrun(config):
+    """The one-process-per-GPU path (`--engine ranks`) at two ranks, both on GPU 0 with the gloo
+    gather (--rehearse): every parity gate holds, for C5 including the gathered diff counts and
+    diff-id lists of every rank."""
+    env = {**os.environ, "MASTER_ADDR": "127.0.0.1"}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--rehearse", "--engine", "ranks", "--config", config,
+           "--no-gather-per-build"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["parity"]["all_ranks_ok"], d["parity"]
+    if config == "c5":
+        assert d["parity"]["c5_gathered_diff_ids"] and d["parity"]["c5_gathered_diff_counts"]
