@@ -19,6 +19,9 @@ per GPU at N = 8); --scaling weak gives every GPU the N = 1 workload instead. Th
 JSON line on rank 0 with `roofline` (the dominant kernel, HIP events on the launch stream),
 `cpu_baseline` (the C restatement on the host cores, rank 0 at N = 1 only) and `parity` (every
 rank's timed build against the C oracle on host-regenerated records of a partition sample).
+Warm-up: W steps as given, or by default at least 3 steps covering at least WARMUP_MIN_MS of
+device time (the shader clock ramps up for 10-20 ms after the idle spell of the host-side parity
+checks); the line reports the W it ran.
 """
 from __future__ import annotations
 
