@@ -316,3 +316,48 @@ def test_disabled_service_serves_every_call_on_its_context(coracle):
         assert st["on_context"] == st["requests"] == 32
     finally:
         sv.close()
+
+
+def _random_server_cases(k, seed=5150):
+    """Seeded random one-call shapes: 1-4 partitions, B from 1 to 1,500 (some past the service's
+    slot limits, which run on its context), fixed 8-byte or variable-length values (0-40 bytes,
+    empty buckets and empty values among them)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(k):
+        P = int(rng.integers(1, 5))
+        B = int(rng.choice([1, 2, 3, 7, 64, 65, 333, 1000, 1500]))
+        fixed = bool(rng.integers(0, 2))
+        n = int(rng.integers(0, 3000))
+        out.append((P, B, fixed, n, int(rng.integers(0, 1 << 30))))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,B,fixed,n,seed", _random_server_cases(12))
+def test_server_random_shapes_match_oracle(coracle, P, B, fixed, n, seed):
+    """The resident service over seeded random shapes, full trees and digest-only builds, every
+    output equal to the C oracle's build of the same records (whatever served it: a resident slot
+    or, for the shapes past its slot limits, the service's context)."""
+    import mydatastore_amd as mde
+    rng = np.random.default_rng(seed)
+    S = P * B
+    cuts = np.sort(rng.integers(0, n + 1, S - 1)) if S > 1 else np.zeros(0, np.int64)
+    seg = np.concatenate([[0], cuts, [n]]).astype(np.uint64)
+    if fixed:
+        vals = rng.integers(0, 256, n * 8, dtype=np.uint8)
+        kw, okw = {"value_stride": 8}, {"stride": 8}
+    else:
+        lens = rng.integers(0, 41, n)
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        vals = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+        kw, okw = {"value_off": off}, {"value_off": off}
+    exp = coracle.build(vals, seg, P, B, **okw)
+    sv = mde.Server(0)
+    try:
+        for tree in (True, False):
+            got = sv.build(vals, seg, P, B, want_tree=tree, **kw)
+            for key in ("digest", "size", "items") + (("root", "nodes") if tree else ()):
+                assert np.array_equal(got[key], exp[key]), (key, tree)
+    finally:
+        sv.close()
