@@ -82,3 +82,55 @@ def test_fused_pipeline_random_shapes_match_oracle(engine, coracle, P, B, V, n, 
     engine.synchronize()
     assert np.array_equal(o["root"].cpu().numpy(), exp["root"])
     assert np.array_equal(o["nodes"].cpu().numpy(), exp["nodes"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,B,V,n,shift,seed", [c for c in _cases(12, seed=4242) if c[2]])
+def test_tagged_pipeline_random_shapes_match_oracle(engine, coracle, P, B, V, n, shift, seed):
+    """Layout B (records grouped by partition in arrival order, one u16 bucket tag each, binned on
+    the device): the same random shapes (fixed-length values) through two pipelined builds, against
+    the C oracle's build of the records sorted by (partition, bucket) -- a bucket's digest, size
+    and item count do not depend on its records' order."""
+    import torch
+    import mydatastore_amd as mde
+    rng = np.random.default_rng(seed)
+    dev = torch.device("cuda:0")
+    engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    ni = mde.tree_internal_nodes(B)
+    builds, keep = [], []
+    for _ in range(2):
+        cuts = np.sort(rng.integers(0, n + 1, P - 1)) if P > 1 else np.zeros(0, np.int64)
+        part_rec = np.concatenate([[0], cuts, [n]]).astype(np.uint64)
+        tags = rng.integers(0, B, n).astype(np.uint16)
+        vals = rng.integers(0, 256, n * V, dtype=np.uint8)
+        # the oracle's layout A: stable sort by (partition, tag)
+        part_of = np.repeat(np.arange(P), np.diff(part_rec).astype(np.int64))
+        order = np.lexsort((tags, part_of)) if n else np.zeros(0, np.int64)
+        sorted_vals = vals.reshape(n, V)[order].reshape(-1) if n else vals
+        counts = np.bincount(part_of * B + tags.astype(np.int64), minlength=P * B) if n else np.zeros(P * B, np.int64)
+        seg = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+        exp = coracle.build(sorted_vals, seg, P, B, stride=V)
+        buf = torch.zeros(vals.size + shift + 16, dtype=torch.uint8, device=dev)
+        buf[shift:shift + vals.size].copy_(torch.from_numpy(vals))
+        d_tag = torch.from_numpy(tags.view(np.int16).copy()).to(dev)
+        d_pr = torch.from_numpy(part_rec.view(np.int64)).to(dev)
+        rec = mde.Records(buf.data_ptr() + shift if vals.size else 0, vals.size, V, mde.LAYOUT_TAGGED, 0, n, P, B, 0,
+                          d_tag.data_ptr() if n else 0, d_pr.data_ptr())
+        o = {"digest": torch.zeros(P * B, dtype=torch.int64, device=dev),
+             "size": torch.zeros(P * B, dtype=torch.int32, device=dev),
+             "items": torch.zeros(P, dtype=torch.int32, device=dev),
+             "root": torch.zeros(P * 32, dtype=torch.uint8, device=dev),
+             "nodes": torch.zeros(P * ni * 32, dtype=torch.uint8, device=dev)}
+        to = mde.TreeOut(*(o[k].data_ptr() for k in ("digest", "size", "items", "root", "nodes")))
+        builds.append((rec, o, to, exp))
+        keep.append((buf, d_tag, d_pr))
+    for rec, o, to, exp in builds:
+        engine.build_pipelined_async(rec, to)
+    engine.build_pipeline_drain_async()
+    engine.synchronize()
+    for i, (rec, o, to, exp) in enumerate(builds):
+        assert np.array_equal(o["digest"].cpu().numpy().view(np.uint64), exp["digest"]), ("digest", i)
+        assert np.array_equal(o["size"].cpu().numpy(), exp["size"]), ("size", i)
+        assert np.array_equal(o["items"].cpu().numpy(), exp["items"]), ("items", i)
+        assert np.array_equal(o["root"].cpu().numpy(), exp["root"]), ("root", i)
+        assert np.array_equal(o["nodes"].cpu().numpy(), exp["nodes"]), ("nodes", i)
