@@ -18,10 +18,6 @@ package main
 import "C"
 
 import (
-	"bytes"
-	"crypto/sha256"
-	"encoding/binary"
-	"hash"
 	"log"
 	"sync"
 	"sync/atomic"
@@ -55,6 +51,8 @@ var (
 	// mdeHostTree: build every returned tree with plain merkletree.NewTree over the device digests
 	// (a digest-only device build; B-1 host SHA-256s per call). Either way the tree is merkletree's
 	// own (mdeNewTree): MerkleRoot(), VerifyTree(), VerifyContent() and RebuildTree() all work on it.
+	// Built with -tags mde_nohashstrategy (merkletree without NewTreeWithHashStrategy,
+	// merkle_gpu_nomemo.go) every tree is a host tree whatever this says (mdeHashStrategy = false).
 	mdeHostTree = false
 	// mdeHostCompressions counts the SHA-256 compressions this process ran on the host for the
 	// trees it returned (the memo's misses, or every node of a host tree); batch_bench reports the
@@ -123,105 +121,19 @@ func mdeServer(partitionId int) (*C.mde_server, error) {
 // crypto/sha256 uses, the device ~2 us (INTEGRATION.md section 3).
 const mdeTopNodes = 64
 
-// mdeMemo -- what the device already hashed, in the order merkletree asks for it. cbergoon/merkletree
-// v0.2.0's construction (buildIntermediate) takes one hasher from the hash strategy per internal
-// node, level 1 first, left to right within a level -- the order of mde_tree_out.nodes -- and writes
-// it that node's message: left.Hash || right.Hash (two 8-byte LE64 leaves at level 1,
-// main/merkle_tree.go:64-71 and utils/utils.go:67-74; two 32-byte hashes above), the duplicate of
-// the last leaf when B is odd, the last node of an odd level paired with itself. The k-th hasher
-// answers with device node k's hash only when the message it was written is exactly node k's
-// message as the device hashed it; otherwise it runs SHA-256. A hit is therefore always the
-// SHA-256 of the bytes merkletree asked about, whatever order or tree it comes from (a tampered
-// leaf, another tree); the order only decides how often it hits. O(1) per node: no map, no copy
-// of the device's nodes.
-type mdeMemo struct {
-	leaf   [][]byte // LE64 leaf hashes (+ the odd-B duplicate)
-	nodes  []byte   // the device's node hashes, level 1 .. root, 32 bytes each
-	have   int      // how many of them the device wrote (its levels; all of them for a whole tree)
-	lvl    []int    // node count of each internal level, level 1 first
-	next   int      // the node merkletree's construction hashes next
-	active bool     // false once the tree exists: later hashers are plain SHA-256
-}
-
-func newMdeMemo(digest []uint64, nodes []byte, have int) *mdeMemo {
-	B := len(digest)
-	m := &mdeMemo{leaf: make([][]byte, B, B+1), nodes: nodes, have: have, active: true}
-	for i := 0; i < B; i++ {
-		m.leaf[i] = make([]byte, 8)
-		binary.LittleEndian.PutUint64(m.leaf[i], digest[i])
-	}
-	if B%2 == 1 {
-		m.leaf = append(m.leaf, m.leaf[B-1])
-	}
-	for n := len(m.leaf); n > 1; {
+// mdeTreeCompressions -- SHA-256 compressions of merkletree.NewTree over B buckets: one per 16-byte
+// level-1 message, two per 64-byte message above (the odd-B duplicate leaf included).
+func mdeTreeCompressions(B int) uint64 {
+	n, c := B+B%2, uint64(0)
+	for lvl := 1; n > 1; lvl++ {
 		n = (n + 1) / 2
-		m.lvl = append(m.lvl, n)
-	}
-	return m
-}
-
-// message of device node k: its children's hashes (nil when k is past the device's nodes)
-func (m *mdeMemo) message(k int) ([]byte, []byte) {
-	if k >= m.have {
-		return nil, nil
-	}
-	off, below, prev := 0, len(m.leaf), -1
-	for _, n := range m.lvl {
-		if k < off+n {
-			j := k - off
-			li, ri := 2*j, 2*j
-			if 2*j+1 < below {
-				ri = 2*j + 1
-			}
-			if prev < 0 {
-				return m.leaf[li], m.leaf[ri]
-			}
-			return m.nodes[(prev+li)*32 : (prev+li+1)*32], m.nodes[(prev+ri)*32 : (prev+ri+1)*32]
+		if lvl == 1 {
+			c += uint64(n)
+		} else {
+			c += 2 * uint64(n)
 		}
-		prev, below, off = off, n, off+n
 	}
-	return nil, nil
-}
-
-// mdeMemoHash -- the hash.Hash the strategy hands merkletree for node k: Write buffers the node's
-// message; Sum returns the device's hash of node k when the message is node k's, else SHA-256.
-type mdeMemoHash struct {
-	m   *mdeMemo
-	k   int
-	buf []byte
-}
-
-func (h *mdeMemoHash) Write(p []byte) (int, error) { h.buf = append(h.buf, p...); return len(p), nil }
-func (h *mdeMemoHash) Reset()                      { h.buf = h.buf[:0] }
-func (h *mdeMemoHash) Size() int                   { return sha256.Size }
-func (h *mdeMemoHash) BlockSize() int              { return sha256.BlockSize }
-func (h *mdeMemoHash) Sum(b []byte) []byte {
-	if l, r := h.m.message(h.k); l != nil && len(h.buf) == len(l)+len(r) &&
-		bytes.Equal(h.buf[:len(l)], l) && bytes.Equal(h.buf[len(l):], r) {
-		return append(b, h.m.nodes[h.k*32:(h.k+1)*32]...) // a copy: merkletree appends to node hashes
-	}
-	atomic.AddUint64(&mdeHostCompressions, uint64(len(h.buf)+8)/64+1)
-	sum := sha256.Sum256(h.buf)
-	return append(b, sum[:]...)
-}
-
-// mdeNewTree -- merkletree's own tree over the buckets, its internal hashes taken from the memo (no
-// host SHA-256 for the nodes the device built): merkletree.NewTreeWithHashStrategy runs its own
-// construction (leafs, the odd-B duplicate, parents, merkleRoot), so MerkleRoot(), VerifyTree(),
-// VerifyContent() and RebuildTree() behave as on a NewTree tree. Once the tree exists the memo is
-// switched off: a later VerifyTree / RebuildTree hashes with real SHA-256, as the reference's trees
-// do.
-func mdeNewTree(cs []merkletree.Content, m *mdeMemo) (*merkletree.MerkleTree, error) {
-	t, err := merkletree.NewTreeWithHashStrategy(cs, func() hash.Hash {
-		if !m.active {
-			return sha256.New()
-		}
-		h := &mdeMemoHash{m: m, k: m.next}
-		m.next++
-		return h
-	})
-	m.active, m.nodes = false, nil
-	return t, err
+	return c
 }
 
 func cU64(v []uint64) unsafe.Pointer { return C.CBytes(unsafe.Slice((*byte)(unsafe.Pointer(&v[0])), len(v)*8)) }
@@ -281,7 +193,7 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 		value_off: (*C.uint64_t)(cOff), n_records: C.uint64_t(len(valueOff) - 1),
 		n_partitions: 1, n_buckets: C.uint32_t(B), seg_rec: (*C.uint64_t)(cSeg),
 	}
-	hostTree := mdeHostTree || B <= mdeHostTreeMaxBuckets
+	hostTree := mdeHostTree || !mdeHashStrategy || B <= mdeHostTreeMaxBuckets
 	out := C.mde_tree_out{digest: (*C.uint64_t)(cDigest), size: (*C.int32_t)(cSize),
 		items: (*C.int32_t)(cItems)}
 	if !hostTree { // else a digest-only build: root and nodes stay NULL
@@ -313,12 +225,11 @@ func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, uppe
 		bucketList[i] = &MerkleBucket{bucketId: int32(i), hasher: &CustomHash{value: int64(digest[i])}, size: size[i]}
 	}
 	if !hostTree { // merkletree's construction, its node hashes from the device (the top levels of a split build hashed here)
-		return mdeNewTree(bucketList, newMdeMemo(digest, unsafe.Slice((*byte)(cNodes), nodeBytes), have))
+		return mdeNewTree(bucketList, digest, unsafe.Slice((*byte)(cNodes), nodeBytes), have)
 	}
 	// merkletree.NewTree over the device digests (B-1 host SHA-256s: one compression per 16-byte
 	// level-1 message, two per 64-byte message above)
-	n1 := uint64(B+1) / 2
-	atomic.AddUint64(&mdeHostCompressions, 2*uint64(C.mde_tree_internal_nodes(C.uint32_t(B)))-n1)
+	atomic.AddUint64(&mdeHostCompressions, mdeTreeCompressions(B))
 	return merkletree.NewTree(bucketList)
 }
 

@@ -8,8 +8,15 @@ import re
 
 from tests.conftest import ROOT
 
-GO = ROOT / "integration" / "go" / "merkle_gpu.go"
+GO_DIR = ROOT / "integration" / "go"
+GO = GO_DIR / "merkle_gpu.go"
+GO_MEMO = GO_DIR / "merkle_gpu_memo.go"          # //go:build !mde_nohashstrategy
+GO_NOMEMO = GO_DIR / "merkle_gpu_nomemo.go"      # //go:build mde_nohashstrategy
 HEADER = ROOT / "include" / "mde.h"
+
+
+def _shim_sources():
+    return {p.name: p.read_text() for p in sorted(GO_DIR.glob("*.go"))}
 
 
 def _header():
@@ -50,7 +57,7 @@ def _call_args(src, start):
 
 def test_shim_names_exist_in_header():
     funcs, consts, types, structs = _header()
-    src = GO.read_text()
+    src = "\n".join(_shim_sources().values())
     code = re.sub(r"//.*", "", src)
     used_funcs = set(re.findall(r"\bC\.(mde_[a-z0-9_]+)\s*\(", code))
     used_types = set(re.findall(r"\bC\.(mde_[a-z0-9_]+)\b(?!\s*\()", code))
@@ -74,7 +81,7 @@ def test_shim_reimplements_the_reference_signatures():
     merkletree itself -- NewTree, or NewTreeWithHashStrategy fed by the memo of device node hashes
     -- never as a struct literal, whose unexported merkleRoot / leaf / dup / Tree fields would stay
     unset (MerkleRoot() nil, VerifyTree() walking into nil children)."""
-    src = GO.read_text()
+    src = "\n".join(_shim_sources().values())
     code = re.sub(r"//.*", "", src)
     assert ("func (manager *Manager) RawPartitionMerkleTree(partitionId int, lowerEpoch, upperEpoch int64) "
             "(*merkletree.MerkleTree, error)") in src
@@ -91,6 +98,44 @@ def test_shim_reimplements_the_reference_signatures():
     assert "bytes.Equal(h.buf[:len(l)], l) && bytes.Equal(h.buf[len(l):], r)" in code
     assert "return append(b, h.m.nodes[h.k*32:(h.k+1)*32]...)" in code
     assert "m.active, m.nodes = false, nil" in code
+
+
+def test_shim_hash_strategy_constructor_is_build_tagged():
+    """The memoised construction names merkletree.NewTreeWithHashStrategy, whose presence at the
+    pinned v0.2.0 (main/go.sum:3) cannot be checked without Go. Go compiles every function of a
+    file it builds, so the fallback must be a build tag, not a variable: the constructor and the
+    memo live only in merkle_gpu_memo.go (//go:build !mde_nohashstrategy); merkle_gpu_nomemo.go
+    (//go:build mde_nohashstrategy) defines mdeNewTree with the same signature as plain NewTree;
+    each defines mdeHashStrategy, and the main file uses only mdeNewTree / mdeHashStrategy."""
+    srcs = _shim_sources()
+    assert set(srcs) == {GO.name, GO_MEMO.name, GO_NOMEMO.name}
+    code = {n: re.sub(r"//.*", "", s) for n, s in srcs.items()}
+    first = {n: s.lstrip().splitlines()[0] for n, s in srcs.items()}
+    assert first[GO_MEMO.name] == "//go:build !mde_nohashstrategy"
+    assert first[GO_NOMEMO.name] == "//go:build mde_nohashstrategy"
+    assert not first[GO.name].startswith("//go:build")
+    for n, c in code.items():
+        assert ("NewTreeWithHashStrategy" in c) == (n == GO_MEMO.name), n
+        assert ("mdeMemo" in c) == (n == GO_MEMO.name), n
+    sig = re.compile(r"^func mdeNewTree\((.*?)\) \((.*?)\) \{", re.M)
+    sigs = {n: sig.findall(c) for n, c in code.items()}
+    assert sigs[GO.name] == []
+    assert len(sigs[GO_MEMO.name]) == 1 and sigs[GO_MEMO.name] == sigs[GO_NOMEMO.name]
+    assert "const mdeHashStrategy = true" in code[GO_MEMO.name]
+    assert "const mdeHashStrategy = false" in code[GO_NOMEMO.name]
+    assert "return merkletree.NewTree(cs)" in code[GO_NOMEMO.name]
+    # without the constructor the device builds digests only: every tree is a host tree
+    assert "hostTree := mdeHostTree || !mdeHashStrategy ||" in code[GO.name]
+    assert "mdeNewTree(bucketList, digest," in code[GO.name]
+    # each file imports what it uses (an unused import is a Go compile error)
+    for n, c in code.items():
+        imports = re.search(r"import \((.*?)\)", c, re.S).group(1)
+        for pkg in re.findall(r'"([\w./-]+)"', imports):
+            name = pkg.rsplit("/", 1)[-1]
+            if pkg == "C":
+                continue
+            body = c[c.index(imports) + len(imports):]
+            assert re.search(r"\b" + re.escape(name) + r"\.", body), (n, pkg)
 
 
 # ---------------------------------------------------------------------------------------------
