@@ -218,6 +218,22 @@ int mde_extract(mde_ctx* ctx, const mde_records* rec, const int32_t* ids, uint64
                 const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
                 uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap);
 
+/* StreamBucketsTask's own list contract (main/manager.go:447-485; replaces the loop over
+ * task.Buckets): for partition p the requested ids ids[p*ids_stride .. +counts[p]) are walked IN
+ * THE ORDER GIVEN -- a repeated id streams its bucket's records again, an id outside [0, n_buckets)
+ * streams nothing (no record carries it) -- and counts[p] == 0 streams every bucket 0..B-1 (the
+ * task's empty list, :448-452); counts[p] < 0 streams nothing. Within a bucket, LSM record order.
+ * Layout A only (MDE_E_INVAL for MDE_LAYOUT_TAGGED). Outputs as mde_extract; rec_cap / bytes_cap
+ * must cover the repeats. mde_extract stays the deduplicated ascending form for VerifyEpoch's
+ * diff set (already an Int32Set, :1086), whose order the reference leaves to Go's map iteration. */
+int mde_stream_buckets_async(mde_ctx* ctx, const mde_records* rec, const int32_t* ids, uint64_t ids_stride,
+                             const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
+                             uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap,
+                             int32_t* status);
+int mde_stream_buckets(mde_ctx* ctx, const mde_records* rec, const int32_t* ids, uint64_t ids_stride,
+                       const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
+                       uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap);
+
 /* EpochTreeObject wire bytes (datap/data.proto:60-68), exactly as proto.Marshal emits them for
  * MerkleTreeToPartitionEpochObject's object (main/merkle_tree.go:118-138, main/manager.go:1045):
  * leaves follow tree.Leafs (an odd B repeats the last bucket), zero scalars omitted, sizes packed.

@@ -38,7 +38,8 @@ EXPORTED_SYMBOLS = (
     "mde_digest_async", "mde_tree_async", "mde_build_pipelined_async", "mde_build_pipeline_drain_async",
     "mde_tree_from_digests", "mde_tree_from_digests_async",
     "mde_decode_bucket_hashes", "mde_diff", "mde_diff_async", "mde_diff_digests", "mde_tag_keys_async", "mde_tag_keys",
-    "mde_extract", "mde_extract_async", "mde_epoch_tree_object_max_bytes",
+    "mde_extract", "mde_extract_async", "mde_stream_buckets", "mde_stream_buckets_async",
+    "mde_epoch_tree_object_max_bytes",
     "mde_encode_epoch_tree_objects", "mde_encode_epoch_tree_objects_async",
     "mde_decode_epoch_tree_objects", "mde_decode_epoch_tree_objects_async", "mde_synth_tags_async", "mde_synth_values_async", "mde_dev_alloc", "mde_dev_free",
     "mde_memcpy_h2d", "mde_memcpy_d2h", "mde_verify_peer_capacity", "mde_verify_epochs",
@@ -149,6 +150,8 @@ def load_library() -> C.CDLL:
         "mde_tag_keys": (C.c_int, [vp, vp, vp, u64, u32, u32, vp, vp]),
         "mde_extract": (C.c_int, [vp, C.POINTER(Records), vp, u64, vp, vp, vp, u64, vp, vp, u64]),
         "mde_extract_async": (C.c_int, [vp, C.POINTER(Records), vp, u64, vp, vp, vp, u64, vp, vp, u64, vp]),
+        "mde_stream_buckets": (C.c_int, [vp, C.POINTER(Records), vp, u64, vp, vp, vp, u64, vp, vp, u64]),
+        "mde_stream_buckets_async": (C.c_int, [vp, C.POINTER(Records), vp, u64, vp, vp, vp, u64, vp, vp, u64, vp]),
         "mde_epoch_tree_object_max_bytes": (u64, [u32]),
         "mde_encode_epoch_tree_objects": (C.c_int, [vp, u32, u32, vp, C.c_int64, C.c_int64, vp, vp, vp, vp, vp, u64, vp]),
         "mde_encode_epoch_tree_objects_async": (C.c_int, [vp, u32, u32, vp, C.c_int64, C.c_int64, vp, vp, vp, vp, vp, u64, vp]),
@@ -489,6 +492,53 @@ class Engine:
         if not want_values:
             return part_off, out_rec[:n], None, None
         return part_off, out_rec[:n], out_vals[:int(out_voff[n])], out_voff[:n + 1]
+
+    def stream_buckets(self, values, seg_rec, n_partitions, n_buckets, ids, ids_stride, counts,
+                       value_stride=0, value_off=None, want_values=True):
+        """mde_stream_buckets: StreamBucketsTask's request-order contract (main/manager.go:447-485)
+        -- ids walked as given, repeats streamed again, ids outside [0, B) stream nothing,
+        counts[p] == 0 streams every bucket. Layout A. Returns (part_off, rec_idx, values_bytes,
+        value_off); the output capacities are the requests' record and byte totals."""
+        values = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1)
+        if value_off is not None:
+            value_off = np.ascontiguousarray(value_off, dtype=np.uint64)
+        n_rec = (value_off.size - 1) if value_off is not None else (
+            values.size // value_stride if value_stride else 0)
+        seg_rec = np.ascontiguousarray(seg_rec, dtype=np.uint64)
+        rec = Records(_ptr(values), values.nbytes, value_stride, 0, _ptr(value_off), n_rec,
+                      n_partitions, n_buckets, _ptr(seg_rec))
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        counts = np.ascontiguousarray(counts, dtype=np.int32)
+        # capacities: every request's run (repeats included)
+        nrec = seg_rec[1:].astype(np.int64) - seg_rec[:-1].astype(np.int64)
+        segb = (value_off[seg_rec.astype(np.int64)] if value_off is not None
+                else seg_rec * np.uint64(value_stride)).astype(np.int64)
+        nbyt = segb[1:] - segb[:-1]
+        need_r = need_b = 0
+        for p in range(n_partitions):
+            c = int(counts[p])
+            req = (np.arange(n_buckets) if c == 0 else
+                   ids[p * ids_stride: p * ids_stride + max(c, 0)].astype(np.int64))
+            req = req[(req >= 0) & (req < n_buckets)] + p * n_buckets
+            need_r += int(nrec[req].sum())
+            need_b += int(nbyt[req].sum())
+        rec_cap, bytes_cap = max(need_r, 1), max(need_b, 1)
+        part_off = np.zeros(n_partitions + 1, np.uint64)
+        out_rec = np.zeros(rec_cap, np.uint64)
+        out_vals = np.zeros(bytes_cap, np.uint8) if want_values else None
+        out_voff = np.zeros(rec_cap + 1, np.uint64) if want_values else None
+        self._call("mde_stream_buckets", C.byref(rec), _ptr(ids), ids_stride, _ptr(counts),
+                   _ptr(part_off), _ptr(out_rec), rec_cap, _ptr(out_vals), _ptr(out_voff), bytes_cap)
+        n = int(part_off[-1])
+        if not want_values:
+            return part_off, out_rec[:n], None, None
+        return part_off, out_rec[:n], out_vals[:int(out_voff[n])], out_voff[:n + 1]
+
+    def stream_buckets_async(self, rec: Records, ids, ids_stride, counts, part_off, out_rec, rec_cap,
+                             out_values, out_value_off, bytes_cap, status):
+        self._call("mde_stream_buckets_async", C.byref(rec), _ptr(ids), ids_stride,
+                   _ptr(counts), _ptr(part_off), _ptr(out_rec), rec_cap,
+                   _ptr(out_values), _ptr(out_value_off), bytes_cap, _ptr(status))
 
     def extract_async(self, rec: Records, ids, ids_stride, counts, part_off, out_rec, rec_cap,
                       out_values, out_value_off, bytes_cap, status):

@@ -16,6 +16,13 @@
 // record's tag against the bitmap (a stream compaction over the partition, 2 bytes of tag read
 // per record) and emitted in arrival order -- a bucket's records are not contiguous there, and
 // the reference's order within a bucket is LSM key order, which write order does not carry.
+//
+// Request-order mode (ExtractLaunch::ordered, mde_stream_buckets): StreamBucketsTask's own list
+// contract (main/manager.go:447-485) -- the ids are walked in the order given, a repeated id streams
+// its bucket's records again, an id outside [0, B) streams nothing (no record carries it), and an
+// empty list (counts[p] == 0) means every bucket 0..B-1 (:448-452). Layout A only. The count
+// kernel sums the runs of the requests; the copy kernel scans the requests 64 at a time and copies
+// each run in turn with the whole workgroup, as extract_copy_kernel does for marked buckets.
 #include "mde_device.hpp"
 #include "mde_internal.hpp"
 
@@ -39,23 +46,67 @@ __device__ void load_bitmap(const ExtractLaunch& a, uint32_t p, uint32_t* bm) {
 
 __device__ __forceinline__ bool marked(const uint32_t* bm, uint32_t b) { return (bm[b >> 5] >> (b & 31)) & 1u; }
 
+// Request-order mode: how many requests partition p has, and the i-th one's bucket id.
+__device__ __forceinline__ uint32_t n_requests(const ExtractLaunch& a, uint32_t p) {
+  const int32_t n = a.counts[p];
+  return n < 0 ? 0u : n == 0 ? a.B : (uint32_t)n;
+}
+__device__ __forceinline__ int32_t request_id(const ExtractLaunch& a, uint32_t p, uint32_t i) {
+  return a.counts[p] == 0 ? (int32_t)i : a.ids[(uint64_t)p * a.ids_stride + i];
+}
+
+// Copies bucket bs's run (records r0..r1, their value bytes) to out_rec[rb..], out_values[bb..]
+// with the whole workgroup.
+__device__ void copy_run(const ExtractLaunch& a, uint32_t bs, uint64_t rb, uint64_t bb) {
+  const uint64_t r0 = a.seg.seg_rec[bs], r1 = a.seg.seg_rec[bs + 1];
+  const uint64_t src0 = segpos(a.seg, bs) - a.seg.shift, src1 = segpos(a.seg, bs + 1) - a.seg.shift;
+  for (uint64_t r = r0 + threadIdx.x; r < r1; r += kThreads) {
+    a.out_rec[rb + (r - r0)] = r;
+    if (a.out_value_off) a.out_value_off[rb + (r - r0)] = bb + (recpos(a.seg, r) - src0);
+  }
+  if (a.out_values) {
+    const uint8_t* src = a.values + src0;
+    uint8_t* dst = a.out_values + bb;
+    const uint64_t len = src1 - src0;
+    if ((((uintptr_t)src | (uintptr_t)dst | len) & 15u) == 0) {
+      const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+      u32x4* d4 = reinterpret_cast<u32x4*>(dst);
+      for (uint64_t i = threadIdx.x; i < len / 16; i += kThreads) d4[i] = __builtin_nontemporal_load(s4 + i);
+    } else {
+      for (uint64_t i = threadIdx.x; i < len; i += kThreads) dst[i] = src[i];
+    }
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void extract_count_kernel(ExtractLaunch a) {
   __shared__ uint32_t bm[kBitmapWords];
   __shared__ unsigned long long tot[2];
   const uint32_t p = blockIdx.x;
   if (threadIdx.x == 0) { tot[0] = 0; tot[1] = 0; }
-  load_bitmap(a, p, bm);
   unsigned long long nr = 0, nb = 0;
-  if (a.tag) {  // layout B: test every record's tag
+  if (a.ordered) {  // request order: every request's run, repeats included
+    __syncthreads();  // tot[] is zero before any thread adds to it
+    const uint32_t n = n_requests(a, p);
+    for (uint32_t i = threadIdx.x; i < n; i += kThreads) {
+      const int32_t b = request_id(a, p, i);
+      if (b < 0 || (uint32_t)b >= a.B) continue;
+      const uint32_t s = p * a.B + (uint32_t)b;
+      nr += a.seg.seg_rec[s + 1] - a.seg.seg_rec[s];
+      nb += segpos(a.seg, s + 1) - segpos(a.seg, s);
+    }
+  } else if (a.tag) {  // layout B: test every record's tag
+    load_bitmap(a, p, bm);
     for (uint64_t r = a.part_rec[p] + threadIdx.x; r < a.part_rec[p + 1]; r += kThreads)
       nr += marked(bm, min((uint32_t)a.tag[r], a.B - 1)) ? 1u : 0u;
     nb = nr * a.stride;
-  }
-  for (uint32_t b = threadIdx.x; b < a.B && !a.tag; b += kThreads) {
-    if (!marked(bm, b)) continue;
-    const uint32_t s = p * a.B + b;
-    nr += a.seg.seg_rec[s + 1] - a.seg.seg_rec[s];
-    nb += segpos(a.seg, s + 1) - segpos(a.seg, s);
+  } else {
+    load_bitmap(a, p, bm);
+    for (uint32_t b = threadIdx.x; b < a.B; b += kThreads) {
+      if (!marked(bm, b)) continue;
+      const uint32_t s = p * a.B + b;
+      nr += a.seg.seg_rec[s + 1] - a.seg.seg_rec[s];
+      nb += segpos(a.seg, s + 1) - segpos(a.seg, s);
+    }
   }
   if (nr) atomicAdd(&tot[0], nr);
   if (nb) atomicAdd(&tot[1], nb);
@@ -185,27 +236,45 @@ __global__ __launch_bounds__(kThreads) void extract_copy_kernel(ExtractLaunch a)
     while (ball) {
       const int k = __ffsll((long long)ball) - 1;
       ball &= ball - 1;
-      const uint32_t bs = p * a.B + b0 + k;
-      const uint64_t rb = __shfl(r_base, k), bb = __shfl(b_base, k);
-      const uint64_t r0 = a.seg.seg_rec[bs], r1 = a.seg.seg_rec[bs + 1];
-      const uint64_t src0 = segpos(a.seg, bs) - a.seg.shift, src1 = segpos(a.seg, bs + 1) - a.seg.shift;
       // every wave computed the same window scan, so all 256 threads copy this bucket together
-      for (uint64_t r = r0 + threadIdx.x; r < r1; r += kThreads) {
-        a.out_rec[rb + (r - r0)] = r;
-        if (a.out_value_off) a.out_value_off[rb + (r - r0)] = bb + (recpos(a.seg, r) - src0);
-      }
-      if (a.out_values) {
-        const uint8_t* src = a.values + src0;
-        uint8_t* dst = a.out_values + bb;
-        const uint64_t len = src1 - src0;
-        if ((((uintptr_t)src | (uintptr_t)dst | len) & 15u) == 0) {
-          const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
-          u32x4* d4 = reinterpret_cast<u32x4*>(dst);
-          for (uint64_t i = threadIdx.x; i < len / 16; i += kThreads) d4[i] = __builtin_nontemporal_load(s4 + i);
-        } else {
-          for (uint64_t i = threadIdx.x; i < len; i += kThreads) dst[i] = src[i];
-        }
-      }
+      copy_run(a, p * a.B + b0 + k, __shfl(r_base, k), __shfl(b_base, k));
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && p == a.P - 1 && a.out_value_off) a.out_value_off[a.part_off[a.P]] = run[1];
+}
+
+// Request order: requests i0..i0+63 per round; lane i's run lands after the runs of the requests
+// before it (a wave scan, computed identically by every wave), then the workgroup copies the
+// non-empty runs in request order.
+__global__ __launch_bounds__(kThreads) void extract_copy_ordered_kernel(ExtractLaunch a) {
+  __shared__ unsigned long long run[2];
+  const uint32_t p = blockIdx.x;
+  if (*a.status != 0) return;  // capacity exceeded: nothing is written
+  if (threadIdx.x == 0) { run[0] = a.part_off[p]; run[1] = a.scratch[2 * (a.P + 1) + p]; }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const uint32_t n = n_requests(a, p);
+  for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const int32_t b = i < n ? request_id(a, p, i) : -1;
+    const bool in = b >= 0 && (uint32_t)b < a.B;
+    const uint32_t s = p * a.B + (in ? (uint32_t)b : 0u);
+    unsigned long long nr = in ? a.seg.seg_rec[s + 1] - a.seg.seg_rec[s] : 0;
+    unsigned long long nb = in ? segpos(a.seg, s + 1) - segpos(a.seg, s) : 0;
+    unsigned long long er = nr, eb = nb;  // inclusive wave scan
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long xr = __shfl_up(er, o), xb = __shfl_up(eb, o);
+      if (lane >= o) { er += xr; eb += xb; }
+    }
+    const unsigned long long r_base = run[0] + er - nr, b_base = run[1] + eb - nb;
+    __syncthreads();
+    if (threadIdx.x == 63) { run[0] += er; run[1] += eb; }
+    unsigned long long ball = __ballot(nr != 0);
+    while (ball) {
+      const int k = __ffsll((long long)ball) - 1;
+      ball &= ball - 1;
+      copy_run(a, __shfl(s, k), __shfl(r_base, k), __shfl(b_base, k));
     }
     __syncthreads();
   }
@@ -218,7 +287,9 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
   if (a.P == 0) return hipSuccess;
   hipLaunchKernelGGL(extract_count_kernel, dim3(a.P), dim3(kThreads), 0, st, a);
   hipLaunchKernelGGL(extract_scan_kernel, dim3(1), dim3(kThreads), 0, st, a);
-  if (a.tag)
+  if (a.ordered)
+    hipLaunchKernelGGL(extract_copy_ordered_kernel, dim3(a.P), dim3(kThreads), 0, st, a);
+  else if (a.tag)
     hipLaunchKernelGGL(extract_copy_tagged_kernel, dim3(a.P), dim3(kThreads), 0, st, a);
   else
     hipLaunchKernelGGL(extract_copy_kernel, dim3(a.P), dim3(kThreads), 0, st, a);

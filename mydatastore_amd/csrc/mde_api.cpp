@@ -682,11 +682,16 @@ int build_pipelined(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
   return MDE_OK;
 }
 
+// ordered: mde_stream_buckets' request-order contract (ExtractLaunch::ordered); else mde_extract's
+// deduplicated ascending set
 int extract_async(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t ids_stride,
                   const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
-                  uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap, int32_t* status) {
+                  uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap, int32_t* status,
+                  bool ordered) {
   if (r->n_buckets > mde::kExtractMaxBuckets)
     return set_err(c, MDE_E_INVAL, "extract supports n_buckets <= %u", mde::kExtractMaxBuckets);
+  if (ordered && r->layout == MDE_LAYOUT_TAGGED)
+    return set_err(c, MDE_E_INVAL, "mde_stream_buckets needs layout A (a bucket's records in LSM order)");
   if (!ids || !counts || !part_off || !out_rec || !status || (out_values && !r->values))
     return set_err(c, MDE_E_INVAL, "bad extract arguments");
   int rc = ensure_buf(c, c->extract_scratch, 3 * ((uint64_t)r->n_partitions + 1) * 8);
@@ -713,6 +718,7 @@ int extract_async(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t
   a.bytes_cap = bytes_cap;
   a.status = status;
   a.scratch = static_cast<uint64_t*>(c->extract_scratch.p);
+  a.ordered = ordered;
   MDE_HIP(c, mde::launch_extract(a, c->stream));
   return MDE_OK;
 }
@@ -1271,14 +1277,25 @@ int mde_extract_async(mde_ctx* c, const mde_records* r, const int32_t* ids, uint
   Guard g(c);
   int rc = check_records(c, r);
   return rc ? rc : extract_async(c, r, ids, ids_stride, counts, part_off, out_rec, rec_cap, out_values,
-                                 out_value_off, bytes_cap, status);
+                                 out_value_off, bytes_cap, status, false);
 }
 
-int mde_extract(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t ids_stride,
-                const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
-                uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap) {
+int mde_stream_buckets_async(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t ids_stride,
+                             const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
+                             uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap,
+                             int32_t* status) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
+  int rc = check_records(c, r);
+  return rc ? rc : extract_async(c, r, ids, ids_stride, counts, part_off, out_rec, rec_cap, out_values,
+                                 out_value_off, bytes_cap, status, true);
+}
+
+namespace {
+// mde_extract / mde_stream_buckets over host buffers: stage, extract, copy back.
+int extract_host(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t ids_stride,
+                 const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
+                 uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap, bool ordered) {
   int rc = check_records(c, r);
   if (rc) return rc;
   if ((rc = check_host_records(c, r))) return rc;
@@ -1310,7 +1327,7 @@ int mde_extract(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t i
                      static_cast<uint64_t*>(dp(6)), rec_cap,
                      out_values ? static_cast<uint8_t*>(dp(7)) : nullptr,
                      out_value_off ? static_cast<uint64_t*>(dp(8)) : nullptr, bytes_cap,
-                     static_cast<int32_t*>(dp(9)));
+                     static_cast<int32_t*>(dp(9)), ordered);
   if (rc) return rc;
   int32_t status = 0;
   MDE_HIP(c, hipMemcpyAsync(&status, dp(9), 4, hipMemcpyDeviceToHost, c->stream));
@@ -1334,6 +1351,25 @@ int mde_extract(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t i
   }
   MDE_HIP(c, hipStreamSynchronize(c->stream));
   return MDE_OK;
+}
+}  // namespace
+
+int mde_extract(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t ids_stride,
+                const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
+                uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  return extract_host(c, r, ids, ids_stride, counts, part_off, out_rec, rec_cap, out_values, out_value_off,
+                      bytes_cap, false);
+}
+
+int mde_stream_buckets(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t ids_stride,
+                       const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
+                       uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  return extract_host(c, r, ids, ids_stride, counts, part_off, out_rec, rec_cap, out_values, out_value_off,
+                      bytes_cap, true);
 }
 
 uint64_t mde_epoch_tree_object_max_bytes(uint32_t B) { return mde::wire_max_bytes(B); }

@@ -197,6 +197,9 @@ struct ExtractLaunch {
   const uint16_t* tag;
   const uint64_t* part_rec;
   uint32_t stride;
+  // request order (mde_stream_buckets, layout A): ids walked as given, repeats streamed again, ids
+  // outside [0, B) stream nothing, counts[p] == 0 means every bucket
+  bool ordered;
 };
 constexpr uint32_t kExtractMaxBuckets = 1u << 16;
 hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st);

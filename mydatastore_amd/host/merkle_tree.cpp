@@ -425,9 +425,6 @@ Error Manager::StreamBuckets(int PartitionId, const std::vector<int32_t>& Bucket
                              int64_t UpperEpoch, std::vector<Value>* out) {
   out->clear();
   const uint32_t B = (uint32_t)partitionBuckets_;
-  std::vector<int32_t> ids = Buckets;
-  if (ids.empty())  // main/manager.go:448-452
-    for (uint32_t b = 0; b < B; b++) ids.push_back((int32_t)b);
   Bytes arena;
   std::vector<uint64_t> value_off, seg_rec;
   std::vector<std::string> keys;
@@ -441,12 +438,23 @@ Error Manager::StreamBuckets(int PartitionId, const std::vector<int32_t>& Bucket
   rec.n_partitions = 1;
   rec.n_buckets = B;
   rec.seg_rec = seg_rec.data();
-  const uint64_t cap = rec.n_records ? rec.n_records : 1;
-  const int32_t count = (int32_t)ids.size();
+  // the task's list as given (main/manager.go:447-453): an empty list is every bucket (count 0),
+  // a repeat streams its bucket again, an id outside [0, B) streams nothing -- the capacities
+  // cover every request's run
+  uint64_t need_rec = 0, need_bytes = 0;
+  for (uint32_t i = 0; i < (Buckets.empty() ? B : (uint32_t)Buckets.size()); i++) {
+    const int64_t b = Buckets.empty() ? (int64_t)i : (int64_t)Buckets[i];
+    if (b < 0 || b >= (int64_t)B) continue;
+    need_rec += seg_rec[b + 1] - seg_rec[b];
+    need_bytes += value_off[seg_rec[b + 1]] - value_off[seg_rec[b]];
+  }
+  const uint64_t cap = need_rec ? need_rec : 1, bcap = need_bytes ? need_bytes : 1;
+  const int32_t count = (int32_t)Buckets.size();
+  const int32_t none = 0;
   std::vector<uint64_t> part_off(2), out_rec(cap), out_voff(cap + 1);
-  Bytes out_vals(arena.size());
-  int rc = mde_extract(eng_.ctx(), &rec, ids.data(), ids.size(), &count, part_off.data(), out_rec.data(), cap,
-                       out_vals.data(), out_voff.data(), out_vals.size());
+  Bytes out_vals(bcap);
+  int rc = mde_stream_buckets(eng_.ctx(), &rec, Buckets.empty() ? &none : Buckets.data(), Buckets.size(), &count,
+                              part_off.data(), out_rec.data(), cap, out_vals.data(), out_voff.data(), bcap);
   if (rc != MDE_OK) return eng_.error(rc);
   for (uint64_t i = 0; i < part_off[1]; i++) {
     int p;

@@ -213,9 +213,9 @@ class Manager {
 
   // StreamBucketsTask (main/manager.go:445-487): every record (key, epoch, timestamp) of the
   // listed buckets of a partition in [LowerEpoch, UpperEpoch); an empty list means all buckets.
-  // The range scans fill one arena and the device extract (mde_extract) selects and gathers the
-  // records: buckets de-duplicated and in ascending order (VerifyEpoch passes an Int32Set), LSM
-  // order inside a bucket.
+  // The range scans fill one arena and the device (mde_stream_buckets) gathers the records in the
+  // task's own order: the buckets as listed, a repeated bucket streamed again, an id outside
+  // [0, PartitionBuckets) streaming nothing, LSM order inside a bucket.
   Error StreamBuckets(int PartitionId, const std::vector<int32_t>& Buckets, int64_t LowerEpoch,
                       int64_t UpperEpoch, std::vector<Value>* out);
 

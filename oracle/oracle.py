@@ -363,6 +363,17 @@ class Manager:
             buckets.append(bucket)
         return new_tree(buckets)
 
+    def stream_buckets(self, partition_id: int, buckets, lower: int, upper: int):
+        """StreamBucketsTask (main/manager.go:445-487): an empty list is every bucket (:448-452);
+        the list is walked in the order given (:453), each bucket's range scan streamed whole
+        (:454-483) -- a repeated bucket streams again, a bucket no record carries streams
+        nothing. Returns [(key, epoch, timestamp)]."""
+        buckets = list(buckets) if len(buckets) else list(range(self.partition_buckets))
+        out = []
+        for b in buckets:
+            out.extend(self.bucket_records(partition_id, b, lower, upper) if b >= 0 else [])
+        return out
+
     def bucket_records(self, partition_id: int, bucket: int, lower: int, upper: int):
         """The records one bucket's range scan yields (StreamBucketsTask main/manager.go:445-487)."""
         lo = build_epoch_index(partition_id, bucket, lower, "").encode()
@@ -554,6 +565,35 @@ def layout_a(parts: np.ndarray, bks: np.ndarray, n_partitions: int, n_buckets: i
     seg_rec = np.zeros(n_partitions * n_buckets + 1, dtype=np.uint64)
     np.cumsum(counts, out=seg_rec[1:])
     return order, seg_rec
+
+
+# ---------------------------------------------------------------------------------------------
+# StreamBucketsTask's list contract over the arena (main/manager.go:447-485): requests in the
+# order given, repeats streamed again, ids outside [0, B) stream nothing, an empty list is every
+# bucket. mde_stream_buckets' checker.
+# ---------------------------------------------------------------------------------------------
+def stream_buckets_from_arena(values, value_off, seg_rec, n_partitions, n_buckets, ids, ids_stride, counts):
+    """Per partition, the requests of ids[p*ids_stride : +counts[p]] in order (counts[p] == 0:
+    buckets 0..B-1; < 0: none), each bucket's records in LSM order. Returns (part_off, rec_idx,
+    value_bytes, value_off_out)."""
+    part_off, recs, chunks, voff = [0], [], [], [0]
+    for p in range(n_partitions):
+        c = int(counts[p])
+        row = (range(n_buckets) if c == 0 else
+               [int(x) for x in ids[p * ids_stride:p * ids_stride + max(c, 0)]])
+        for b in row:
+            if not 0 <= b < n_buckets:
+                continue
+            s = p * n_buckets + b
+            for r in range(int(seg_rec[s]), int(seg_rec[s + 1])):
+                recs.append(r)
+                v = values[int(value_off[r]):int(value_off[r + 1])]
+                chunks.append(v)
+                voff.append(voff[-1] + len(v))
+        part_off.append(len(recs))
+    vb = np.concatenate(chunks) if chunks else np.zeros(0, np.uint8)
+    return (np.asarray(part_off, np.uint64), np.asarray(recs, np.uint64), vb.astype(np.uint8),
+            np.asarray(voff, np.uint64))
 
 
 # ---------------------------------------------------------------------------------------------

@@ -266,23 +266,48 @@ static void TestStreamBucketsTask(Engine& eng, int writeValuesNum) {
   for (const Value& v : items) CHECK(v.Epoch == 1 && v.Key.rfind("key", 0) == 0, "epoch-1 records");
   CHECK_OK(manager.StreamBuckets(0, {}, 0, 3, &items));
   CHECK((int)items.size() == 2 * writeValuesNum, "itemCount is wrong");
-  // a subset (with a duplicate and an out-of-range id): exactly the records of those buckets
+  // a list with a repeat and an out-of-range id, streamed as the task walks it
+  // (main/manager.go:453-485): b1's records, bucket 99's, b0's, b1's again, nothing for 1000
   uint64_t b0 = 0, b1 = 0;
   int p0;
   CHECK_OK(manager.KeyTags(items.front().Key, &b0, &p0));
   CHECK_OK(manager.KeyTags(items.back().Key, &b1, &p0));
   std::vector<Value> sub;
   CHECK_OK(manager.StreamBuckets(0, {(int32_t)b1, 99, (int32_t)b0, (int32_t)b1, 1000}, 0, 3, &sub));
-  size_t want = 0;
+  std::vector<Value> want;
+  for (uint64_t req : {b1, (uint64_t)99, b0, b1})
+    for (const Value& v : items) {  // items: all buckets, ascending, LSM order inside each
+      uint64_t b;
+      int p;
+      CHECK_OK(manager.KeyTags(v.Key, &b, &p));
+      if (b == req) want.push_back(v);
+    }
+  CHECK(!want.empty(), "the list holds records");
+  CHECK(sub.size() == want.size(), "request-order stream size");
+  for (size_t i = 0; i < want.size() && i < sub.size(); i++)
+    CHECK(sub[i].Key == want[i].Key && sub[i].Epoch == want[i].Epoch &&
+              sub[i].UnixTimestamp == want[i].UnixTimestamp,
+          "request-order stream: b1, 99, b0, b1 (repeats streamed again)");
+  size_t nb1 = 0;
+  for (const Value& v : sub) {
+    uint64_t b;
+    int p;
+    CHECK_OK(manager.KeyTags(v.Key, &b, &p));
+    nb1 += b == b1;
+  }
+  size_t once = 0;
   for (const Value& v : items) {
     uint64_t b;
     int p;
     CHECK_OK(manager.KeyTags(v.Key, &b, &p));
-    want += (b == b0 || b == b1 || b == 99) ? 1 : 0;
+    once += b == b1;
   }
-  CHECK(want >= 1, "the subset holds records");
-  CHECK(sub.size() == want, "subset stream");
-  std::printf("STREAM n%d %zu %zu %zu\n", writeValuesNum, items.size(), sub.size(), want);
+  CHECK(nb1 == (2 + (b1 == b0) + (b1 == 99)) * once, "b1 streamed once per request");
+  const size_t wantN = want.size();
+  std::printf("STREAMSEQ n%d %llu %llu", writeValuesNum, (unsigned long long)b0, (unsigned long long)b1);
+  for (const Value& v : sub) std::printf(" %s:%lld:%lld", v.Key.c_str(), (long long)v.Epoch, (long long)v.UnixTimestamp);
+  std::printf("\n");
+  std::printf("STREAM n%d %zu %zu %zu\n", writeValuesNum, items.size(), sub.size(), wantN);
 }
 
 // TestGetEpochTreeLastValidObjectTask (main/manager_test.go:213-301): no stored object -> the

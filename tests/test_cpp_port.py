@@ -34,6 +34,22 @@ def test_cpp_port_matches_golden(golden):
     for n in (100, 10):  # TestStreamBucketsTask: 2N records in [0,3); the subset equals its buckets
         total, sub, want = map(int, stream[f"n{n}"])
         assert total == 2 * n and sub == want
+    # the request-order list b1, 99, b0, b1, 1000 against the oracle's StreamBucketsTask
+    # (main/manager.go:445-487): repeats streamed again, 1000 (>= B) streams nothing
+    seq = {ln.split()[1]: ln.split()[2:] for ln in r.stdout.splitlines() if ln.startswith("STREAMSEQ")}
+    for n in (100, 10):
+        from oracle import oracle as O
+        m = O.Manager(1, 100)
+        for i in range(n):
+            m.set_value(f"key{i}", f"val{i}", 1, 0)
+        for i in range(n):
+            m.set_value(f"keyz{i}", f"valz{i}", 2, 0)
+        allrec = m.stream_buckets(0, [], 0, 3)
+        b0 = O.get_key_bucket(allrec[0][0].encode(), 100)
+        b1 = O.get_key_bucket(allrec[-1][0].encode(), 100)
+        assert seq[f"n{n}"][:2] == [str(b0), str(b1)]
+        want = [f"{k}:{e}:{t}" for k, e, t in m.stream_buckets(0, [b1, 99, b0, b1, 1000], 0, 3)]
+        assert seq[f"n{n}"][2:] == want
     got = {ln.split()[1]: ln.split()[2:] for ln in r.stdout.splitlines() if ln.startswith("VERIFY")}
     for name, res in _verify_expected().items():
         diff = ",".join(map(str, res["diff"]))
