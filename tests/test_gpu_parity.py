@@ -415,22 +415,23 @@ def test_stream_buckets_request_order_matches_oracle(engine, golden, coracle):
 
 
 def test_stream_buckets_repeats_and_order(engine, golden):
-    """The verdict's list b1, 99, b0, b1 on the TestMerkleTreeRaw N=100 arena (B = 100): b1's
-    records, 99's, b0's, then b1's again, in that order; 1000 streams nothing. The deduplicated
-    mde_extract on the same list returns each bucket once, ascending."""
+    """A list with repeats and out-of-range ids on the TestMerkleTreeRaw N=100 arena (B = 30):
+    b1's records, bm's, b0's, then b1's again, in that order; 99, 1000 and -1 stream nothing. The
+    deduplicated mde_extract on the same list returns each bucket once, ascending."""
     fix = golden("testmerkletreeraw_n100.json")
     B = fix["n_buckets"]
     vals, seg = mtr_arena(fix, 0, 3)
     nonempty = [b for b in range(B) if seg[b + 1] > seg[b]]
-    b0, b1 = nonempty[0], nonempty[-1]
-    req = np.array([b1, 99, b0, b1, 1000], np.int32)
+    b0, bm, b1 = nonempty[0], nonempty[len(nonempty) // 2], nonempty[-1]
+    req = np.array([b1, 99, bm, -1, b0, b1, 1000], np.int32)
     part_off, rec, vbytes, voff = engine.stream_buckets(vals, seg, 1, B, req, len(req),
                                                         np.array([len(req)], np.int32), 8)
-    runs = [list(range(int(seg[b]), int(seg[b + 1]))) for b in (b1, 99, b0, b1)]
+    runs = [list(range(int(seg[b]), int(seg[b + 1]))) for b in (b1, bm, b0, b1)]
     assert rec.tolist() == [r for run in runs for r in run]
     assert vbytes.tobytes() == b"".join(vals[r * 8:(r + 1) * 8].tobytes() for run in runs for r in run)
+    assert voff.tolist() == list(range(0, 8 * len(rec) + 1, 8))
     _, drec, _, _ = engine.extract(vals, seg, 1, B, req, len(req), np.array([len(req)], np.int32), 8)
-    assert drec.tolist() == [r for b in sorted({b0, b1, 99}) for r in range(int(seg[b]), int(seg[b + 1]))]
+    assert drec.tolist() == [r for b in sorted({b0, bm, b1}) for r in range(int(seg[b]), int(seg[b + 1]))]
 
 
 def test_stream_buckets_rejects_layout_b(engine):
