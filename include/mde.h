@@ -445,7 +445,12 @@ int mde_batch_verify(mde_batcher* b, uint32_t n_buckets, int32_t partition, int6
  * mde_batch_build's contract (layout A, host pointers read only during the call, its own error
  * message in err); a request one workgroup cannot take (more partitions than it holds, more than
  * 256 KiB of packed inputs, n_buckets > max_buckets) runs as mde_build on the service's own
- * context. Thread-safe; mde_server_destroy must not race with calls in flight. */
+ * context. Thread-safe; mde_server_destroy must not race with calls in flight.
+ * Teardown: the launch runs on a CU-masked stream (a hardware queue of its own). By default that
+ * stream is never destroyed -- mde_server_destroy parks it for the next service on the device --
+ * because destroying a masked stream hung the runtime when a stream created before it was destroyed
+ * after it. With MDE_SERVER_CUMASK=1 (destroy it with the service) create the
+ * service before, and destroy it after, every other context of the device. */
 typedef struct mde_server mde_server;
 int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_server** out);
 void mde_server_destroy(mde_server* s);
@@ -481,7 +486,8 @@ int mde_server_stats(mde_server* s, uint64_t* requests, uint64_t* launches, uint
  * request timed out (30 s), or mde_server_disable -- after which every call runs as mde_build /
  * mde_verify_epochs on the service's context (same results, a launch per call), so one transient
  * stall does not fail later calls. mde_server_disable takes the resident launch out of service
- * (e.g. to give its CUs back to bulk builds); `why` is kept for diagnostics. */
+ * (e.g. to give its CUs back to bulk builds): the resident workgroups of idle slots exit at once,
+ * a slot serving a call exits when that call returns; `why` is kept for diagnostics. */
 int mde_server_usable(mde_server* s);
 int mde_server_disable(mde_server* s, const char* why);
 

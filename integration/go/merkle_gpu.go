@@ -82,16 +82,18 @@ func mdeEngine(partitionId int) (*C.mde_batcher, error) {
 		for _, d := range ords {
 			var b *C.mde_batcher
 			var sv *C.mde_server
+			// the service first (include/mde.h: services are created before, and destroyed after,
+			// every other context of the device); 16 request slots (>= partition_concurrency),
+			// buckets up to 1,024 in the resident launch
+			if rc := C.mde_server_create(d, 16, 1024, &sv); rc != C.MDE_OK {
+				log.Printf("mde: GPU %d skipped: mde_server_create: %s", int(d), C.GoString(C.mde_strerror(rc)))
+				continue
+			}
 			// at most 256 partitions per batch, no wait window: a batch is whatever queued while the
 			// previous batches ran
 			if rc := C.mde_batcher_create(d, 256, 0, &b); rc != C.MDE_OK {
 				log.Printf("mde: GPU %d skipped: mde_batcher_create: %s", int(d), C.GoString(C.mde_strerror(rc)))
-				continue
-			}
-			// 16 request slots (>= partition_concurrency), buckets up to 1,024 in the resident launch
-			if rc := C.mde_server_create(d, 16, 1024, &sv); rc != C.MDE_OK {
-				log.Printf("mde: GPU %d skipped: mde_server_create: %s", int(d), C.GoString(C.mde_strerror(rc)))
-				C.mde_batcher_destroy(b)
+				C.mde_server_destroy(sv)
 				continue
 			}
 			mdeBatchers = append(mdeBatchers, b)

@@ -676,9 +676,177 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
   return s;
 }
 
+// digest_range_rec8 with the per-step scan work cut down to what the boundaries need
+// (r06, VERDICT r05 item 3: the rec8 stream's VALU per 4 KiB step, 128 -> ~50):
+//   * the wave's range and everything derived from it (step position, current bucket, its bounds,
+//     the window base, the bucket's running sum) are wave-uniform SGPR values: the buffer resource
+//     is an SGPR quadruple (no per-load readfirstlane loop) and the bookkeeping is scalar;
+//   * the window holds each bucket start as a 32-bit record slot relative to the wave's range
+//     (int32: < 0 before it, clamped far past it), so a step's slot of every start is one
+//     subtract and one med3 -- no 64-bit compares, subtracts or shifts per step;
+//   * the record-space prefix scan of digest_range_rec8 is unchanged (record sums -> LDS, the
+//     transposed read, a 7-add local scan, one DPP wave scan), and only the window lanes of the
+//     buckets a step touches use its result: bucket i's bytes in the step = F(y_{i+1}) - F(y_i);
+//   * finished buckets park 32-bit step sums in their window lane (a bucket wholly inside one step
+//     holds < 2^32 bytes); only the bucket the wave carries across steps needs 64 bits, and it is
+//     a scalar.
+template <bool NT>
+__device__ __forceinline__ uint32_t digest_range_rec8s(const DigestLaunch& a, uint64_t beg_v, uint64_t end_v,
+                                                       uint32_t s_lo, int lane, uint32_t* lds, uint64_t first,
+                                                       uint64_t last) {
+  constexpr int ROWS = 4;
+  constexpr uint32_t kRecs = 128u * ROWS;        // record slots per step
+  constexpr uint32_t kLaneRecs = 2u * ROWS;      // record slots per lane after the transpose
+  constexpr uint32_t kFoldSteps = 16384 / ROWS;  // fast steps per lane fold: exact in 32 bits
+  constexpr int32_t kFar = 0x3fffffff;           // a start past every slot of the range
+  const SegDesc& d = a.seg;
+  uint32_t* R = lds;                             // record sums, then exclusive local prefixes (swizzled)
+  uint32_t* E = lds + rec8_sums_words(ROWS);     // lane exclusive prefixes; E[64] = the step's total
+  const uint64_t beg = readlane64(beg_v, 0), end = readlane64(end_v, 0);  // wave-uniform
+  const uint64_t span = ((end - beg) + 15) & ~15ull;                      // <= kMaxWaveBytes
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(d.base + beg), (short)0, (int)span, 0x00020000);
+  u32x4 va[ROWS], vb[ROWS];
+  load_rec8<NT, ROWS>(va, rs, 0, lane);  // the first step's loads before the bucket search
+  if (lane == 0) R[kRecs] = 0;           // F(kRecs) = E[64] + 0
+  // the window as record slots of the range: lane i = bucket base + i
+  auto rel_of = [&](uint64_t st) -> int32_t {
+    return st < beg ? -1 : (int32_t)min<uint64_t>((st - beg) >> 3, (uint64_t)kFar);
+  };
+  uint32_t base;
+  int32_t rel;
+  auto win_load = [&](uint32_t b) {
+    base = b;
+    const uint32_t idx = b + (uint32_t)lane;
+    rel = idx <= d.S ? rel_of(segpos(d, idx)) : kFar;
+  };
+  {
+    SegWindow w0;
+    const uint32_t s0 = seg_start(d, s_lo, beg, first, last, lane, w0);
+    base = __builtin_amdgcn_readfirstlane(w0.base);
+    rel = rel_of(w0.start);
+    s_lo = __builtin_amdgcn_readfirstlane(s0);
+  }
+#ifdef MDE_WAVE_STAMPS
+  wave_stamp(1);
+#endif
+  uint32_t s = s_lo;  // the bucket the wave is in (uniform)
+  int32_t sbr = __builtin_amdgcn_readlane(rel, (int)(s - base));        // its first slot
+  int32_t ser = __builtin_amdgcn_readlane(rel, (int)(s - base + 1u));   // the next bucket's
+  uint32_t wlo = 0, whi = 0;   // this lane's window bucket (base + lane): its finished sum
+  uint32_t acc = 0;            // lane accumulator of whole steps inside bucket s
+  uint32_t acc_steps = 0;      // uniform: fast steps in acc
+  uint64_t accs = 0;           // uniform: bucket s's bytes folded out of acc and from scan steps
+  uint32_t* const wrow = R + rec8_swz<ROWS>(2u * (uint32_t)lane);
+  uint32_t* rd[ROWS / 2];
+#pragma unroll
+  for (int j = 0; j < ROWS / 2; j++) rd[j] = R + rec8_swz<ROWS>(kLaneRecs * (uint32_t)lane + 4u * j);
+
+  auto fold = [&]() {
+    if (acc_steps) accs += wave_sum_u32(acc);
+    acc = 0;
+    acc_steps = 0;
+  };
+  auto window_out = [&]() {  // one coalesced atomic for the window's finished buckets
+    const uint64_t w = ((uint64_t)whi << 32) | wlo;
+    if (w) atomicAdd(a.sums + base + (uint32_t)lane, (unsigned long long)w);
+    wlo = whi = 0;
+  };
+  // P = the step's first slot in the range, kq = its slots (< kRecs only on the range's last step)
+  auto process = [&](const u32x4 (&v)[ROWS], int32_t P, uint32_t kq) {
+    if (kq == kRecs && sbr <= P && P + (int32_t)kRecs <= ser) {  // the whole step inside bucket s
+#pragma unroll
+      for (int u = 0; u < ROWS; u++) {
+        acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
+        acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
+      }
+      if (++acc_steps == kFoldSteps) fold();
+      return;
+    }
+#pragma unroll
+    for (int u = 0; u < ROWS; u++) {
+      const uint32_t r0 = __builtin_amdgcn_sad_u8(v[u].y, 0u, __builtin_amdgcn_sad_u8(v[u].x, 0u, 0u));
+      const uint32_t r1 = __builtin_amdgcn_sad_u8(v[u].w, 0u, __builtin_amdgcn_sad_u8(v[u].z, 0u, 0u));
+      *reinterpret_cast<uint2*>(wrow + 128u * u) = make_uint2(r0, r1);
+    }
+    uint32_t c[kLaneRecs + 1];
+    c[0] = 0u;
+#pragma unroll
+    for (int j = 0; j < ROWS / 2; j++) {
+      const uint4 x = *reinterpret_cast<const uint4*>(rd[j]);
+      c[4 * j + 1] = c[4 * j] + x.x;
+      c[4 * j + 2] = c[4 * j + 1] + x.y;
+      c[4 * j + 3] = c[4 * j + 2] + x.z;
+      c[4 * j + 4] = c[4 * j + 3] + x.w;
+    }
+    const uint32_t tot = c[kLaneRecs];
+    const uint32_t incl = wave_incl_scan_u32(tot);
+#pragma unroll
+    for (int j = 0; j < ROWS / 2; j++)
+      *reinterpret_cast<uint4*>(rd[j]) = make_uint4(c[4 * j], c[4 * j + 1], c[4 * j + 2], c[4 * j + 3]);
+    E[lane] = incl - tot;
+    if (lane == 63) E[64] = incl;
+    for (;;) {
+      const int32_t t = rel - P;  // this lane's bucket start, as a slot of the step
+      const uint32_t k = (uint32_t)min(max(t, 0), (int32_t)kq);  // clamped to [0, kq] (v_med3_i32)
+      const uint32_t F = R[rec8_swz<ROWS>(k)] + E[k / kLaneRecs];
+      // lane i: bucket base + i's bytes in the step (lanes 0..62), F of the next lane (wave_shl:1)
+      const uint32_t cb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)F, 0x130, 0xf, 0xf, true) - F;
+      const uint32_t k0 = s - base;
+      const uint32_t cnt = (uint32_t)__popcll(__ballot(t < (int32_t)kq));  // starts before the step's end
+      accs += (uint32_t)__builtin_amdgcn_readlane((int)cb, (int)k0);
+      const uint32_t m = cnt - 1u;  // the last bucket starting before the step's end
+      if (cnt == 64u || m > k0) {
+        // bucket k0 is finished, and every bucket between it and m lies inside this step
+        fold();
+        const uint32_t hi_end = cnt == 64u ? 63u : m;
+        if ((uint32_t)lane == k0) {
+          wlo = (uint32_t)accs;
+          whi = (uint32_t)(accs >> 32);
+        } else if ((uint32_t)lane > k0 && (uint32_t)lane < hi_end) {
+          wlo = cb;
+        }
+        if (cnt == 64u) {  // the step runs past the window: its sums go out, the next 63 come in
+          window_out();
+          win_load(base + 63u);
+          s = base;
+          accs = 0;
+          sbr = __builtin_amdgcn_readlane(rel, 0);
+          ser = __builtin_amdgcn_readlane(rel, 1);
+          continue;
+        }
+        s = base + m;
+        sbr = __builtin_amdgcn_readlane(rel, (int)m);
+        ser = __builtin_amdgcn_readlane(rel, (int)(m + 1u));
+        accs = (uint32_t)__builtin_amdgcn_readlane((int)cb, (int)m);
+      }
+      return;
+    }
+  };
+
+  const uint32_t nslots = (uint32_t)((end - beg + 7) >> 3);
+  for (uint32_t P = 0;; P += 2 * kRecs) {
+    load_rec8<NT, ROWS>(vb, rs, (P + kRecs) * 8u, lane);  // always issued (bounded by the range)
+    process(va, (int32_t)P, min(kRecs, nslots - P));
+    if (P + kRecs >= nslots) break;
+    load_rec8<NT, ROWS>(va, rs, (P + 2 * kRecs) * 8u, lane);
+    process(vb, (int32_t)(P + kRecs), min(kRecs, nslots - P - kRecs));
+    if (P + 2 * kRecs >= nslots) break;
+  }
+  fold();
+  if ((uint32_t)lane == s - base) {
+    wlo = (uint32_t)accs;
+    whi = (uint32_t)(accs >> 32);
+  }
+  window_out();
+  return s;
+}
+
 // One contiguous range of wave_bytes per wave. `block` = this workgroup's index among the digest
 // workgroups of the launch.
-template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, int REC8 = 0>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, int REC8 = 0, bool R8S = false>
 __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t block, uint32_t* lds = nullptr) {
   // Streaming waves issue little VALU; when tree waves (back-to-back SHA-256 VALU) share the CU,
   // a raised priority keeps the loads flowing and the SHA waves take the slack.
@@ -694,7 +862,10 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
 #ifdef MDE_WAVE_STAMPS
   wave_stamp(0);
 #endif
-  if (REC8)
+  if (R8S)
+    digest_range_rec8s<NT>(a, beg, min(beg + a.wave_bytes, last), 0u, lane,
+                           lds + (threadIdx.x >> 6) * rec8_wave_words(4), first, last);
+  else if (REC8)
     digest_range_rec8<NT, REC8 ? REC8 : 4>(a, beg, min(beg + a.wave_bytes, last), 0u, lane,
                                            lds + (threadIdx.x >> 6) * rec8_wave_words(REC8), first, last);
   else if (WIN)
@@ -709,7 +880,7 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
 // Interleaved pieces (DigestLaunch::pieces): the wave streams `pieces` ranges of wave_bytes,
 // piece_stride apart, so the whole grid sweeps the arena front to back together. Each piece is a
 // digest_range (its own bucket search, from the previous piece's last bucket on, and flush).
-template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, int REC8 = 0>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, int REC8 = 0, bool R8S = false>
 __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32_t block, uint32_t* lds = nullptr) {
   if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const int lane = threadIdx.x & 63;
@@ -725,7 +896,9 @@ __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32
   wave_stamp(1);
 #endif
   for (uint32_t j = 0; j < a.pieces && beg < last; j++, beg += a.piece_stride)
-    s = REC8  ? digest_range_rec8<NT, REC8 ? REC8 : 4>(a, beg, min(beg + a.wave_bytes, last), s, lane,
+    s = R8S   ? digest_range_rec8s<NT>(a, beg, min(beg + a.wave_bytes, last), s, lane,
+                                       lds + (threadIdx.x >> 6) * rec8_wave_words(4), first, last)
+        : REC8  ? digest_range_rec8<NT, REC8 ? REC8 : 4>(a, beg, min(beg + a.wave_bytes, last), s, lane,
                                                        lds + (threadIdx.x >> 6) * rec8_wave_words(REC8), first, last)
         : WIN ? digest_range_win<U, NT, PIPE, A8>(a, beg, min(beg + a.wave_bytes, last), s, lane)
               : digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), s, lane);
@@ -932,12 +1105,16 @@ __device__ __forceinline__ void digest_body_steal(const DigestLaunch& a, uint32_
 // records with the prefix scan in record space (digest_range_rec8, 4 KiB steps; LDS:
 // rec8_lds_bytes); 7 and 8 = 5 and 6 with 8 KiB steps.
 __host__ __device__ constexpr int mode_rec8_rows(int mode) {
-  return (mode == 5 || mode == 6) ? 4 : ((mode == 7 || mode == 8) ? 8 : 0);
+  return (mode == 5 || mode == 6 || (mode >= 9 && mode <= 12)) ? 4 : ((mode == 7 || mode == 8) ? 8 : 0);
 }
 template <int U, bool NT, int PIPE, int PRIO, int MODE, bool A8>
 __device__ __forceinline__ void digest_dispatch(const DigestLaunch& a, uint32_t block, uint32_t* lds) {
   if (MODE == 1)
     digest_body_steal<U, NT, PRIO>(a, block);
+  else if (MODE == 9 || MODE == 11)
+    digest_body<U, NT, PIPE, PRIO, false, A8, 0, true>(a, block, lds);
+  else if (MODE == 10 || MODE == 12)
+    digest_body_pieces<U, NT, PIPE, PRIO, false, A8, 0, true>(a, block, lds);
   else if (MODE == 2 || MODE == 4 || MODE == 6 || MODE == 8)
     digest_body_pieces<U, NT, PIPE, PRIO, MODE == 4, A8, mode_rec8_rows(MODE)>(a, block, lds);
   else
@@ -1020,6 +1197,7 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
   }
   const uint32_t db = blockIdx.x - tree_blocks;
 #endif
+  if (MODE == 11 || MODE == 12) asm volatile("" ::: "v79");  // probe: the step kernel at >= 80 VGPRs
   digest_dispatch<U, NT, PIPE, PRIO, MODE, false>(a, db, lds);
 }
 
@@ -1255,7 +1433,9 @@ const Variant kVariants[] = {
     MDE_VARIANT(4, true, 2, 2, 2),      MDE_VARIANT(4, true, 2, 2, 3),
     MDE_VARIANT(4, true, 2, 2, 4),      MDE_VARIANT(4, true, 2, 2, 5),
     MDE_VARIANT(4, true, 2, 2, 6),      MDE_VARIANT(4, true, 2, 2, 7),
-    MDE_VARIANT(4, true, 2, 2, 8),
+    MDE_VARIANT(4, true, 2, 2, 8),      MDE_VARIANT(4, true, 2, 2, 9),
+    MDE_VARIANT(4, true, 2, 2, 10),     MDE_VARIANT(4, true, 2, 2, 11),
+    MDE_VARIANT(4, true, 2, 2, 12),
 #ifdef MDE_PROBE_EXTRA_VARIANTS  // probe only: the rec8 stream (mode 5) at issue priority 0, 1, 3
     MDE_VARIANT(4, true, 2, 0, 5),      MDE_VARIANT(4, true, 2, 1, 5),
     MDE_VARIANT(4, true, 2, 3, 5),
@@ -1392,7 +1572,7 @@ hipError_t launch_server(ServerSlot* slots, uint32_t n_slots, uint64_t lifetime_
 bool bucket_digest_steals(int v) { return variant(v).mode == 1; }
 bool bucket_digest_pieces(int v) {
   const int m = variant(v).mode;
-  return m == 2 || m == 4 || m == 6 || m == 8;
+  return m == 2 || m == 4 || m == 6 || m == 8 || m == 10 || m == 12;
 }
 bool bucket_digest_rec8(int v) { return mode_rec8_rows(variant(v).mode) != 0; }
 uint32_t bucket_digest_rec8_lds_bytes(int v) {
@@ -1405,6 +1585,8 @@ int bucket_digest_pieces_sibling(int v) {  // the same kernel with interleaved p
     case 13: return 14;
     case 15: return 16;
     case 17: return 18;
+    case 19: return 20;
+    case 21: return 22;
     default: return v;
   }
 }

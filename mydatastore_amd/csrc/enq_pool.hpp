@@ -5,8 +5,10 @@
 // runtime's launch path), so one thread launching for 8 GPUs spends 8x that per step against a
 // device step of ~0.2 ms (C4 at N = 8). EnqPool::run hands share i to thread i (share 0 to the
 // caller) and returns when every share has run: the host cost per call is one device's, not G
-// devices'. Workers spin on their job word for kSpin after each job -- a run of group calls keeps
-// them hot -- then sleep on a condition variable.
+// devices'. After a job a worker spins on its job word for kSpin only while calls come back to
+// back (the gap before its previous job was under kSpin: a run of pipelined group calls keeps it
+// hot), else for kSpinCold -- a process calling now and then does not burn G-1 cores for 200 us
+// after every call -- then sleeps on a condition variable.
 //
 // Host-only (no HIP): tests/cpp/enq_pool_test.cpp drives it under ThreadSanitizer.
 #pragma once
@@ -27,6 +29,7 @@ namespace mde {
 class EnqPool {
  public:
   static constexpr auto kSpin = std::chrono::microseconds(200);
+  static constexpr auto kSpinCold = std::chrono::microseconds(5);
 
   // `shares` = the number of shares per call (the group's devices); threads for shares 1.. start
   // here and stop in the destructor.
@@ -98,12 +101,17 @@ class EnqPool {
   void loop(uint32_t i) {
     Worker& w = *w_[i];
     uint64_t last = 0;
+    bool hot = false;  // the previous job came within kSpin of the one before it
     for (;;) {
       uint64_t p = w.posted.load();
       auto t0 = std::chrono::steady_clock::now();
+      const auto budget = hot ? std::chrono::duration_cast<std::chrono::steady_clock::duration>(kSpin)
+                              : std::chrono::duration_cast<std::chrono::steady_clock::duration>(kSpinCold);
+      bool slept = false;
       for (uint32_t spin = 1; p == last && !w.quit.load(); spin++) {
         _mm_pause();
-        if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > kSpin) {
+        if ((spin & 63) == 0 && std::chrono::steady_clock::now() - t0 > budget) {
+          slept = true;
           std::unique_lock<std::mutex> lk(w.m);
           w.sleeping.store(true);
           w.cv.wait(lk, [&] { return w.posted.load() != last || w.quit.load(); });
@@ -113,6 +121,7 @@ class EnqPool {
         p = w.posted.load();
       }
       if (p == last) return;  // quit
+      hot = !slept && std::chrono::steady_clock::now() - t0 <= kSpin;
       w.rc = (*job_)(i);
       last = p;
       w.finished.store(p);

@@ -290,6 +290,13 @@ int post_and_wait(mde_server* s, uint32_t i, std::string* msg) {
   }
 }
 
+// Once the service is out of service no request is posted again: the workgroup of an idle slot is
+// told to exit (kServerStop), so the launch gives its CUs back as its slots go idle instead of
+// polling until its lifetime ends. Called under s->m for a slot no caller holds.
+void stop_idle_slot(mde_server* s, uint32_t i) {
+  __atomic_store_n(&s->slot(i)->req, mde::kServerStop, __ATOMIC_RELEASE);
+}
+
 // A free slot, or UINT32_MAX once the service is broken. Callers finding none queue in FIFO order
 // and sleep on a condition variable of their own; give_slot hands a returned slot straight to the
 // first of them (one wakeup per handoff: a shared condition variable woke callers that found the
@@ -307,7 +314,10 @@ uint32_t take_slot(mde_server* s) {
     s->slot_waiters.push_back(&w);
     w.cv.wait(lk, [&] { return w.slot != UINT32_MAX || s->broken.load(); });
     if (s->broken.load()) {  // give back a slot handed over meanwhile, leave the queue
-      if (w.slot != UINT32_MAX) s->free_slots.push_back(w.slot);
+      if (w.slot != UINT32_MAX) {
+        stop_idle_slot(s, w.slot);
+        s->free_slots.push_back(w.slot);
+      }
       auto it = std::find(s->slot_waiters.begin(), s->slot_waiters.end(), &w);
       if (it != s->slot_waiters.end()) s->slot_waiters.erase(it);
     } else {
@@ -329,7 +339,10 @@ void mark_broken(mde_server* s, const std::string& msg) {
 
 void give_slot(mde_server* s, uint32_t i) {
   std::lock_guard<std::mutex> lk(s->m);
-  if (!s->slot_waiters.empty()) {
+  if (s->broken.load()) {  // out of service: no waiter is served by the launch any more
+    stop_idle_slot(s, i);
+    s->free_slots.push_back(i);
+  } else if (!s->slot_waiters.empty()) {
     SlotWaiter* w = s->slot_waiters.front();
     s->slot_waiters.pop_front();
     w->slot = i;
@@ -420,17 +433,20 @@ int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_se
   std::vector<uint32_t> mask((size_t)std::max(1, (cus + 31) / 32), 0u);
   for (int c = 0; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
   // The launch's stream: a CU-masked stream (all CUs) gets a hardware queue of its own, so no other
-  // stream of the process queues behind the persistent kernel; it is destroyed with the service.
-  // Round 4 kept it for the process instead, because destroying it made a later hipStreamDestroy
-  // hang (profiles/r04/r04n_service_streams.txt). Round 5 found the order that hangs: the
-  // service's own context, created before this stream and destroyed after it
-  // (profiles/r05/r05g_teardown_bisect.txt); the context is now created after the stream and
-  // destroyed before it, and destroy-with-service passes the service tests, including a context
-  // that outlives the service (r05h). MDE_SERVER_CUMASK=0: a plain non-blocking stream instead;
-  // 2: the round-4 pool (a CU-masked stream kept for the process, reused by a later service on
-  // the device, never by two live ones).
+  // stream of the process queues behind the persistent kernel. By default (MDE_SERVER_CUMASK=2) it
+  // is never destroyed: it goes back to a per-device pool and a later service on the device reuses
+  // it (never two live ones). Destroying a CU-masked stream is what hung: hipStreamDestroy of a
+  // stream created BEFORE the masked stream and destroyed AFTER it, with work of that stream run
+  // while the persistent launch was live (profiles/r04/r04n_service_streams.txt,
+  // profiles/r05/r05g_teardown_bisect.txt; the runtime-side wait was not identified -- DESIGN.md
+  // section 7). The service's own context is created after the stream and destroyed before it
+  // either way, but a caller's context created before the service and destroyed after it (the Go
+  // shim's batchers, two services destroyed in creation order) would recreate the pattern if the
+  // masked stream were destroyed, so the pool stays the default. MDE_SERVER_CUMASK=1: destroy it
+  // with the service (callers then create every other context of the device after the service,
+  // or destroy it before the service -- include/mde.h); 0: a plain non-blocking stream.
   const char* cm = std::getenv("MDE_SERVER_CUMASK");
-  const int cmode = cm ? std::atoi(cm) : 1;
+  const int cmode = cm ? std::atoi(cm) : 2;
   s->keep_stream = cmode == 2 && device >= 0 && device < kKeptDevices;
   hipError_t se = hipSuccess;
   if (cmode == 0) {
@@ -472,6 +488,12 @@ int mde_server_create(int device, uint32_t n_slots, uint32_t max_buckets, mde_se
   return MDE_OK;
 }
 
+// Teardown contract: the launch stream is a CU-masked stream, and with the
+// default MDE_SERVER_CUMASK=2 it is parked in the device's pool here, never destroyed -- the only
+// teardown order known to hang is hipStreamDestroy of a masked stream while a stream created before
+// it (used during the persistent launch) is destroyed after it. With MDE_SERVER_CUMASK=1 the
+// caller must keep that order out: create services before, and destroy them after, every other
+// context / stream of the device.
 void mde_server_destroy(mde_server* s) {
   if (!s) return;
   DeviceScope ds(s->device);
@@ -823,6 +845,10 @@ int mde_server_usable(mde_server* s) { return s && !s->broken.load() ? 1 : 0; }
 int mde_server_disable(mde_server* s, const char* why) {
   if (!s) return MDE_E_INVAL;
   mark_broken(s, why && *why ? why : "disabled by the caller");
+  // the idle slots' workgroups exit now; a slot serving a call exits when its caller gives it back
+  std::lock_guard<std::mutex> lk(s->m);
+  for (uint32_t i : s->free_slots) stop_idle_slot(s, i);
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
   return MDE_OK;
 }
 

@@ -536,13 +536,14 @@ int main(int argc, char** argv) {
   if (getenv("MDE_TOP_NODES")) g_top = (uint32_t)atoi(getenv("MDE_TOP_NODES"));
   const char* wait_env = getenv("MDE_BATCH_WAIT_US");
   const uint32_t wait_us = wait_env ? (uint32_t)atoi(wait_env) : 0u;
-  if ((rc = mde_batcher_create(0, 256, wait_us, &batcher))) return 1;
-  /* MDE_SERVER_SLOTS: the service's request slots (0 = its default, 16) */
+  /* MDE_SERVER_SLOTS: the service's request slots (0 = its default, 16); the service first
+   * (include/mde.h teardown contract) */
   const uint32_t slots = getenv("MDE_SERVER_SLOTS") ? (uint32_t)atoi(getenv("MDE_SERVER_SLOTS")) : 0u;
   if ((rc = mde_server_create(0, slots, 0, &server))) {
     fprintf(stderr, "mde_server_create: %d\n", rc);
     return 1;
   }
+  if ((rc = mde_batcher_create(0, 256, wait_us, &batcher))) return 1;
   printf("{\"host_sha_extensions\": %s, \"batcher_wait_us\": %u, \"server_slots\": %u}\n", oracle_sha_ni() ? "true" : "false",
          wait_us, mde_server_slots(server));
   if (argc > 3) {

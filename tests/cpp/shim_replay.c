@@ -288,8 +288,10 @@ int main(int argc, char** argv) {
   mde_batcher* batcher = NULL;
   mde_server* server = NULL;
   mde_ctx* ctx = NULL;
-  int rc = mde_batcher_create(0, 256, 0, &batcher);
-  if (!rc) rc = mde_server_create(0, 16, 1024, &server);
+  /* the service first (include/mde.h teardown contract: services created before, destroyed after,
+   * every other context of the device), as merkle_gpu.go's mdeEngine does */
+  int rc = mde_server_create(0, 16, 1024, &server);
+  if (!rc) rc = mde_batcher_create(0, 256, 0, &batcher);
   if (rc || (rc = mde_create(0, &ctx))) {
     fprintf(stderr, "create: %d (%s)\n", rc, mde_strerror(rc));
     return 1;
@@ -455,8 +457,8 @@ int main(int argc, char** argv) {
     }
   }
   fclose(f);
-  mde_server_destroy(server);
   mde_batcher_destroy(batcher);
+  mde_server_destroy(server);
   mde_destroy(ctx);
   return 0;
 }

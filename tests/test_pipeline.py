@@ -505,8 +505,10 @@ def test_default_variant_choice_b1000_full_size(engine, value_len, n_keys, n_buc
         engine.set_digest_piece_bytes(-1)
 
 
-# digest.hip: fixed 8-byte records, record-space prefix scan (+ pieces), 4 KiB and 8 KiB steps
-REC8_VARIANTS = (15, 16, 17, 18)
+# digest.hip: fixed 8-byte records, record-space prefix scan (+ pieces), 4 KiB and 8 KiB steps, and
+# the scalar-bookkeeping form (19, 20: digest_range_rec8s)
+REC8_VARIANTS = (15, 16, 17, 18, 19, 20)
+REC8_PIECES = (16, 18, 20)
 
 
 @pytest.mark.parametrize("start", [0, 8])
@@ -530,8 +532,8 @@ def test_rec8_ragged_arena_matches_torch_sums(engine, coracle, start, P, B, max_
         [np.frombuffer(coracle.tree(want_np[p * B:(p + 1) * B], B)[0], np.uint8) for p in range(P)]).copy())
     want_items = counts.view(P, B).sum(1).to(torch.int32)
     try:
-        for v, pbs in [(-1, (-1,)), (REC8_VARIANTS[0], (-1,)), (REC8_VARIANTS[1], (1024, 8192, 1 << 20)),
-                       (REC8_VARIANTS[2], (-1,)), (REC8_VARIANTS[3], (1024, 8192, 1 << 20))]:
+        for v, pbs in [(-1, (-1,))] + [(v, (1024, 8192, 1 << 20) if v in REC8_PIECES else (-1,))
+                                       for v in REC8_VARIANTS]:
             engine.set_tuning(v, -1)
             for pb in pbs:
                 engine.set_digest_piece_bytes(pb)

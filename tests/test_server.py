@@ -9,6 +9,7 @@ import subprocess
 import threading
 
 import numpy as np
+from pathlib import Path
 import pytest
 
 from tests.conftest import ROOT
@@ -260,6 +261,35 @@ def test_server_levels_on_the_service_context(coracle, B, n):
     assert np.array_equal(got["nodes"].reshape(-1, 32)[:pre], exp["nodes"].reshape(-1, 32)[:pre])
     assert np.array_equal(got["digest"], exp["digest"]) and np.array_equal(got["size"], exp["size"])
     assert np.array_equal(got["items"], exp["items"])
+
+
+@pytest.mark.gpu
+def test_disable_ends_the_resident_launch():
+    """mde_server_disable posts the stop word to the idle slots, so the persistent launch gives its
+    CUs back at once instead of polling until its lifetime ends: with a 60 s lifetime, a service
+    disabled after serving a call is destroyed in well under a second (a launch left running would
+    hold mde_server_destroy for its 10 s bound and keep its buffers)."""
+    import subprocess
+    import sys
+    code = (
+        "import time, numpy as np, mydatastore_amd as mde\n"
+        "sv = mde.Server(0)\n"
+        "vals = np.arange(800, dtype=np.uint8)\n"
+        "seg = np.array([0, 40, 100], np.uint64)\n"
+        "sv.build(vals, seg, 1, 2, value_stride=8)\n"
+        "assert sv.stats()['on_context'] == 0\n"
+        "sv.disable('test')\n"
+        "time.sleep(0.2)\n"
+        "t0 = time.perf_counter()\n"
+        "sv.close()\n"
+        "print('CLOSE', time.perf_counter() - t0)\n")
+    import os
+    env = dict(os.environ, MDE_SERVER_LIFETIME_MS="60000")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=100, env=env,
+                       cwd=str(Path(__file__).resolve().parents[1]))
+    assert r.returncode == 0, r.stderr
+    dt = float(r.stdout.split("CLOSE")[1])
+    assert dt < 1.0 and "did not end" not in r.stderr, (dt, r.stderr)
 
 
 @pytest.mark.gpu

@@ -9,6 +9,7 @@ SIMD holds. One JSON line per repetition.
 import collections
 import ctypes
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -35,6 +36,8 @@ def main():
     eng = mde.Engine(0)
     dev = torch.device("cuda:0")
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    if os.environ.get("MDE_AB_VARIANT"):
+        eng.set_tuning(int(os.environ["MDE_AB_VARIANT"]), -1)
     w = make_workload(eng, n_partitions=1024, n_buckets=B, value_len=V, part_mode="mod", n_keys=n)
     sets = [w._outs() for _ in range(2)]
     lib = eng.lib

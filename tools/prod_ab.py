@@ -54,8 +54,19 @@ def main():
         torch.cuda.synchronize(dev)
         us.append(round(a.elapsed_time(b) * 1e3 / 40, 2))
     ok = bool(np.array_equal(sets[1][0]["root"].cpu().numpy(), ref))  # build 39 -> set 1
+    dg = []  # the digest kernel alone, warm, 40 launches per bracket
+    for _ in range(reps):
+        builds(n_warm)
+        eng.build_pipeline_drain_async()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        for _ in range(40):
+            w.digest_async()
+        b.record(st)
+        torch.cuda.synchronize(dev)
+        dg.append(round(a.elapsed_time(b) * 1e3 / 40, 2))
     print(json.dumps({"lib": tag, "warmup_builds": n_warm, "us_per_build": us, "median_us": float(np.median(us)),
-                      "roots_ok": ok}), flush=True)
+                      "digest_us": dg, "digest_median_us": float(np.median(dg)), "roots_ok": ok}), flush=True)
     eng.close()
 
 

@@ -9,6 +9,7 @@ spell of `idle_s`), to read the clock the step sustains against the one it start
 
     MDE_LIBRARY=... python tools/step_probe.py [n_keys] [B] [value_len] [reps] [warm_ms] [idle_s]
 """
+import os
 import time
 import ctypes
 import json
@@ -33,6 +34,8 @@ def main():
     eng = mde.Engine(0)
     dev = torch.device("cuda:0")
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    if os.environ.get("MDE_AB_VARIANT"):
+        eng.set_tuning(int(os.environ["MDE_AB_VARIANT"]), -1)
     w = make_workload(eng, n_partitions=1024, n_buckets=B, value_len=V, part_mode="mod", n_keys=n, rank=0, world=1)
     sets = [w._outs() for _ in range(2)]
     lib = eng.lib
