@@ -24,6 +24,8 @@
 #include "verify_body.hpp"
 #include <algorithm>
 #include <cstddef>
+#include <cstdlib>
+#include <cstring>
 
 
 namespace mde {
@@ -690,7 +692,7 @@ __device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uin
 //   * finished buckets park 32-bit step sums in their window lane (a bucket wholly inside one step
 //     holds < 2^32 bytes); only the bucket the wave carries across steps needs 64 bits, and it is
 //     a scalar.
-template <bool NT>
+template <bool NT, bool SCALAR = true>
 __device__ __forceinline__ uint32_t digest_range_rec8s(const DigestLaunch& a, uint64_t beg_v, uint64_t end_v,
                                                        uint32_t s_lo, int lane, uint32_t* lds, uint64_t first,
                                                        uint64_t last) {
@@ -702,7 +704,8 @@ __device__ __forceinline__ uint32_t digest_range_rec8s(const DigestLaunch& a, ui
   const SegDesc& d = a.seg;
   uint32_t* R = lds;                             // record sums, then exclusive local prefixes (swizzled)
   uint32_t* E = lds + rec8_sums_words(ROWS);     // lane exclusive prefixes; E[64] = the step's total
-  const uint64_t beg = readlane64(beg_v, 0), end = readlane64(end_v, 0);  // wave-uniform
+  const uint64_t beg = SCALAR ? readlane64(beg_v, 0) : beg_v;  // wave-uniform (SGPRs)
+  const uint64_t end = SCALAR ? readlane64(end_v, 0) : end_v;
   const uint64_t span = ((end - beg) + 15) & ~15ull;                      // <= kMaxWaveBytes
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)(d.base + beg), (short)0, (int)span, 0x00020000);
@@ -846,7 +849,7 @@ __device__ __forceinline__ uint32_t digest_range_rec8s(const DigestLaunch& a, ui
 
 // One contiguous range of wave_bytes per wave. `block` = this workgroup's index among the digest
 // workgroups of the launch.
-template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, int REC8 = 0, bool R8S = false>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, int REC8 = 0, int R8S = 0>
 __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t block, uint32_t* lds = nullptr) {
   // Streaming waves issue little VALU; when tree waves (back-to-back SHA-256 VALU) share the CU,
   // a raised priority keeps the loads flowing and the SHA waves take the slack.
@@ -863,7 +866,7 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
   wave_stamp(0);
 #endif
   if (R8S)
-    digest_range_rec8s<NT>(a, beg, min(beg + a.wave_bytes, last), 0u, lane,
+    digest_range_rec8s<NT, R8S == 1>(a, beg, min(beg + a.wave_bytes, last), 0u, lane,
                            lds + (threadIdx.x >> 6) * rec8_wave_words(4), first, last);
   else if (REC8)
     digest_range_rec8<NT, REC8 ? REC8 : 4>(a, beg, min(beg + a.wave_bytes, last), 0u, lane,
@@ -880,7 +883,7 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
 // Interleaved pieces (DigestLaunch::pieces): the wave streams `pieces` ranges of wave_bytes,
 // piece_stride apart, so the whole grid sweeps the arena front to back together. Each piece is a
 // digest_range (its own bucket search, from the previous piece's last bucket on, and flush).
-template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, int REC8 = 0, bool R8S = false>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, int REC8 = 0, int R8S = 0>
 __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32_t block, uint32_t* lds = nullptr) {
   if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const int lane = threadIdx.x & 63;
@@ -896,7 +899,7 @@ __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32
   wave_stamp(1);
 #endif
   for (uint32_t j = 0; j < a.pieces && beg < last; j++, beg += a.piece_stride)
-    s = R8S   ? digest_range_rec8s<NT>(a, beg, min(beg + a.wave_bytes, last), s, lane,
+    s = R8S   ? digest_range_rec8s<NT, R8S == 1>(a, beg, min(beg + a.wave_bytes, last), s, lane,
                                        lds + (threadIdx.x >> 6) * rec8_wave_words(4), first, last)
         : REC8  ? digest_range_rec8<NT, REC8 ? REC8 : 4>(a, beg, min(beg + a.wave_bytes, last), s, lane,
                                                        lds + (threadIdx.x >> 6) * rec8_wave_words(REC8), first, last)
@@ -1112,9 +1115,9 @@ __device__ __forceinline__ void digest_dispatch(const DigestLaunch& a, uint32_t 
   if (MODE == 1)
     digest_body_steal<U, NT, PRIO>(a, block);
   else if (MODE == 9 || MODE == 11)
-    digest_body<U, NT, PIPE, PRIO, false, A8, 0, true>(a, block, lds);
+    digest_body<U, NT, PIPE, PRIO, false, A8, 0, MODE == 9 ? 1 : 2>(a, block, lds);
   else if (MODE == 10 || MODE == 12)
-    digest_body_pieces<U, NT, PIPE, PRIO, false, A8, 0, true>(a, block, lds);
+    digest_body_pieces<U, NT, PIPE, PRIO, false, A8, 0, MODE == 10 ? 1 : 2>(a, block, lds);
   else if (MODE == 2 || MODE == 4 || MODE == 6 || MODE == 8)
     digest_body_pieces<U, NT, PIPE, PRIO, MODE == 4, A8, mode_rec8_rows(MODE)>(a, block, lds);
   else
@@ -1197,7 +1200,6 @@ __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, Tr
   }
   const uint32_t db = blockIdx.x - tree_blocks;
 #endif
-  if (MODE == 11 || MODE == 12) asm volatile("" ::: "v79");  // probe: the step kernel at >= 80 VGPRs
   digest_dispatch<U, NT, PIPE, PRIO, MODE, false>(a, db, lds);
 }
 
@@ -1701,7 +1703,8 @@ uint32_t duo_step_kw_word(uint32_t B, uint32_t* lds_bytes) {
   return n1 * 8u >= 128u * 8u + kw_words ? 4u + 128u * 8u : 0u;
 }
 
-void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint32_t* lds_bytes, uint32_t* duo_kw_word) {
+void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint32_t* lds_bytes, uint32_t* duo_kw_word,
+                     uint64_t stream_bytes) {
   *duo_kw_word = 0;
   // One packed tree wave per partition (Q = 1, B > 128) has a critical path of 34 dependent
   // compressions at B = 1,000; two waves per partition (tree_body over 128 threads) cut it to 24.
@@ -1719,6 +1722,26 @@ void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint
   // (a probe, wrong roots) took 8-byte values to 193-197 us: the top levels' six dependent node
   // hashes, not their instruction count, hold the step.
   const uint32_t q = build_step_tree_q(B);
+  // r06: few wide trees beside a short stream -- the whole workgroup per partition (tree_body_duo,
+  // 128 hashing + 128 schedule threads: ~16 dependent compression-equivalents at B = 1,000 against
+  // ~34 for the packed wave and ~24 for the two-wave form). Same process, alternating, warm
+  // (profiles/r06/r06g_tree_forms.jsonl, r06h_tree_forms.jsonl; packed / two-wave / whole, us per
+  // fused build): 8-byte values at B = 1,000 over 128 partitions (the production shape's N = 8
+  // shard, 100 MB) 112 / 71 / 61, 256 partitions 126 / 86 / 69, 512 partitions 172 / 128 / 103;
+  // 64-byte values over 128 partitions 120 / 80 / 69. Where the stream outlasts every tree form
+  // (C4 at B = 1,000 on its N = 8 shard, 1.28 GB: 213-214 / 217 / 216-217; B = 300 within noise)
+  // the packed wave's smaller footprint stays; 1,024 partitions keep the two-wave form (whole:
+  // 211 vs 166). The rule: whole for at most kStepTreeWideMinPartitions partitions when the stream
+  // is under kStepTreeWholeMaxBytes (~120 us at 6.5 TB/s, the packed trees' critical path).
+  const bool whole_fits = P <= kStepTreeWideMinPartitions && stream_bytes && stream_bytes < kStepTreeWholeMaxBytes;
+  if (q == 1 && (B + 1) / 2 > 64 && tree_duo_enabled() && whole_fits) {
+    *Q = kStepTreeWholeWG;
+    *blocks = P;
+    const uint32_t words = (tree_lds_words(B) + 3u) & ~3u;
+    *duo_kw_word = words;
+    *lds_bytes = words * 4u + duo_kw_bytes(kStepTreeWideThreads);
+    return;
+  }
   if (q == 1 && (B + 1) / 2 > 64 && P >= kStepTreeWideMinPartitions) {
     *Q = 0;
     *blocks = P;
@@ -1737,9 +1760,11 @@ hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStre
     // every partition of a fused step has t->B buckets (no per-tree n_in)
     if (!build_step_fusable(t->B) || !t->sums_in || t->n_in) return hipErrorInvalidValue;
     uint32_t tree_lds = 0;
-    plan_step_trees(t->B, t->P, &Q, &tree_blocks, &tree_lds, &kw_word);
+    plan_step_trees(t->B, t->P, &Q, &tree_blocks, &tree_lds, &kw_word,
+                    a.wave_bytes * a.n_waves * (uint64_t)(a.pieces ? a.pieces : 1u));
     // every workgroup of the dispatch reserves the tree waves' LDS; kStepTreeLdsMax keeps the
-    // streaming grid fully resident
+    // streaming grid fully resident (the whole-workgroup form's 40 KB leaves 3 per CU: at most
+    // 512 tree workgroups beside the 2-per-CU stream, the short streams that form is chosen for)
     lds = std::max<uint32_t>(lds, tree_lds);
   }
   const uint32_t digest_blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);

@@ -150,8 +150,14 @@ uint32_t build_step_tree_q(uint32_t B);  // partitions per packed tree wave
 // tree_body); blocks = tree workgroups, lds_bytes = their LDS.
 constexpr uint32_t kStepTreeWideThreads = 128;
 constexpr uint32_t kStepTreeWideMinPartitions = 512;
+// Q value: one partition per whole tree workgroup (tree_body_duo over 256 threads, half = 128) --
+// the latency form for builds of few wide trees (plan_step_trees).
+constexpr uint32_t kStepTreeWholeWG = 0xffffffffu;
 // duo_kw_word: see TreeLaunch::duo_kw_word (may raise lds_bytes within kStepTreeLdsMax).
-void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint32_t* lds_bytes, uint32_t* duo_kw_word);
+// stream_bytes: the build's arena bytes (0 = unknown: no whole-workgroup form).
+void plan_step_trees(uint32_t B, uint32_t P, uint32_t* Q, uint32_t* blocks, uint32_t* lds_bytes, uint32_t* duo_kw_word,
+                     uint64_t stream_bytes);
+constexpr uint64_t kStepTreeWholeMaxBytes = 768ull << 20;
 hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStream_t st);
 // One-launch build of a small layout-A arena (digest.hip small_build_kernel): each workgroup sums
 // its partitions' buckets into LDS and builds their trees from there (t.sums_in is not used).

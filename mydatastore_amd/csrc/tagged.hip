@@ -397,7 +397,9 @@ hipError_t launch_tagged_step(TaggedLaunch& a, const TreeLaunch* t, hipStream_t 
   if (t && t->P) {
     if (!build_step_fusable(t->B) || !t->sums_in || t->n_in) return hipErrorInvalidValue;
     uint32_t tree_lds = 0;
-    plan_step_trees(t->B, t->P, &Q, &tree_blocks, &tree_lds, &kw_word);
+    // stream bytes 0: layout B keeps the packed / two-wave forms (its bins already take 33 KiB
+    // per binning workgroup; the whole-workgroup trees' 40 KB would cut its residency)
+    plan_step_trees(t->B, t->P, &Q, &tree_blocks, &tree_lds, &kw_word, 0);
     lds = std::max<size_t>(lds, (size_t)tree_lds);
   }
   const uint32_t blocks = (a.n_waves + (kThreads / 64) - 1) / (kThreads / 64);

@@ -492,9 +492,13 @@ __host__ __device__ inline uint32_t tree_lds_words(uint32_t B) {
 
 // A tree workgroup of a fused build step (plan_step_trees): Q > 0 -> its first wave builds Q
 // partitions (tree_body_packed); Q == 0 -> its first kStepTreeWideThreads threads (two waves)
-// build one partition (tree_body; the other waves leave at once).
+// build one partition (tree_body; the other waves leave at once); Q == kStepTreeWholeWG -> the
+// whole workgroup builds one partition (tree_body_duo, half = 128).
 __device__ __forceinline__ void step_trees(const TreeLaunch& t, uint32_t Q, uint32_t block, uint32_t* lds) {
-  if (Q)
+  if (Q == kStepTreeWholeWG)  // few wide trees: all 256 threads per partition, the upper 128 as helpers
+    tree_body_duo(t, 2u * kStepTreeWideThreads, tree_lds_words(t.B), block, lds, kStepTreeWideThreads,
+                  reinterpret_cast<u32x4*>(lds + t.duo_kw_word));
+  else if (Q)
     tree_body_packed(t, Q, block, lds);
   else {
 #ifdef MDE_STEP_WIDE_PRIO  // probe only: wide-tree waves at this priority beside the stream

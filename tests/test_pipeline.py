@@ -404,6 +404,32 @@ def test_fused_step_trees_many_builds(engine, layout, n_buckets, world):
             assert torch.equal(o[k], ref[k]), (i, k)
 
 
+@pytest.mark.parametrize("P,n_buckets", [(131, 129), (131, 257), (3, 999), (131, 1000), (512, 1023), (1, 1024)])
+def test_whole_workgroup_step_trees_match_oracle(engine, coracle, P, n_buckets):
+    """Few wide trees beside a short stream (plan_step_trees' whole-workgroup form, r06: the
+    production shape's N = 8 shard): the fused step's trees over all 256 threads of a workgroup,
+    the upper half as schedule helpers -- odd and even B, the level of <= 128 nodes that starts the
+    split levels (129, 257), the fused step's LDS limit (1,024), 1 to 512 partitions. A run of
+    pipelined builds equals the C oracle, nodes included."""
+    import numpy as np
+    import torch
+    from mydatastore_amd.workload import make_workload
+    V = 8
+    w = make_workload(engine, n_partitions=P, n_buckets=n_buckets, value_len=V, part_mode="mod",
+                      n_keys=min(300 * P, 1_500_000), rank=0, world=1, layout="a")
+    exp = coracle.build(w.values.cpu().numpy(), w.seg_rec.cpu().numpy().view(np.uint64), P, n_buckets,
+                        stride=V, threads=8)
+    sets = [w._outs() for _ in range(3)]
+    for o, to in sets:
+        engine.build_pipelined_async(w.rec, to)
+    engine.build_pipeline_drain_async()
+    engine.synchronize()
+    for i, (o, _) in enumerate(sets):
+        for k in ("digest", "size", "items", "root", "nodes"):
+            got = o[k].cpu().numpy().view(exp[k].dtype).reshape(-1)
+            assert np.array_equal(got, exp[k].reshape(-1)), (i, k)
+
+
 @pytest.mark.parametrize("n_buckets", [129, 257, 999, 1000, 1024])
 def test_pair_trees_odd_shapes_match_oracle(engine, coracle, n_buckets):
     """Wide trees of >= 512 partitions: the standalone tree kernel's pair shape (two partitions

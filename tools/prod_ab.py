@@ -30,7 +30,12 @@ def main():
     if os.environ.get("MDE_AB_VARIANT"):  # an explicit digest variant (e.g. 17: rec8 with 8 KiB steps)
         eng.set_tuning(*map(int, os.environ["MDE_AB_VARIANT"].split(",")))  # variant[,blocks/CU[,oversub]]
         tag += "+v" + os.environ["MDE_AB_VARIANT"]
-    w = make_workload(eng, n_partitions=1024, n_buckets=1000, value_len=8, part_mode="mod", n_keys=100_000_000)
+    # MDE_AB_SHAPE="n_keys,B,value_len,world" (default: the production shape, N = 1)
+    n_keys, B, V, world = (int(x) for x in os.environ.get("MDE_AB_SHAPE", "100000000,1000,8,1").split(","))
+    if os.environ.get("MDE_AB_SHAPE"):
+        tag += "@" + os.environ["MDE_AB_SHAPE"]
+    w = make_workload(eng, n_partitions=1024, n_buckets=B, value_len=V, part_mode="mod", n_keys=n_keys,
+                      rank=0, world=world)
     sets = [w._outs() for _ in range(2)]
     ref = w.build()["root"].cpu().numpy()
 
