@@ -60,13 +60,21 @@ def build_engine(verbose: bool = True) -> Path:
     OBJ.mkdir(exist_ok=True)
     headers = list(CSRC.glob("*.hpp")) + [ROOT / "include" / "mde.h"]
     sources = sorted(CSRC.glob("*.hip")) + [CSRC / "mde_api.cpp", CSRC / "batch.cpp", CSRC / "group.cpp", CSRC / "server.cpp"]
-    objs = []
+    objs, jobs = [], []
     for src in sources:
         obj = OBJ / (src.stem + ".o")
         if _stale(obj, [src, *headers]):
             lang = ["-x", "hip"] if src.suffix == ".hip" else []
-            _run([HIPCC, *HIP_FLAGS, *lang, "-c", src, "-o", obj], verbose)
+            jobs.append([HIPCC, *HIP_FLAGS, *lang, "-c", src, "-o", obj])
         objs.append(obj)
+    # the translation units compile independently: in parallel, up to the CPU share
+    # (MAX_JOBS / OMP_NUM_THREADS on a GPU box, else the cores, at most 8)
+    from concurrent.futures import ThreadPoolExecutor
+    share = os.environ.get("MAX_JOBS") or os.environ.get("OMP_NUM_THREADS") or str(os.cpu_count() or 1)
+    workers = max(1, min(8, int(share) if share.isdigit() else 1, len(jobs) or 1))
+    with ThreadPoolExecutor(workers) as ex:
+        for f in [ex.submit(_run, j, verbose) for j in jobs]:
+            f.result()
     if _stale(LIB, objs):
         _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-pthread", "-o", LIB, *objs, "-ldl"], verbose)
     return LIB

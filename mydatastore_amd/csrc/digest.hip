@@ -32,10 +32,8 @@ namespace mde {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr uint64_t kMaxStepBytes = 16ull * 1024ull;  // largest wave step over all variants
+constexpr uint64_t kMaxStepBytes = 16ull * 1024ull;  // wave ranges are multiples of this (4 steps)
 constexpr uint64_t kMaxWaveBytes = 256ull << 20;    // largest contiguous range per wave
-constexpr uint32_t kStealHeads = 16;                 // ticket counters of the tail pool
-constexpr uint32_t kStageSteps = 3;                  // steps between chunk-acquisition stages
 
 // Largest s in [lo, S) with segpos(s) <= x (lo if none). 64-ary search: one vector load and one
 // ballot per round, log64(S) rounds. Must be called by all 64 lanes.
@@ -451,10 +449,7 @@ __device__ __forceinline__ uint32_t digest_range_win(const DigestLaunch& a, uint
 
 // digest_range for fixed 8-byte records (the production epoch-index value is the LE64 write
 // timestamp, main/manager.go:816) with short buckets (the reference's default B = 1,000 puts a
-// bucket start every ~100 records). Counters showed the register-window kernel's prefix-scan path
-// issue-bound there: ~300 VALU per 4 KiB step (four wave scans of the vector sums, a 64-bit window
-// walk, per-row shuffles to gather each start's prefix; profiles/r02ae_digest_sq_counters.json).
-// Here the scan runs in RECORD space, once per step:
+// bucket start every ~100 records): the prefix scan runs in RECORD space, once per 4 KiB step.
 //   * each lane byte-sums its 8 records (two per 16-byte vector of each of the 4 coalesced 1 KiB
 //     rows) and writes the 8 sums to LDS at their record index; the wave reads them back
 //     transposed -- lane l gets records 8l .. 8l+7 of the step -- so ONE wave scan of the lane
@@ -464,253 +459,60 @@ __device__ __forceinline__ uint32_t digest_range_win(const DigestLaunch& a, uint
 //     lane of every bucket starting in the step reads F(start) = bytes of the step before it with
 //     two ds_read_b32 -- bucket i's bytes in the step are F(y_{i+1}) - F(y_i), as in
 //     digest_range_win's scan path;
-//   * the buckets' step sums accumulate in a wave-uniform u64 (no per-bucket wave reduction); a
-//     step inside one bucket just byte-sums into the lane accumulators;
-//   * loads are buffer loads bounded by the wave range (no per-load address clamping; the last
-//     vector of the range may extend past its end, whose slots the prefix clamp at q excludes).
+//   * a step inside one bucket just byte-sums into the lane accumulators.
 // Needs value_stride == 8 and an 8-byte-aligned arena start (segpos multiples of 8).
-// ROWS = 1 KiB rows per step: 4 (4 KiB steps, 8 records per lane) or 8 (8 KiB steps, 16 records
-// per lane: the per-step scan, window walk and LDS round trips amortised over twice the bytes, and
-// twice the bytes in flight per wave -- at 8 KiB steps, ~20 VGPRs more).
-// LDS swizzles (XOR inside 16-byte chunks): the row writes (lane l: words 128u + 2l, +1) and the
-// transposed ds_read_b128 (lane l: its 2 x ROWS records) both conflict-free.
-template <int ROWS>
-__device__ __forceinline__ uint32_t rec8_swz(uint32_t w) {
-  return ROWS == 4 ? w ^ (((w >> 6) & 1u) << 2) : w ^ (((w >> 5) & 3u) << 2);
-}
-__host__ __device__ constexpr uint32_t rec8_sums_words(int rows) { return 128u * (uint32_t)rows + 16u; }  // + word 128 x rows = 0
-__host__ __device__ constexpr uint32_t rec8_wave_words(int rows) { return rec8_sums_words(rows) + 80u; }  // + 65 lane prefixes
-__host__ __device__ constexpr uint32_t rec8_lds_bytes(int rows) { return rec8_wave_words(rows) * 4u * (kThreads / 64); }
+// LDS swizzle (XOR inside 16-byte chunks): the row writes (lane l: words 128u + 2l, +1) and the
+// transposed ds_read_b128 (lane l: its 8 records) both conflict-free.
+constexpr int kRec8Rows = 4;  // 1 KiB rows per step
+__device__ __forceinline__ uint32_t rec8_swz(uint32_t w) { return w ^ (((w >> 6) & 1u) << 2); }
+__host__ __device__ constexpr uint32_t rec8_sums_words() { return 128u * kRec8Rows + 16u; }  // + word 512 = 0
+__host__ __device__ constexpr uint32_t rec8_wave_words() { return rec8_sums_words() + 80u; }  // + 65 lane prefixes
+__host__ __device__ constexpr uint32_t rec8_lds_bytes() { return rec8_wave_words() * 4u * (kThreads / 64); }
 
-#ifdef MDE_WAVE_STAMPS  // probe only: per-wave entry / first step / exit times (s_memrealtime, 100 MHz)
-// and shader-clock counts at the same points (s_memtime): a wave's clock = d(memtime) / d(realtime)
-constexpr uint32_t kStampWaves = 16384;
-__device__ unsigned long long g_wave_stamps[3 * kStampWaves];
-__device__ unsigned long long g_tree_stamps[2 * kStampWaves];  // fused step: tree waves' entry, exit
-__device__ unsigned long long g_wave_clk[3 * kStampWaves];
-__device__ unsigned long long g_tree_clk[2 * kStampWaves];
-// where each wave ran: HW_ID (wave, SIMD, CU, SH, SE ids) in the low word, XCC_ID in the high
-__device__ unsigned long long g_wave_hw[kStampWaves];
-__device__ unsigned long long g_tree_hw[kStampWaves];
-__device__ __forceinline__ unsigned long long hw_where() {
-  const unsigned hw = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID, 32 bits
-  const unsigned xcc = (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID, 4 bits
-  return ((unsigned long long)xcc << 32) | hw;
-}
-__device__ __forceinline__ void wave_stamp(int k) {
-  const uint32_t w = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-  const unsigned long long c = __builtin_amdgcn_s_memtime();
-  if ((threadIdx.x & 63) == 0 && w < kStampWaves) {
-    g_wave_stamps[3 * w + k] = t;
-    g_wave_clk[3 * w + k] = c;
-    if (k == 0) g_wave_hw[w] = hw_where();
-  }
-}
-#endif
-
-template <bool NT, int ROWS>
-__device__ __forceinline__ void load_rec8(u32x4 (&v)[ROWS], __amdgpu_buffer_rsrc_t rs, uint32_t off, int lane) {
+template <bool NT>
+__device__ __forceinline__ void load_rec8(u32x4 (&v)[kRec8Rows], __amdgpu_buffer_rsrc_t rs, uint32_t off, int lane) {
 #pragma unroll
-  for (int u = 0; u < ROWS; u++)
+  for (int u = 0; u < kRec8Rows; u++)
     v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(u * 64 + lane) * 16u,
                                                                           off, NT ? 2 : 0));
 }
 
-template <bool NT, int ROWS>
-__device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uint64_t beg, uint64_t end, uint32_t s_lo,
-                                                      int lane, uint32_t* lds, uint64_t first, uint64_t last) {
-  constexpr uint64_t kStep = 1024ull * ROWS;
-  constexpr uint32_t kRecs = 128u * ROWS;      // records per step
-  constexpr uint32_t kLaneRecs = 2u * ROWS;    // records per lane after the transpose
-  constexpr uint32_t kFoldSteps = 16384 / ROWS;  // fast steps per lane fold: 255 x 16 MiB < 2^32 exact
-  const SegDesc& d = a.seg;
-  uint32_t* R = lds;                            // record sums, then exclusive local prefixes (swizzled)
-  uint32_t* E = lds + rec8_sums_words(ROWS);    // lane exclusive prefixes; E[64] = the step's total
-  // beg / end stay where the compiler puts them (VGPRs: they derive from threadIdx.x >> 6), so the
-  // resource below is a VGPR quadruple and every buffer load runs as a one-iteration readfirstlane
-  // loop. Moving them to SGPRs was measured (r03): the digest alone unchanged (134-139 us at 8-byte
-  // values, B = 1,000), the fused build step SLOWER, 174-176 -> 187-191 us per build -- the slower
-  // issue of the stream leaves SIMD cycles to the co-resident tree waves, whose dependent SHA-256
-  // chain bounds that step; a deliberate s_sleep per scan step or priority 0 did not do as well
-  // (profiles/r03y_rec8_scalar_ab.txt, r03z_rec8_throttle_ab.txt).
-#ifdef MDE_PROBE_REC8_SRSRC  // probe only: the range (and so the buffer resource) wave-uniform in SGPRs
-  beg = readlane64(beg, 0);
-  end = readlane64(end, 0);
-#endif
-  const uint64_t span = ((end - beg) + 15) & ~15ull;  // <= kMaxWaveBytes
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(d.base + beg), (short)0, (int)span, 0x00020000);
-  u32x4 va[ROWS], vb[ROWS];
-  load_rec8<NT, ROWS>(va, rs, 0, lane);  // the first step's loads before the bucket search
-  if (lane == 0) R[kRecs] = 0;           // F(kRecs) = E[64] + 0 (rec8_swz(kRecs) == kRecs)
-  SegWindow win;
-  uint32_t s = seg_start(d, s_lo, beg, first, last, lane, win);
-  const uint32_t k_start = __builtin_amdgcn_readfirstlane(s - win.base);
-#ifdef MDE_WAVE_STAMPS
-  wave_stamp(1);
-#endif
-  uint64_t sb = readlane64(win.start, k_start), se = readlane64(win.start, k_start + 1u);
-  uint64_t wsum = 0;       // this lane's window bucket (win.base + lane): its finished sum
-  uint32_t acc = 0;        // lane accumulator of whole steps inside bucket s
-  uint32_t acc_steps = 0;  // wave-uniform: fast steps in acc (0: acc is all zero)
-  uint64_t accs = 0;       // wave-uniform: bucket s's bytes folded out of acc and from scan steps
-  // lane-invariant LDS addresses (a row offset 128u leaves the swizzle bits alone)
-  uint32_t* const wrow = R + rec8_swz<ROWS>(2u * (uint32_t)lane);
-  uint32_t* rd[ROWS / 2];
-#pragma unroll
-  for (int j = 0; j < ROWS / 2; j++) rd[j] = R + rec8_swz<ROWS>(kLaneRecs * (uint32_t)lane + 4u * j);
-
-  auto fold = [&]() {  // acc -> accs (exact: acc_steps <= kFoldSteps)
-    if (acc_steps) accs += wave_sum_u32(acc);
-    acc = 0;
-    acc_steps = 0;
-  };
-  auto retire = [&]() {  // bucket s is left: its sum into its window lane
-    fold();
-    const uint32_t k = __builtin_amdgcn_readfirstlane(s - win.base);
-    if ((uint32_t)lane == k) wsum = accs;
-    accs = 0;
-  };
-  auto window_out = [&]() {  // one coalesced atomic for the window's finished buckets
-    if (wsum) atomicAdd(a.sums + win.base + (uint32_t)lane, (unsigned long long)wsum);
-    wsum = 0;
-  };
-  auto process = [&](const u32x4 (&v)[ROWS], uint64_t p) {
-    const uint64_t q = min(p + kStep, end);
-    if (q == p + kStep && sb <= p && q <= se) {  // the whole step inside bucket s
-#pragma unroll
-      for (int u = 0; u < ROWS; u++) {
-        acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
-        acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
-        acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
-        acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
-      }
-      if (++acc_steps == kFoldSteps) fold();
-      return;
-    }
-    // record sums -> LDS at their record index (row u, lane l: records 128u + 2l, 128u + 2l + 1)
-#pragma unroll
-    for (int u = 0; u < ROWS; u++) {
-      const uint32_t r0 = __builtin_amdgcn_sad_u8(v[u].y, 0u, __builtin_amdgcn_sad_u8(v[u].x, 0u, 0u));
-      const uint32_t r1 = __builtin_amdgcn_sad_u8(v[u].w, 0u, __builtin_amdgcn_sad_u8(v[u].z, 0u, 0u));
-      *reinterpret_cast<uint2*>(wrow + 128u * u) = make_uint2(r0, r1);
-    }
-    // transposed: this lane's records kLaneRecs * l .. +kLaneRecs-1, their local exclusive
-    // prefixes, one wave scan of the lane totals
-    uint32_t c[kLaneRecs + 1];
-    c[0] = 0u;
-#pragma unroll
-    for (int j = 0; j < ROWS / 2; j++) {
-      const uint4 x = *reinterpret_cast<const uint4*>(rd[j]);
-      c[4 * j + 1] = c[4 * j] + x.x;
-      c[4 * j + 2] = c[4 * j + 1] + x.y;
-      c[4 * j + 3] = c[4 * j + 2] + x.z;
-      c[4 * j + 4] = c[4 * j + 3] + x.w;
-    }
-    const uint32_t tot = c[kLaneRecs];
-    const uint32_t incl = wave_incl_scan_u32(tot);
-#pragma unroll
-    for (int j = 0; j < ROWS / 2; j++)
-      *reinterpret_cast<uint4*>(rd[j]) = make_uint4(c[4 * j], c[4 * j + 1], c[4 * j + 2], c[4 * j + 3]);
-    E[lane] = incl - tot;
-    if (lane == 63) E[64] = incl;
-    // F(y) for this lane's bucket start y, clamped to [p, q]: record slot k = (y - p) / 8
-    const uint32_t kq = (uint32_t)((q - p) >> 3);
-    for (;;) {
-      const uint64_t st = win.start;
-      const uint32_t k = st <= p ? 0u : (st >= q ? kq : (uint32_t)((st - p) >> 3));
-      const uint32_t F = R[rec8_swz<ROWS>(k)] + E[k / kLaneRecs];
-      // bucket base + lane's bytes in the step, lanes 0..62: F of the next lane (DPP wave_shl:1)
-      const uint32_t c = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)F, 0x130, 0xf, 0xf, true) - F;
-      const uint32_t k0 = __builtin_amdgcn_readfirstlane(s - win.base);
-      const uint32_t cnt = (uint32_t)__popcll(__ballot(st < q));
-      accs += (uint32_t)__builtin_amdgcn_readlane((int)c, (int)k0);
-      if (cnt == 64u) {  // the step runs past the window: buckets k0..62 all end inside it
-        retire();
-        if ((uint32_t)lane > k0 && lane < 63) wsum = c;
-        window_out();
-        win.load(d, win.base + 63u, lane);
-        s = win.base;
-        sb = readlane64(win.start, 0);
-        se = readlane64(win.start, 1);
-        continue;
-      }
-      const uint32_t m = cnt - 1u;  // the last bucket starting before q: it runs on past q
-      if (m > k0) {
-        retire();
-        if ((uint32_t)lane > k0 && (uint32_t)lane < m) wsum = c;
-        s = win.base + m;
-        sb = readlane64(st, m);
-        se = readlane64(st, m + 1u);
-        accs = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)m);
-      }
-      return;
-    }
-  };
-
-#ifdef MDE_PROBE_REC8_DEPTH3  // probe only: three steps in flight per wave instead of two
-  u32x4 vc[ROWS];
-  load_rec8<NT, ROWS>(vb, rs, (uint32_t)kStep, lane);
-  for (uint64_t p = beg;; p += 3 * kStep) {
-    load_rec8<NT, ROWS>(vc, rs, (uint32_t)(p + 2 * kStep - beg), lane);  // always issued (bounded by the range)
-    process(va, p);
-    if (p + kStep >= end) break;
-    load_rec8<NT, ROWS>(va, rs, (uint32_t)(p + 3 * kStep - beg), lane);
-    process(vb, p + kStep);
-    if (p + 2 * kStep >= end) break;
-    load_rec8<NT, ROWS>(vb, rs, (uint32_t)(p + 4 * kStep - beg), lane);
-    process(vc, p + 2 * kStep);
-    if (p + 3 * kStep >= end) break;
-  }
-#else
-  for (uint64_t p = beg;; p += 2 * kStep) {
-    load_rec8<NT, ROWS>(vb, rs, (uint32_t)(p + kStep - beg), lane);  // always issued (bounded by the range)
-    process(va, p);
-    if (p + kStep >= end) break;
-    load_rec8<NT, ROWS>(va, rs, (uint32_t)(p + 2 * kStep - beg), lane);
-    process(vb, p + kStep);
-    if (p + 2 * kStep >= end) break;
-  }
-#endif
-  retire();
-  window_out();
-  return s;
-}
-
-// digest_range_rec8 with the per-step scan work cut down to what the boundaries need
-// (r06, VERDICT r05 item 3: the rec8 stream's VALU per 4 KiB step, 128 -> ~50):
-//   * the wave's range and everything derived from it (step position, current bucket, its bounds,
-//     the window base, the bucket's running sum) are wave-uniform SGPR values: the buffer resource
-//     is an SGPR quadruple (no per-load readfirstlane loop) and the bookkeeping is scalar;
+// The rec8 stream's bookkeeping (r06, VERDICT r05 item 3: the VALU per 4 KiB step):
 //   * the window holds each bucket start as a 32-bit record slot relative to the wave's range
 //     (int32: < 0 before it, clamped far past it), so a step's slot of every start is one
 //     subtract and one med3 -- no 64-bit compares, subtracts or shifts per step;
-//   * the record-space prefix scan of digest_range_rec8 is unchanged (record sums -> LDS, the
-//     transposed read, a 7-add local scan, one DPP wave scan), and only the window lanes of the
-//     buckets a step touches use its result: bucket i's bytes in the step = F(y_{i+1}) - F(y_i);
-//   * finished buckets park 32-bit step sums in their window lane (a bucket wholly inside one step
-//     holds < 2^32 bytes); only the bucket the wave carries across steps needs 64 bits, and it is
-//     a scalar.
-template <bool NT, bool SCALAR = true>
-__device__ __forceinline__ uint32_t digest_range_rec8s(const DigestLaunch& a, uint64_t beg_v, uint64_t end_v,
+//   * the step position, the current bucket, its bounds, the window base and the bucket's running
+//     sum are wave-uniform scalars, and finished buckets park 32-bit step sums in their window lane
+//     (a bucket wholly inside one step holds < 2^32 bytes); only the bucket the wave carries
+//     across steps needs 64 bits, and it is a scalar;
+//   * the record-space prefix scan is as described above; only the window lanes of the buckets a
+//     step touches use its result.
+// Counted in the ISA (gfx950): 58 VALU per scan step for the bookkeeping and the scan (the round-5
+// form: ~117 with the per-load readfirstlane loops), plus the 4 loads' readfirstlane loops (below).
+// The wave's range stays in VGPRs (it derives from threadIdx.x >> 6), so each of the 4 loads per
+// step is a one-iteration readfirstlane loop (6 VALU). Measured with the range in SGPRs as well
+// (no loops, 58 VALU per step): the digest alone 136-138 us either way, but the fused production
+// step SLOWER, 176-180 vs 166-167 us per build, the tree waves 154-155 vs 139-143 us each
+// (profiles/r06/r06c_rec8_timeline.jsonl, r06e_rec8_ab.jsonl; the same as round 3's SGPR-range
+// probe): what the co-resident SHA-256 waves lose is not the stream's VALU count.
+template <bool NT>
+__device__ __forceinline__ uint32_t digest_range_rec8(const DigestLaunch& a, uint64_t beg_v, uint64_t end_v,
                                                        uint32_t s_lo, int lane, uint32_t* lds, uint64_t first,
                                                        uint64_t last) {
-  constexpr int ROWS = 4;
+  constexpr int ROWS = kRec8Rows;
   constexpr uint32_t kRecs = 128u * ROWS;        // record slots per step
   constexpr uint32_t kLaneRecs = 2u * ROWS;      // record slots per lane after the transpose
   constexpr uint32_t kFoldSteps = 16384 / ROWS;  // fast steps per lane fold: exact in 32 bits
   constexpr int32_t kFar = 0x3fffffff;           // a start past every slot of the range
   const SegDesc& d = a.seg;
   uint32_t* R = lds;                             // record sums, then exclusive local prefixes (swizzled)
-  uint32_t* E = lds + rec8_sums_words(ROWS);     // lane exclusive prefixes; E[64] = the step's total
-  const uint64_t beg = SCALAR ? readlane64(beg_v, 0) : beg_v;  // wave-uniform (SGPRs)
-  const uint64_t end = SCALAR ? readlane64(end_v, 0) : end_v;
+  uint32_t* E = lds + rec8_sums_words();        // lane exclusive prefixes; E[64] = the step's total
+  const uint64_t beg = beg_v, end = end_v;
   const uint64_t span = ((end - beg) + 15) & ~15ull;                      // <= kMaxWaveBytes
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)(d.base + beg), (short)0, (int)span, 0x00020000);
   u32x4 va[ROWS], vb[ROWS];
-  load_rec8<NT, ROWS>(va, rs, 0, lane);  // the first step's loads before the bucket search
+  load_rec8<NT>(va, rs, 0, lane);  // the first step's loads before the bucket search
   if (lane == 0) R[kRecs] = 0;           // F(kRecs) = E[64] + 0
   // the window as record slots of the range: lane i = bucket base + i
   auto rel_of = [&](uint64_t st) -> int32_t {
@@ -730,9 +532,6 @@ __device__ __forceinline__ uint32_t digest_range_rec8s(const DigestLaunch& a, ui
     rel = rel_of(w0.start);
     s_lo = __builtin_amdgcn_readfirstlane(s0);
   }
-#ifdef MDE_WAVE_STAMPS
-  wave_stamp(1);
-#endif
   uint32_t s = s_lo;  // the bucket the wave is in (uniform)
   int32_t sbr = __builtin_amdgcn_readlane(rel, (int)(s - base));        // its first slot
   int32_t ser = __builtin_amdgcn_readlane(rel, (int)(s - base + 1u));   // the next bucket's
@@ -740,10 +539,10 @@ __device__ __forceinline__ uint32_t digest_range_rec8s(const DigestLaunch& a, ui
   uint32_t acc = 0;            // lane accumulator of whole steps inside bucket s
   uint32_t acc_steps = 0;      // uniform: fast steps in acc
   uint64_t accs = 0;           // uniform: bucket s's bytes folded out of acc and from scan steps
-  uint32_t* const wrow = R + rec8_swz<ROWS>(2u * (uint32_t)lane);
+  uint32_t* const wrow = R + rec8_swz(2u * (uint32_t)lane);
   uint32_t* rd[ROWS / 2];
 #pragma unroll
-  for (int j = 0; j < ROWS / 2; j++) rd[j] = R + rec8_swz<ROWS>(kLaneRecs * (uint32_t)lane + 4u * j);
+  for (int j = 0; j < ROWS / 2; j++) rd[j] = R + rec8_swz(kLaneRecs * (uint32_t)lane + 4u * j);
 
   auto fold = [&]() {
     if (acc_steps) accs += wave_sum_u32(acc);
@@ -794,7 +593,7 @@ __device__ __forceinline__ uint32_t digest_range_rec8s(const DigestLaunch& a, ui
     for (;;) {
       const int32_t t = rel - P;  // this lane's bucket start, as a slot of the step
       const uint32_t k = (uint32_t)min(max(t, 0), (int32_t)kq);  // clamped to [0, kq] (v_med3_i32)
-      const uint32_t F = R[rec8_swz<ROWS>(k)] + E[k / kLaneRecs];
+      const uint32_t F = R[rec8_swz(k)] + E[k / kLaneRecs];
       // lane i: bucket base + i's bytes in the step (lanes 0..62), F of the next lane (wave_shl:1)
       const uint32_t cb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)F, 0x130, 0xf, 0xf, true) - F;
       const uint32_t k0 = s - base;
@@ -831,10 +630,10 @@ __device__ __forceinline__ uint32_t digest_range_rec8s(const DigestLaunch& a, ui
 
   const uint32_t nslots = (uint32_t)((end - beg + 7) >> 3);
   for (uint32_t P = 0;; P += 2 * kRecs) {
-    load_rec8<NT, ROWS>(vb, rs, (P + kRecs) * 8u, lane);  // always issued (bounded by the range)
+    load_rec8<NT>(vb, rs, (P + kRecs) * 8u, lane);  // always issued (bounded by the range)
     process(va, (int32_t)P, min(kRecs, nslots - P));
     if (P + kRecs >= nslots) break;
-    load_rec8<NT, ROWS>(va, rs, (P + 2 * kRecs) * 8u, lane);
+    load_rec8<NT>(va, rs, (P + 2 * kRecs) * 8u, lane);
     process(vb, (int32_t)(P + kRecs), min(kRecs, nslots - P - kRecs));
     if (P + 2 * kRecs >= nslots) break;
   }
@@ -849,7 +648,7 @@ __device__ __forceinline__ uint32_t digest_range_rec8s(const DigestLaunch& a, ui
 
 // One contiguous range of wave_bytes per wave. `block` = this workgroup's index among the digest
 // workgroups of the launch.
-template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, int REC8 = 0, int R8S = 0>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, bool REC8 = false>
 __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t block, uint32_t* lds = nullptr) {
   // Streaming waves issue little VALU; when tree waves (back-to-back SHA-256 VALU) share the CU,
   // a raised priority keeps the loads flowing and the SHA waves take the slack.
@@ -862,28 +661,19 @@ __device__ __forceinline__ void digest_body(const DigestLaunch& a, uint32_t bloc
   const uint64_t last = segpos(d, d.S);
   const uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
   if (beg >= last) return;
-#ifdef MDE_WAVE_STAMPS
-  wave_stamp(0);
-#endif
-  if (R8S)
-    digest_range_rec8s<NT, R8S == 1>(a, beg, min(beg + a.wave_bytes, last), 0u, lane,
-                           lds + (threadIdx.x >> 6) * rec8_wave_words(4), first, last);
-  else if (REC8)
-    digest_range_rec8<NT, REC8 ? REC8 : 4>(a, beg, min(beg + a.wave_bytes, last), 0u, lane,
-                                           lds + (threadIdx.x >> 6) * rec8_wave_words(REC8), first, last);
+  if (REC8)
+    digest_range_rec8<NT>(a, beg, min(beg + a.wave_bytes, last), 0u, lane,
+                          lds + (threadIdx.x >> 6) * rec8_wave_words(), first, last);
   else if (WIN)
     digest_range_win<U, NT, PIPE, A8>(a, beg, min(beg + a.wave_bytes, last), 0u, lane);
   else
     digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), 0u, lane);
-#ifdef MDE_WAVE_STAMPS
-  wave_stamp(2);
-#endif
 }
 
 // Interleaved pieces (DigestLaunch::pieces): the wave streams `pieces` ranges of wave_bytes,
 // piece_stride apart, so the whole grid sweeps the arena front to back together. Each piece is a
 // digest_range (its own bucket search, from the previous piece's last bucket on, and flush).
-template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, int REC8 = 0, int R8S = 0>
+template <int U, bool NT, int PIPE, int PRIO = 0, bool WIN = false, bool A8 = false, bool REC8 = false>
 __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32_t block, uint32_t* lds = nullptr) {
   if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const int lane = threadIdx.x & 63;
@@ -894,234 +684,24 @@ __device__ __forceinline__ void digest_body_pieces(const DigestLaunch& a, uint32
   const uint64_t last = segpos(d, d.S);
   uint32_t s = 0;
   uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
-#ifdef MDE_WAVE_STAMPS
-  wave_stamp(0);
-  wave_stamp(1);
-#endif
   for (uint32_t j = 0; j < a.pieces && beg < last; j++, beg += a.piece_stride)
-    s = R8S   ? digest_range_rec8s<NT, R8S == 1>(a, beg, min(beg + a.wave_bytes, last), s, lane,
-                                       lds + (threadIdx.x >> 6) * rec8_wave_words(4), first, last)
-        : REC8  ? digest_range_rec8<NT, REC8 ? REC8 : 4>(a, beg, min(beg + a.wave_bytes, last), s, lane,
-                                                       lds + (threadIdx.x >> 6) * rec8_wave_words(REC8), first, last)
+    s = REC8  ? digest_range_rec8<NT>(a, beg, min(beg + a.wave_bytes, last), s, lane,
+                                      lds + (threadIdx.x >> 6) * rec8_wave_words(), first, last)
         : WIN ? digest_range_win<U, NT, PIPE, A8>(a, beg, min(beg + a.wave_bytes, last), s, lane)
               : digest_range<U, NT, PIPE>(a, beg, min(beg + a.wave_bytes, last), s, lane);
-#ifdef MDE_WAVE_STAMPS
-  wave_stamp(2);
-#endif
 }
 
-
-// Tail stealing (fixed-length values). Wave w owns [first + w*wave_bytes, +wave_bytes) as in
-// digest_body, but streams only its head (the first head_bytes); the tails of all waves, cut into
-// tail_chunks pieces of chunk_bytes, form a pool the waves drain through one atomic ticket
-// counter once their heads are done. Why: under a static split wave end times spread by ~5 %
-// (whole XCDs stream consistently slower; measured per wave with s_memrealtime), and the launch
-// lasts as long as the slowest wave.
-// A chunk switch must not stall the wave's memory pipeline, so the next chunk is acquired while
-// the current one streams: one stage per step -- ticket atomic, then the rounds of a 64-ary
-// search of the chunk's first bucket (seg_rec is L2-resident), then that bucket's bounds -- and
-// the first step of the next chunk is prefetched across the switch like any other step.
-template <int U, bool NT, int PRIO = 0>
-__device__ __forceinline__ void digest_body_steal(const DigestLaunch& a, uint32_t block) {
-  constexpr uint64_t kStep = 1024ull * U;
-  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave = block * (kThreads / 64) + (threadIdx.x >> 6);
-  if (wave >= a.n_waves) return;
-  const SegDesc& d = a.seg;
-  // Ticket heads: kStealHeads counters + an exhausted-heads mask per parity. One returning atomic
-  // word saturates near 90 dequeues/us (MI355X_MICROARCH.md "dequeue"), far below what 2,048
-  // waves draw, so head h serves the tickets t = h + kStealHeads * k; a wave starts at head
-  // wave % kStealHeads, and moves on (skipping heads the mask marks empty) when its head runs dry.
-  unsigned long long* heads = a.steal + a.steal_parity * (kStealHeads + 1);
-  unsigned long long* mask = heads + kStealHeads;
-  if (wave == 0 && lane <= kStealHeads)  // the next launch's heads and mask
-    a.steal[(a.steal_parity ^ 1u) * (kStealHeads + 1) + lane] = 0ull;
-  const uint64_t first = segpos(d, 0) & ~15ull;
-  const uint64_t last = segpos(d, d.S);
-  const uint64_t tickets = (uint64_t)a.n_waves * a.tail_chunks;
-  const u32x4* lane_base = reinterpret_cast<const u32x4*>(d.base) + lane;
-  const uint64_t stride = d.stride;
-  const uint64_t nrec = d.n_records;
-
-  // Acquisition state of the next chunk (wave-uniform): 0 = ticket not requested, 1 = ticket
-  // in flight, 2 = search round in flight, 3 = bounds in flight, 4 = ready, 5 = pool empty,
-  // -1 = head mask in flight (the current head ran dry): every non-final state is below 4.
-  int nst = 0;
-  unsigned long long tk = 0, mk = 0, dry = 0;
-  uint32_t h = wave % kStealHeads;
-  uint64_t nb = 0, ne = 0, nsb = 0, nse = 0, sval = 0;
-  uint32_t lo = 0, hi = 0, stp = 0, ns = 0;
-  auto pos_of = [&](uint64_t r) {  // segpos from a loaded seg_rec value
-    const uint64_t p = d.shift + (r < nrec ? r : nrec) * stride;
-    return p < d.end ? p : d.end;
-  };
-  auto issue_round = [&]() {
-    stp = (hi - lo + 63u) / 64u;
-    const uint32_t idx = lo + (uint32_t)lane * stp;
-    sval = idx < hi ? d.seg_rec[idx] : 0ull;
-  };
-  auto advance = [&]() {  // one acquisition stage
-    if (nst == 0) {
-      if (lane == 0) tk = atomicAdd(heads + h, 1ull);
-      nst = 1;
-    } else if (nst == -1) {
-      // heads this wave found dry itself, plus those others marked before its atomicOr (the
-      // atomic's return value: a plain load could hit a stale line in this XCD's L2)
-      const unsigned long long m = __shfl(mk, 0) | dry;
-      if (m == (1ull << kStealHeads) - 1ull) {
-        nst = 5;
-        return;
-      }
-      while ((m >> h) & 1ull) h = (h + 1u) % kStealHeads;
-      nst = 0;
-    } else if (nst == 1) {
-      const unsigned long long t = (unsigned long long)h + kStealHeads * __shfl(tk, 0);
-      if (t >= tickets) {  // head h is dry: mark it; the returned old mask says which are left
-        dry |= 1ull << h;
-        if (lane == 0) mk = atomicOr(mask, 1ull << h);
-        nst = -1;
-        return;
-      }
-      const uint32_t owner = (uint32_t)(t % a.n_waves), piece = (uint32_t)(t / a.n_waves);
-      const uint64_t ob = first + (uint64_t)owner * a.wave_bytes;
-      const uint64_t oe = min(ob + a.wave_bytes, last);
-      nb = ob + a.head_bytes + (uint64_t)piece * a.chunk_bytes;
-      if (ob >= last || nb >= oe) {  // an empty piece: take another ticket
-        nst = 0;
-        return;
-      }
-      ne = min(nb + a.chunk_bytes, oe);
-      lo = 0;
-      hi = d.S;
-      issue_round();
-      nst = 2;
-    } else if (nst == 2) {
-      const uint32_t idx = lo + (uint32_t)lane * stp;
-      const bool pred = idx < hi && pos_of(sval) <= nb;
-      const uint32_t c = (uint32_t)__popcll(__ballot(pred));
-      bool done = c == 0;
-      if (!done) {
-        lo = lo + (c - 1u) * stp;
-        hi = min(lo + stp, hi);
-        done = hi - lo <= 1u;
-      }
-      if (done) {
-        ns = lo;
-        sval = lane < 2 ? d.seg_rec[ns + (uint32_t)lane] : 0ull;
-        nst = 3;
-      } else {
-        issue_round();
-      }
-    } else if (nst == 3) {
-      nsb = pos_of(__shfl(sval, 0));
-      nse = pos_of(__shfl(sval, 1));
-      nst = 4;
-    }
-  };
-
-  // First segment: this wave's head, or (a wave with an empty range) a stolen chunk.
-  uint64_t cb, ce, sb, se;
-  uint32_t s;
-  const uint64_t beg = first + (uint64_t)wave * a.wave_bytes;
-  if (beg < last) {
-    cb = beg;
-    ce = min(beg + a.head_bytes, min(beg + a.wave_bytes, last));
-    s = seg_search(d, 0u, cb, lane);
-    sb = segpos(d, s);
-    se = segpos(d, s + 1);
-  } else {
-    while (nst < 4) advance();
-    if (nst == 5) return;
-    cb = nb; ce = ne; s = ns; sb = nsb; se = nse;
-    nst = 0;
-  }
-  uint32_t acc = 0;
-  u32x4 cur[U];
-  load_step<U, NT>(cur, lane_base + (cb >> 4), cb, ce, lane, cb + kStep <= ce);
-  uint64_t p = cb;
-  uint32_t tick = 0;
-  for (;;) {
-    // one acquisition stage every kStageSteps steps: an atomic's or a search load's latency
-    // (1-3 us under a full stream) is then covered by the steps streamed meanwhile instead of
-    // stalling the wave's in-order load queue
-    if (nst < 4 && ++tick % kStageSteps == 0) advance();
-    // prefetch the next step: in this segment, or the first step of the next chunk
-    const uint64_t pn = p + kStep;
-    const bool last_step = pn >= ce;
-    u32x4 nxt[U];
-    if (!last_step) {
-      load_step<U, NT>(nxt, lane_base + (pn >> 4), pn, ce, lane, pn + kStep <= ce);
-    } else if (nst == 4) {
-      load_step<U, NT>(nxt, lane_base + (nb >> 4), nb, ne, lane, nb + kStep <= ne);
-    }
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) { v[u] = cur[u]; cur[u] = nxt[u]; }
-    const bool full = !last_step || pn == ce;
-    if (full && sb <= p && pn <= se) {
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        acc = __builtin_amdgcn_sad_u8(v[u].x, 0u, acc);
-        acc = __builtin_amdgcn_sad_u8(v[u].y, 0u, acc);
-        acc = __builtin_amdgcn_sad_u8(v[u].z, 0u, acc);
-        acc = __builtin_amdgcn_sad_u8(v[u].w, 0u, acc);
-      }
-    } else {
-      const uint64_t q = min(pn, ce);
-      for (;;) {
-        const uint64_t lo_b = max(sb, p), hi_b = min(se, q);
-        if (lo_b < hi_b) {
-#pragma unroll
-          for (int u = 0; u < U; u++) {
-            const int64_t x = (int64_t)(p + (uint64_t)u * 1024u + (uint64_t)lane * 16u);
-            acc = masked_sum16(v[u], (int64_t)lo_b - x, (int64_t)hi_b - x, acc);
-          }
-        }
-        if (se >= q) break;
-        flush(a.sums, s, acc);
-        acc = 0;
-        s = seg_next(d, s, se, lane);
-        sb = segpos(d, s);
-        se = segpos(d, s + 1);
-      }
-    }
-    if (!last_step) {
-      p = pn;
-      continue;
-    }
-    // segment done: switch to the next chunk
-    flush(a.sums, s, acc);
-    acc = 0;
-    const bool prefetched = nst == 4;
-    while (nst < 4) advance();  // not ready yet (short segment): finish synchronously
-    if (nst == 5) return;
-    cb = nb; ce = ne; s = ns; sb = nsb; se = nse;
-    p = cb;
-    nst = 0;
-    if (!prefetched) load_step<U, NT>(cur, lane_base + (cb >> 4), cb, ce, lane, cb + kStep <= ce);
-  }
-}
-
-// MODE: 0 = one static range per wave, 1 = tail stealing, 2 = interleaved pieces; 3 and 4 = 0 and
-// 2 with the bucket bounds in a register window (SegWindow); 5 and 6 = 0 and 2 for fixed 8-byte
-// records with the prefix scan in record space (digest_range_rec8, 4 KiB steps; LDS:
-// rec8_lds_bytes); 7 and 8 = 5 and 6 with 8 KiB steps.
-__host__ __device__ constexpr int mode_rec8_rows(int mode) {
-  return (mode == 5 || mode == 6 || (mode >= 9 && mode <= 12)) ? 4 : ((mode == 7 || mode == 8) ? 8 : 0);
-}
+// MODE: 0 = one static range per wave, 2 = interleaved pieces; 3 and 4 = 0 and 2 with the bucket
+// bounds in a register window (SegWindow); 5 and 6 = 0 and 2 for fixed 8-byte records with the
+// prefix scan in record space (digest_range_rec8; LDS: rec8_lds_bytes).
+__host__ __device__ constexpr bool mode_rec8(int mode) { return mode == 5 || mode == 6; }
+__host__ __device__ constexpr bool mode_pieces(int mode) { return mode == 2 || mode == 4 || mode == 6; }
 template <int U, bool NT, int PIPE, int PRIO, int MODE, bool A8>
 __device__ __forceinline__ void digest_dispatch(const DigestLaunch& a, uint32_t block, uint32_t* lds) {
-  if (MODE == 1)
-    digest_body_steal<U, NT, PRIO>(a, block);
-  else if (MODE == 9 || MODE == 11)
-    digest_body<U, NT, PIPE, PRIO, false, A8, 0, MODE == 9 ? 1 : 2>(a, block, lds);
-  else if (MODE == 10 || MODE == 12)
-    digest_body_pieces<U, NT, PIPE, PRIO, false, A8, 0, MODE == 10 ? 1 : 2>(a, block, lds);
-  else if (MODE == 2 || MODE == 4 || MODE == 6 || MODE == 8)
-    digest_body_pieces<U, NT, PIPE, PRIO, MODE == 4, A8, mode_rec8_rows(MODE)>(a, block, lds);
+  if (mode_pieces(MODE))
+    digest_body_pieces<U, NT, PIPE, PRIO, MODE == 4, A8, mode_rec8(MODE)>(a, block, lds);
   else
-    digest_body<U, NT, PIPE, PRIO, MODE == 3, A8, mode_rec8_rows(MODE)>(a, block, lds);
+    digest_body<U, NT, PIPE, PRIO, MODE == 3, A8, mode_rec8(MODE)>(a, block, lds);
 }
 
 template <int U, bool NT, int PIPE, int PRIO = 0, int MODE = 0>
@@ -1129,8 +709,6 @@ __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a)
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   digest_dispatch<U, NT, PIPE, PRIO, MODE, true>(a, blockIdx.x, lds);
 }
-
-
 
 // Fused build step (software pipelining of consecutive builds in ONE launch): workgroups
 // [0, tree_blocks) build the trees of the PREVIOUS build from its byte sums (tree_body, LDS
@@ -1141,66 +719,15 @@ __global__ __launch_bounds__(kThreads) void bucket_digest_kernel(DigestLaunch a)
 // wave per workgroup up to B = 128, the rest exit at once), so the SHA waves spread over many
 // CUs instead of crowding a few; tree workgroups come first so the dispatcher places them before
 // the streaming grid (sized to be fully resident) fills the remaining slots.
-#ifdef MDE_STEP_STAMPS  // probe only: first start / last end (s_memrealtime) of the tree and stream waves
-__device__ unsigned long long g_step_stamps[4];
-__device__ __forceinline__ void step_stamp(int role, unsigned long long t0) {
-  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-  if ((threadIdx.x & 63) == 0) {
-    atomicMin(&g_step_stamps[2 * role], t0);
-    atomicMax(&g_step_stamps[2 * role + 1], t1);
-  }
-}
-#endif
-
 template <int U, bool NT, int PIPE, int PRIO = 0, int MODE = 0>
 __global__ __launch_bounds__(kThreads) void build_step_kernel(DigestLaunch a, TreeLaunch t, uint32_t tree_blocks,
                                                               uint32_t Q) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-#ifdef MDE_STEP_STAMPS
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   if (blockIdx.x < tree_blocks) {
     step_trees(t, Q, blockIdx.x, lds);
-    step_stamp(0, t0);
     return;
   }
   digest_dispatch<U, NT, PIPE, PRIO, MODE, false>(a, blockIdx.x - tree_blocks, lds);
-  step_stamp(1, t0);
-  return;
-#endif
-#ifdef MDE_STEP_TREES_LAST
-  const uint32_t digest_blocks = gridDim.x - tree_blocks;
-  if (blockIdx.x >= digest_blocks) {
-    step_trees(t, Q, blockIdx.x - digest_blocks, lds);
-    return;
-  }
-  const uint32_t db = blockIdx.x;
-#else
-  if (blockIdx.x < tree_blocks) {
-#ifdef MDE_PROBE_TREE_PRIO  // probe only: the tree waves' issue priority (the stream's is PRIO)
-    __builtin_amdgcn_s_setprio(MDE_PROBE_TREE_PRIO);
-#endif
-#ifdef MDE_WAVE_STAMPS  // probe only: every tree wave's entry and exit
-    const unsigned long long te = __builtin_amdgcn_s_memrealtime();
-    const unsigned long long ce = __builtin_amdgcn_s_memtime();
-#endif
-#ifndef MDE_STEP_SKIP_TREES  // probe only: the dispatch shape without the tree work
-    step_trees(t, Q, blockIdx.x, lds);
-#endif
-#ifdef MDE_WAVE_STAMPS
-    const uint32_t tw = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-    if ((threadIdx.x & 63) == 0 && tw < kStampWaves) {
-      g_tree_stamps[2 * tw] = te;
-      g_tree_stamps[2 * tw + 1] = __builtin_amdgcn_s_memrealtime();
-      g_tree_clk[2 * tw] = ce;
-      g_tree_clk[2 * tw + 1] = __builtin_amdgcn_s_memtime();
-      g_tree_hw[tw] = hw_where();
-    }
-#endif
-    return;
-  }
-  const uint32_t db = blockIdx.x - tree_blocks;
-#endif
-  digest_dispatch<U, NT, PIPE, PRIO, MODE, false>(a, db, lds);
 }
 
 // First LDS word of the small build's bucket sums (after `groups` tree regions, 16-byte aligned).
@@ -1235,9 +762,6 @@ __host__ __device__ __forceinline__ uint32_t small_build_kw_word(uint32_t groups
 template <bool kDuo>
 __device__ __forceinline__ void small_build_body(const SegDesc& d, const TreeLaunch& t, uint32_t G, uint32_t words,
                                                  uint32_t blk, uint32_t* lds) {
-#ifdef MDE_SMALL_PROF  // probe only: digest-phase / tree-phase split of a one-workgroup launch
-  const uint64_t prof0 = wall_clock64();
-#endif
   const u32x4* base = reinterpret_cast<const u32x4*>(d.base);
   const uint32_t groups = small_build_groups(G, kDuo);
   const uint32_t s_beg = min(blk * groups * t.B, d.S), s_end = min((blk + 1) * groups * t.B, d.S);
@@ -1280,20 +804,12 @@ __device__ __forceinline__ void small_build_body(const SegDesc& d, const TreeLau
     leaves_waves(tl, p0 + threadIdx.x / 64u, (uint32_t)kThreads / 64u, p0 + groups);
     return;
   }
-#ifdef MDE_SMALL_PROF
-  const uint64_t prof1 = wall_clock64();
-#endif
   if (kDuo) {
     u32x4* kw = reinterpret_cast<u32x4*>(lds + small_build_kw_word(groups, words, t.B));
     tree_body_duo(tl, G, words, blk, lds, (uint32_t)kThreads / 2, kw);
   } else {
     tree_body<true>(tl, G, words, blk, lds, kThreads);
   }
-#ifdef MDE_SMALL_PROF
-  __syncthreads();
-  if (gridDim.x == 1 && threadIdx.x == 0)
-    printf("small_prof digest %lu tree %lu (x10ns)\n", prof1 - prof0, wall_clock64() - prof1);
-#endif
 }
 
 template <bool kDuo>
@@ -1415,78 +931,46 @@ __global__ __launch_bounds__(kThreads) void server_kernel(ServerSlot* slots, uin
 typedef void (*DigestKernel)(DigestLaunch);
 typedef void (*StepKernel)(DigestLaunch, TreeLaunch, uint32_t, uint32_t);
 struct Variant {
+  int id;
   DigestKernel fn;
   StepKernel step;
-  int unroll;
   int mode;
 };
 
-#define MDE_VARIANT(U, NT, PIPE, PRIO, MODE) \
-  { bucket_digest_kernel<U, NT, PIPE, PRIO, MODE>, build_step_kernel<U, NT, PIPE, PRIO, MODE>, U, MODE }
+#define MDE_VARIANT(ID, MODE) \
+  { ID, bucket_digest_kernel<4, true, 2, 2, MODE>, build_step_kernel<4, true, 2, 2, MODE>, MODE }
 
-// Kernel variants (tuning knob mde_set_tuning digest_variant = index; default in mde_api.cpp).
+// Kernel variants (the tuning knob mde_set_tuning's digest_variant = id; plan_digest picks one per
+// build). Every variant: 4 KiB steps (4 x 16-byte nontemporal loads per lane), the next step's
+// loads issued before the current one is reduced and the first step's before the bucket search,
+// issue priority 2. Round 1-5 variants measured and rejected (other unrolls and cache policies,
+// tail stealing, 8 KiB rec8 steps, other priorities; DESIGN.md sections 4.1, 4.9) were removed in
+// round 6; the ids of the shipped ones are unchanged.
 const Variant kVariants[] = {
-    MDE_VARIANT(8, true, false, 0, 0),  MDE_VARIANT(8, false, false, 0, 0),
-    MDE_VARIANT(16, true, false, 0, 0), MDE_VARIANT(4, true, false, 0, 0),
-    MDE_VARIANT(4, true, true, 0, 0),   MDE_VARIANT(8, true, true, 0, 0),
-    MDE_VARIANT(16, false, false, 0, 0), MDE_VARIANT(4, true, true, 2, 0),
-    MDE_VARIANT(4, true, true, 3, 0),   MDE_VARIANT(4, true, true, 2, 1),
-    MDE_VARIANT(8, true, true, 2, 1),    MDE_VARIANT(4, true, 2, 2, 0),
-    MDE_VARIANT(4, true, 2, 2, 2),      MDE_VARIANT(4, true, 2, 2, 3),
-    MDE_VARIANT(4, true, 2, 2, 4),      MDE_VARIANT(4, true, 2, 2, 5),
-    MDE_VARIANT(4, true, 2, 2, 6),      MDE_VARIANT(4, true, 2, 2, 7),
-    MDE_VARIANT(4, true, 2, 2, 8),      MDE_VARIANT(4, true, 2, 2, 9),
-    MDE_VARIANT(4, true, 2, 2, 10),     MDE_VARIANT(4, true, 2, 2, 11),
-    MDE_VARIANT(4, true, 2, 2, 12),
-#ifdef MDE_PROBE_EXTRA_VARIANTS  // probe only: the rec8 stream (mode 5) at issue priority 0, 1, 3
-    MDE_VARIANT(4, true, 2, 0, 5),      MDE_VARIANT(4, true, 2, 1, 5),
-    MDE_VARIANT(4, true, 2, 3, 5),
-#endif
+    MDE_VARIANT(11, 0),  // one static range per wave (byte sums per 16-byte vector)
+    MDE_VARIANT(12, 2),  // 11 with interleaved pieces (large shares)
+    MDE_VARIANT(13, 3),  // register window over the bucket bounds + prefix-scan steps (short buckets)
+    MDE_VARIANT(14, 4),  // 13 with interleaved pieces
+    MDE_VARIANT(15, 5),  // fixed 8-byte records: record-space prefix scan (the production value)
+    MDE_VARIANT(16, 6),  // 15 with interleaved pieces
 };
 #undef MDE_VARIANT
 
-constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
-const Variant& variant(int v) { return kVariants[(v >= 0 && v < kNumVariants) ? v : 0]; }
+const Variant& variant(int v) {
+  for (const Variant& x : kVariants)
+    if (x.id == v) return x;
+  return kVariants[0];
+}
 
 }  // namespace
 
-int bucket_digest_variants() { return kNumVariants; }
+bool bucket_digest_variant_valid(int v) {
+  for (const Variant& x : kVariants)
+    if (x.id == v) return true;
+  return false;
+}
 
-#ifdef MDE_WAVE_STAMPS
-}  // namespace mde
-extern "C" int mde_probe_wave_stamps(unsigned long long* host, uint64_t n) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mde::g_wave_stamps), n * 8 > sizeof(mde::g_wave_stamps) ? sizeof(mde::g_wave_stamps) : n * 8);
-}
-extern "C" int mde_probe_tree_stamps(unsigned long long* host, uint64_t n, int reset) {
-  const size_t bytes = n * 8 > sizeof(mde::g_tree_stamps) ? sizeof(mde::g_tree_stamps) : n * 8;
-  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(mde::g_tree_stamps), bytes) != hipSuccess) return -1;
-  if (reset) {
-    static const unsigned long long zero[3 * mde::kStampWaves] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(mde::g_tree_stamps), zero, sizeof(mde::g_tree_stamps)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(mde::g_wave_stamps), zero, sizeof(mde::g_wave_stamps)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(mde::g_tree_clk), zero, sizeof(mde::g_tree_clk)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(mde::g_wave_clk), zero, sizeof(mde::g_wave_clk)) != hipSuccess)
-      return -1;
-  }
-  return 0;
-}
-// which = 0 / 1: the streaming / tree waves' placement (hw_where, one per wave)
-extern "C" int mde_probe_hw_where(unsigned long long* host, uint64_t n, int which) {
-  const size_t cap = which ? sizeof(mde::g_tree_hw) : sizeof(mde::g_wave_hw);
-  const size_t bytes = n * 8 > cap ? cap : n * 8;
-  return which ? (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mde::g_tree_hw), bytes)
-               : (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mde::g_wave_hw), bytes);
-}
-// which = 0: the streaming waves' shader-clock counts (3 per wave), 1: the tree waves' (2 per wave)
-extern "C" int mde_probe_clock_stamps(unsigned long long* host, uint64_t n, int which) {
-  const size_t cap = which ? sizeof(mde::g_tree_clk) : sizeof(mde::g_wave_clk);
-  const size_t bytes = n * 8 > cap ? cap : n * 8;
-  return which ? (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mde::g_tree_clk), bytes)
-               : (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mde::g_wave_clk), bytes);
-}
-namespace mde {
-#endif
 
 // LDS of one small-build workgroup: tree regions, bucket sums and counts, and in the split-schedule
 // form the K+W ring.
@@ -1571,40 +1055,16 @@ hipError_t launch_server(ServerSlot* slots, uint32_t n_slots, uint64_t lifetime_
   return hipGetLastError();
 }
 
-bool bucket_digest_steals(int v) { return variant(v).mode == 1; }
-bool bucket_digest_pieces(int v) {
-  const int m = variant(v).mode;
-  return m == 2 || m == 4 || m == 6 || m == 8 || m == 10 || m == 12;
-}
-bool bucket_digest_rec8(int v) { return mode_rec8_rows(variant(v).mode) != 0; }
-uint32_t bucket_digest_rec8_lds_bytes(int v) {
-  const int rows = mode_rec8_rows(variant(v).mode);
-  return rows ? rec8_lds_bytes(rows) : 0u;
-}
+bool bucket_digest_pieces(int v) { return mode_pieces(variant(v).mode); }
+bool bucket_digest_rec8(int v) { return mode_rec8(variant(v).mode); }
+uint32_t bucket_digest_rec8_lds_bytes(int v) { return bucket_digest_rec8(v) ? rec8_lds_bytes() : 0u; }
 int bucket_digest_pieces_sibling(int v) {  // the same kernel with interleaved pieces
   switch (v) {
     case 11: return 12;
     case 13: return 14;
     case 15: return 16;
-    case 17: return 18;
-    case 19: return 20;
-    case 21: return 22;
     default: return v;
   }
-}
-
-void plan_steal(uint64_t wave_bytes, uint64_t* head_bytes, uint64_t* chunk_bytes, uint32_t* tail_chunks) {
-  // Tail = about 1/6 of each wave range in up to 16 pieces of >= 16 KiB (the max step), at most
-  // 1/4 of the range. The pool absorbs a ~5 % spread of head finish times; pieces are small
-  // enough (~15 us per wave at C4) that the last ones do not leave a tail of their own.
-  uint64_t c = wave_bytes / 96 / kMaxStepBytes * kMaxStepBytes;
-  if (c < 4 * kMaxStepBytes) c = 4 * kMaxStepBytes;
-  uint32_t n = 16;
-  while (n > 1 && (uint64_t)n * c * 4 > wave_bytes) n /= 2;
-  if ((uint64_t)n * c * 4 > wave_bytes) n = 0;  // range too short to split
-  *chunk_bytes = c;
-  *tail_chunks = n;
-  *head_bytes = wave_bytes - (uint64_t)n * c;
 }
 
 int bucket_digest_blocks_per_cu(int v, int cap) {
@@ -1680,10 +1140,7 @@ uint32_t build_step_tree_q(uint32_t B) {
   const uint32_t n1 = (B + 1) / 2;
   const uint32_t per = (n1 + (n1 + 1) / 2) * 8u * 4u;  // bytes of level buffers per partition
   const uint32_t q = (kStepTreeLdsMax - 64u) / per;
-#ifndef MDE_STEP_TREE_QMAX
-#define MDE_STEP_TREE_QMAX 8u
-#endif
-  return q > MDE_STEP_TREE_QMAX ? MDE_STEP_TREE_QMAX : q;
+  return q > 8u ? 8u : q;
 }
 
 bool build_step_fusable(uint32_t B) { return B >= 1 && build_step_tree_q(B) >= 1; }
@@ -1777,14 +1234,3 @@ hipError_t launch_build_step(const DigestLaunch& a, const TreeLaunch* t, hipStre
 }
 
 }  // namespace mde
-
-#ifdef MDE_STEP_STAMPS
-extern "C" int mde_probe_step_stamps(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mde::g_step_stamps), sizeof(unsigned long long) * 4) != hipSuccess) return -1;
-  if (reset) {
-    const unsigned long long init[4] = {~0ull, 0ull, ~0ull, 0ull};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(mde::g_step_stamps), init, sizeof init) != hipSuccess) return -1;
-  }
-  return 0;
-}
-#endif

@@ -26,7 +26,6 @@
 // Digest-kernel tuning defaults (tools/digest_sweep.sh, profiles/r01_digest_sweep.json).
 constexpr int kDefaultDigestVariant = 11;  // U=4 nontemporal, register-prefetched (first step before
                                            // the bucket search), s_setprio 2
-constexpr int kStaticDigestVariant = 11;  // used when a stealing variant cannot steal
 constexpr int kDefaultDigestCap = 2;      // 2 workgroups (8 waves) per CU
 constexpr int kDefaultDigestOversub = 1;  // grid = resident slots x oversub
 // Interleaved pieces (digest variant 12): by default a wave whose share of
@@ -86,10 +85,6 @@ struct mde_ctx {
     bool dirty = false;
   };
   Slot pipe[2];
-  // Tail-stealing ticket heads of the digest kernel (two parities, zeroed at allocation; each
-  // stealing launch uses one parity and zeroes the other for the next launch).
-  unsigned long long* steal = nullptr;
-  uint32_t steal_parity = 0;
   struct Pending {
     bool active = false;
     int slot = 0;
@@ -394,7 +389,6 @@ int plan_digest(mde_ctx* c, uint64_t bytes, mde::DigestLaunch* a) {
   } else if (mde::bucket_digest_pieces(a->variant)) {
     piece_bytes = c->digest_piece_bytes;
   }
-  const bool steals = mde::bucket_digest_steals(a->variant);
   // grid from the resident workgroups of the variant that actually runs (the window and rec8
   // kernels may fit fewer per CU than the default under a raised cap: then every wave of the
   // equal-range grid is still co-resident, no tail)
@@ -406,24 +400,6 @@ int plan_digest(mde_ctx* c, uint64_t bytes, mde::DigestLaunch* a) {
   a->piece_stride = (uint64_t)a->n_waves * a->wave_bytes;
   a->lds_bytes = c->digest_oversub > 1 ? (uint32_t)((160u * 1024u) / (uint32_t)c->digest_blocks_per_cu) & ~255u : 0u;
   if (mde::bucket_digest_rec8(a->variant)) a->lds_bytes = std::max(a->lds_bytes, mde::bucket_digest_rec8_lds_bytes(a->variant));
-  // Tail stealing needs fixed-length values and a split range; otherwise the static sibling.
-  if (steals) {
-    mde::plan_steal(a->wave_bytes, &a->head_bytes, &a->chunk_bytes, &a->tail_chunks);
-    if (!a->seg.stride || !a->tail_chunks) {
-      a->variant = kStaticDigestVariant;
-    } else {
-      if (!c->steal) {
-        if (hipMalloc(&c->steal, mde::kStealScratchBytes) != hipSuccess) {
-          c->steal = nullptr;
-          return set_err(c, MDE_E_NOMEM, "steal counter allocation failed");
-        }
-        MDE_HIP(c, hipMemsetAsync(c->steal, 0, mde::kStealScratchBytes, c->stream));
-      }
-      a->steal = c->steal;
-      a->steal_parity = c->steal_parity;
-      c->steal_parity ^= 1u;
-    }
-  }
   return MDE_OK;
 }
 
@@ -663,9 +639,6 @@ int build_pipelined(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
       mde_ctx::Slot& ps = c->pipe[pd.slot];
       rc = tree_launch_for(c, &pd.rec, &pd.out, ps.sums, ps.counts, &t);
       if (rc) return rc;
-#ifdef MDE_PROBE_STEP_TOP_NODES  // probe only (wrong roots): the trees stop at their first level of <= N nodes
-      t.top_nodes = MDE_PROBE_STEP_TOP_NODES;
-#endif
     }
     hipError_t e = mde::launch_build_step(a, pd.active ? &t : nullptr, c->stream);
     if (e != hipSuccess) {
@@ -840,7 +813,6 @@ void mde_destroy(mde_ctx* c) {
     step("free device buffers");
     if (c->sums) (void)hipFree(c->sums);
     if (c->counts) (void)hipFree(c->counts);
-    if (c->steal) (void)hipFree(c->steal);
     for (auto& sl : c->pipe) {
       if (sl.sums) (void)hipFree(sl.sums);
       if (sl.counts) (void)hipFree(sl.counts);
@@ -895,8 +867,8 @@ uint64_t mde_last_error_copy(mde_ctx* c, char* buf, uint64_t cap) {
 int mde_set_tuning(mde_ctx* c, int digest_variant, int digest_blocks_per_cu, int digest_oversub) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
-  if (digest_variant >= mde::bucket_digest_variants())
-    return set_err(c, MDE_E_INVAL, "digest variant %d out of range", digest_variant);
+  if (digest_variant >= 0 && !mde::bucket_digest_variant_valid(digest_variant))
+    return set_err(c, MDE_E_INVAL, "digest variant %d is not one of 11..16", digest_variant);
   c->digest_variant = digest_variant < 0 ? kDefaultDigestVariant : digest_variant;
   c->digest_auto = digest_variant < 0;
   c->digest_cap = digest_blocks_per_cu < 0 ? kDefaultDigestCap : digest_blocks_per_cu;

@@ -36,17 +36,8 @@ struct DigestLaunch {
   unsigned long long* sums;   // [S] u64 accumulators (zero on entry)
   uint64_t wave_bytes;        // contiguous bytes per wave (multiple of the 16 KiB max step)
   uint32_t n_waves;
-  int variant;                // kernel variant (unroll / load policy), see digest.hip
+  int variant;                // kernel variant id (digest.hip kVariants)
   uint32_t lds_bytes;         // residency cap for oversubscribed grids (0 = none)
-  // Tail stealing (variants with bucket_digest_steals; fixed-length values only): two parities of
-  // ticket heads + exhausted-heads mask (kStealScratchBytes) -- a launch uses parity
-  // steal_parity and zeroes the other for the next launch of the same context (launches of one
-  // context are stream-ordered).
-  unsigned long long* steal;
-  uint32_t steal_parity;
-  uint64_t head_bytes;        // bytes of each wave range its owner streams
-  uint64_t chunk_bytes;       // tail piece size (multiple of the 16 KiB max step)
-  uint32_t tail_chunks;       // tail pieces per wave
   // Interleaved pieces (static variants): wave w streams `pieces` ranges of wave_bytes each,
   // [first + (j * n_waves + w) * wave_bytes, +wave_bytes) for j < pieces; piece_stride =
   // n_waves * wave_bytes. pieces = 1 is one contiguous range per wave.
@@ -60,15 +51,11 @@ hipError_t launch_bucket_digest(const DigestLaunch& a, hipStream_t st);
 void plan_bucket_digest(uint64_t bytes, int cus, int blocks_per_cu, int oversub, uint64_t piece_bytes,
                         uint64_t* wave_bytes, uint32_t* n_waves, uint32_t* pieces);
 int bucket_digest_blocks_per_cu(int variant, int cap);
-int bucket_digest_variants();
-bool bucket_digest_steals(int variant);
+bool bucket_digest_variant_valid(int variant);
 bool bucket_digest_pieces(int variant);  // interleaved-pieces variant (DigestLaunch::pieces)
 int bucket_digest_pieces_sibling(int variant);  // its interleaved-pieces form (itself if none)
 bool bucket_digest_rec8(int variant);  // fixed 8-byte records, record-space scan (needs LDS)
 uint32_t bucket_digest_rec8_lds_bytes(int variant);
-constexpr uint64_t kStealScratchBytes = 512;
-// Head / tail split of each wave range for tail stealing (tail_chunks = 0: no split).
-void plan_steal(uint64_t wave_bytes, uint64_t* head_bytes, uint64_t* chunk_bytes, uint32_t* tail_chunks);
 
 struct TaggedLaunch {
   const uint8_t* base;        // values rounded down to 16 B

@@ -501,9 +501,6 @@ __device__ __forceinline__ void step_trees(const TreeLaunch& t, uint32_t Q, uint
   else if (Q)
     tree_body_packed(t, Q, block, lds);
   else {
-#ifdef MDE_STEP_WIDE_PRIO  // probe only: wide-tree waves at this priority beside the stream
-    __builtin_amdgcn_s_setprio(MDE_STEP_WIDE_PRIO);
-#endif
     if (t.duo_kw_word)  // the second wave computes the first's message schedules on its <= 64-node levels
       tree_body_duo(t, kStepTreeWideThreads, tree_lds_words(t.B), block, lds, kStepTreeWideThreads / 2,
                     reinterpret_cast<u32x4*>(lds + t.duo_kw_word));

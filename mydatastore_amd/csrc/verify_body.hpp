@@ -15,14 +15,6 @@ constexpr uint32_t kVerifyWords = kVerifyMaxBuckets / 32;
 constexpr uint32_t kVerifyFusedWords = kVerifyFusedMaxCap / 32;
 constexpr uint32_t kVerifyStageMaxBytes = 24u * 1024u;  // per wave: a whole object up to B = 1024 (20.5 KB)
 
-// Phase timestamps of a one-workgroup fused launch (build with -DMDE_VERIFY_PROF; diagnostics only).
-#ifdef MDE_VERIFY_PROF
-#define MDE_PROF_MARK(k) \
-  if (gridDim.x == 1 && threadIdx.x == 0) prof_t[k] = wall_clock64()
-#else
-#define MDE_PROF_MARK(k)
-#endif
-
 // Partition p's fold by all 256 threads (uniform: contains barriers). bits: >= ceil(B/32) words.
 __device__ __forceinline__ void verify_body(const VerifyLaunch& a, uint32_t p, uint32_t* bits, uint32_t* wave_tot) {
   const uint32_t t = threadIdx.x;
@@ -113,10 +105,6 @@ __device__ __forceinline__ void verify_fused_body(const VerifyFusedLaunch& f, ui
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t R = f.fold.R, B = f.fold.B, cap = f.dec.cap;
   const uint64_t i0 = (uint64_t)p * R;
-#ifdef MDE_VERIFY_PROF
-  uint64_t prof_t[8] = {};
-#endif
-  MDE_PROF_MARK(0);
 
   // 1. EpochTreeObjectToMerkleTree, decode half: wave w takes peers w, w + 4, ...
   uint8_t* stage = reinterpret_cast<uint8_t*>(dyn) + (uint64_t)wid * stage_bytes;
@@ -133,7 +121,6 @@ __device__ __forceinline__ void verify_fused_body(const VerifyFusedLaunch& f, ui
       if (n + 4 <= stage_bytes) staged = stage_object<kDeep ? 16 : 8>(obj, n, stage, lane);
     }
     __syncthreads();
-    MDE_PROF_MARK(1);
     if (r < R) {
       // two call sites, so the staged one reads LDS (ds_read) rather than through flat loads
       // kDeep (B > 64): 256 canonical bucket entries per step instead of 64
@@ -144,7 +131,6 @@ __device__ __forceinline__ void verify_fused_body(const VerifyFusedLaunch& f, ui
     }
     __syncthreads();
   }
-  MDE_PROF_MARK(2);
 
   // 2. Rebuild only the peer trees whose shape (leaf count incl. the odd duplicate) differs from
   // the local tree's; same-shape peers are diffed on their leaves.
@@ -179,7 +165,6 @@ __device__ __forceinline__ void verify_fused_body(const VerifyFusedLaunch& f, ui
     for (uint32_t blk = 0; blk * groups < R; blk++) tree_body<true>(t, G, words, blk, dyn, kVerifyThreads);
   }
 
-  MDE_PROF_MARK(3);
   // 3. DifferentMerkleTreeBuckets(myTree, otherTree) per peer.
   // 3a. Same-shape peers: one wave per peer, lane v of step k walks path 64k + v, and the wave's
   // ballots give the DFS output order directly (diff_body's leaf-only rule, without its
@@ -257,10 +242,8 @@ __device__ __forceinline__ void verify_fused_body(const VerifyFusedLaunch& f, ui
   }
   __syncthreads();
 
-  MDE_PROF_MARK(4);
   // 4. validCount / validDiff / diffSet.
   verify_body(f.fold, p, bits, wave_tot);
-  MDE_PROF_MARK(5);
 
   // 5. The object VerifyEpoch persists.
   if (f.enc.n) {
@@ -271,13 +254,6 @@ __device__ __forceinline__ void verify_fused_body(const VerifyFusedLaunch& f, ui
       encode_object(f.enc, p, lane);
     }
   }
-  MDE_PROF_MARK(6);
-#ifdef MDE_VERIFY_PROF
-  if (gridDim.x == 1 && threadIdx.x == 0)
-    printf("verify_prof stage %lu decode %lu shape %lu diff %lu fold %lu encode %lu (x10ns)\n", prof_t[1] - prof_t[0],
-           prof_t[2] - prof_t[1], prof_t[3] - prof_t[2], prof_t[4] - prof_t[3], prof_t[5] - prof_t[4],
-           prof_t[6] - prof_t[5]);
-#endif
 }
 
 }  // namespace mde

@@ -126,30 +126,32 @@ def test_pipelined_full_size_equals_standalone(engine):
             assert torch.equal(o[k], ref[k]), k
 
 
-def _variant_count(engine):
+def _variant_ids(engine):
+    """The digest-kernel variant ids mde_set_tuning accepts (digest.hip kVariants: 11..16)."""
     import mydatastore_amd as mde
-    n = 0
-    while True:
+    ids = []
+    for v in range(64):
         try:
-            engine.set_tuning(n, -1)
+            engine.set_tuning(v, -1)
+            ids.append(v)
         except mde.MdeError:
-            break
-        n += 1
+            pass
     engine.set_tuning(-1, -1)
-    return n
+    return ids
 
 
 def test_every_digest_variant_matches_golden(engine, golden, coracle):
-    """Every digest-kernel variant (static ranges, tail stealing; U = 4..16; both cache policies)
-    through both the standalone and the fused path gives the golden outputs."""
+    """Every digest-kernel variant (one range, pieces, register window, record-space rec8; the
+    rec8 ids fall back to the window kernel for other record shapes) through both the standalone
+    and the fused path gives the golden outputs."""
     import torch
     dev = torch.device("cuda:0")
     engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    nv = _variant_count(engine)
-    assert nv >= 10
+    ids = _variant_ids(engine)
+    assert ids == [11, 12, 13, 14, 15, 16]
     cases = golden("synth_cases.json")
     try:
-        for v in range(nv):
+        for v in ids:
             engine.set_tuning(v, -1)
             built = []
             for c in cases:
@@ -168,19 +170,18 @@ def test_every_digest_variant_matches_golden(engine, golden, coracle):
 
 
 def test_every_digest_variant_full_size(engine):
-    """C4 at N=1 and the N=8 shard: every variant's roots equal the default build's (stealing
-    variants hand tail chunks between waves; any lost or doubled chunk changes the roots)."""
+    """C4 at N=1 and the N=8 shard: every variant's roots equal the default build's."""
     import torch
     from mydatastore_amd.workload import make_workload
-    nv = _variant_count(engine)
+    ids = _variant_ids(engine)
     for world in (8, 1):
         w = make_workload(engine, n_partitions=1024, n_buckets=64, value_len=1024, part_mode="mod",
                           n_keys=10_000_000, rank=0, world=world)
         ref = w.build()
         try:
-            for v in range(nv):
+            for v in ids:
                 engine.set_tuning(v, -1)
-                for _ in range(2):  # twice: the stealing counters alternate between launches
+                for _ in range(2):
                     o = w.build()
                     for k in ("digest", "root"):
                         assert torch.equal(o[k], ref[k]), (world, v, k)
@@ -189,11 +190,11 @@ def test_every_digest_variant_full_size(engine):
         del w
 
 
-def test_stealing_skewed_arena_matches_torch_sums(engine):
-    """Tail stealing on a 300 MB arena with skew: 13-byte records (never 16-byte aligned), the
-    arena start 5 bytes past an allocation, 37 partitions x 100 buckets with empty buckets and
-    partitions and a few buckets of tens of MB. Digests of every variant equal per-bucket byte
-    sums computed by torch (cumsum over per-record sums) mod 999999."""
+def test_skewed_arena_every_variant_matches_torch_sums(engine):
+    """A 300 MB arena with skew: 13-byte records (never 16-byte aligned), the arena start 5 bytes
+    past an allocation, 37 partitions x 100 buckets with empty buckets and partitions and a few
+    buckets of tens of MB. Digests of every variant equal per-bucket byte sums computed by torch
+    (cumsum over per-record sums) mod 999999."""
     import torch
     import mydatastore_amd as mde
     dev = torch.device("cuda:0")
@@ -215,10 +216,10 @@ def test_stealing_skewed_arena_matches_torch_sums(engine):
     dseg = seg.to(dev)
     want = ((cs[dseg[1:]] - cs[dseg[:-1]]) % 999999).cpu()
     rec = mde.Records(vals.data_ptr(), n * V, V, mde.LAYOUT_SORTED, 0, n, P, B, dseg.data_ptr())
-    nv = _variant_count(engine)
+    ids = _variant_ids(engine)
     roots = {}
     try:
-        for v in range(nv):
+        for v in ids:
             engine.set_tuning(v, -1)
             for rep in range(2):
                 o = {"digest": torch.zeros(P * B, dtype=torch.int64, device=dev),
@@ -531,10 +532,9 @@ def test_default_variant_choice_b1000_full_size(engine, value_len, n_keys, n_buc
         engine.set_digest_piece_bytes(-1)
 
 
-# digest.hip: fixed 8-byte records, record-space prefix scan (+ pieces), 4 KiB and 8 KiB steps, and
-# the scalar-bookkeeping form (19, 20: digest_range_rec8s)
-REC8_VARIANTS = (15, 16, 17, 18, 19, 20)
-REC8_PIECES = (16, 18, 20)
+# digest.hip: fixed 8-byte records, record-space prefix scan (+ pieces)
+REC8_VARIANTS = (15, 16)
+REC8_PIECES = (16,)
 
 
 @pytest.mark.parametrize("start", [0, 8])
