@@ -46,6 +46,16 @@ GATHER_BUCKET = 8  # builds per root-gather collective in fused mode at N > 1
 # ~170 after 100, while C4 (HBM bound) moves < 0.5 % (profiles/r05/r05p_clock_ramp.jsonl).
 WARMUP_MIN_MS = 25.0
 
+# How each line is timed (the same for every N on the group engine; the ranks engine states its own)
+TIMER_GROUP = ("ms_per_step: host wall clock over exactly K steps between barrier + synchronize of every GPU on "
+               "both sides (rank 0's process drives all N GPUs); roofline.kernel_ms: HIP events on GPU 0's "
+               "launch stream bracketing the same K launches")
+TIMER_RANKS = ("ms_per_step: host wall clock over exactly K steps between barrier + synchronize on both sides, "
+               "max over ranks; roofline.kernel_ms: HIP events on the launch stream, max over ranks")
+PIPELINE_FUSED = ("one build_step_kernel launch per build: this build's digest workgroups + the previous build's "
+                  "tree workgroups (mde_build_pipelined_async / mde_group_build_pipelined_async); the last "
+                  "build's trees in the drain")
+
 CONFIGS = {
     # name: (n_keys, n_partitions, value_len, n_buckets, part_mode, description)
     "c4": (10_000_000, 1024, 1024, 64, "mod",
@@ -283,7 +293,7 @@ def production_shape(torch, eng, dev, threads, reps=10):
     return res
 
 
-def end_to_end(torch, eng, w, B, reps=3):
+def end_to_end(torch, eng, w, B, reps=3, ref_root=None):
     """Host-resident records -> device -> Merkle build -> host results, PCIe included
     (mde_build_streamed from a pinned host arena; mde_build for comparison). Reported beside
     `value`, never as it."""
@@ -306,7 +316,7 @@ def end_to_end(torch, eng, w, B, reps=3):
             out = fn()
         dt = (time.perf_counter() - t0) / reps
         res[name] = {"GiB_per_s": round(w.value_bytes / 2**30 / dt, 3), "s_per_build": round(dt, 4)}
-    ok = bool(np.array_equal(out["root"], w.out["root"].cpu().numpy()))
+    ok = bool(np.array_equal(out["root"], ref_root if ref_root is not None else w.out["root"].cpu().numpy()))
     t0 = time.perf_counter()
     torch.cuda.synchronize()
     h2d = torch.empty_like(w.values)
@@ -364,6 +374,12 @@ def main_group(args):
                 "build both, device DFS-order diff, out-of-sync range extract of B")
     g = mde.Group(devices)
     lib = mde.load_library()
+    if args.tuning:  # A/B only: the digest variant / residency on every member's context
+        tv = [int(x) for x in args.tuning.split(",")] + [-1, -1, -1]
+        for i in range(N):
+            check_rc = lib.mde_set_tuning(lib.mde_group_ctx(g.g, i), tv[0], tv[1], tv[2])
+            if check_rc != mde.MDE_OK:
+                raise SystemExit(f"--tuning {args.tuning}: mde_set_tuning failed ({check_rc})")
     engines = {}
     for d in sorted(set(devices)):
         engines[d] = mde.Engine(d)
@@ -555,9 +571,11 @@ def main_group(args):
     o0 = {k: v.cpu().numpy() for k, v in sets[0][last % 2][0].items()}
     r0 = main_run.send[kset][0].view(bk, slab * width)[row, :s_n * 32].cpu().numpy()
     ok_oracle = (np.array_equal(o0["digest"][:s_n * B].view(np.uint64), ref["digest"]) and
-                 np.array_equal(o0["size"][:s_n * B], ref["size"]) and np.array_equal(r0, ref["root"]))
+                 np.array_equal(o0["size"][:s_n * B], ref["size"]) and
+                 np.array_equal(o0["items"][:s_n], ref["items"]) and np.array_equal(r0, ref["root"]))
     parity["oracle_sample_partitions"] = int(s_n)
-    parity["shard0_equals_c_oracle_on_sample"] = bool(ok_oracle)
+    # GPU 0's shard (the whole arena at N = 1): its last timed build against the C oracle
+    parity["timed_build_equals_c_oracle_on_sample"] = bool(ok_oracle)
     if c5:  # every shard's gathered diff counts and id lists: exactly its perturbed partitions and
         # buckets (B = 64: no odd level, so no DFS duplicates); shard 0's extract
         ok_cnt = ok_ids = True
@@ -607,6 +625,20 @@ def main_group(args):
     total = sum(w.value_bytes for w in shards) * (2 if c5 else 1)
     launches = 2 if c5 else 1
     achieved = shards[0].value_bytes * launches / (dev0_ms * 1e-3) / 1e9
+    # N = 1 (the driver's BENCH line): the CPU baseline, the PCIe-inclusive rate and the production
+    # shape, on GPU 0's engine, after the timed runs (never part of `value`)
+    extras = {"cpu_baseline": None, "end_to_end": None, "production_shape": None}
+    if N == 1 and world == 1 and not args.profile:
+        if not args.no_cpu_baseline:
+            extras["cpu_baseline"] = cpu_baseline(co, s_vals, s_seg, s_n, (n_keys, P, V, B, mode, desc),
+                                                  args.cpu_baseline_seconds, threads, info)
+        e0 = engines[devices[0]]
+        e0.set_stream(torch.cuda.current_stream(sdev[0]).cuda_stream)
+        if not args.no_e2e and not c5:  # against the timed build's roots (its slab row: all P at N = 1)
+            roots0 = main_run.send[kset][0].view(bk, slab * width)[row, :P * 32].cpu().numpy()
+            extras["end_to_end"] = end_to_end(torch, e0, shards[0], B, ref_root=roots0)
+        if not args.no_production_shape and not c5:
+            extras["production_shape"] = production_shape(torch, e0, sdev[0], threads)
     result = {
         "metric": METRIC, "value": round(total / 2**30 / (ms * 1e-3), 3), "unit": "GiB/s", "n_gpus": N,
         "steps": args.steps, "warmup": warmup, "ms_per_step": round(ms, 5), "higher_is_better": True,
@@ -624,16 +656,18 @@ def main_group(args):
         "roofline": {"bound": "hbm", "kernel": "build_step_kernel (GPU 0's launches"
                                                + (" + the compare kernels, counted against it)" if c5 else ")"),
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": pmc_traffic("c4" if c5 else args.config, shards[0].value_bytes),
                      "kernel_ms": round(dev0_ms / launches, 5), "algorithmic_bytes_per_launch": shards[0].value_bytes},
+        "timer": TIMER_GROUP,
         "parity": parity,
         "host_timing": host_timing,
-        "cpu_baseline": None,
+        "simulated_shard_of_world": None,
+        "pipeline": PIPELINE_FUSED + ("; C5: per step, replica A's and B's launches, the diff and the extract" if c5 else ""),
+        **extras,
     }
-    if per_build is not None:
-        result["root_gather_per_build"] = per_build
-    if world > 1:
-        result["launcher_ranks"] = world
+    result["root_gather_per_build"] = per_build
+    result["launcher_ranks"] = world
     print(json.dumps(result), flush=True)
     g.close()
     for e in engines.values():
@@ -646,8 +680,11 @@ def main_group(args):
 def main():
     args = parse()
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.engine == "group" or (args.engine == "auto" and max(world_env, args.gpus) > 1
-                                  and args.layout == "a" and not args.rccl_selftest and not args.simulate_world):
+    # one engine and one timer over the whole scaling curve: the group engine
+    # at every N, N = 1 included; the one-process-per-GPU engine only on request or where the group
+    # path does not apply (layout B, --simulate-world, --rccl-selftest)
+    if args.engine == "group" or (args.engine == "auto" and args.layout == "a" and not args.rccl_selftest
+                                  and not args.simulate_world):
         return main_group(args)
     import torch
     import torch.distributed as dist
@@ -1095,7 +1132,7 @@ def main():
             "config": {"workload": desc, "layout": "A (sorted by partition, bucket)" if args.layout == "a"
                        else "B (arrival order + bucket tags, binned on device)", "n_keys": n_keys, "value_len": V, "n_partitions": P,
                        "n_buckets": B, "bytes_hashed_per_step": total_bytes,
-                       "partitions_per_gpu": Pl, "parallelism": f"partition-shard x{world}",
+                       "partitions_per_gpu": Pl, "parallelism": f"partition-shard x{world}", "engine": "ranks",
                        "root_gather": (("gloo all_gather (rehearsal, staged through the host)" if args.rehearse
                                         else "rccl all_gather_into_tensor")
                                        + f" of ceil(P/N) x {68 + 4 * cap if c5 else 32} B slabs on a side stream, "
@@ -1111,6 +1148,7 @@ def main():
                                                 local_bytes),
                          "kernel_ms": round(kern_ms, 5),
                          "algorithmic_bytes_per_launch": local_bytes},
+            "timer": TIMER_RANKS,
             "parity": parity,
             "host_timing": host_timing,
             "simulated_shard_of_world": shard_world if shard_world != world else None,
@@ -1123,8 +1161,9 @@ def main():
                                     "second stream, overlapping the next build's digest kernel",
                          "off": None}[mode],
         }
-        if per_build is not None:
-            result["root_gather_per_build"] = per_build
+        result["root_gather_per_build"] = per_build
+        result["launcher_ranks"] = world
+        result["end_to_end"] = result["production_shape"] = None
         if world == 1 and not args.no_cpu_baseline and not args.profile:
             result["cpu_baseline"] = cpu_baseline(co, s_vals, s_seg, s_n, cfg, args.cpu_baseline_seconds,
                                                   threads, info)

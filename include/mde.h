@@ -121,6 +121,10 @@ int mde_device_info(mde_ctx* ctx, int* cu_count, char* arch_name, int arch_cap);
  * B = 1000 -- with interleaved pieces for large shares). Results are identical for every setting;
  * only speed changes. */
 int mde_set_tuning(mde_ctx* ctx, int digest_variant, int digest_blocks_per_cu, int digest_oversub);
+/* Work accounting since the context was created: builds enqueued on it (mde_build[_async],
+ * mde_build_pipelined_async, each chunk of mde_build_streamed), their partitions and value bytes.
+ * On a group member's context (mde_group_ctx) it shows which GPU built what. */
+int mde_ctx_stats(mde_ctx* ctx, uint64_t* builds, uint64_t* partitions, uint64_t* value_bytes);
 /* Tuning hook: layout-A digest work split. 0 = one contiguous range per resident wave; N > 0 =
  * with the interleaved-pieces digest variant, each wave's share cut into pieces of about N bytes,
  * interleaved across the grid so all waves sweep the arena front to back together (used when a
@@ -336,9 +340,11 @@ uint64_t mde_group_last_error_copy(mde_group* group, char* buf, uint64_t cap);
  * partition range), builds them, the root slabs (ceil(P/G) roots each) are all-gathered, and the
  * outputs land in the caller's arrays in partition order. root == NULL: digest-only, no gather. */
 int mde_multi_build(mde_group* group, const mde_records* rec, const mde_tree_out* out);
-/* Host ingest over the group (arenas larger than HBM, nothing resident): each device streams one
- * contiguous block of partitions (one contiguous host range per PCIe link) through
- * mde_build_streamed on that device, concurrently. Same contract and results as mde_multi_build. */
+/* Host ingest over the group (arenas larger than HBM, nothing resident): partition p on device
+ * p % G as everywhere else in the group API (mde_group_partitions); each device streams its
+ * partitions in chunks of ~chunk_bytes (0: 256 MiB) through a two-slot device ring, one host copy
+ * per partition range, concurrently with the other devices. Same contract and results as
+ * mde_multi_build. */
 int mde_multi_build_streamed(mde_group* group, const mde_records* rec, const mde_tree_out* out,
                              uint64_t chunk_bytes);
 /* Device-resident use, each call enqueued on every device's context stream (mde_group_ctx,

@@ -52,7 +52,7 @@ EXPORTED_SYMBOLS = (
     "mde_server_create", "mde_server_destroy", "mde_server_slots", "mde_server_build", "mde_server_build_levels", "mde_server_verify", "mde_server_stats",
     "mde_tree_prefix_nodes", "mde_group_gather_overlapped_async", "mde_group_gather_wait_async",
     "mde_group_diff_async", "mde_group_extract_async", "mde_device_list", "mde_server_usable",
-    "mde_server_disable",
+    "mde_server_disable", "mde_ctx_stats",
 )
 
 
@@ -125,6 +125,7 @@ def load_library() -> C.CDLL:
         "mde_set_stream": (C.c_int, [vp, vp]),
         "mde_use_own_stream": (C.c_int, [vp]),
         "mde_set_tuning": (C.c_int, [vp, C.c_int, C.c_int, C.c_int]),
+        "mde_ctx_stats": (C.c_int, [vp, vp, vp, vp]),
         "mde_set_digest_piece_bytes": (C.c_int, [vp, u64]),
         "mde_set_verify_mode": (C.c_int, [vp, C.c_int]),
         "mde_get_stream": (vp, [vp]),
@@ -708,6 +709,12 @@ class Group:
 
     def ctx(self, i: int):
         return self.lib.mde_group_ctx(self.g, i)
+
+    def ctx_stats(self, i: int):
+        """mde_ctx_stats of device i's context: {"builds", "partitions", "value_bytes"}."""
+        v = [C.c_uint64() for _ in range(3)]
+        self._check(self.lib.mde_ctx_stats(self.ctx(i), *[C.byref(x) for x in v]))
+        return dict(zip(("builds", "partitions", "value_bytes"), (int(x.value) for x in v)))
 
     def _check(self, rc):
         if rc != MDE_OK:

@@ -414,6 +414,151 @@ int upload_and_build(mde_group* g, uint32_t i, const mde_records* r, bool tree, 
   return rc ? ctx_err(g, i, rc, msg) : MDE_OK;
 }
 
+// mde_multi_build_streamed's member i: its partitions i, i + G, ... streamed in chunks through a
+// two-slot device ring (see there). Host index arrays are kept until the member is done (the
+// copies from them are asynchronous).
+int stream_member(mde_group* g, uint32_t i, const mde_records* r, const mde_tree_out* o, uint64_t chunk_bytes,
+                  std::string& msg) {
+  const uint32_t G = (uint32_t)g->ctx.size(), P = r->n_partitions, B = r->n_buckets;
+  const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
+  const uint64_t NI = mde_tree_internal_nodes(B), Pi = parts_on(P, G, i);
+  const bool nodes = o->nodes != nullptr;
+  auto pos = [&](uint64_t k) { return r->value_stride ? k * r->value_stride : r->value_off[k]; };
+  auto first_rec = [&](uint64_t p) { return tagged ? r->part_rec[p] : r->seg_rec[p * B]; };
+  auto part = [&](uint64_t k) { return (uint64_t)i + k * G; };  // list entry k -> partition
+  // chunks of list entries, ~chunk_bytes each (at least one partition)
+  std::vector<uint64_t> cuts{0};
+  uint64_t max_bytes = 0, max_recs = 0, max_parts = 0;
+  for (uint64_t k = 0; k < Pi;) {
+    uint64_t q = k, bytes = 0, recs = 0;
+    do {
+      const uint64_t p = part(q);
+      bytes += pos(first_rec(p + 1)) - pos(first_rec(p));
+      recs += first_rec(p + 1) - first_rec(p);
+      q++;
+    } while (q < Pi && bytes + pos(first_rec(part(q) + 1)) - pos(first_rec(part(q))) <= chunk_bytes);
+    cuts.push_back(q);
+    max_bytes = std::max(max_bytes, bytes);
+    max_recs = std::max(max_recs, recs);
+    max_parts = std::max(max_parts, q - k);
+    k = q;
+  }
+  const uint64_t seg_per = tagged ? 1 : B;
+  GHIP(hipSetDevice(g->dev[i]));
+  hipStream_t st = static_cast<hipStream_t>(mde_get_stream(g->ctx[i]));
+  // ring: 2 x (values, index, value_off or tags); outputs of every list entry
+  struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() {
+      if (p) (void)hipFree(p);
+    }
+  };
+  DevBuf vals[2], idx[2], aux[2], d_dig, d_size, d_items, d_root, d_nodes;
+  const uint64_t aux_bytes = tagged ? max_recs * 2 + 16 : (r->value_stride ? 0 : (max_recs + 1) * 8);
+  for (int s = 0; s < 2; s++) {
+    GHIP(hipMalloc(&vals[s].p, max_bytes + 16));
+    GHIP(hipMalloc(&idx[s].p, (max_parts * seg_per + 1) * 8));
+    if (aux_bytes) GHIP(hipMalloc(&aux[s].p, aux_bytes));
+  }
+  GHIP(hipMalloc(&d_dig.p, std::max<uint64_t>(Pi * B * 8, 8)));
+  GHIP(hipMalloc(&d_size.p, std::max<uint64_t>(Pi * B * 4, 8)));
+  GHIP(hipMalloc(&d_items.p, std::max<uint64_t>(Pi * 4, 8)));
+  GHIP(hipMalloc(&d_root.p, std::max<uint64_t>(Pi * 32, 8)));
+  if (nodes) GHIP(hipMalloc(&d_nodes.p, std::max<uint64_t>(Pi * NI * 32, 8)));
+  hipStream_t cs = nullptr;
+  hipEvent_t loaded[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+  struct Cleanup {
+    hipStream_t& cs;
+    hipEvent_t* l;
+    hipEvent_t* d;
+    ~Cleanup() {
+      for (int s = 0; s < 2; s++) {
+        if (l[s]) (void)hipEventDestroy(l[s]);
+        if (d[s]) (void)hipEventDestroy(d[s]);
+      }
+      if (cs) (void)hipStreamDestroy(cs);
+    }
+  } cleanup{cs, loaded, done};
+  GHIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  for (int s = 0; s < 2; s++) {
+    GHIP(hipEventCreateWithFlags(&loaded[s], hipEventDisableTiming));
+    GHIP(hipEventCreateWithFlags(&done[s], hipEventDisableTiming));
+    GHIP(hipEventRecord(done[s], st));
+  }
+  std::vector<std::vector<uint64_t>> host_idx(cuts.size()), host_voff(cuts.size());
+  for (size_t c = 0; c + 1 < cuts.size(); c++) {
+    const int s = (int)(c & 1);
+    const uint64_t k0 = cuts[c], k1 = cuts[c + 1];
+    std::vector<uint64_t>& hi = host_idx[c];
+    std::vector<uint64_t>& hv = host_voff[c];
+    hi.resize((k1 - k0) * seg_per + 1);
+    uint64_t rb = 0, bb = 0;
+    GHIP(hipStreamWaitEvent(cs, done[s], 0));  // the build two chunks back released this slot
+    for (uint64_t k = k0; k < k1; k++) {
+      const uint64_t p = part(k), r0 = first_rec(p), r1 = first_rec(p + 1), b0 = pos(r0), b1 = pos(r1);
+      if (tagged) {
+        hi[k - k0] = rb;
+      } else {
+        for (uint32_t b = 0; b < B; b++) hi[(k - k0) * B + b] = r->seg_rec[p * B + b] - r0 + rb;
+      }
+      if (!r->value_stride && !tagged)
+        for (uint64_t j = r0; j < r1; j++) hv.push_back(r->value_off[j] - b0 + bb);
+      if (b1 > b0)
+        GHIP(hipMemcpyAsync(static_cast<uint8_t*>(vals[s].p) + bb, r->values + b0, b1 - b0, hipMemcpyHostToDevice, cs));
+      if (tagged && r1 > r0)
+        GHIP(hipMemcpyAsync(static_cast<uint8_t*>(aux[s].p) + rb * 2, r->bucket_tag + r0, (r1 - r0) * 2,
+                            hipMemcpyHostToDevice, cs));
+      rb += r1 - r0;
+      bb += b1 - b0;
+    }
+    hi.back() = rb;
+    GHIP(hipMemcpyAsync(idx[s].p, hi.data(), hi.size() * 8, hipMemcpyHostToDevice, cs));
+    if (!r->value_stride && !tagged) {
+      hv.push_back(bb);
+      GHIP(hipMemcpyAsync(aux[s].p, hv.data(), hv.size() * 8, hipMemcpyHostToDevice, cs));
+    }
+    GHIP(hipEventRecord(loaded[s], cs));
+    GHIP(hipStreamWaitEvent(st, loaded[s], 0));
+    mde_records dr{};
+    dr.values = static_cast<const uint8_t*>(vals[s].p);
+    dr.values_bytes = bb;
+    dr.value_stride = r->value_stride;
+    dr.layout = r->layout;
+    dr.value_off = (r->value_stride || tagged) ? nullptr : static_cast<const uint64_t*>(aux[s].p);
+    dr.n_records = rb;
+    dr.n_partitions = (uint32_t)(k1 - k0);
+    dr.n_buckets = B;
+    if (tagged) {
+      dr.part_rec = static_cast<const uint64_t*>(idx[s].p);
+      dr.bucket_tag = static_cast<const uint16_t*>(aux[s].p);
+    } else {
+      dr.seg_rec = static_cast<const uint64_t*>(idx[s].p);
+    }
+    mde_tree_out dout{static_cast<uint64_t*>(d_dig.p) + k0 * B, static_cast<int32_t*>(d_size.p) + k0 * B,
+                      static_cast<int32_t*>(d_items.p) + k0, static_cast<uint8_t*>(d_root.p) + k0 * 32,
+                      nodes ? static_cast<uint8_t*>(d_nodes.p) + k0 * NI * 32 : nullptr};
+    if (int rc = mde_build_async(g->ctx[i], &dr, &dout)) return ctx_err(g, i, rc, msg);
+    GHIP(hipEventRecord(done[s], st));
+  }
+  // the member's outputs home in list order, then to partition order
+  std::vector<uint8_t> h;
+  auto home = [&](const void* src, uint64_t row_bytes, uint8_t* dst) -> int {
+    h.resize(Pi * row_bytes);
+    GHIP(hipMemcpyAsync(h.data(), src, Pi * row_bytes, hipMemcpyDeviceToHost, st));
+    GHIP(hipStreamSynchronize(st));
+    for (uint64_t k = 0; k < Pi; k++) std::memcpy(dst + part(k) * row_bytes, h.data() + k * row_bytes, row_bytes);
+    return MDE_OK;
+  };
+  int rc;
+  if (o->digest && (rc = home(d_dig.p, (uint64_t)B * 8, reinterpret_cast<uint8_t*>(o->digest)))) return rc;
+  if (o->size && (rc = home(d_size.p, (uint64_t)B * 4, reinterpret_cast<uint8_t*>(o->size)))) return rc;
+  if (o->items && (rc = home(d_items.p, 4, reinterpret_cast<uint8_t*>(o->items)))) return rc;
+  if ((rc = home(d_root.p, 32, o->root))) return rc;
+  if (nodes && (rc = home(d_nodes.p, NI * 32, o->nodes))) return rc;
+  GHIP(hipStreamSynchronize(cs));
+  return MDE_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -698,9 +843,15 @@ int mde_multi_build(mde_group* g, const mde_records* r, const mde_tree_out* o) {
   return MDE_OK;
 }
 
-// Host ingest over the group (arenas larger than HBM): nothing stays resident, so each device
-// streams one contiguous block of partitions -- one contiguous host range per PCIe link -- through
-// mde_build_streamed's two-slot ring, concurrently. Same results as mde_multi_build.
+// Host ingest over the group (arenas larger than HBM): nothing stays resident. Partition p goes to
+// member p % G, the placement of every other group entry point (mde_multi_build, the
+// device-resident calls, mde_group_partitions). Member i streams its partitions i, i + G, ... in
+// chunks of about chunk_bytes through a two-slot device ring on its own thread: a copy stream
+// packs chunk k's partitions back to back into slot k % 2 -- one host-to-device copy per partition
+// range (a partition's records are contiguous in the host arena) plus the chunk's rebased index
+// arrays -- while the context stream builds chunk k - 1 from the other slot. The member's outputs
+// collect on its device in list order and come home once, scattered to partition order. Same
+// results as mde_multi_build.
 int mde_multi_build_streamed(mde_group* g, const mde_records* r, const mde_tree_out* o, uint64_t chunk_bytes) {
   if (!g || g->ctx.empty()) return MDE_E_INVAL;
   DeviceScope keep(g->dev[0]);
@@ -709,57 +860,19 @@ int mde_multi_build_streamed(mde_group* g, const mde_records* r, const mde_tree_
   int rc = check(r, o, g->err);
   if (rc) return rc;
   if (!o->root) return fail(g->err, MDE_E_INVAL, "out/root is NULL");
-  const uint32_t G = (uint32_t)g->ctx.size(), P = r->n_partitions, B = r->n_buckets;
-  const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
-  const uint64_t NI = mde_tree_internal_nodes(B);
-  struct Shard {
-    mde_records rec;
-    mde_tree_out out;
-    std::vector<uint64_t> seg, voff;
-    int rc = MDE_OK;
-    bool live = false;
-  };
-  std::vector<Shard> sh(G);
-  for (uint32_t i = 0; i < G; i++) {
-    const uint64_t p0 = (uint64_t)P * i / G, p1 = (uint64_t)P * (i + 1) / G;
-    if (p0 == p1) continue;
-    Shard& s = sh[i];
-    s.live = true;
-    s.rec = *r;
-    s.rec.n_partitions = (uint32_t)(p1 - p0);
-    const uint64_t r0 = tagged ? r->part_rec[p0] : r->seg_rec[p0 * B];
-    const uint64_t r1 = tagged ? r->part_rec[p1] : r->seg_rec[p1 * B];
-    const uint64_t b0 = r->value_stride ? r0 * r->value_stride : r->value_off[r0];
-    const uint64_t b1 = r->value_stride ? r1 * r->value_stride : r->value_off[r1];
-    s.rec.values = r->values + b0;
-    s.rec.values_bytes = b1 - b0;
-    s.rec.n_records = r1 - r0;
-    if (tagged) {
-      s.seg.assign(r->part_rec + p0, r->part_rec + p1 + 1);
-      s.rec.part_rec = s.seg.data();
-      s.rec.bucket_tag = r->bucket_tag ? r->bucket_tag + r0 : nullptr;
-    } else {
-      s.seg.assign(r->seg_rec + p0 * B, r->seg_rec + p1 * B + 1);
-      s.rec.seg_rec = s.seg.data();
-    }
-    for (uint64_t& x : s.seg) x -= r0;
-    if (!r->value_stride) {
-      s.voff.assign(r->value_off + r0, r->value_off + r1 + 1);
-      for (uint64_t& x : s.voff) x -= b0;
-      s.rec.value_off = s.voff.data();
-    }
-    s.out.digest = o->digest ? o->digest + p0 * B : nullptr;
-    s.out.size = o->size ? o->size + p0 * B : nullptr;
-    s.out.items = o->items ? o->items + p0 : nullptr;
-    s.out.root = o->root + p0 * 32;
-    s.out.nodes = o->nodes ? o->nodes + p0 * NI * 32 : nullptr;
-  }
+  if (!chunk_bytes) chunk_bytes = 256ull << 20;
+  const uint32_t G = (uint32_t)g->ctx.size(), P = r->n_partitions;
+  std::vector<int> rcs(G, MDE_OK);
+  std::vector<std::string> errs(G);
   std::vector<std::thread> th;
-  for (uint32_t i = 0; i < G; i++)
-    if (sh[i].live) th.emplace_back([&, i] { sh[i].rc = mde_build_streamed(g->ctx[i], &sh[i].rec, &sh[i].out, chunk_bytes); });
+  for (uint32_t i = 0; i < G && i < P; i++)
+    th.emplace_back([&, i] { rcs[i] = stream_member(g, i, r, o, chunk_bytes, errs[i]); });
   for (auto& t : th) t.join();
   for (uint32_t i = 0; i < G; i++)
-    if (sh[i].rc != MDE_OK) return ctx_err(g, i, sh[i].rc, g->err);
+    if (rcs[i]) {
+      g->err = errs[i];
+      return rcs[i];
+    }
   return MDE_OK;
 }
 

@@ -85,6 +85,9 @@ struct mde_ctx {
     bool dirty = false;
   };
   Slot pipe[2];
+  // Work accounting (mde_ctx_stats): builds enqueued on this context, their partitions and value
+  // bytes -- which GPU of a group built what.
+  uint64_t st_builds = 0, st_parts = 0, st_bytes = 0;
   struct Pending {
     bool active = false;
     int slot = 0;
@@ -554,7 +557,14 @@ int tree_async(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
 
 // digest + tree of one build on the context stream: one launch for a small layout-A arena
 // (latency of the one-partition calls), else the digest kernel then the tree kernel.
+void count_build(mde_ctx* c, const mde_records* r, uint64_t bytes) {
+  c->st_builds++;
+  c->st_parts += r->n_partitions;
+  c->st_bytes += bytes;
+}
+
 int build_async_impl(mde_ctx* c, const mde_records* r, const mde_tree_out* o) {
+  count_build(c, r, r->values_bytes);
   const uint64_t S = (uint64_t)r->n_partitions * r->n_buckets;
   if (r->layout == MDE_LAYOUT_SORTED && S && r->n_records && r->values_bytes &&
       mde::small_build_fits(r->values_bytes + 16, r->n_partitions, r->n_buckets)) {
@@ -878,6 +888,15 @@ int mde_set_tuning(mde_ctx* c, int digest_variant, int digest_blocks_per_cu, int
   return MDE_OK;
 }
 
+int mde_ctx_stats(mde_ctx* c, uint64_t* builds, uint64_t* partitions, uint64_t* value_bytes) {
+  if (!c) return MDE_E_INVAL;
+  Guard g(c);
+  if (builds) *builds = c->st_builds;
+  if (partitions) *partitions = c->st_parts;
+  if (value_bytes) *value_bytes = c->st_bytes;
+  return MDE_OK;
+}
+
 int mde_set_digest_piece_bytes(mde_ctx* c, uint64_t piece_bytes) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
@@ -971,6 +990,7 @@ int mde_build_pipelined_async(mde_ctx* c, const mde_records* r, const mde_tree_o
   int rc = check_records(c, r);
   if (rc) return rc;
   if (!o || !o->root) return set_err(c, MDE_E_INVAL, "out/root is NULL");
+  count_build(c, r, r->values_bytes);
   return build_pipelined(c, r, o);
 }
 
@@ -1104,6 +1124,7 @@ int mde_build_streamed(mde_ctx* c, const mde_records* r, const mde_tree_out* o, 
     }
     mde_tree_out co{d_digest + (uint64_t)p0 * B, d_size + (uint64_t)p0 * B, d_items + p0,
                     d_root + (uint64_t)p0 * 32, d_nodes ? d_nodes + (uint64_t)p0 * NI * 32 : nullptr};
+    count_build(c, &cr, byte1 - byte0);
     if (byte1 > byte0 && (rc = digest_async_biased(c, &cr, byte1, byte1 - byte0))) return rc;
     if ((rc = tree_async(c, &cr, &co))) return rc;
     MDE_HIP(c, hipEventRecord(c->ev_done[slot], c->stream));

@@ -1,7 +1,10 @@
 """The default bench line against the driver's contract (the JSON line the round-end BENCH run
 parses): every required key, roofline and cpu_baseline objects of the prescribed shape, value ==
 bytes hashed / ms_per_step, frac == achieved / peak, the timed build checked against the C oracle.
-Runs bench.py as the driver does (no flags but a short timed region), on the GPU."""
+Runs bench.py as the driver does (no flags but a short timed region), on the GPU. One engine and
+one timer over the whole scaling curve: the N = 1 line and a rehearsed N = 8 line (all eight
+shards on GPU 0) come from the same group engine with the same field set, and the one-process-per-GPU
+engine agrees with it at N = 1."""
 import json
 import subprocess
 import sys
@@ -11,14 +14,27 @@ import pytest
 from tests.conftest import ROOT
 
 
-@pytest.mark.gpu
-def test_default_bench_line_keeps_the_contract():
-    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "5", "--cpu-baseline-seconds", "2",
-                        "--no-e2e", "--no-production-shape"], capture_output=True, text=True, timeout=600, cwd=ROOT)
+def _line(*args, timeout=600):
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
-    d = json.loads(lines[0])
+    return json.loads(lines[0])
+
+
+_N1 = {}
+
+
+def _default_line():
+    if "d" not in _N1:
+        _N1["d"] = _line("--steps", "5", "--cpu-baseline-seconds", "2", "--no-e2e", "--no-production-shape")
+    return _N1["d"]
+
+
+@pytest.mark.gpu
+def test_default_bench_line_keeps_the_contract():
+    d = _default_line()
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in d, k
@@ -37,3 +53,23 @@ def test_default_bench_line_keeps_the_contract():
         assert k in cb, k
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0
     assert d["parity"]["all_ranks_ok"] and d["parity"]["timed_build_equals_c_oracle_on_sample"]
+
+
+@pytest.mark.gpu
+def test_scaling_curve_one_engine_one_timer():
+    """The driver's 1 -> 8 ratio divides like by like: the N = 1 line and a rehearsed N = 8 line
+    (bench.py --gpus 8 --rehearse: the eight shards of the strong-scaling split on GPU 0, copy
+    gather) share the engine, the timer text and the top-level field set; the one-process-per-GPU
+    engine (--engine ranks) measures the same N = 1 step within 1 %."""
+    d1 = _default_line()
+    d8 = _line("--gpus", "8", "--rehearse", "--steps", "5", "--no-gather-per-build")
+    assert d1["config"]["engine"] == d8["config"]["engine"] == "group"
+    assert d1["timer"] == d8["timer"]
+    assert set(d1) == set(d8), set(d1) ^ set(d8)
+    assert d8["n_gpus"] == 8 and d8["cpu_baseline"] is None and d8["parity"]["all_ranks_ok"]
+    assert d8["config"]["bytes_hashed_per_step"] == d1["config"]["bytes_hashed_per_step"]
+    dr = _line("--engine", "ranks", "--steps", "20", "--no-cpu-baseline", "--no-e2e", "--no-production-shape")
+    dg = _line("--steps", "20", "--no-cpu-baseline", "--no-e2e", "--no-production-shape")
+    assert dr["config"]["engine"] == "ranks" and dg["config"]["engine"] == "group"
+    assert set(dr) == set(dg), set(dr) ^ set(dg)
+    assert abs(dr["value"] - dg["value"]) / dg["value"] < 0.01, (dr["value"], dg["value"])

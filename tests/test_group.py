@@ -35,8 +35,9 @@ def _node_shas(out, P, B):
 @pytest.mark.parametrize("streamed", [False, True], ids=["direct", "streamed"])
 def test_multi_build_group(golden, coracle, devices, streamed):
     """mde_multi_build (partition p on device p % G, per-partition copies, RCCL or copy root
-    gather) and mde_multi_build_streamed (contiguous blocks through each device's ring, 4 KiB
-    chunks) equal the golden single builds, layouts A and B, nodes included."""
+    gather) and mde_multi_build_streamed (the same placement, each device's partitions streamed
+    through its two-slot ring, 4 KiB chunks) equal the golden single builds, layouts A and B,
+    nodes included."""
     import mydatastore_amd as mde
     g = mde.Group(devices)
     assert len(g) == len(devices)
@@ -66,6 +67,71 @@ def test_multi_build_group(golden, coracle, devices, streamed):
         ob = g.build(vb, P, B, V, part_rec=part_rec, bucket_tag=bk[order].astype(np.uint16), **kw)
         assert ob["digest"].tolist() == case["digest"], case["name"]
         assert _roots(ob, P) == case["root"], case["name"]
+    g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["a", "b", "var"])
+def test_every_group_entry_point_places_partition_p_on_member_p_mod_g(engine, layout):
+    """One placement for the whole group API: mde_multi_build,
+    mde_multi_build_streamed (several chunks per member) and the device-resident calls (a shard i
+    built from partitions i, i + G, ...) all build partition p on member p % G. Observed through
+    each member context's work accounting (mde_ctx_stats): the partitions and value bytes it built
+    equal those of partitions p % G == i, on an arena whose partitions all differ in size."""
+    import torch
+    import mydatastore_amd as mde
+    from mydatastore_amd.workload import make_workload
+    G, P, B = 3, 11, 16
+    rng = np.random.default_rng(5)
+    counts = rng.integers(0, 40, P * B)
+    counts[::7] = 0
+    seg = np.zeros(P * B + 1, np.uint64)
+    seg[1:] = np.cumsum(counts)
+    n = int(seg[-1])
+    V = 8
+    voff = None
+    if layout == "var":
+        lens = rng.integers(0, 30, n)
+        voff = np.zeros(n + 1, np.uint64)
+        voff[1:] = np.cumsum(lens)
+        values = rng.integers(0, 256, int(voff[-1]), dtype=np.uint8)
+        V = 0
+    else:
+        values = rng.integers(0, 256, n * V, dtype=np.uint8)
+    pos = (lambda r: int(voff[r])) if voff is not None else (lambda r: r * V)
+    part_bytes = [pos(int(seg[(p + 1) * B])) - pos(int(seg[p * B])) for p in range(P)]
+    want = [(sum(1 for p in range(P) if p % G == i), sum(part_bytes[p] for p in range(P) if p % G == i))
+            for i in range(G)]
+    assert len({b for _, b in want}) == G  # the members' byte totals tell the placements apart
+    g = mde.Group([0] * G)
+
+    def delta(fn):
+        before = [g.ctx_stats(i) for i in range(G)]
+        fn()
+        after = [g.ctx_stats(i) for i in range(G)]
+        return [(a["partitions"] - b["partitions"], a["value_bytes"] - b["value_bytes"]) for a, b in zip(after, before)]
+
+    if layout == "b":
+        part_rec = seg[::B].copy()
+        tags = np.repeat(np.tile(np.arange(B, dtype=np.uint16), P), counts)
+        kw = dict(part_rec=part_rec, bucket_tag=tags)
+    else:
+        kw = dict(value_off=voff, seg_rec=seg)
+    ref = g.build(values, P, B, V, **kw)
+    assert delta(lambda: g.build(values, P, B, V, **kw)) == want
+    st = delta(lambda: g.build(values, P, B, V, streamed=True, chunk_bytes=256, **kw))
+    assert st == want, (st, want)
+    got = g.build(values, P, B, V, streamed=True, chunk_bytes=256, **kw)
+    for k in ("digest", "size", "items", "root", "nodes"):
+        assert np.array_equal(got[k], ref[k]), k
+    if layout == "a":  # device-resident: shard i = partitions i, i + G, ... (make_workload's split)
+        shards = [make_workload(engine, n_partitions=P, n_buckets=B, value_len=8, part_mode="mod", n_keys=3000,
+                                rank=i, world=G) for i in range(G)]
+        for i, w in enumerate(shards):
+            assert list(w.partition_ids) == list(range(i, P, G)) and w.n_partitions == g.partitions(P, i)
+        outs = [w._outs() for w in shards]
+        d = delta(lambda: (g.build_async([w.rec for w in shards], [o[1] for o in outs]), g.synchronize()))
+        assert d == [(len(range(i, P, G)), shards[i].value_bytes) for i in range(G)]
     g.close()
 
 
@@ -389,7 +455,7 @@ def test_bench_group_under_torchrun(config):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert d["parity"]["all_ranks_ok"] and d["launcher_ranks"] == 2 and d["config"]["engine"] == "group"
-    assert ("root_gather_per_build" in d) == (config == "c4")
+    assert (d["root_gather_per_build"] is not None) == (config == "c4")
 
 
 @pytest.mark.gpu
