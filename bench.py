@@ -125,7 +125,9 @@ def resolve_warmup(args, calibrate):
     3 extra untimed steps run to completion, returning their wall ms."""
     if args.warmup is not None:
         return args.warmup
-    ms = calibrate(3)
+    # the per-step time from the faster of two 3-step calibrations: the first after an idle spell
+    # runs at the ramping clock (and pays first-launch costs), which would undercount W
+    ms = min(calibrate(3), calibrate(3))
     return max(3, int(np.ceil(WARMUP_MIN_MS / max(ms / 3, 1e-3))))
 
 
@@ -363,6 +365,11 @@ def main_group(args):
             dist.barrier()
         dist.destroy_process_group()
         return
+    # stdout carries exactly one JSON line: what the runtimes print on the way (RCCL's version
+    # banner at communicator creation) goes to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     N = args.gpus
     n_dev = torch.cuda.device_count()
     devices = [0] * N if args.rehearse else list(range(N))
@@ -668,7 +675,9 @@ def main_group(args):
     }
     result["root_gather_per_build"] = per_build
     result["launcher_ranks"] = world
-    print(json.dumps(result), flush=True)
+    sys.stdout.flush()
+    os.write(json_fd, (json.dumps(result) + "\n").encode())
+    os.close(json_fd)
     g.close()
     for e in engines.values():
         e.close()

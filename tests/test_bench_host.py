@@ -86,8 +86,8 @@ def test_group_bench_ranks_join_rank0s_barriers():
 
 def test_default_warmup_covers_the_clock_ramp():
     """--warmup W is taken as given; the default is >= 3 steps covering >= WARMUP_MIN_MS of device
-    time, from 3 calibration steps (the VALU-bound production step reads
-    ~12 % slow after 3 warm-up builds that follow an idle spell)."""
+    time, from the faster of two 3-step calibrations (the VALU-bound
+    production step reads ~12 % slow after 3 warm-up builds that follow an idle spell)."""
     import argparse
     import bench
     calls = []
@@ -102,7 +102,7 @@ def test_default_warmup_covers_the_clock_ramp():
     c4 = bench.resolve_warmup(argparse.Namespace(warmup=None), calibrate(1.48))
     prod = bench.resolve_warmup(argparse.Namespace(warmup=None), calibrate(0.17))
     c3 = bench.resolve_warmup(argparse.Namespace(warmup=None), calibrate(12.0))
-    assert calls == [3, 3, 3]
+    assert calls == [3] * 6
     assert c4 * 1.48 >= bench.WARMUP_MIN_MS and (c4 - 1) * 1.48 < bench.WARMUP_MIN_MS
     assert prod * 0.17 >= bench.WARMUP_MIN_MS and c3 == 3
 

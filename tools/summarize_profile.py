@@ -39,9 +39,9 @@ def main(src, tag, cfg):
         out["kernels"].setdefault(short(r["Name"]), {
             "calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
             "max_ns": float(r["MaxNs"]), "pct": float(r["Percentage"])})
-    bench = json.loads((src / "bench_trace.json").read_text())
+    bench = json.loads([x for x in (src / "bench_trace.json").read_text().splitlines() if x.startswith("{")][-1])
     alg = bench["roofline"]["algorithmic_bytes_per_launch"]
-    kern = bench["roofline"].get("kernel", "bucket_digest_kernel")
+    kern = bench["roofline"].get("kernel", "bucket_digest_kernel").split(" ")[0]
     out["dominant_kernel"] = kern
     for kind, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         f = src / f"pmc_{kind}" / "run_counter_collection.csv"
