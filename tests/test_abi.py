@@ -88,3 +88,29 @@ def test_last_error_copy_truncates_and_terminates(lib):
     big = C.create_string_buffer(64)
     assert lib.mde_group_last_error_copy(None, big, 64) == len(b"null group")
     assert big.value == b"null group"
+
+
+def test_product_sources_carry_no_probe_code():
+    """the product kernels compile only the variants plan_digest can select
+    (ids 11..16) and no probe sites -- no preprocessor conditional on an MDE_* macro anywhere in
+    the library's sources, so no stray -D can change what libmde.so computes. The per-wave
+    timeline stamps live in tools/probe_stamps.patch, applied to a scratch copy by
+    tools/build_probe_lib.sh; the patch must still apply to today's sources."""
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+    from tests.conftest import ROOT
+    csrc = ROOT / "mydatastore_amd" / "csrc"
+    for f in sorted(csrc.iterdir()):
+        if f.suffix in (".hip", ".cpp", ".hpp"):
+            bad = [ln for ln in f.read_text().splitlines() if re.match(r"\s*#\s*(if|ifdef|ifndef|elif)\b.*\bMDE_", ln)]
+            assert not bad, (f.name, bad)
+    digest = (csrc / "digest.hip").read_text()
+    assert re.findall(r"MDE_VARIANT\((\d+),", digest) == [str(i) for i in range(11, 17)]
+    if shutil.which("patch"):
+        with tempfile.TemporaryDirectory() as d:
+            shutil.copy(csrc / "digest.hip", d)
+            r = subprocess.run(["patch", "-p1", "--dry-run", "-i", str(ROOT / "tools" / "probe_stamps.patch")],
+                               cwd=d, capture_output=True, text=True)
+            assert r.returncode == 0, r.stdout + r.stderr
