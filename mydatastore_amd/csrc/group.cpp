@@ -98,8 +98,14 @@ struct mde_group {
   std::string err;
   // mde_multi_build staging, per device: values, value_off, seg_rec / part_rec, bucket_tag,
   // digest, size, items, root slab, nodes, gathered roots
-  enum { kVals, kVoff, kSeg, kTag, kDig, kSize, kItems, kRoot, kNodes, kRecv, kBufs };
+  // mde_multi_build_streamed's two-slot ring per device: values, index arrays, value_off or tags
+  enum { kVals, kVoff, kSeg, kTag, kDig, kSize, kItems, kRoot, kNodes, kRecv,
+         kRingV0, kRingV1, kRingI0, kRingI1, kRingA0, kRingA1, kBufs };
   std::vector<std::vector<Buf>> stage;
+  // and its copy stream + events per device (created on first use): [4 i + {loaded 0, loaded 1,
+  // done 0, done 1}]
+  std::vector<hipStream_t> copy;
+  std::vector<hipEvent_t> ring_ev;
   // Per-device enqueue threads (run_all, enq_pool.hpp): devices 1..G-1 each have one; the calling
   // thread enqueues device 0's share. Started on the first device-resident call of a group of
   // G > 1 (MDE_GROUP_THREADS=0: the calling thread enqueues every device's share in turn).
@@ -446,45 +452,32 @@ int stream_member(mde_group* g, uint32_t i, const mde_records* r, const mde_tree
   const uint64_t seg_per = tagged ? 1 : B;
   GHIP(hipSetDevice(g->dev[i]));
   hipStream_t st = static_cast<hipStream_t>(mde_get_stream(g->ctx[i]));
-  // ring: 2 x (values, index, value_off or tags); outputs of every list entry
-  struct DevBuf {
-    void* p = nullptr;
-    ~DevBuf() {
-      if (p) (void)hipFree(p);
-    }
-  };
-  DevBuf vals[2], idx[2], aux[2], d_dig, d_size, d_items, d_root, d_nodes;
+  // ring: 2 x (values, index, value_off or tags) and the member's outputs in list order, in the
+  // group's grow-only staging; the copy stream and its events persist with the group
   const uint64_t aux_bytes = tagged ? max_recs * 2 + 16 : (r->value_stride ? 0 : (max_recs + 1) * 8);
-  for (int s = 0; s < 2; s++) {
-    GHIP(hipMalloc(&vals[s].p, max_bytes + 16));
-    GHIP(hipMalloc(&idx[s].p, (max_parts * seg_per + 1) * 8));
-    if (aux_bytes) GHIP(hipMalloc(&aux[s].p, aux_bytes));
+  int rc;
+  for (int s = 0; s < 2; s++)
+    if ((rc = grow(g, i, mde_group::kRingV0 + s, max_bytes + 16, msg)) ||
+        (rc = grow(g, i, mde_group::kRingI0 + s, (max_parts * seg_per + 1) * 8, msg)) ||
+        (aux_bytes && (rc = grow(g, i, mde_group::kRingA0 + s, aux_bytes, msg))))
+      return rc;
+  if ((rc = grow(g, i, mde_group::kDig, Pi * B * 8, msg)) || (rc = grow(g, i, mde_group::kSize, Pi * B * 4, msg)) ||
+      (rc = grow(g, i, mde_group::kItems, Pi * 4, msg)) || (rc = grow(g, i, mde_group::kRoot, Pi * 32, msg)) ||
+      (nodes && (rc = grow(g, i, mde_group::kNodes, Pi * NI * 32, msg))))
+    return rc;
+  auto sp = [&](int k) { return g->stage[i][k].p; };
+  void* vals[2] = {sp(mde_group::kRingV0), sp(mde_group::kRingV1)};
+  void* idx[2] = {sp(mde_group::kRingI0), sp(mde_group::kRingI1)};
+  void* aux[2] = {sp(mde_group::kRingA0), sp(mde_group::kRingA1)};
+  GHIP(hipSetDevice(g->dev[i]));
+  if (!g->copy[i]) {
+    GHIP(hipStreamCreateWithFlags(&g->copy[i], hipStreamNonBlocking));
+    for (int k = 0; k < 4; k++) GHIP(hipEventCreateWithFlags(&g->ring_ev[4 * i + k], hipEventDisableTiming));
   }
-  GHIP(hipMalloc(&d_dig.p, std::max<uint64_t>(Pi * B * 8, 8)));
-  GHIP(hipMalloc(&d_size.p, std::max<uint64_t>(Pi * B * 4, 8)));
-  GHIP(hipMalloc(&d_items.p, std::max<uint64_t>(Pi * 4, 8)));
-  GHIP(hipMalloc(&d_root.p, std::max<uint64_t>(Pi * 32, 8)));
-  if (nodes) GHIP(hipMalloc(&d_nodes.p, std::max<uint64_t>(Pi * NI * 32, 8)));
-  hipStream_t cs = nullptr;
-  hipEvent_t loaded[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
-  struct Cleanup {
-    hipStream_t& cs;
-    hipEvent_t* l;
-    hipEvent_t* d;
-    ~Cleanup() {
-      for (int s = 0; s < 2; s++) {
-        if (l[s]) (void)hipEventDestroy(l[s]);
-        if (d[s]) (void)hipEventDestroy(d[s]);
-      }
-      if (cs) (void)hipStreamDestroy(cs);
-    }
-  } cleanup{cs, loaded, done};
-  GHIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-  for (int s = 0; s < 2; s++) {
-    GHIP(hipEventCreateWithFlags(&loaded[s], hipEventDisableTiming));
-    GHIP(hipEventCreateWithFlags(&done[s], hipEventDisableTiming));
-    GHIP(hipEventRecord(done[s], st));
-  }
+  hipStream_t cs = g->copy[i];
+  hipEvent_t* loaded = &g->ring_ev[4 * i];
+  hipEvent_t* done = &g->ring_ev[4 * i + 2];
+  for (int s = 0; s < 2; s++) GHIP(hipEventRecord(done[s], st));
   std::vector<std::vector<uint64_t>> host_idx(cuts.size()), host_voff(cuts.size());
   for (size_t c = 0; c + 1 < cuts.size(); c++) {
     const int s = (int)(c & 1);
@@ -504,40 +497,42 @@ int stream_member(mde_group* g, uint32_t i, const mde_records* r, const mde_tree
       if (!r->value_stride && !tagged)
         for (uint64_t j = r0; j < r1; j++) hv.push_back(r->value_off[j] - b0 + bb);
       if (b1 > b0)
-        GHIP(hipMemcpyAsync(static_cast<uint8_t*>(vals[s].p) + bb, r->values + b0, b1 - b0, hipMemcpyHostToDevice, cs));
+        GHIP(hipMemcpyAsync(static_cast<uint8_t*>(vals[s]) + bb, r->values + b0, b1 - b0, hipMemcpyHostToDevice, cs));
       if (tagged && r1 > r0)
-        GHIP(hipMemcpyAsync(static_cast<uint8_t*>(aux[s].p) + rb * 2, r->bucket_tag + r0, (r1 - r0) * 2,
+        GHIP(hipMemcpyAsync(static_cast<uint8_t*>(aux[s]) + rb * 2, r->bucket_tag + r0, (r1 - r0) * 2,
                             hipMemcpyHostToDevice, cs));
       rb += r1 - r0;
       bb += b1 - b0;
     }
     hi.back() = rb;
-    GHIP(hipMemcpyAsync(idx[s].p, hi.data(), hi.size() * 8, hipMemcpyHostToDevice, cs));
+    GHIP(hipMemcpyAsync(idx[s], hi.data(), hi.size() * 8, hipMemcpyHostToDevice, cs));
     if (!r->value_stride && !tagged) {
       hv.push_back(bb);
-      GHIP(hipMemcpyAsync(aux[s].p, hv.data(), hv.size() * 8, hipMemcpyHostToDevice, cs));
+      GHIP(hipMemcpyAsync(aux[s], hv.data(), hv.size() * 8, hipMemcpyHostToDevice, cs));
     }
     GHIP(hipEventRecord(loaded[s], cs));
     GHIP(hipStreamWaitEvent(st, loaded[s], 0));
     mde_records dr{};
-    dr.values = static_cast<const uint8_t*>(vals[s].p);
+    dr.values = static_cast<const uint8_t*>(vals[s]);
     dr.values_bytes = bb;
     dr.value_stride = r->value_stride;
     dr.layout = r->layout;
-    dr.value_off = (r->value_stride || tagged) ? nullptr : static_cast<const uint64_t*>(aux[s].p);
+    dr.value_off = (r->value_stride || tagged) ? nullptr : static_cast<const uint64_t*>(aux[s]);
     dr.n_records = rb;
     dr.n_partitions = (uint32_t)(k1 - k0);
     dr.n_buckets = B;
     if (tagged) {
-      dr.part_rec = static_cast<const uint64_t*>(idx[s].p);
-      dr.bucket_tag = static_cast<const uint16_t*>(aux[s].p);
+      dr.part_rec = static_cast<const uint64_t*>(idx[s]);
+      dr.bucket_tag = static_cast<const uint16_t*>(aux[s]);
     } else {
-      dr.seg_rec = static_cast<const uint64_t*>(idx[s].p);
+      dr.seg_rec = static_cast<const uint64_t*>(idx[s]);
     }
-    mde_tree_out dout{static_cast<uint64_t*>(d_dig.p) + k0 * B, static_cast<int32_t*>(d_size.p) + k0 * B,
-                      static_cast<int32_t*>(d_items.p) + k0, static_cast<uint8_t*>(d_root.p) + k0 * 32,
-                      nodes ? static_cast<uint8_t*>(d_nodes.p) + k0 * NI * 32 : nullptr};
-    if (int rc = mde_build_async(g->ctx[i], &dr, &dout)) return ctx_err(g, i, rc, msg);
+    mde_tree_out dout{static_cast<uint64_t*>(sp(mde_group::kDig)) + k0 * B,
+                      static_cast<int32_t*>(sp(mde_group::kSize)) + k0 * B,
+                      static_cast<int32_t*>(sp(mde_group::kItems)) + k0,
+                      static_cast<uint8_t*>(sp(mde_group::kRoot)) + k0 * 32,
+                      nodes ? static_cast<uint8_t*>(sp(mde_group::kNodes)) + k0 * NI * 32 : nullptr};
+    if ((rc = mde_build_async(g->ctx[i], &dr, &dout))) return ctx_err(g, i, rc, msg);
     GHIP(hipEventRecord(done[s], st));
   }
   // the member's outputs home in list order, then to partition order
@@ -549,12 +544,11 @@ int stream_member(mde_group* g, uint32_t i, const mde_records* r, const mde_tree
     for (uint64_t k = 0; k < Pi; k++) std::memcpy(dst + part(k) * row_bytes, h.data() + k * row_bytes, row_bytes);
     return MDE_OK;
   };
-  int rc;
-  if (o->digest && (rc = home(d_dig.p, (uint64_t)B * 8, reinterpret_cast<uint8_t*>(o->digest)))) return rc;
-  if (o->size && (rc = home(d_size.p, (uint64_t)B * 4, reinterpret_cast<uint8_t*>(o->size)))) return rc;
-  if (o->items && (rc = home(d_items.p, 4, reinterpret_cast<uint8_t*>(o->items)))) return rc;
-  if ((rc = home(d_root.p, 32, o->root))) return rc;
-  if (nodes && (rc = home(d_nodes.p, NI * 32, o->nodes))) return rc;
+  if (o->digest && (rc = home(sp(mde_group::kDig), (uint64_t)B * 8, reinterpret_cast<uint8_t*>(o->digest)))) return rc;
+  if (o->size && (rc = home(sp(mde_group::kSize), (uint64_t)B * 4, reinterpret_cast<uint8_t*>(o->size)))) return rc;
+  if (o->items && (rc = home(sp(mde_group::kItems), 4, reinterpret_cast<uint8_t*>(o->items)))) return rc;
+  if ((rc = home(sp(mde_group::kRoot), 32, o->root))) return rc;
+  if (nodes && (rc = home(sp(mde_group::kNodes), NI * 32, o->nodes))) return rc;
   GHIP(hipStreamSynchronize(cs));
   return MDE_OK;
 }
@@ -603,6 +597,8 @@ int mde_group_create(const int* devices, uint32_t n, mde_group** out) {
   g->ready.assign(n, nullptr);
   g->copied.assign(n, nullptr);
   g->side.assign(n, nullptr);
+  g->copy.assign(n, nullptr);
+  g->ring_ev.assign(4 * (size_t)n, nullptr);
   g->done.assign((size_t)mde_group::kRing * n, nullptr);
   for (uint32_t i = 0; i < n; i++) {
     (void)hipSetDevice(g->dev[i]);
@@ -635,6 +631,12 @@ void mde_group_destroy(mde_group* g) {
   const size_t n = g->dev.size();
   for (size_t i = 0; i < g->ready.size(); i++) {
     (void)hipSetDevice(g->dev[i]);
+    if (i < g->copy.size() && g->copy[i]) {
+      (void)hipStreamSynchronize(g->copy[i]);
+      (void)hipStreamDestroy(g->copy[i]);
+    }
+    for (size_t k = 0; k < 4 && 4 * i + k < g->ring_ev.size(); k++)
+      if (g->ring_ev[4 * i + k]) (void)hipEventDestroy(g->ring_ev[4 * i + k]);
     if (g->ready[i]) (void)hipEventDestroy(g->ready[i]);
     if (i < g->copied.size() && g->copied[i]) (void)hipEventDestroy(g->copied[i]);
     for (size_t k = 0; k < mde_group::kRing && k * n + i < g->done.size(); k++)
