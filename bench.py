@@ -531,6 +531,7 @@ def main_group(args):
             torch.cuda.synchronize(d)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         run.gather_s = 0.0
+        c0 = time.process_time()  # CPU time of every thread of the process (enqueue workers included)
         t0 = time.perf_counter()
         e0.record(ext)
         run.run(steps)
@@ -538,6 +539,7 @@ def main_group(args):
         e1.record(ext)
         g.synchronize()
         t1 = time.perf_counter()
+        c1 = time.process_time()
         run.tickets.clear()
         if world > 1:
             dist.barrier()
@@ -547,7 +549,11 @@ def main_group(args):
               "device_calls_per_step": N * (4 if c5 else 1),
               # of enqueue_ms: the gathers and their waits (the copy gather of a rehearsal issues
               # N x N copies from this thread; the RCCL gather N grouped calls)
-              "gather_enqueue_ms_per_step": round(run.gather_s * 1e3 / steps, 4)}
+              "gather_enqueue_ms_per_step": round(run.gather_s * 1e3 / steps, 4),
+              # host CPU the group engine burns (the enqueue threads' spin, the waits): cores busy
+              # on average over the timed region; MDE_GROUP_THREADS=0 enqueues from this thread
+              "host_cpu_ms_per_step": round((c1 - c0) * 1e3 / steps, 4),
+              "host_cpu_cores": round((c1 - c0) / max(t1 - t0, 1e-9), 3)}
         return ms, e0.elapsed_time(e1) / steps, ht
 
     main_run = Run(1 if c5 else GATHER_BUCKET)

@@ -68,6 +68,8 @@ def test_scaling_curve_one_engine_one_timer():
     assert set(d1) == set(d8), set(d1) ^ set(d8)
     assert d8["n_gpus"] == 8 and d8["cpu_baseline"] is None and d8["parity"]["all_ranks_ok"]
     assert d8["config"]["bytes_hashed_per_step"] == d1["config"]["bytes_hashed_per_step"]
+    for d in (d1, d8):  # the host CPU the engine burns is on the line (enq_pool spin)
+        assert 0 < d["host_timing"]["host_cpu_cores"] and d["host_timing"]["host_cpu_ms_per_step"] > 0
     dr = _line("--engine", "ranks", "--steps", "20", "--no-cpu-baseline", "--no-e2e", "--no-production-shape")
     dg = _line("--steps", "20", "--no-cpu-baseline", "--no-e2e", "--no-production-shape")
     assert dr["config"]["engine"] == "ranks" and dg["config"]["engine"] == "group"
