@@ -255,8 +255,8 @@ def production_shape(torch, eng, dev, threads, reps=10):
             eng.build_pipelined_async(w.rec, sets[i % 2][1])
         eng.build_pipeline_drain_async()
 
-    # each timed run right behind >= WARMUP_MIN_MS of builds (this runs after the CPU baseline has
-    # left the GPU idle for seconds; the step is shader-clock sensitive, see WARMUP_MIN_MS)
+    # each timed run right behind >= WARMUP_MIN_MS of builds (the step is shader-clock sensitive,
+    # see WARMUP_MIN_MS; a GPU idle for seconds before it reads it slow)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     run(reps)
@@ -642,16 +642,18 @@ def main_group(args):
     # shape, on GPU 0's engine, after the timed runs (never part of `value`)
     extras = {"cpu_baseline": None, "end_to_end": None, "production_shape": None}
     if N == 1 and world == 1 and not args.profile:
+        e0 = engines[devices[0]]
+        e0.set_stream(torch.cuda.current_stream(sdev[0]).cuda_stream)
+        # the production shape first, on the warm GPU: measured after the end-to-end leg, the
+        # standalone digest of this process read 155-159 us instead of 138-141
+        if not args.no_production_shape and not c5:
+            extras["production_shape"] = production_shape(torch, e0, sdev[0], threads)
         if not args.no_cpu_baseline:
             extras["cpu_baseline"] = cpu_baseline(co, s_vals, s_seg, s_n, (n_keys, P, V, B, mode, desc),
                                                   args.cpu_baseline_seconds, threads, info)
-        e0 = engines[devices[0]]
-        e0.set_stream(torch.cuda.current_stream(sdev[0]).cuda_stream)
         if not args.no_e2e and not c5:  # against the timed build's roots (its slab row: all P at N = 1)
             roots0 = main_run.send[kset][0].view(bk, slab * width)[row, :P * 32].cpu().numpy()
             extras["end_to_end"] = end_to_end(torch, e0, shards[0], B, ref_root=roots0)
-        if not args.no_production_shape and not c5:
-            extras["production_shape"] = production_shape(torch, e0, sdev[0], threads)
     result = {
         "metric": METRIC, "value": round(total / 2**30 / (ms * 1e-3), 3), "unit": "GiB/s", "n_gpus": N,
         "steps": args.steps, "warmup": warmup, "ms_per_step": round(ms, 5), "higher_is_better": True,
@@ -1179,6 +1181,8 @@ def main():
         result["root_gather_per_build"] = per_build
         result["launcher_ranks"] = world
         result["end_to_end"] = result["production_shape"] = None
+        if world == 1 and not args.no_production_shape and not args.profile and not c5 and args.layout == "a":
+            result["production_shape"] = production_shape(torch, eng, dev, threads)  # first, as main_group
         if world == 1 and not args.no_cpu_baseline and not args.profile:
             result["cpu_baseline"] = cpu_baseline(co, s_vals, s_seg, s_n, cfg, args.cpu_baseline_seconds,
                                                   threads, info)
@@ -1186,8 +1190,6 @@ def main():
             result["cpu_baseline"] = None
         if world == 1 and not args.no_e2e and not args.profile and not c5:
             result["end_to_end"] = end_to_end(torch, eng, w, B)
-        if world == 1 and not args.no_production_shape and not args.profile and not c5 and args.layout == "a":
-            result["production_shape"] = production_shape(torch, eng, dev, threads)
         print(json.dumps(result), flush=True)
     if use_dist:
         dist.barrier()
