@@ -5,6 +5,7 @@ parsing, that every C function, constant, type and struct field it names exists 
 with the argument count the shim passes.
 """
 import re
+from pathlib import Path
 
 from tests.conftest import ROOT
 
@@ -15,8 +16,19 @@ GO_NOMEMO = GO_DIR / "merkle_gpu_nomemo.go"      # //go:build mde_nohashstrategy
 HEADER = ROOT / "include" / "mde.h"
 
 
+GO_TEST = GO_DIR / "merkle_gpu_test.go"         # go test: the shim against the reference + oracle
+
+
 def _shim_sources():
-    return {p.name: p.read_text() for p in sorted(GO_DIR.glob("*.go"))}
+    return {p.name: p.read_text() for p in sorted(GO_DIR.glob("*.go")) if not p.name.endswith("_test.go")}
+
+
+def _imports_used(code, name):
+    imports = re.search(r"import \((.*?)\)", code, re.S).group(1)
+    body = code[code.index(imports) + len(imports):]
+    for pkg in re.findall(r'"([\w./-]+)"', imports):
+        if pkg != "C":
+            assert re.search(r"\b" + re.escape(pkg.rsplit("/", 1)[-1]) + r"\.", body), (name, pkg)
 
 
 def _header():
@@ -129,13 +141,50 @@ def test_shim_hash_strategy_constructor_is_build_tagged():
     assert "mdeNewTree(bucketList, digest," in code[GO.name]
     # each file imports what it uses (an unused import is a Go compile error)
     for n, c in code.items():
-        imports = re.search(r"import \((.*?)\)", c, re.S).group(1)
-        for pkg in re.findall(r'"([\w./-]+)"', imports):
-            name = pkg.rsplit("/", 1)[-1]
-            if pkg == "C":
-                continue
-            body = c[c.index(imports) + len(imports):]
-            assert re.search(r"\b" + re.escape(name) + r"\.", body), (n, pkg)
+        _imports_used(c, n)
+
+
+def test_go_parity_test_pins_the_oracle_fixtures():
+    """integration/go/merkle_gpu_test.go is the test a maintainer with Go and a GPU runs to pin the
+    oracle's tree bytes against the reference's own construction (merkletree v0.2.0 + Go's SHA-256):
+    its predicted roots and diff lists are exactly tests/golden/testmerkletreeraw_n{10,100}.json's,
+    it runs every path of the shim, and it names only the shim's and the reference's functions."""
+    import json
+    src = GO_TEST.read_text()
+    code = re.sub(r"//.*", "", src)
+    assert src.startswith("// merkle_gpu_test.go") and "package main" in code
+    _imports_used(code, GO_TEST.name)
+    for n in (10, 100):
+        fx = json.loads((ROOT / "tests" / "golden" / f"testmerkletreeraw_n{n}.json").read_text())
+        m = re.search(r"\b%d: \{\[3\]string\{(.*?)\},\s*\[\]int32\{(.*?)\}\}" % n, code, re.S)
+        assert m, n
+        roots = re.findall(r'"([0-9a-f]{64})"', m.group(1))
+        assert roots == [fx["trees"][k]["root"] for k in ("0_3", "1_3", "2_3")], n
+        assert [int(x) for x in re.findall(r"-?\d+", m.group(2))] == fx["diffs"]["t1_t3"], n
+        assert fx["n_buckets"] == 30 and fx["n"] == n
+    assert "c.Manager.PartitionBuckets = 30" in code and "n = 10" in code and "n := 100" in code
+    # every path: resident service / batcher x device tree / host tree
+    assert "for _, resident := range []bool{true, false}" in code
+    assert "for _, hostTree := range []bool{false, true}" in code
+    assert "manager.RawPartitionMerkleTree(0, r[0], r[1])" in code and "mdeSameTree(t, what, got, want)" in code
+    # the reference's construction, restated over the same store (main/merkle_tree.go:86-116)
+    assert "leaf.hasher.Add(it.Value())" in code and "return merkletree.NewTree(cs)" in code
+    # no second definition of anything the shim or the reference defines
+    shim = "\n".join(_shim_sources().values())
+    defined = set(re.findall(r"^func (?:\([^)]*\) )?(\w+)", code, re.M))
+    assert defined == {"mdeRefTree", "mdeSameTree", "TestMdeRawPartitionMerkleTreeMatchesReference"}
+    assert not any(re.search(r"^func (?:\([^)]*\) )?%s\(" % d, shim, re.M) for d in defined)
+    called = {"mdeEngine", "NewManager", "initMetrics", "BuildEpochIndex", "DifferentMerkleTreeBuckets"}
+    for f in called:
+        assert re.search(r"\b%s\(" % f, code), f
+    assert re.search(r"^func mdeEngine\(", shim, re.M)
+    ref = Path("/root/reference/main")
+    if ref.is_dir():  # this container only: the reference's package defines the rest
+        refsrc = "\n".join(p.read_text() for p in ref.glob("*.go") if not p.name.endswith("_test.go"))
+        for f in called - {"mdeEngine"}:
+            assert re.search(r"^func (?:\([^)]*\) )?%s\(" % f, refsrc, re.M), f
+        assert re.search(r"^func \(\w+ \*Manager\) SetValue\(", refsrc, re.M)
+        assert not re.search(r"^func (?:\([^)]*\) )?(mdeRefTree|mdeSameTree|mdePredicted)\b", refsrc, re.M)
 
 
 # ---------------------------------------------------------------------------------------------
