@@ -240,7 +240,7 @@ def pmc_traffic(config_name: str, local_bytes: int):
 PROD_SHAPE = (100_000_000, 1024, 8, 1000, "mod", "8-byte LE timestamps x 100M, 1024 partitions, B=1000")
 
 
-def production_shape(torch, eng, dev, threads, reps=10):
+def production_shape(torch, eng, dev, threads, reps=20):
     """Steady-state fused pipelined builds of PROD_SHAPE on this device (HIP events; a run of 2n
     builds minus a run of n, so the drain's tree launch cancels), the standalone digest kernel, and
     the C-oracle check of a sample of the last build. Reported beside `value`, never as it."""
