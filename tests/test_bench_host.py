@@ -121,3 +121,19 @@ def test_gpurun_upload_keeps_what_the_bench_reads():
             hit = (any(fnmatch.fnmatch(x, p) for x in prefixes) if p.startswith("./")
                    else any(fnmatch.fnmatch(x, p) for x in parts[1:]))
             assert not hit, (path, p)
+
+
+def test_production_shape_is_measured_before_the_host_legs():
+    """The N = 1 line measures the production shape first, on the warm GPU: measured after the
+    end-to-end leg, the standalone digest of the bench process read 12 % slow (DESIGN.md 4.9,
+    profiles/r06/r06s_*.json). Both engines keep that order: production shape, CPU baseline,
+    end to end."""
+    import re
+    from tests.conftest import ROOT
+    src = (ROOT / "bench.py").read_text()
+    for start in ("def main_group(", "def main("):
+        body = src[src.index(start):]
+        body = body[:body.index("\ndef ", 1)] if "\ndef " in body[1:] else body
+        pos = [m.start() for m in (re.search(r"= production_shape\(", body), re.search(r"= cpu_baseline\(", body),
+                                   re.search(r"= end_to_end\(", body))]
+        assert pos == sorted(pos), (start, pos)
