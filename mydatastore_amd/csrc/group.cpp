@@ -343,6 +343,16 @@ void stop_workers(mde_group* g) { g->pool.reset(); }
     if (e_ != hipSuccess) return fail(msg, MDE_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_));    \
   } while (0)
 
+// Waits for the given streams when it goes out of scope: a host-pointer entry point that returns
+// early (an error) must not leave copies in flight from host vectors about to be freed.
+struct StreamDrain {
+  hipStream_t a, b;
+  ~StreamDrain() {
+    if (a) (void)hipStreamSynchronize(a);
+    if (b) (void)hipStreamSynchronize(b);
+  }
+};
+
 // Shard i of a host-pointer build: its partitions' records copied to device i (one copy per
 // partition range: partition p's records are contiguous in the host arena), rebased, and the
 // build enqueued on the device's context stream.
@@ -374,6 +384,7 @@ int upload_and_build(mde_group* g, uint32_t i, const mde_records* r, bool tree, 
   std::vector<uint64_t> seg(nseg), voff(r->value_stride ? 0 : recs + 1);
   uint64_t rb = 0, bb = 0, k = 0;
   hipStream_t st = static_cast<hipStream_t>(mde_get_stream(g->ctx[i]));
+  StreamDrain drain{st, nullptr};  // an early return waits for the copies from seg / voff
   GHIP(hipSetDevice(g->dev[i]));
   for (uint64_t p = i; p < P; p += G, k++) {
     const uint64_t r0 = first_rec(p), r1 = first_rec(p + 1), b0 = pos(r0), b1 = pos(r1);
@@ -479,6 +490,9 @@ int stream_member(mde_group* g, uint32_t i, const mde_records* r, const mde_tree
   hipEvent_t* done = &g->ring_ev[4 * i + 2];
   for (int s = 0; s < 2; s++) GHIP(hipEventRecord(done[s], st));
   std::vector<std::vector<uint64_t>> host_idx(cuts.size()), host_voff(cuts.size());
+  // every return, an error one included, waits for the copies and builds issued from here: they
+  // read host_idx / host_voff and the caller's arena
+  StreamDrain drain{cs, st};
   for (size_t c = 0; c + 1 < cuts.size(); c++) {
     const int s = (int)(c & 1);
     const uint64_t k0 = cuts[c], k1 = cuts[c + 1];
