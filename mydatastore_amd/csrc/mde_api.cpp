@@ -179,6 +179,11 @@ constexpr uint64_t kPackedCallMax = 8ull << 20;
 class HostIo {
  public:
   explicit HostIo(mde_ctx* c) : c_(c) {}
+  // a call that returns between upload() and download() (an error) still waits for the copies
+  // it issued: they read the caller's buffers and the entry point's host vectors
+  ~HostIo() {
+    if (issued_) (void)hipStreamSynchronize(c_->stream);
+  }
   int in(const void* src, uint64_t copy_bytes, uint64_t dev_bytes) {
     pieces_[n_] = {const_cast<void*>(src), copy_bytes, dev_bytes, pin_.add(dev_bytes), true, false};
     return n_++;
@@ -211,6 +216,7 @@ class HostIo {
         else dev_[i] = static_cast<uint8_t*>(c_->packed_out.p) + q.off;
         if (q.input && q.host && q.copy) std::memcpy(hi + q.off, q.host, q.copy);
       }
+      issued_ = true;
       MDE_HIP(c_, hipMemcpyAsync(c_->packed_in.p, hi, pin_.total, hipMemcpyHostToDevice, c_->stream));
       return MDE_OK;
     }
@@ -218,6 +224,7 @@ class HostIo {
       const Piece& q = pieces_[i];
       if ((rc = ensure_buf(c_, c_->stage[i], q.dev))) return rc;
       dev_[i] = c_->stage[i].p;
+      issued_ = true;
       if (q.input && q.host && q.copy)
         MDE_HIP(c_, hipMemcpyAsync(dev_[i], q.host, q.copy, hipMemcpyHostToDevice, c_->stream));
     }
@@ -228,6 +235,7 @@ class HostIo {
       uint8_t* ho = static_cast<uint8_t*>(c_->pin_out.p);
       if (copy_bytes_) MDE_HIP(c_, hipMemcpyAsync(ho, c_->packed_out.p, copy_bytes_, hipMemcpyDeviceToHost, c_->stream));
       MDE_HIP(c_, hipStreamSynchronize(c_->stream));
+      issued_ = false;
       for (int i = 0; i < n_; i++) {
         const Piece& q = pieces_[i];
         if (!q.input && q.host && q.copy) std::memcpy(q.host, ho + (q.direct ? pcopy_.total : 0) + q.off, q.copy);
@@ -240,6 +248,7 @@ class HostIo {
         MDE_HIP(c_, hipMemcpyAsync(q.host, dev_[i], q.copy, hipMemcpyDeviceToHost, c_->stream));
     }
     MDE_HIP(c_, hipStreamSynchronize(c_->stream));
+    issued_ = false;
     return MDE_OK;
   }
 
@@ -256,6 +265,7 @@ class HostIo {
   int n_ = 0;
   Pack pin_, pcopy_, pdir_;
   bool packed_ = false;
+  bool issued_ = false;  // copies issued that download() has not waited for
 };
 
 int ensure_sums(mde_ctx* c, uint64_t S) {
@@ -321,6 +331,13 @@ struct Guard {
   std::lock_guard<std::mutex> lk;
   DeviceScope ds;
   explicit Guard(mde_ctx* ctx) : c(ctx), lk(ctx->mu), ds(ctx->device) { c->err.clear(); }
+};
+
+// Waits for the context stream when it goes out of scope: a synchronous entry point that returns
+// early (an error) must not leave copies in flight from host memory about to be freed.
+struct SyncOnReturn {
+  hipStream_t s;
+  ~SyncOnReturn() { (void)hipStreamSynchronize(s); }
 };
 
 int check_records(mde_ctx* c, const mde_records* r) {
@@ -1451,6 +1468,7 @@ int mde_decode_epoch_tree_objects(mde_ctx* c, uint32_t n, const uint8_t* bytes, 
   for (int i = 0; i < 10; i++)
     if ((rc = ensure_buf(c, c->stage[i], sz[i]))) return rc;
   std::vector<uint64_t> rel(N + 1);
+  SyncOnReturn drain{c->stream};  // declared after rel: an early return waits before rel is freed
   for (uint64_t i = 0; i <= N; i++) rel[i] = off[i] - off[0];
   if (nbytes) MDE_HIP(c, hipMemcpyAsync(c->stage[0].p, bytes + off[0], nbytes, hipMemcpyHostToDevice, c->stream));
   MDE_HIP(c, hipMemcpyAsync(c->stage[1].p, rel.data(), (N + 1) * 8, hipMemcpyHostToDevice, c->stream));
