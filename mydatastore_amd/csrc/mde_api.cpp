@@ -1067,6 +1067,8 @@ int mde_build_streamed(mde_ctx* c, const mde_records* r, const mde_tree_out* o, 
       MDE_HIP(c, hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming));
     }
   }
+  // every return waits for the copies and builds this call issued (they read the caller's arena)
+  SyncOnReturn drain_copy{c->copy_stream}, drain{c->stream};
   const uint32_t P = r->n_partitions, B = r->n_buckets;
   const bool tagged = r->layout == MDE_LAYOUT_TAGGED;
   const uint64_t NI = mde::tree_internal(B);
@@ -1166,6 +1168,7 @@ int mde_tree_from_digests(mde_ctx* c, uint32_t n_trees, uint32_t B, const uint64
                           uint8_t* root, uint8_t* nodes) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
+  SyncOnReturn drain{c->stream};  // every return waits for the copies this call issued
   if (B == 0 || !digest || !root) return set_err(c, MDE_E_INVAL, "bad tree_from_digests arguments");
   const uint64_t T = n_trees, NI = mde::tree_internal(B);
   int rc;
@@ -1244,6 +1247,7 @@ int mde_diff_digests(mde_ctx* c, uint32_t n_pairs, uint32_t Ba, const uint64_t* 
                      const uint64_t* db, int32_t* out_ids, uint64_t out_stride, int32_t* out_count) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
+  SyncOnReturn drain{c->stream};  // every return waits for the copies this call issued
   if (!Ba || !Bb || !da || !db || !out_ids || !out_count)
     return set_err(c, MDE_E_INVAL, "bad diff arguments");
   if (out_stride < mde_diff_capacity(Ba, Bb))
@@ -1306,6 +1310,7 @@ namespace {
 int extract_host(mde_ctx* c, const mde_records* r, const int32_t* ids, uint64_t ids_stride,
                  const int32_t* counts, uint64_t* part_off, uint64_t* out_rec, uint64_t rec_cap,
                  uint8_t* out_values, uint64_t* out_value_off, uint64_t bytes_cap, bool ordered) {
+  SyncOnReturn drain{c->stream};  // every return waits for the copies this call issued
   int rc = check_records(c, r);
   if (rc) return rc;
   if ((rc = check_host_records(c, r))) return rc;
@@ -1403,6 +1408,7 @@ int mde_encode_epoch_tree_objects(mde_ctx* c, uint32_t n, uint32_t B, const int3
                                   uint64_t out_stride, uint32_t* out_len) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
+  SyncOnReturn drain{c->stream};  // every return waits for the copies this call issued
   if ((B && (!digest || !size)) || !out || !out_len) return set_err(c, MDE_E_INVAL, "bad encode arguments");
   if (out_stride < mde::wire_max_bytes(B)) return set_err(c, MDE_E_CAPACITY, "out_stride too small");
   const uint64_t N = n;
@@ -1689,6 +1695,7 @@ int mde_tag_keys(mde_ctx* c, const uint8_t* keys, const uint64_t* key_off, uint6
                  uint32_t P, uint32_t* bucket, uint32_t* partition) {
   if (!c) return MDE_E_INVAL;
   Guard g(c);
+  SyncOnReturn drain{c->stream};  // every return waits for the copies this call issued
   if ((bucket && !B) || (partition && !P) || (n && (!keys || !key_off)))
     return set_err(c, MDE_E_INVAL, "bad tag_keys arguments");
   if (n == 0) return MDE_OK;
