@@ -29,7 +29,9 @@
  *    (copied under the context lock -- use it when the context is shared), or mde_last_error (a
  *    pointer into the context, valid until the next call on it: single-threaded use only).
  *  - Host input buffers are read only during the call and never retained (cgo pointer rules).
- *    Outputs are caller-allocated.
+ *    Outputs are caller-allocated. A synchronous call returns only after every copy and launch
+ *    it issued has finished, a failing call too: the caller may reuse or free its buffers as soon
+ *    as it returns.
  */
 #ifndef MDE_H_
 #define MDE_H_
