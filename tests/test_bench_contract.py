@@ -70,8 +70,11 @@ def test_scaling_curve_one_engine_one_timer():
     assert d8["config"]["bytes_hashed_per_step"] == d1["config"]["bytes_hashed_per_step"]
     for d in (d1, d8):  # the host CPU the engine burns is on the line (enq_pool spin)
         assert 0 < d["host_timing"]["host_cpu_cores"] and d["host_timing"]["host_cpu_ms_per_step"] > 0
-    dr = _line("--engine", "ranks", "--steps", "20", "--no-cpu-baseline", "--no-e2e", "--no-production-shape")
-    dg = _line("--steps", "20", "--no-cpu-baseline", "--no-e2e", "--no-production-shape")
+    short = ("--steps", "20", "--no-cpu-baseline", "--no-e2e", "--no-production-shape")
+    # each engine's best of two alternating runs, so one noisy run on a shared box does not decide
+    runs = [_line("--engine", "ranks", *short), _line(*short), _line("--engine", "ranks", *short), _line(*short)]
+    dr = max(runs[0::2], key=lambda d: d["value"])
+    dg = max(runs[1::2], key=lambda d: d["value"])
     assert dr["config"]["engine"] == "ranks" and dg["config"]["engine"] == "group"
     assert set(dr) == set(dg), set(dr) ^ set(dg)
-    assert abs(dr["value"] - dg["value"]) / dg["value"] < 0.01, (dr["value"], dg["value"])
+    assert abs(dr["value"] - dg["value"]) / dg["value"] < 0.01, ([d["value"] for d in runs])
